@@ -1,0 +1,160 @@
+"""ORACLE (test infrastructure only) -- ctypes binding of oracle/pgo_oracle.c.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module.  The product path (graphslam_amd/) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+
+class OrcParams(C.Structure):
+    _fields_ = [("max_iterations", C.c_int), ("relative_error_tol", C.c_double),
+                ("absolute_error_tol", C.c_double), ("error_tol", C.c_double),
+                ("lambda_initial", C.c_double), ("lambda_factor", C.c_double),
+                ("lambda_upper_bound", C.c_double), ("lambda_lower_bound", C.c_double),
+                ("min_model_fidelity", C.c_double), ("use_fixed_lambda_factor", C.c_int),
+                ("algorithm", C.c_int), ("max_outer", C.c_int)]
+
+
+class OrcStats(C.Structure):
+    _fields_ = [("status", C.c_int), ("iterations", C.c_int), ("inner_iterations", C.c_int),
+                ("linearizations", C.c_int), ("initial_error", C.c_double),
+                ("final_error", C.c_double), ("t_total", C.c_double), ("t_linearize", C.c_double),
+                ("t_factor", C.c_double), ("t_solve", C.c_double), ("t_error", C.c_double),
+                ("factor_flops", C.c_double), ("nnz_l", C.c_double), ("nsuper", C.c_int),
+                ("t_symbolic", C.c_double)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        L.orc_create.restype = C.c_void_p
+        L.orc_create.argtypes = [C.c_int, C.c_int, ip, ip, dp, dp, C.c_int, ip, dp, dp, C.POINTER(C.c_int)]
+        L.orc_destroy.argtypes = [C.c_void_p]
+        L.orc_default_params.argtypes = [C.POINTER(OrcParams)]
+        L.orc_optimize.argtypes = [C.c_void_p, dp, C.POINTER(OrcParams), dp, C.POINTER(OrcStats), dp,
+                                   C.c_int, C.POINTER(C.c_int)]
+        L.orc_linearize.argtypes = [C.c_void_p, dp, dp, dp, dp, dp]
+        L.orc_solve.argtypes = [C.c_void_p, dp, C.c_double, dp]
+        L.orc_error.argtypes = [C.c_void_p, dp]
+        L.orc_error.restype = C.c_double
+        L.orc_information.argtypes = [dp, dp]
+        _lib = L
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _ip(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def information(cov):
+    cov = np.ascontiguousarray(cov, dtype=np.float64).reshape(9)
+    om = np.zeros(9)
+    rc = lib().orc_information(_dp(cov), _dp(om))
+    return rc, om.reshape(3, 3)
+
+
+@dataclass
+class OracleResult:
+    poses: np.ndarray
+    stats: dict
+    trace: np.ndarray
+
+
+class Oracle:
+    """CPU restatement of LevenbergMarquardtOptimizer(graph, initial).optimize()."""
+
+    def __init__(self, g):
+        L = lib()
+        ei, ej = g.edge_index()
+        self._keep = dict(
+            ei=np.ascontiguousarray(ei, dtype=np.int32), ej=np.ascontiguousarray(ej, dtype=np.int32),
+            ez=np.ascontiguousarray(g.edge_z, dtype=np.float64),
+            ec=np.ascontiguousarray(g.edge_cov, dtype=np.float64),
+            pi=np.ascontiguousarray(g.prior_index(), dtype=np.int32),
+            pz=np.ascontiguousarray(g.prior_pose, dtype=np.float64),
+            pc=np.ascontiguousarray(g.prior_cov, dtype=np.float64))
+        k = self._keep
+        st = C.c_int(0)
+        self.n = g.num_poses
+        self.ne = g.num_edges
+        self.h = L.orc_create(self.n, self.ne, _ip(k["ei"]), _ip(k["ej"]), _dp(k["ez"]), _dp(k["ec"]),
+                              len(k["pi"]), _ip(k["pi"]), _dp(k["pz"]), _dp(k["pc"]), C.byref(st))
+        self.status = st.value
+        if not self.h:
+            raise ValueError(f"oracle rejected graph: status {st.value}")
+        self.initial = np.ascontiguousarray(g.initial, dtype=np.float64)
+
+    def close(self):
+        if self.h:
+            lib().orc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def params(**kw):
+        p = OrcParams()
+        lib().orc_default_params(C.byref(p))
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+    def optimize(self, init=None, trace_cap=4096, **kw) -> OracleResult:
+        init = self.initial if init is None else np.ascontiguousarray(init, dtype=np.float64)
+        out = np.zeros((self.n, 3))
+        tr = np.zeros((trace_cap, 7))
+        ntr = C.c_int(0)
+        st = OrcStats()
+        p = self.params(**kw)
+        lib().orc_optimize(self.h, _dp(init), C.byref(p), _dp(out), C.byref(st), _dp(tr), trace_cap,
+                           C.byref(ntr))
+        stats = {f: getattr(st, f) for f, _ in OrcStats._fields_}
+        return OracleResult(out, stats, tr[: ntr.value].copy())
+
+    def linearize(self, poses=None):
+        poses = self.initial if poses is None else np.ascontiguousarray(poses, dtype=np.float64)
+        hd = np.zeros((self.n, 3, 3))
+        ho = np.zeros((self.ne, 3, 3))
+        g = np.zeros((self.n, 3))
+        err = C.c_double(0)
+        lib().orc_linearize(self.h, _dp(poses), _dp(hd), _dp(ho), _dp(g), C.byref(err))
+        return hd, ho, g, err.value
+
+    def solve(self, lam, poses=None):
+        poses = self.initial if poses is None else np.ascontiguousarray(poses, dtype=np.float64)
+        d = np.zeros((self.n, 3))
+        rc = lib().orc_solve(self.h, _dp(poses), lam, _dp(d))
+        return rc, d
+
+    def error(self, poses=None):
+        poses = self.initial if poses is None else np.ascontiguousarray(poses, dtype=np.float64)
+        return lib().orc_error(self.h, _dp(poses))
