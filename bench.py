@@ -1,0 +1,196 @@
+"""Benchmark: GN iterations/s + ms-to-chi^2 convergence on the 100k-pose Manhattan graph.
+
+A step = one complete pgo_optimize() (GTSAM-default Levenberg-Marquardt) of the
+C3 graph (100k poses / 500k between factors, BASELINE.json configs[2]) from its
+dead-reckoned initial values; the values are restored on the device (no PCIe)
+before every step, the graph stays resident in HBM.  pgo_optimize returns only
+after its HIP stream has drained (it reads the final error back), so the host
+clock brackets all device work.
+
+value = linearisations ("GN iterations": linearise + solve(s) + retract + chi^2)
+summed over all ranks / max-over-ranks wall time of the K timed steps.
+
+Multi-GPU: the path runs as independent replicas (one process per GPU, each
+optimising its own copy of the graph; no data-path collective) -> "weak"
+scaling.  The RCCL-sharded solve is future work.
+
+    python bench.py [--gpus N --steps K --warmup W --config C3 --no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def spmv_bytes(n, slots):
+    """Algorithmic bytes of one k_pcg_spmv launch (DESIGN.md 'Roofline'):
+    per slot V 72 B + column 4 B; per row row_ptr 4 B + D 48 B + p 24 B + q 24 B."""
+    return 76 * slots + 100 * n
+
+
+def linearize_bytes(n, ne):
+    """Algorithmic bytes of one k_linearize launch: per factor ids 8 + z 32 + Omega 48
+    read, two 72 B blocks written; per pose 32 B read, D 48 + g 24 written."""
+    return ne * (8 + 32 + 48 + 144) + n * (32 + 48 + 24)
+
+
+def cpu_baseline(g, max_outer):
+    """The C oracle (same LM, sparse Cholesky) on a bounded sample: the first
+    max_outer linearisations from the same initial values."""
+    from oracle.oracle import Oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    o = Oracle(g)
+    r = o.optimize(max_outer=max_outer)
+    s = r.stats
+    t = s["t_total"]
+    return {
+        "value": s["linearizations"] / t,
+        "unit": "GN iterations/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"first {s['linearizations']} LM linearisations ({s['inner_iterations']} Cholesky solves, "
+                   f"{s['factor_flops'] / 1e9:.1f} GFLOP each, nnz(L) {s['nnz_l'] / 1e6:.0f}M) of {g.name} "
+                   f"from the same initial values, {t:.1f} s, oracle/pgo_oracle.c AMD + supernodal "
+                   f"multifrontal Cholesky, OMP_NUM_THREADS={threads}"),
+        "ms_per_linearization": 1e3 * t / max(s["linearizations"], 1),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--profile-every", type=int, default=16)
+    ap.add_argument("--cpu-outer", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from graphslam_amd import datasets
+    from graphslam_amd.pose_graph import PoseGraph, default_params
+
+    g = datasets.make(args.config)
+    pg = PoseGraph.from_dataset(g, device=local_rank)
+    pg.save_values()                     # upload graph + values once; snapshot the initial values
+    params = default_params(profile_every=args.profile_every)
+
+    for _ in range(args.warmup):
+        pg.restore_values()
+        pg.optimize(params)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    totals = dict(linearizations=0, inner=0, pcg=0, spmv_ms=0.0, spmv_n=0, lin_ms=0.0, lin_n=0)
+    last = None
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pg.restore_values()
+        st = pg.optimize(params)
+        totals["linearizations"] += st["linearizations"]
+        totals["inner"] += st["inner_iterations"]
+        totals["pcg"] += st["pcg_iterations"]
+        totals["spmv_ms"] += st["kernel_spmv_ms"]
+        totals["spmv_n"] += st["kernel_spmv_count"]
+        totals["lin_ms"] += st["kernel_linearize_ms"]
+        totals["lin_n"] += st["kernel_linearize_count"]
+        last = st
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    lin_total = totals["linearizations"]
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([float(lin_total)], dtype=torch.float64)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        lin_total = int(c.item())
+
+    if rank == 0:
+        n, ne = g.num_poses, g.num_edges
+        slots = 2 * ne
+        spmv_avg_ms = totals["spmv_ms"] / max(totals["spmv_n"], 1)
+        achieved = spmv_bytes(n, slots) / (spmv_avg_ms * 1e-3) / 1e9 if totals["spmv_n"] else None
+        lin_avg_ms = totals["lin_ms"] / max(totals["lin_n"], 1)
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get(args.config, {}).get("k_pcg_spmv_bytes_per_launch")
+        out = {
+            "metric": "GN iterations/sec + ms-to-chi2 convergence, 100k-pose Manhattan graph",
+            "value": lin_total / elapsed,
+            "unit": "GN iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "ms_to_convergence": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.config}: {n} poses / {ne} between factors + 1 prior, Manhattan walk "
+                            f"(seed {g.meta.get('seed')}), GTSAM-default LM from dead-reckoned values",
+                "poses": n, "edges": ne, "parallelism": f"replicas{world}",
+                "solver": "block-Jacobi PCG, rel tol %.0e" % params.pcg_relative_tol,
+            },
+            "per_step": {
+                "linearizations": last["linearizations"], "lm_tries": last["inner_iterations"],
+                "accepted": last["iterations"], "pcg_iterations": last["pcg_iterations"],
+                "initial_error": last["initial_error"], "final_error": last["final_error"],
+                "ms_linearize": last["ms_linearize"], "ms_solve": last["ms_solve"], "ms_update": last["ms_update"],
+            },
+            "roofline": {
+                "kernel": "k_pcg_spmv",
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS if achieved else None,
+                "traffic": traffic,
+                "bytes_per_launch": spmv_bytes(n, slots),
+                "avg_launch_ms": spmv_avg_ms,
+                "timed_launches": totals["spmv_n"],
+            },
+            "linearize_kernel": {
+                "kernel": "k_linearize",
+                "avg_launch_ms": lin_avg_ms,
+                "bytes_per_launch": linearize_bytes(n, ne),
+                "achieved_gbs": linearize_bytes(n, ne) / (lin_avg_ms * 1e-3) / 1e9 if totals["lin_n"] else None,
+            },
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(g, args.cpu_outer)
+        print(json.dumps(out))
+    pg.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

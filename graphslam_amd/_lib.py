@@ -1,0 +1,124 @@
+"""ctypes binding of libpgo.so (include/pgo.h).
+
+The library is built in-tree (graphslam_amd/libpgo.so, see csrc/Makefile).
+There is no fallback: if the HIP library is missing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpgo.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "pgo.h")
+
+PGO_OK = 0
+PGO_E_ARG = -1
+PGO_E_DUP_KEY = -2
+PGO_E_NO_KEY = -3
+PGO_E_BAD_COV = -4
+PGO_E_INDETERMINANT = -5
+PGO_E_NONFINITE = -6
+PGO_E_HIP = -7
+PGO_E_NO_DEVICE = -8
+PGO_E_NOMEM = -9
+PGO_E_BAD_EDGE = -10
+PGO_W_MAXITER = 1
+PGO_ALG_LM = 0
+PGO_ALG_GN = 1
+
+
+class PgoOpts(C.Structure):
+    _fields_ = [("device", C.c_int), ("reserved", C.c_int * 7)]
+
+
+class PgoParams(C.Structure):
+    _fields_ = [("max_iterations", C.c_int), ("relative_error_tol", C.c_double),
+                ("absolute_error_tol", C.c_double), ("error_tol", C.c_double),
+                ("lambda_initial", C.c_double), ("lambda_factor", C.c_double),
+                ("lambda_upper_bound", C.c_double), ("lambda_lower_bound", C.c_double),
+                ("min_model_fidelity", C.c_double), ("use_fixed_lambda_factor", C.c_int),
+                ("algorithm", C.c_int), ("linear_solver", C.c_int), ("pcg_relative_tol", C.c_double),
+                ("pcg_max_iterations", C.c_int), ("pcg_check_interval", C.c_int), ("max_outer", C.c_int),
+                ("profile_every", C.c_int)]
+
+
+class PgoStats(C.Structure):
+    _fields_ = [("status", C.c_int), ("iterations", C.c_int), ("inner_iterations", C.c_int),
+                ("linearizations", C.c_int), ("initial_error", C.c_double), ("final_error", C.c_double),
+                ("pcg_iterations", C.c_longlong), ("ms_total", C.c_double), ("ms_upload", C.c_double),
+                ("ms_linearize", C.c_double), ("ms_solve", C.c_double), ("ms_update", C.c_double),
+                ("kernel_spmv_ms", C.c_double), ("kernel_spmv_count", C.c_longlong),
+                ("kernel_linearize_ms", C.c_double), ("kernel_linearize_count", C.c_longlong),
+                ("reserved", C.c_double * 4)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", os.path.join(HERE, "csrc")], check=True)
+
+
+def declared_symbols():
+    """Every function name include/pgo.h declares."""
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(pgo_[a-z_0-9]+)\s*\(", text)))
+
+
+_lib = None
+
+
+def lib():
+    """Load libpgo.so; raise (never fall back) if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libpgo.so not built at {LIB_PATH}: run `make -C graphslam_amd/csrc` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, dp, u64p = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)
+    sig = {
+        "pgo_create": (vp, [C.POINTER(PgoOpts)]),
+        "pgo_destroy": (None, [vp]),
+        "pgo_last_error": (C.c_char_p, [vp]),
+        "pgo_status_string": (C.c_char_p, [C.c_int]),
+        "pgo_abi_version": (C.c_int, []),
+        "pgo_default_params": (None, [C.POINTER(PgoParams)]),
+        "pgo_add_vertex": (C.c_int, [vp, C.c_uint64, C.c_double, C.c_double, C.c_double]),
+        "pgo_add_vertices": (C.c_int, [vp, C.c_size_t, u64p, dp]),
+        "pgo_add_prior": (C.c_int, [vp, C.c_uint64, dp, dp]),
+        "pgo_add_edge": (C.c_int, [vp, C.c_uint64, C.c_uint64, dp, dp]),
+        "pgo_add_edges": (C.c_int, [vp, C.c_size_t, u64p, u64p, dp, dp, C.c_int]),
+        "pgo_optimize": (C.c_int, [vp, C.POINTER(PgoParams), C.POINTER(PgoStats)]),
+        "pgo_get_pose": (C.c_int, [vp, C.c_uint64, dp]),
+        "pgo_get_poses": (C.c_int, [vp, C.c_size_t, u64p, dp]),
+        "pgo_set_poses": (C.c_int, [vp, C.c_size_t, u64p, dp]),
+        "pgo_save_values": (C.c_int, [vp]),
+        "pgo_restore_values": (C.c_int, [vp]),
+        "pgo_num_factors": (C.c_size_t, [vp]),
+        "pgo_num_vertices": (C.c_size_t, [vp]),
+        "pgo_error": (C.c_int, [vp, dp]),
+        "pgo_debug_linearize": (C.c_int, [vp, dp, dp, dp, dp]),
+        "pgo_debug_spmv": (C.c_int, [vp, C.c_double, dp, dp]),
+        "pgo_debug_solve": (C.c_int, [vp, C.c_double, C.POINTER(PgoParams), dp, C.POINTER(C.c_int)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.pgo_abi_version() != 1:
+        raise RuntimeError("libpgo.so ABI version mismatch")
+    _lib = L
+    return L
+
+
+def dptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double)) if a is not None else None
+
+
+def u64ptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint64)) if a is not None else None

@@ -1,0 +1,802 @@
+// libpgo.so: host side of the C-ABI in include/pgo.h.
+//
+// Mirrors, call for call, what /root/reference/src/graph/src/graph.cpp does
+// through GTSAM (insert / add / optimize / at / nrFactors), keeps the graph and
+// its values resident in HBM between calls, and drives the device kernels of
+// pgo_kernels.hip with GTSAM's Levenberg-Marquardt control logic
+// (tryLambda / decreaseLambda / increaseLambda / checkConvergence, GTSAM 4.0
+// defaults) running on host scalars read back once per lambda try.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "pgo.h"
+#include "pgo_device.h"
+
+using pgo::DevGraph;
+
+struct pgo_graph {
+  int device = 0;
+  std::string last_error;
+  // ---- host copy of the factor graph (insertion order) ----
+  std::unordered_map<uint64_t, int32_t> index;
+  std::vector<uint64_t> keys;
+  std::vector<double> xyt;                  // current values (x, y, theta)
+  std::vector<uint64_t> ek1, ek2;
+  std::vector<double> ez;                   // 3 per between factor
+  std::vector<double> eom;                  // 6 per factor: O00 O01 O02 O11 O12 O22
+  std::vector<uint64_t> pk;
+  std::vector<double> pz, pom;
+  // ---- device state ----
+  bool hip_ready = false;
+  bool dev_structure = false;               // device graph matches host graph
+  bool dev_values = false;                  // device pose == host xyt
+  bool host_values = true;                  // host xyt == device pose
+  DevGraph d;
+  std::vector<int> edge_slot0;              // side-0 slot of every between factor
+  double* h_scal = nullptr;                 // pinned
+  int* h_ctrl = nullptr;                    // pinned
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  static constexpr int kProfPairs = 64;     // sampled SpMV timings per read-back
+  hipEvent_t pev[2 * kProfPairs] = {};
+  int pk_iter[kProfPairs] = {};
+};
+
+namespace {
+
+int fail(pgo_graph* g, int code, const std::string& msg) {
+  if (g) g->last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(g, expr)                                                                       \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return fail(g, PGO_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));            \
+  } while (0)
+
+// noiseModel::Gaussian::Covariance(Q) (graph.cpp:45,83,103) -> Omega upper 6.
+// GTSAM's smart check: all |off-diagonal| <= 1e-9 -> Diagonal::Variances;
+// otherwise Information(Q^-1) with R = LLT(Q^-1).matrixU(): the lower triangle
+// of Q^-1 is what counts, mirrored.
+int information(const double* q, double* om6) {
+  for (int i = 0; i < 9; i++)
+    if (!std::isfinite(q[i])) return PGO_E_BAD_COV;
+  bool full = false;
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++)
+      if (i != j && std::fabs(q[3 * i + j]) > 1e-9) full = true;
+  if (!full) {
+    for (int i = 0; i < 3; i++)
+      if (!(q[4 * i] > 0.0)) return PGO_E_BAD_COV;
+    om6[0] = 1.0 / q[0]; om6[1] = 0; om6[2] = 0;
+    om6[3] = 1.0 / q[4]; om6[4] = 0;
+    om6[5] = 1.0 / q[8];
+    return PGO_OK;
+  }
+  const double a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5], g = q[6], h = q[7], k = q[8];
+  const double A = e * k - f * h, B = -(d * k - f * g), C = d * h - e * g;
+  const double det = a * A + b * B + c * C;
+  if (!(std::fabs(det) > 0.0) || !std::isfinite(det)) return PGO_E_BAD_COV;
+  // lower triangle of the inverse: (1,0)=B/det, (2,0)=C/det, (2,1)=-(a h - b g)/det
+  const double l00 = A / det, l10 = B / det, l20 = C / det;
+  const double l11 = (a * k - c * g) / det, l21 = -(a * h - b * g) / det, l22 = (a * e - b * d) / det;
+  // LLT must succeed
+  if (!(l00 > 0)) return PGO_E_BAD_COV;
+  const double r00 = std::sqrt(l00), r10 = l10 / r00, r20 = l20 / r00;
+  const double s11 = l11 - r10 * r10;
+  if (!(s11 > 0)) return PGO_E_BAD_COV;
+  const double r11 = std::sqrt(s11), r21 = (l21 - r20 * r10) / r11;
+  if (!(l22 - r20 * r20 - r21 * r21 > 0)) return PGO_E_BAD_COV;
+  om6[0] = l00; om6[1] = l10; om6[2] = l20; om6[3] = l11; om6[4] = l21; om6[5] = l22;
+  return PGO_OK;
+}
+
+void free_device(pgo_graph* g) {
+  DevGraph& d = g->d;
+  void* ptrs[] = {d.eij, d.ez, d.eom, d.prior_ptr, d.prior_vtx, d.pz, d.pom, d.row_ptr, d.slot_edge, d.slot_col, d.V,
+                  d.D, d.g, d.pose, d.pose_cand, d.pose_saved, d.x, d.r, d.z, d.p, d.q, d.Minv, d.part, d.scal, d.ctrl};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  hipStream_t s = d.stream;
+  d = DevGraph();
+  d.stream = s;
+  g->dev_structure = false;
+  g->dev_values = false;
+}
+
+int ensure_hip(pgo_graph* g) {
+  if (g->hip_ready) return PGO_OK;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+    return fail(g, PGO_E_NO_DEVICE, "no HIP device available");
+  if (g->device < 0 || g->device >= count) return fail(g, PGO_E_NO_DEVICE, "device ordinal out of range");
+  HIP_TRY(g, hipSetDevice(g->device));
+  HIP_TRY(g, hipStreamCreateWithFlags(&g->d.stream, hipStreamNonBlocking));
+  HIP_TRY(g, hipHostMalloc((void**)&g->h_scal, 16 * sizeof(double), hipHostMallocDefault));
+  HIP_TRY(g, hipHostMalloc((void**)&g->h_ctrl, 4 * sizeof(int), hipHostMallocDefault));
+  for (auto& e : g->ev) HIP_TRY(g, hipEventCreate(&e));
+  for (auto& e : g->pev) HIP_TRY(g, hipEventCreate(&e));
+  g->hip_ready = true;
+  return PGO_OK;
+}
+
+template <class T>
+int dev_alloc(pgo_graph* g, T** p, size_t count) {
+  HIP_TRY(g, hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T)));
+  return PGO_OK;
+}
+
+template <class T>
+int h2d(pgo_graph* g, T* dst, const T* src, size_t count) {
+  if (count == 0) return PGO_OK;
+  HIP_TRY(g, hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, g->d.stream));
+  return PGO_OK;
+}
+
+#define RC_TRY(expr)          \
+  do {                        \
+    int rc_ = (expr);         \
+    if (rc_ != PGO_OK) return rc_; \
+  } while (0)
+
+// Host values -> device pose (Pose2(x, y, theta): Rot2::fromAngle)
+int upload_values(pgo_graph* g) {
+  const size_t n = g->keys.size();
+  std::vector<double4> h(n);
+  for (size_t i = 0; i < n; i++) {
+    const double th = g->xyt[3 * i + 2];
+    h[i] = make_double4(g->xyt[3 * i], g->xyt[3 * i + 1], std::cos(th), std::sin(th));
+  }
+  RC_TRY(h2d(g, g->d.pose, h.data(), n));
+  HIP_TRY(g, hipStreamSynchronize(g->d.stream));
+  g->dev_values = true;
+  return PGO_OK;
+}
+
+// Device pose -> host values (Values::at<Pose2>(k).x()/y()/theta(), graph.cpp:123-125)
+int download_values(pgo_graph* g) {
+  if (g->host_values) return PGO_OK;
+  const size_t n = g->keys.size();
+  std::vector<double4> h(n);
+  if (n) {
+    HIP_TRY(g, hipMemcpyAsync(h.data(), g->d.pose, n * sizeof(double4), hipMemcpyDeviceToHost, g->d.stream));
+    HIP_TRY(g, hipStreamSynchronize(g->d.stream));
+  }
+  for (size_t i = 0; i < n; i++) {
+    g->xyt[3 * i] = h[i].x;
+    g->xyt[3 * i + 1] = h[i].y;
+    g->xyt[3 * i + 2] = std::atan2(h[i].w, h[i].z);
+  }
+  g->host_values = true;
+  return PGO_OK;
+}
+
+// Build the device graph: resolve keys (GTSAM raises ValuesKeyDoesNotExist at
+// optimize time for a factor on an unknown key), block-CSR slots, priors.
+int upload_structure(pgo_graph* g) {
+  RC_TRY(ensure_hip(g));
+  RC_TRY(download_values(g));
+  const int n = (int)g->keys.size();
+  const int ne = (int)g->ek1.size();
+  const int np = (int)g->pk.size();
+  std::vector<int2> eij(ne);
+  for (int e = 0; e < ne; e++) {
+    auto a = g->index.find(g->ek1[e]), b = g->index.find(g->ek2[e]);
+    if (a == g->index.end() || b == g->index.end()) {
+      const uint64_t k = a == g->index.end() ? g->ek1[e] : g->ek2[e];
+      return fail(g, PGO_E_NO_KEY, "between factor " + std::to_string(e) + " references key " +
+                                       std::to_string(k) + " with no inserted value");
+    }
+    eij[e] = make_int2(a->second, b->second);
+  }
+  std::vector<int> pv(np);
+  for (int q = 0; q < np; q++) {
+    auto a = g->index.find(g->pk[q]);
+    if (a == g->index.end())
+      return fail(g, PGO_E_NO_KEY, "prior factor on key " + std::to_string(g->pk[q]) + " with no inserted value");
+    pv[q] = a->second;
+  }
+  // block-CSR rows: every factor owns a slot in row ei (side 0) and row ej (side 1)
+  const int ns = 2 * ne;
+  std::vector<int> row_ptr(n + 1, 0);
+  for (int e = 0; e < ne; e++) {
+    row_ptr[eij[e].x + 1]++;
+    row_ptr[eij[e].y + 1]++;
+  }
+  for (int i = 0; i < n; i++) row_ptr[i + 1] += row_ptr[i];
+  std::vector<int> fillp(row_ptr.begin(), row_ptr.end() - 1);
+  std::vector<int> slot_edge(ns), slot_col(ns);
+  for (int e = 0; e < ne; e++) {
+    int s0 = fillp[eij[e].x]++;
+    slot_edge[s0] = e << 1;
+    slot_col[s0] = eij[e].y;
+    int s1 = fillp[eij[e].y]++;
+    slot_edge[s1] = (e << 1) | 1;
+    slot_col[s1] = eij[e].x;
+  }
+  // order each row by column (locality of the x gathers)
+  std::vector<std::pair<int, int>> tmp;
+  for (int i = 0; i < n; i++) {
+    const int b = row_ptr[i], en = row_ptr[i + 1];
+    if (en - b < 2) continue;
+    tmp.clear();
+    for (int k = b; k < en; k++) tmp.emplace_back(slot_col[k], slot_edge[k]);
+    std::sort(tmp.begin(), tmp.end());
+    for (int k = b; k < en; k++) {
+      slot_col[k] = tmp[k - b].first;
+      slot_edge[k] = tmp[k - b].second;
+    }
+  }
+  g->edge_slot0.assign(ne, -1);
+  for (int k = 0; k < ns; k++)
+    if ((slot_edge[k] & 1) == 0) g->edge_slot0[slot_edge[k] >> 1] = k;
+  // priors CSR by vertex
+  std::vector<int> prior_ptr(n + 1, 0);
+  for (int q = 0; q < np; q++) prior_ptr[pv[q] + 1]++;
+  for (int i = 0; i < n; i++) prior_ptr[i + 1] += prior_ptr[i];
+  std::vector<int> porder(np);
+  {
+    std::vector<int> f(prior_ptr.begin(), prior_ptr.end() - 1);
+    for (int q = 0; q < np; q++) porder[f[pv[q]]++] = q;
+  }
+  std::vector<double4> hz(ne), hpz(np);
+  std::vector<double2> hom(3 * (size_t)ne), hpom(3 * (size_t)np);
+  for (int e = 0; e < ne; e++) {
+    const double th = g->ez[3 * e + 2];
+    hz[e] = make_double4(g->ez[3 * e], g->ez[3 * e + 1], std::cos(th), std::sin(th));
+    const double* o = &g->eom[6 * (size_t)e];
+    hom[3 * e] = make_double2(o[0], o[1]);
+    hom[3 * e + 1] = make_double2(o[2], o[3]);
+    hom[3 * e + 2] = make_double2(o[4], o[5]);
+  }
+  for (int t = 0; t < np; t++) {
+    const int q = porder[t];
+    const double th = g->pz[3 * q + 2];
+    hpz[t] = make_double4(g->pz[3 * q], g->pz[3 * q + 1], std::cos(th), std::sin(th));
+    const double* o = &g->pom[6 * (size_t)q];
+    hpom[3 * t] = make_double2(o[0], o[1]);
+    hpom[3 * t + 1] = make_double2(o[2], o[3]);
+    hpom[3 * t + 2] = make_double2(o[4], o[5]);
+  }
+  free_device(g);
+  DevGraph& d = g->d;
+  d.n = n;
+  d.ne = ne;
+  d.np = np;
+  d.nslots = ns;
+  // lanes per row: smallest power of two >= mean degree, in [4, 32]
+  const double mean_deg = n ? (double)ns / n : 0.0;
+  d.G = 4;
+  while (d.G < 32 && d.G < mean_deg) d.G *= 2;
+  RC_TRY(dev_alloc(g, &d.eij, ne));
+  RC_TRY(dev_alloc(g, &d.ez, ne));
+  RC_TRY(dev_alloc(g, &d.eom, 3 * (size_t)ne));
+  RC_TRY(dev_alloc(g, &d.prior_ptr, n + 1));
+  RC_TRY(dev_alloc(g, &d.prior_vtx, np));
+  RC_TRY(dev_alloc(g, &d.pz, np));
+  RC_TRY(dev_alloc(g, &d.pom, 3 * (size_t)np));
+  RC_TRY(dev_alloc(g, &d.row_ptr, n + 1));
+  RC_TRY(dev_alloc(g, &d.slot_edge, ns));
+  RC_TRY(dev_alloc(g, &d.slot_col, ns));
+  RC_TRY(dev_alloc(g, &d.V, 9 * (size_t)ns));
+  RC_TRY(dev_alloc(g, &d.D, 6 * (size_t)n));
+  RC_TRY(dev_alloc(g, &d.g, 3 * (size_t)n));
+  RC_TRY(dev_alloc(g, &d.pose, n));
+  RC_TRY(dev_alloc(g, &d.pose_cand, n));
+  RC_TRY(dev_alloc(g, &d.x, 3 * (size_t)n));
+  RC_TRY(dev_alloc(g, &d.r, 3 * (size_t)n));
+  RC_TRY(dev_alloc(g, &d.z, 3 * (size_t)n));
+  RC_TRY(dev_alloc(g, &d.p, 3 * (size_t)n));
+  RC_TRY(dev_alloc(g, &d.q, 3 * (size_t)n));
+  RC_TRY(dev_alloc(g, &d.Minv, 6 * (size_t)n));
+  RC_TRY(dev_alloc(g, &d.part, (size_t)pgo::kMaxBlocks * pgo::kPartSlices));
+  RC_TRY(dev_alloc(g, &d.scal, 16));
+  RC_TRY(dev_alloc(g, &d.ctrl, 4));
+  std::vector<int> pvs(np);
+  for (int t = 0; t < np; t++) pvs[t] = pv[porder[t]];
+  RC_TRY(h2d(g, d.eij, eij.data(), ne));
+  RC_TRY(h2d(g, d.ez, hz.data(), ne));
+  RC_TRY(h2d(g, d.eom, hom.data(), 3 * (size_t)ne));
+  RC_TRY(h2d(g, d.prior_ptr, prior_ptr.data(), n + 1));
+  RC_TRY(h2d(g, d.prior_vtx, pvs.data(), np));
+  RC_TRY(h2d(g, d.pz, hpz.data(), np));
+  RC_TRY(h2d(g, d.pom, hpom.data(), 3 * (size_t)np));
+  RC_TRY(h2d(g, d.row_ptr, row_ptr.data(), n + 1));
+  RC_TRY(h2d(g, d.slot_edge, slot_edge.data(), ns));
+  RC_TRY(h2d(g, d.slot_col, slot_col.data(), ns));
+  HIP_TRY(g, hipMemsetAsync(d.part, 0, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices, d.stream));
+  HIP_TRY(g, hipStreamSynchronize(d.stream));
+  g->dev_structure = true;
+  return upload_values(g);
+}
+
+int ensure_device(pgo_graph* g) {
+  if (!g->dev_structure) RC_TRY(upload_structure(g));
+  else if (!g->dev_values) RC_TRY(upload_values(g));
+  return PGO_OK;
+}
+
+int sync_scalars(pgo_graph* g, int count) {
+  HIP_TRY(g, hipMemcpyAsync(g->h_scal, g->d.scal, count * sizeof(double), hipMemcpyDeviceToHost, g->d.stream));
+  HIP_TRY(g, hipStreamSynchronize(g->d.stream));
+  return PGO_OK;
+}
+
+int device_error(pgo_graph* g, const double4* pose, double* err) {
+  HIP_TRY(g, pgo::launch_error(g->d, pose, g->d.scal));
+  RC_TRY(sync_scalars(g, 1));
+  *err = g->h_scal[0];
+  return PGO_OK;
+}
+
+struct PcgResult {
+  int flag = pgo::kRunning;
+  int iterations = 0;
+};
+
+double ms_between(hipEvent_t a, hipEvent_t b);
+
+// PCG solve of (H + lambda I) x = -g at the current linearisation.  With
+// profile_every = k > 0, every k-th SpMV launch is bracketed by HIP events on
+// the handle's stream; launches that ran after convergence (early-exit no-ops)
+// are not counted.
+int pcg_solve(pgo_graph* g, const pgo_params& p, double lam, PcgResult* out, pgo_stats* st) {
+  const DevGraph& d = g->d;
+  HIP_TRY(g, pgo::launch_pcg_init(d, lam));
+  const double tol2 = p.pcg_relative_tol * p.pcg_relative_tol;
+  const int chk = std::max(1, p.pcg_check_interval);
+  const int prof = st ? p.profile_every : 0;
+  int k = 0;
+  out->flag = pgo::kRunning;
+  while (k < p.pcg_max_iterations) {
+    const int stop = std::min(p.pcg_max_iterations, k + chk);
+    int npairs = 0;
+    for (; k < stop; k++) {
+      const bool timed = prof > 0 && (k % prof) == 0 && npairs < pgo_graph::kProfPairs;
+      if (timed) HIP_TRY(g, hipEventRecord(g->pev[2 * npairs], d.stream));
+      HIP_TRY(g, pgo::launch_pcg_spmv(d, lam));
+      if (timed) {
+        HIP_TRY(g, hipEventRecord(g->pev[2 * npairs + 1], d.stream));
+        g->pk_iter[npairs++] = k;
+      }
+      HIP_TRY(g, pgo::launch_pcg_vec(d, k, tol2));
+    }
+    HIP_TRY(g, hipMemcpyAsync(g->h_ctrl, d.ctrl, 2 * sizeof(int), hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(g, hipStreamSynchronize(d.stream));
+    for (int t = 0; t < npairs; t++)
+      if (g->pk_iter[t] < g->h_ctrl[1] || (g->h_ctrl[0] == pgo::kRunning)) {
+        st->kernel_spmv_ms += ms_between(g->pev[2 * t], g->pev[2 * t + 1]);
+        st->kernel_spmv_count++;
+      }
+    if (g->h_ctrl[0] != pgo::kRunning) break;
+  }
+  out->flag = g->h_ctrl[0];
+  out->iterations = g->h_ctrl[1];
+  return PGO_OK;
+}
+
+double ms_between(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
+  return ms;
+}
+
+bool check_convergence(const pgo_params& p, double cur, double nw) {  // NonlinearOptimizer.cpp
+  if (nw <= p.error_tol) return true;
+  const double absd = cur - nw;
+  const double reld = absd / cur;
+  return (p.relative_error_tol != 0.0 && reld <= p.relative_error_tol) || absd <= p.absolute_error_tol;
+}
+
+}  // namespace
+
+// ============================================================== C-ABI
+extern "C" {
+
+int pgo_abi_version(void) { return PGO_ABI_VERSION; }
+
+const char* pgo_status_string(int s) {
+  switch (s) {
+    case PGO_OK: return "ok";
+    case PGO_E_ARG: return "invalid argument";
+    case PGO_E_DUP_KEY: return "ValuesKeyAlreadyExists: key already inserted";
+    case PGO_E_NO_KEY: return "ValuesKeyDoesNotExist: key has no value";
+    case PGO_E_BAD_COV: return "covariance is not symmetric positive definite";
+    case PGO_E_INDETERMINANT: return "IndeterminantLinearSystemException: linear system is singular";
+    case PGO_E_NONFINITE: return "non-finite value";
+    case PGO_E_HIP: return "HIP runtime error";
+    case PGO_E_NO_DEVICE: return "no HIP device";
+    case PGO_E_NOMEM: return "out of memory";
+    case PGO_E_BAD_EDGE: return "between factor connects a key to itself";
+    case PGO_W_MAXITER: return "stopped at max_iterations";
+    default: return "unknown status";
+  }
+}
+
+void pgo_default_params(pgo_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->max_iterations = 100;
+  p->relative_error_tol = 1e-5;
+  p->absolute_error_tol = 1e-5;
+  p->error_tol = 0.0;
+  p->lambda_initial = 1e-5;
+  p->lambda_factor = 10.0;
+  p->lambda_upper_bound = 1e5;
+  p->lambda_lower_bound = 0.0;
+  p->min_model_fidelity = 1e-3;
+  p->use_fixed_lambda_factor = 1;
+  p->algorithm = PGO_ALG_LM;
+  p->linear_solver = PGO_SOLVER_PCG;
+  p->pcg_relative_tol = 1e-10;
+  p->pcg_max_iterations = 20000;
+  p->pcg_check_interval = 32;
+  p->max_outer = 0;
+  p->profile_every = 0;
+}
+
+pgo_graph* pgo_create(const pgo_opts* opts) {
+  pgo_graph* g = new (std::nothrow) pgo_graph();
+  if (!g) return nullptr;
+  if (opts) g->device = opts->device;
+  return g;
+}
+
+void pgo_destroy(pgo_graph* g) {
+  if (!g) return;
+  if (g->hip_ready) {
+    (void)hipSetDevice(g->device);
+    (void)hipStreamSynchronize(g->d.stream);
+    free_device(g);
+    for (auto& e : g->ev)
+      if (e) (void)hipEventDestroy(e);
+    if (g->h_scal) (void)hipHostFree(g->h_scal);
+    if (g->h_ctrl) (void)hipHostFree(g->h_ctrl);
+    for (auto& e : g->pev)
+      if (e) (void)hipEventDestroy(e);
+    if (g->d.stream) (void)hipStreamDestroy(g->d.stream);
+  }
+  delete g;
+}
+
+const char* pgo_last_error(const pgo_graph* g) { return g ? g->last_error.c_str() : "null handle"; }
+
+int pgo_add_vertex(pgo_graph* g, uint64_t key, double x, double y, double theta) {
+  if (!g) return PGO_E_ARG;
+  if (!std::isfinite(x) || !std::isfinite(y) || !std::isfinite(theta))
+    return fail(g, PGO_E_NONFINITE, "non-finite initial value for key " + std::to_string(key));
+  if (g->index.count(key)) return fail(g, PGO_E_DUP_KEY, "key " + std::to_string(key) + " already inserted");
+  RC_TRY(download_values(g));
+  g->index.emplace(key, (int32_t)g->keys.size());
+  g->keys.push_back(key);
+  g->xyt.insert(g->xyt.end(), {x, y, theta});
+  g->dev_structure = false;
+  return PGO_OK;
+}
+
+int pgo_add_vertices(pgo_graph* g, size_t n, const uint64_t* keys, const double* xyt) {
+  if (!g || (n && (!keys || !xyt))) return PGO_E_ARG;
+  for (size_t i = 0; i < n; i++) RC_TRY(pgo_add_vertex(g, keys[i], xyt[3 * i], xyt[3 * i + 1], xyt[3 * i + 2]));
+  return PGO_OK;
+}
+
+int pgo_add_prior(pgo_graph* g, uint64_t key, const double pose[3], const double cov[9]) {
+  if (!g || !pose || !cov) return PGO_E_ARG;
+  for (int a = 0; a < 3; a++)
+    if (!std::isfinite(pose[a])) return fail(g, PGO_E_NONFINITE, "non-finite prior pose");
+  double om[6];
+  if (information(cov, om) != PGO_OK) return fail(g, PGO_E_BAD_COV, "prior covariance not positive definite");
+  g->pk.push_back(key);
+  g->pz.insert(g->pz.end(), pose, pose + 3);
+  g->pom.insert(g->pom.end(), om, om + 6);
+  g->dev_structure = false;
+  return PGO_OK;
+}
+
+int pgo_add_edge(pgo_graph* g, uint64_t k1, uint64_t k2, const double z[3], const double cov[9]) {
+  if (!g || !z || !cov) return PGO_E_ARG;
+  if (k1 == k2) return fail(g, PGO_E_BAD_EDGE, "between factor on key " + std::to_string(k1) + " and itself");
+  for (int a = 0; a < 3; a++)
+    if (!std::isfinite(z[a])) return fail(g, PGO_E_NONFINITE, "non-finite measurement");
+  double om[6];
+  if (information(cov, om) != PGO_OK)
+    return fail(g, PGO_E_BAD_COV, "between factor covariance not positive definite");
+  if (g->ek1.size() >= (size_t)(1 << 30)) return fail(g, PGO_E_NOMEM, "too many factors");
+  g->ek1.push_back(k1);
+  g->ek2.push_back(k2);
+  g->ez.insert(g->ez.end(), z, z + 3);
+  g->eom.insert(g->eom.end(), om, om + 6);
+  g->dev_structure = false;
+  return PGO_OK;
+}
+
+int pgo_add_edges(pgo_graph* g, size_t n, const uint64_t* k1, const uint64_t* k2, const double* z,
+                  const double* cov, int cov_stride) {
+  if (!g || (n && (!k1 || !k2 || !z || !cov)) || (cov_stride != 0 && cov_stride != 9)) return PGO_E_ARG;
+  g->ek1.reserve(g->ek1.size() + n);
+  g->ek2.reserve(g->ek2.size() + n);
+  g->ez.reserve(g->ez.size() + 3 * n);
+  g->eom.reserve(g->eom.size() + 6 * n);
+  for (size_t i = 0; i < n; i++) RC_TRY(pgo_add_edge(g, k1[i], k2[i], z + 3 * i, cov + (size_t)cov_stride * i));
+  return PGO_OK;
+}
+
+size_t pgo_num_factors(const pgo_graph* g) { return g ? g->ek1.size() + g->pk.size() : 0; }
+size_t pgo_num_vertices(const pgo_graph* g) { return g ? g->keys.size() : 0; }
+
+int pgo_get_pose(pgo_graph* g, uint64_t key, double out[3]) {
+  if (!g || !out) return PGO_E_ARG;
+  auto it = g->index.find(key);
+  if (it == g->index.end()) return fail(g, PGO_E_NO_KEY, "key " + std::to_string(key) + " has no value");
+  RC_TRY(download_values(g));
+  std::memcpy(out, &g->xyt[3 * (size_t)it->second], 3 * sizeof(double));
+  return PGO_OK;
+}
+
+int pgo_get_poses(pgo_graph* g, size_t n, const uint64_t* keys, double* out) {
+  if (!g || (n && !out)) return PGO_E_ARG;
+  RC_TRY(download_values(g));
+  if (!keys) {
+    if (n != g->keys.size()) return fail(g, PGO_E_ARG, "n must equal the number of vertices when keys is NULL");
+    std::memcpy(out, g->xyt.data(), 3 * n * sizeof(double));
+    return PGO_OK;
+  }
+  for (size_t i = 0; i < n; i++) {
+    auto it = g->index.find(keys[i]);
+    if (it == g->index.end()) return fail(g, PGO_E_NO_KEY, "key " + std::to_string(keys[i]) + " has no value");
+    std::memcpy(out + 3 * i, &g->xyt[3 * (size_t)it->second], 3 * sizeof(double));
+  }
+  return PGO_OK;
+}
+
+int pgo_set_poses(pgo_graph* g, size_t n, const uint64_t* keys, const double* xyt) {
+  if (!g || (n && !xyt)) return PGO_E_ARG;
+  RC_TRY(download_values(g));
+  for (size_t i = 0; i < 3 * n; i++)
+    if (!std::isfinite(xyt[i])) return fail(g, PGO_E_NONFINITE, "non-finite value");
+  if (!keys) {
+    if (n != g->keys.size()) return fail(g, PGO_E_ARG, "n must equal the number of vertices when keys is NULL");
+    std::memcpy(g->xyt.data(), xyt, 3 * n * sizeof(double));
+  } else {
+    for (size_t i = 0; i < n; i++) {
+      auto it = g->index.find(keys[i]);
+      if (it == g->index.end()) return fail(g, PGO_E_NO_KEY, "key " + std::to_string(keys[i]) + " has no value");
+      std::memcpy(&g->xyt[3 * (size_t)it->second], xyt + 3 * i, 3 * sizeof(double));
+    }
+  }
+  g->dev_values = false;
+  return PGO_OK;
+}
+
+int pgo_save_values(pgo_graph* g) {
+  if (!g) return PGO_E_ARG;
+  RC_TRY(ensure_device(g));
+  DevGraph& d = g->d;
+  if (!d.pose_saved) RC_TRY(dev_alloc(g, &d.pose_saved, d.n));
+  if (d.n)
+    HIP_TRY(g, hipMemcpyAsync(d.pose_saved, d.pose, d.n * sizeof(double4), hipMemcpyDeviceToDevice, d.stream));
+  HIP_TRY(g, hipStreamSynchronize(d.stream));
+  return PGO_OK;
+}
+
+int pgo_restore_values(pgo_graph* g) {
+  if (!g) return PGO_E_ARG;
+  DevGraph& d = g->d;
+  if (!g->dev_structure || !d.pose_saved) return fail(g, PGO_E_ARG, "no saved values (graph changed or never saved)");
+  if (d.n)
+    HIP_TRY(g, hipMemcpyAsync(d.pose, d.pose_saved, d.n * sizeof(double4), hipMemcpyDeviceToDevice, d.stream));
+  g->dev_values = true;
+  g->host_values = false;
+  return PGO_OK;
+}
+
+int pgo_error(pgo_graph* g, double* err) {
+  if (!g || !err) return PGO_E_ARG;
+  RC_TRY(ensure_device(g));
+  return device_error(g, g->d.pose, err);
+}
+
+int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
+  if (!g) return PGO_E_ARG;
+  pgo_params p;
+  if (params) p = *params;
+  else pgo_default_params(&p);
+  pgo_stats st;
+  std::memset(&st, 0, sizeof(st));
+  const auto T0 = std::chrono::steady_clock::now();
+  auto upload0 = std::chrono::steady_clock::now();
+  int rc = ensure_device(g);
+  if (rc != PGO_OK) return rc;
+  st.ms_upload = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - upload0).count();
+  DevGraph& d = g->d;
+  HIP_TRY(g, hipSetDevice(g->device));
+  double err = 0.0;
+  RC_TRY(device_error(g, d.pose, &err));
+  st.initial_error = err;
+  if (!std::isfinite(err)) {
+    st.status = PGO_E_NONFINITE;
+    if (stats) *stats = st;
+    return fail(g, PGO_E_NONFINITE, "initial error is not finite");
+  }
+  double lam = p.lambda_initial, factor = p.lambda_factor;
+  int iters = 0, inner = 0;
+  int status = PGO_OK;
+  hipEvent_t* ev = g->ev;
+  if (!(err <= p.error_tol) && iters < p.max_iterations && d.n > 0) {
+    double new_err = err;
+    for (;;) {
+      const double cur_err = new_err;
+      HIP_TRY(g, hipEventRecord(ev[0], d.stream));
+      HIP_TRY(g, pgo::launch_linearize(d));
+      HIP_TRY(g, hipEventRecord(ev[1], d.stream));
+      st.linearizations++;
+      bool first_try = true;
+      for (;;) {  // tryLambda (GN: one plain step)
+        const double lam_try = p.algorithm == PGO_ALG_GN ? 0.0 : lam;
+        PcgResult pr;
+        RC_TRY(pcg_solve(g, p, lam_try, &pr, &st));
+        HIP_TRY(g, hipEventRecord(ev[2], d.stream));
+        if (first_try) {
+          const double lin_ms = ms_between(ev[0], ev[1]);
+          st.ms_linearize += lin_ms;
+          if (p.profile_every > 0) {
+            st.kernel_linearize_ms += lin_ms;
+            st.kernel_linearize_count++;
+          }
+          st.ms_solve += ms_between(ev[1], ev[2]);
+          first_try = false;
+        } else {
+          st.ms_solve += ms_between(ev[3], ev[2]);
+        }
+        st.pcg_iterations += pr.iterations;
+        const bool solved = pr.flag != pgo::kBreakdown;
+        if (p.algorithm == PGO_ALG_GN) {
+          if (!solved) {
+            status = PGO_E_INDETERMINANT;
+            break;
+          }
+          HIP_TRY(g, pgo::launch_retract(d, d.x));
+          HIP_TRY(g, pgo::launch_error(d, d.pose_cand, d.scal));
+          HIP_TRY(g, hipEventRecord(ev[3], d.stream));
+          RC_TRY(sync_scalars(g, 1));
+          st.ms_update += ms_between(ev[2], ev[3]);
+          std::swap(d.pose, d.pose_cand);
+          err = g->h_scal[0];
+          iters++;
+          inner++;
+          break;
+        }
+        double fidelity = 0.0, new_e = INFINITY;
+        bool success = false, stop = false;
+        if (solved) {
+          // linear model decrease = -(g'delta + 0.5 delta'H delta), retract, new error:
+          // one read-back for all three scalars
+          HIP_TRY(g, pgo::launch_model_decrease(d, d.x, d.scal + 1));
+          HIP_TRY(g, pgo::launch_retract(d, d.x));
+          HIP_TRY(g, pgo::launch_error(d, d.pose_cand, d.scal));
+          HIP_TRY(g, hipEventRecord(ev[3], d.stream));
+          RC_TRY(sync_scalars(g, 3));
+          st.ms_update += ms_between(ev[2], ev[3]);
+          const double xhx = g->h_scal[1], gx = g->h_scal[2];
+          const double lin_change = -(gx + 0.5 * xhx);
+          if (lin_change >= 0) {
+            new_e = g->h_scal[0];
+            const double cost_change = err - new_e;
+            if (lin_change > 2.220446049250313e-16 * err) {
+              fidelity = cost_change / lin_change;
+              success = fidelity > p.min_model_fidelity;
+            }
+            if (std::fabs(cost_change) < p.relative_error_tol * err) stop = true;
+          }
+        } else {
+          HIP_TRY(g, hipEventRecord(ev[3], d.stream));
+        }
+        if (success) {  // decreaseLambda
+          if (p.use_fixed_lambda_factor) {
+            lam /= p.lambda_factor;
+          } else {
+            const double q = 2.0 * fidelity - 1.0;
+            lam *= std::max(1.0 / 3.0, 1.0 - q * q * q);
+            factor *= 2.0;
+          }
+          lam = std::max(p.lambda_lower_bound, lam);
+          std::swap(d.pose, d.pose_cand);
+          err = new_e;
+          iters++;
+          inner++;
+          break;
+        }
+        if (!stop) {  // increaseLambda
+          lam *= factor;
+          inner++;
+          if (!p.use_fixed_lambda_factor) factor *= 2.0;
+          if (lam >= p.lambda_upper_bound) break;
+          continue;
+        }
+        break;
+      }
+      if (status != PGO_OK) break;
+      new_err = err;
+      if (p.max_outer > 0 && st.linearizations >= p.max_outer) break;
+      if (!(iters < p.max_iterations && !check_convergence(p, cur_err, new_err) && std::isfinite(cur_err))) break;
+    }
+  }
+  if (status == PGO_OK && iters >= p.max_iterations && p.max_iterations > 0) status = PGO_W_MAXITER;
+  g->host_values = false;
+  st.status = status;
+  st.iterations = iters;
+  st.inner_iterations = inner;
+  st.final_error = err;
+  st.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count();
+  if (stats) *stats = st;
+  if (status < 0) return fail(g, status, pgo_status_string(status));
+  return status;
+}
+
+int pgo_debug_linearize(pgo_graph* g, double* hdiag, double* hoff, double* grad, double* err) {
+  if (!g) return PGO_E_ARG;
+  RC_TRY(ensure_device(g));
+  DevGraph& d = g->d;
+  HIP_TRY(g, pgo::launch_linearize(d));
+  HIP_TRY(g, pgo::launch_error(d, d.pose, d.scal));  // overwrites partial slice A
+  std::vector<double> V(9 * (size_t)d.nslots), D(6 * (size_t)d.n), G(3 * (size_t)d.n);
+  if (d.nslots) HIP_TRY(g, hipMemcpyAsync(V.data(), d.V, V.size() * 8, hipMemcpyDeviceToHost, d.stream));
+  if (d.n) {
+    HIP_TRY(g, hipMemcpyAsync(D.data(), d.D, D.size() * 8, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(g, hipMemcpyAsync(G.data(), d.g, G.size() * 8, hipMemcpyDeviceToHost, d.stream));
+  }
+  RC_TRY(sync_scalars(g, 1));
+  if (err) *err = g->h_scal[0];
+  if (hdiag)
+    for (int i = 0; i < d.n; i++) {
+      const double* s = &D[6 * (size_t)i];
+      double* o = hdiag + 9 * (size_t)i;
+      o[0] = s[0]; o[1] = s[1]; o[2] = s[2];
+      o[3] = s[1]; o[4] = s[3]; o[5] = s[4];
+      o[6] = s[2]; o[7] = s[4]; o[8] = s[5];
+    }
+  if (hoff)
+    for (int e = 0; e < d.ne; e++) std::memcpy(hoff + 9 * (size_t)e, &V[9 * (size_t)g->edge_slot0[e]], 72);
+  if (grad) std::memcpy(grad, G.data(), G.size() * 8);
+  return PGO_OK;
+}
+
+int pgo_debug_spmv(pgo_graph* g, double lambda, const double* x, double* y) {
+  if (!g || !x || !y) return PGO_E_ARG;
+  RC_TRY(ensure_device(g));
+  DevGraph& d = g->d;
+  HIP_TRY(g, pgo::launch_linearize(d));
+  RC_TRY(h2d(g, d.p, x, 3 * (size_t)d.n));
+  HIP_TRY(g, pgo::launch_spmv(d, lambda, d.p, d.q));
+  if (d.n) HIP_TRY(g, hipMemcpyAsync(y, d.q, 3 * (size_t)d.n * 8, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(g, hipStreamSynchronize(d.stream));
+  return PGO_OK;
+}
+
+int pgo_debug_solve(pgo_graph* g, double lambda, const pgo_params* params, double* delta, int* pcg_iterations) {
+  if (!g || !delta) return PGO_E_ARG;
+  pgo_params p;
+  if (params) p = *params;
+  else pgo_default_params(&p);
+  RC_TRY(ensure_device(g));
+  DevGraph& d = g->d;
+  HIP_TRY(g, pgo::launch_linearize(d));
+  PcgResult pr;
+  RC_TRY(pcg_solve(g, p, lambda, &pr, nullptr));
+  if (d.n) HIP_TRY(g, hipMemcpyAsync(delta, d.x, 3 * (size_t)d.n * 8, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(g, hipStreamSynchronize(d.stream));
+  if (pcg_iterations) *pcg_iterations = pr.iterations;
+  if (pr.flag == pgo::kBreakdown) return fail(g, PGO_E_INDETERMINANT, "PCG breakdown");
+  return PGO_OK;
+}
+
+}  // extern "C"

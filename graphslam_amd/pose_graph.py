@@ -1,0 +1,206 @@
+"""Native handle over libpgo.so: a device-resident pose graph.
+
+``PoseGraph`` is the bulk, zero-copy-ish entry point (numpy arrays in, numpy
+arrays out) used by the GTSAM-named mirror in ``graphslam_amd.gtsam`` and by
+bench.py.  Every call goes through the C-ABI of include/pgo.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+class PgoError(RuntimeError):
+    def __init__(self, status, message):
+        super().__init__(f"[{status}] {message}")
+        self.status = status
+
+
+class ValuesKeyAlreadyExists(PgoError, KeyError):
+    """gtsam::ValuesKeyAlreadyExists (Values::insert on an existing key)."""
+
+
+class ValuesKeyDoesNotExist(PgoError, KeyError):
+    """gtsam::ValuesKeyDoesNotExist (Values::at / a factor on a missing key)."""
+
+
+class IndeterminantLinearSystemException(PgoError):
+    """gtsam::IndeterminantLinearSystemException (singular Gauss-Newton system)."""
+
+
+class BadCovariance(PgoError, ValueError):
+    """Covariance is not symmetric positive definite (GTSAM's LLT would fail)."""
+
+
+_EXC = {
+    L.PGO_E_DUP_KEY: ValuesKeyAlreadyExists,
+    L.PGO_E_NO_KEY: ValuesKeyDoesNotExist,
+    L.PGO_E_INDETERMINANT: IndeterminantLinearSystemException,
+    L.PGO_E_BAD_COV: BadCovariance,
+}
+
+
+def default_params(**kw) -> L.PgoParams:
+    p = L.PgoParams()
+    L.lib().pgo_default_params(C.byref(p))
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise AttributeError(f"pgo_params has no field {k!r}")
+        setattr(p, k, v)
+    return p
+
+
+class PoseGraph:
+    """One pgo_graph handle (one HIP stream, graph + values resident in HBM)."""
+
+    def __init__(self, device: int = 0):
+        self._L = L.lib()
+        opts = L.PgoOpts()
+        opts.device = device
+        self._h = self._L.pgo_create(C.byref(opts))
+        if not self._h:
+            raise MemoryError("pgo_create failed")
+        self.last_stats = None
+
+    # ------------------------------------------------------------------ utils
+    def _check(self, rc):
+        if rc < 0:
+            msg = self._L.pgo_last_error(self._h).decode()
+            raise _EXC.get(rc, PgoError)(rc, msg)
+        return rc
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.pgo_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ------------------------------------------------------------ construction
+    def add_vertex(self, key, x, y, theta):
+        self._check(self._L.pgo_add_vertex(self._h, int(key), float(x), float(y), float(theta)))
+
+    def add_vertices(self, keys, xyt):
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
+        self._check(self._L.pgo_add_vertices(self._h, len(keys), L.u64ptr(keys), L.dptr(xyt)))
+
+    def add_prior(self, key, pose, cov):
+        pose = np.ascontiguousarray(pose, dtype=np.float64).reshape(3)
+        cov = np.ascontiguousarray(cov, dtype=np.float64).reshape(9)
+        self._check(self._L.pgo_add_prior(self._h, int(key), L.dptr(pose), L.dptr(cov)))
+
+    def add_edge(self, k1, k2, z, cov):
+        z = np.ascontiguousarray(z, dtype=np.float64).reshape(3)
+        cov = np.ascontiguousarray(cov, dtype=np.float64).reshape(9)
+        self._check(self._L.pgo_add_edge(self._h, int(k1), int(k2), L.dptr(z), L.dptr(cov)))
+
+    def add_edges(self, k1, k2, z, cov):
+        k1 = np.ascontiguousarray(k1, dtype=np.uint64)
+        k2 = np.ascontiguousarray(k2, dtype=np.uint64)
+        z = np.ascontiguousarray(z, dtype=np.float64).reshape(-1, 3)
+        cov = np.ascontiguousarray(cov, dtype=np.float64)
+        stride = 0 if cov.size == 9 else 9
+        if stride and cov.reshape(-1, 9).shape[0] != len(k1):
+            raise ValueError("cov must be one [9] or [E,9]")
+        self._check(self._L.pgo_add_edges(self._h, len(k1), L.u64ptr(k1), L.u64ptr(k2), L.dptr(z),
+                                          L.dptr(cov), stride))
+
+    @classmethod
+    def from_dataset(cls, g, device=0):
+        """Load a graphslam_amd.datasets.PoseGraph (vertices, priors, edges)."""
+        pg = cls(device)
+        pg.add_vertices(g.keys, g.initial)
+        for k, p, c in zip(g.prior_keys, g.prior_pose, g.prior_cov):
+            pg.add_prior(int(k), p, c)
+        pg.add_edges(g.edge_k1, g.edge_k2, g.edge_z, g.edge_cov)
+        return pg
+
+    # -------------------------------------------------------------- optimise
+    def optimize(self, params: L.PgoParams | None = None, **kw):
+        p = params if params is not None else default_params(**kw)
+        st = L.PgoStats()
+        rc = self._L.pgo_optimize(self._h, C.byref(p), C.byref(st))
+        self.last_stats = st.as_dict()
+        self._check(rc)
+        return self.last_stats
+
+    # ---------------------------------------------------------------- values
+    @property
+    def num_vertices(self):
+        return int(self._L.pgo_num_vertices(self._h))
+
+    @property
+    def num_factors(self):
+        return int(self._L.pgo_num_factors(self._h))
+
+    def pose(self, key):
+        out = np.zeros(3)
+        self._check(self._L.pgo_get_pose(self._h, int(key), L.dptr(out)))
+        return out
+
+    def poses(self, keys=None):
+        if keys is None:
+            n = self.num_vertices
+            out = np.zeros((n, 3))
+            self._check(self._L.pgo_get_poses(self._h, n, None, L.dptr(out)))
+            return out
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        out = np.zeros((len(keys), 3))
+        self._check(self._L.pgo_get_poses(self._h, len(keys), L.u64ptr(keys), L.dptr(out)))
+        return out
+
+    def set_poses(self, xyt, keys=None):
+        xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
+        kp = None
+        if keys is not None:
+            keys = np.ascontiguousarray(keys, dtype=np.uint64)
+            kp = L.u64ptr(keys)
+        self._check(self._L.pgo_set_poses(self._h, xyt.shape[0], kp, L.dptr(xyt)))
+
+    def save_values(self):
+        self._check(self._L.pgo_save_values(self._h))
+
+    def restore_values(self):
+        self._check(self._L.pgo_restore_values(self._h))
+
+    def error(self):
+        e = C.c_double(0)
+        self._check(self._L.pgo_error(self._h, C.byref(e)))
+        return e.value
+
+    # ------------------------------------------------------------ diagnostics
+    def debug_linearize(self, num_edges):
+        n = self.num_vertices
+        hd = np.zeros((n, 3, 3))
+        ho = np.zeros((num_edges, 3, 3))
+        g = np.zeros((n, 3))
+        e = C.c_double(0)
+        self._check(self._L.pgo_debug_linearize(self._h, L.dptr(hd), L.dptr(ho), L.dptr(g), C.byref(e)))
+        return hd, ho, g, e.value
+
+    def debug_spmv(self, x, lam=0.0):
+        x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1, 3)
+        y = np.zeros_like(x)
+        self._check(self._L.pgo_debug_spmv(self._h, float(lam), L.dptr(x), L.dptr(y)))
+        return y
+
+    def debug_solve(self, lam, params=None, **kw):
+        p = params if params is not None else default_params(**kw)
+        d = np.zeros((self.num_vertices, 3))
+        it = C.c_int(0)
+        self._check(self._L.pgo_debug_solve(self._h, float(lam), C.byref(p), L.dptr(d), C.byref(it)))
+        return d, it.value

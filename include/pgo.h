@@ -1,0 +1,165 @@
+/*
+ * pgo.h -- C-ABI of the MI355X-native SE(2) pose-graph optimisation backend.
+ *
+ * Drop-in boundary for the one hot path of Sergimech/GraphSLAM: the src/graph
+ * node's Levenberg-Marquardt solve over Pose2 prior + between factors, which
+ * the reference performs in-process through GTSAM (/root/reference paths):
+ *
+ *   graph.cpp:58,86      initial.insert(Key, Pose2)             -> pgo_add_vertex
+ *   graph.cpp:57         graph.add(PriorFactor<Pose2>(...))      -> pgo_add_prior
+ *   graph.cpp:87-92,     graph.add(BetweenFactor<Pose2>(...))    -> pgo_add_edge
+ *            106-111
+ *   graph.cpp:45,83,103  noiseModel::Gaussian::Covariance(Q)     -> the cov[9] argument
+ *   graph.hpp:45-58      covariance_to_eigen: row-major float64[9] -> same layout
+ *   graph.cpp:119        LevenbergMarquardtOptimizer(graph, initial).optimize()
+ *                                                                -> pgo_optimize
+ *   graph.cpp:123-125    poses_opti.at<Pose2>(id).x()/y()/theta() -> pgo_get_pose(s)
+ *   graph.cpp:130        initial = poses_opti (warm start)       -> in-place update
+ *   graph.cpp:60,94,112  graph.nrFactors()                       -> pgo_num_factors
+ *
+ * Plain C types only: no exceptions, no torch types, caller buffers are
+ * borrowed for the duration of a call.  Keys are 64-bit like gtsam::Key
+ * (the reference's int8 ids, Factor.msg:1-2, wrap after 127).
+ * A handle is single-threaded (like the reference's one ROS spinner,
+ * graph.cpp:214); distinct handles are independent; each owns one HIP stream.
+ */
+#ifndef PGO_H
+#define PGO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGO_ABI_VERSION 1
+
+/* ---- status codes (GTSAM exception each one replaces) -------------------- */
+#define PGO_OK 0
+#define PGO_E_ARG (-1)           /* null handle / bad size                          */
+#define PGO_E_DUP_KEY (-2)       /* gtsam::ValuesKeyAlreadyExists  (Values::insert) */
+#define PGO_E_NO_KEY (-3)        /* gtsam::ValuesKeyDoesNotExist   (Values::at, or a
+                                    factor on a key never inserted, at optimize)    */
+#define PGO_E_BAD_COV (-4)       /* covariance not positive definite (LLT failure)   */
+#define PGO_E_INDETERMINANT (-5) /* gtsam::IndeterminantLinearSystemException (GN)  */
+#define PGO_E_NONFINITE (-6)     /* non-finite input or error                       */
+#define PGO_E_HIP (-7)           /* HIP runtime failure (pgo_last_error has text)   */
+#define PGO_E_NO_DEVICE (-8)     /* no usable MI355X / HIP device                   */
+#define PGO_E_NOMEM (-9)
+#define PGO_E_BAD_EDGE (-10)     /* between factor with key1 == key2                */
+#define PGO_W_MAXITER 1          /* informational: stopped at max_iterations        */
+
+/* ---- algorithms / solvers ------------------------------------------------ */
+#define PGO_ALG_LM 0             /* gtsam::LevenbergMarquardtOptimizer (graph.cpp:119) */
+#define PGO_ALG_GN 1             /* gtsam::GaussNewtonOptimizer                      */
+#define PGO_SOLVER_PCG 0         /* block-Jacobi preconditioned CG on the 3x3 BSR H  */
+
+typedef struct pgo_graph pgo_graph;
+
+typedef struct {
+  int device;        /* HIP device ordinal (default 0) */
+  int reserved[7];
+} pgo_opts;
+
+typedef struct {
+  /* gtsam::NonlinearOptimizerParams (defaults in brackets) */
+  int max_iterations;           /* [100]  */
+  double relative_error_tol;    /* [1e-5] */
+  double absolute_error_tol;    /* [1e-5] */
+  double error_tol;             /* [0]    */
+  /* gtsam::LevenbergMarquardtParams */
+  double lambda_initial;        /* [1e-5] */
+  double lambda_factor;         /* [10]   */
+  double lambda_upper_bound;    /* [1e5]  */
+  double lambda_lower_bound;    /* [0]    */
+  double min_model_fidelity;    /* [1e-3] */
+  int use_fixed_lambda_factor;  /* [1]    */
+  int algorithm;                /* [PGO_ALG_LM] */
+  /* linear solver (the GPU replacement for GTSAM's multifrontal Cholesky) */
+  int linear_solver;            /* [PGO_SOLVER_PCG] */
+  double pcg_relative_tol;      /* stop when r'M^-1 r <= tol^2 * r0'M^-1 r0 [1e-10] */
+  int pcg_max_iterations;       /* [20000] */
+  int pcg_check_interval;       /* iterations enqueued between convergence reads [32] */
+  int max_outer;                /* >0: stop after this many linearisations [0] */
+  int profile_every;            /* >0: time every k-th PCG SpMV launch and every
+                                   linearisation with HIP events on the handle's
+                                   stream (pgo_stats.kernel_*) [0] */
+} pgo_params;
+
+typedef struct {
+  int status;                   /* PGO_OK / PGO_W_MAXITER / error                 */
+  int iterations;               /* accepted steps (gtsam iterations())            */
+  int inner_iterations;         /* lambda tries (LM) / steps (GN)                 */
+  int linearizations;
+  double initial_error;         /* graph.error(initial) = 0.5 chi^2               */
+  double final_error;
+  long long pcg_iterations;     /* summed over all solves                          */
+  double ms_total;              /* wall time inside pgo_optimize                   */
+  double ms_upload;             /* host->device graph upload (0 when resident)     */
+  double ms_linearize;          /* device time of linearisation kernels            */
+  double ms_solve;              /* device time of PCG                              */
+  double ms_update;             /* retract + error + model-decrease kernels        */
+  double kernel_spmv_ms;        /* summed device time of the timed SpMV launches   */
+  long long kernel_spmv_count;  /* number of timed SpMV launches                   */
+  double kernel_linearize_ms;   /* summed device time of the linearisation kernel  */
+  long long kernel_linearize_count;
+  double reserved[4];
+} pgo_stats;
+
+/* ---- lifetime ------------------------------------------------------------ */
+pgo_graph *pgo_create(const pgo_opts *opts);        /* NULL opts: device 0 */
+void pgo_destroy(pgo_graph *g);
+const char *pgo_last_error(const pgo_graph *g);
+const char *pgo_status_string(int status);
+int pgo_abi_version(void);
+void pgo_default_params(pgo_params *p);
+
+/* ---- graph construction (graph.cpp:27-113) ------------------------------- */
+/* Values::insert(key, Pose2(x, y, theta)); duplicate key -> PGO_E_DUP_KEY */
+int pgo_add_vertex(pgo_graph *g, uint64_t key, double x, double y, double theta);
+int pgo_add_vertices(pgo_graph *g, size_t n, const uint64_t *keys, const double *xyt);
+/* graph.add(PriorFactor<Pose2>(key, pose, Covariance(cov))), cov row-major 3x3 */
+int pgo_add_prior(pgo_graph *g, uint64_t key, const double pose[3], const double cov[9]);
+/* graph.add(BetweenFactor<Pose2>(k1, k2, z, Covariance(cov))) */
+int pgo_add_edge(pgo_graph *g, uint64_t k1, uint64_t k2, const double z[3], const double cov[9]);
+/* bulk form; cov_stride 9 = one covariance per edge, 0 = one shared covariance */
+int pgo_add_edges(pgo_graph *g, size_t n, const uint64_t *k1, const uint64_t *k2,
+                  const double *z, const double *cov, int cov_stride);
+
+/* ---- optimisation (graph.cpp:119, write-back :122-130) ------------------- */
+/* Runs the optimiser from the handle's current values and replaces them with
+ * the result (the reference's `initial = poses_opti`).  NULL params: defaults. */
+int pgo_optimize(pgo_graph *g, const pgo_params *params, pgo_stats *stats);
+
+/* ---- values access ------------------------------------------------------- */
+int pgo_get_pose(pgo_graph *g, uint64_t key, double out[3]);           /* Values::at */
+/* keys NULL: all poses in insertion order (out holds 3*n doubles) */
+int pgo_get_poses(pgo_graph *g, size_t n, const uint64_t *keys, double *out);
+/* Values::update: overwrite current values (keys NULL: insertion order) */
+int pgo_set_poses(pgo_graph *g, size_t n, const uint64_t *keys, const double *xyt);
+/* Device-side copy of the current values into a snapshot slot / back (no PCIe
+ * traffic): re-run a solve from the same initial values (graph.cpp:130 keeps
+ * `initial` around the same way). */
+int pgo_save_values(pgo_graph *g);
+int pgo_restore_values(pgo_graph *g);
+size_t pgo_num_factors(const pgo_graph *g);   /* graph.nrFactors() */
+size_t pgo_num_vertices(const pgo_graph *g);  /* initial.size()    */
+/* graph.error(values) = 0.5 sum e^T Omega e at the current values (device). */
+int pgo_error(pgo_graph *g, double *err);
+
+/* ---- diagnostics (parity tests; device results at the current values) ---- */
+/* H diagonal blocks (9 doubles row-major per vertex, insertion order), the
+ * off-diagonal block H_{k1,k2} = J1^T Omega of every between factor (9 per
+ * factor, insertion order), gradient g = J^T Omega e (3 per vertex), error. */
+int pgo_debug_linearize(pgo_graph *g, double *hdiag, double *hoff, double *grad, double *err);
+/* y = (H + lambda I) x at the current linearisation (x, y: 3 per vertex) */
+int pgo_debug_spmv(pgo_graph *g, double lambda, const double *x, double *y);
+/* delta = PCG solve of (H + lambda I) delta = -g at the current values */
+int pgo_debug_solve(pgo_graph *g, double lambda, const pgo_params *params, double *delta,
+                    int *pcg_iterations);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PGO_H */

@@ -1,0 +1,126 @@
+"""The C-ABI boundary without a GPU: libpgo.so loads, exports every symbol
+include/pgo.h declares, is consumable from plain C, and its host-side logic
+(key map, covariance checks, error codes) behaves like the GTSAM calls it
+replaces.  No compute is launched here."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from graphslam_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DIAG = np.diag([0.0025, 0.0025, 7.6e-5]).ravel()
+
+
+def test_exports_every_declared_symbol(pgo_lib):
+    syms = _lib.declared_symbols()
+    assert len(syms) >= 20
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (pgo_\w+)", out))
+    assert set(syms) <= exported, set(syms) - exported
+
+
+def test_header_constants_match_binding():
+    text = open(os.path.join(ROOT, "include", "pgo.h")).read()
+    defs = dict(re.findall(r"#define (PGO_\w+) \(?(-?\d+)\)?", text))
+    for name, val in defs.items():
+        if hasattr(_lib, name):
+            assert getattr(_lib, name) == int(val), name
+
+
+def test_plain_c_consumer(tmp_path, pgo_lib):
+    src = tmp_path / "use.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include "pgo.h"
+int main(void) {
+  pgo_graph *g = pgo_create(NULL);
+  double cov[9] = {0.01,0,0, 0,0.01,0, 0,0,0.01}, z[3] = {1,0,0}, p0[3] = {0,0,0};
+  if (pgo_add_vertex(g, 1, 0, 0, 0) || pgo_add_vertex(g, 2, 1, 0, 0)) return 1;
+  if (pgo_add_vertex(g, 2, 0, 0, 0) != PGO_E_DUP_KEY) return 2;
+  if (pgo_add_prior(g, 1, p0, cov) || pgo_add_edge(g, 1, 2, z, cov)) return 3;
+  if (pgo_num_factors(g) != 2 || pgo_num_vertices(g) != 2) return 4;
+  pgo_params p; pgo_default_params(&p);
+  if (p.max_iterations != 100 || p.lambda_initial != 1e-5) return 5;
+  pgo_destroy(g);
+  printf("ok %d\n", pgo_abi_version());
+  return 0;
+}
+''')
+    exe = tmp_path / "use"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", f"-I{ROOT}/include", str(src), "-o", str(exe),
+                    _lib.LIB_PATH, f"-Wl,-rpath,{os.path.dirname(_lib.LIB_PATH)}"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.startswith("ok 1"), (r.returncode, r.stdout, r.stderr)
+
+
+def test_default_params_are_gtsam_defaults(pgo_lib):
+    from graphslam_amd.pose_graph import default_params
+    p = default_params()
+    assert (p.max_iterations, p.relative_error_tol, p.absolute_error_tol, p.error_tol) == (100, 1e-5, 1e-5, 0.0)
+    assert (p.lambda_initial, p.lambda_factor, p.lambda_upper_bound, p.lambda_lower_bound) == (1e-5, 10.0, 1e5, 0.0)
+    assert p.min_model_fidelity == 1e-3 and p.use_fixed_lambda_factor == 1 and p.algorithm == 0
+
+
+def test_host_logic_error_codes(pgo_lib):
+    from graphslam_amd.pose_graph import (BadCovariance, PgoError, PoseGraph, ValuesKeyAlreadyExists,
+                                          ValuesKeyDoesNotExist)
+    pg = PoseGraph()
+    pg.add_vertex(1, 0, 0, 0)
+    pg.add_vertex(2 ** 40, 1, 2, 3)                      # 64-bit keys (reference int8 ids wrap)
+    with pytest.raises(ValuesKeyAlreadyExists):
+        pg.add_vertex(1, 5, 5, 5)
+    with pytest.raises(BadCovariance):
+        pg.add_edge(1, 2 ** 40, [1, 0, 0], np.diag([0.01, -1, 0.01]))
+    with pytest.raises(PgoError) as ei:
+        pg.add_edge(1, 1, [1, 0, 0], DIAG)
+    assert ei.value.status == _lib.PGO_E_BAD_EDGE
+    with pytest.raises(PgoError) as ei:
+        pg.add_edge(1, 2 ** 40, [np.nan, 0, 0], DIAG)
+    assert ei.value.status == _lib.PGO_E_NONFINITE
+    pg.add_edge(1, 2 ** 40, [1, 0, 0], DIAG)
+    pg.add_edge(2 ** 40, 777, [1, 0, 0], DIAG)            # key never inserted: error at optimize (like GTSAM)
+    pg.add_prior(1, [0, 0, 0], np.diag([0.01] * 3))
+    assert pg.num_factors == 3 and pg.num_vertices == 2
+    assert np.allclose(pg.pose(2 ** 40), [1, 2, 3])
+    with pytest.raises(ValuesKeyDoesNotExist):
+        pg.pose(777)
+    with pytest.raises(PgoError) as ei:
+        pg.optimize()
+    # on a GPU box the missing key is reported; without a device, no device
+    assert ei.value.status in (_lib.PGO_E_NO_KEY, _lib.PGO_E_NO_DEVICE)
+    pg.close()
+
+
+def test_set_get_poses_roundtrip(pgo_lib):
+    from graphslam_amd.pose_graph import PoseGraph
+    pg = PoseGraph()
+    keys = np.array([10, 20, 30], dtype=np.uint64)
+    xyt = np.array([[0, 0, 0.1], [1, 2, -3.0], [5, 6, 3.1]])
+    pg.add_vertices(keys, xyt)
+    assert np.allclose(pg.poses(), xyt)
+    pg.set_poses([[9, 9, 0.5]], keys=[20])
+    assert np.allclose(pg.poses([20, 10]), [[9, 9, 0.5], [0, 0, 0.1]])
+
+
+def test_gtsam_mirror_host_side(pgo_lib):
+    from graphslam_amd import gtsam as gt
+    v = gt.Values()
+    v.insert(1, gt.Pose2(0, 0, 0))
+    with pytest.raises(gt.ValuesKeyAlreadyExists):
+        v.insert(1, gt.Pose2(1, 1, 1))
+    with pytest.raises(gt.ValuesKeyDoesNotExist):
+        v.atPose2(2)
+    assert abs(gt.Pose2(0, 0, 3 * np.pi).theta() - np.pi) < 1e-12
+    graph = gt.NonlinearFactorGraph()
+    noise = gt.noiseModel.Gaussian.Covariance(np.diag([0.01, 0.01, 0.01]))
+    graph.add(gt.PriorFactorPose2(1, gt.Pose2(0, 0, 0), noise))
+    graph.add(gt.BetweenFactorPose2(1, 2, gt.Pose2(1, 0, 0), noise))
+    assert graph.nrFactors() == 2
+    p = gt.LevenbergMarquardtParams()
+    p.setMaxIterations(7)
+    assert p.raw.max_iterations == 7

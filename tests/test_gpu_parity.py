@@ -1,0 +1,274 @@
+"""GPU parity: libpgo.so (HIP, gfx950) against the CPU oracle, through the C-ABI.
+
+Tolerances (fp64 throughout):
+* linearisation (H blocks, gradient, error): rtol 1e-10 -- same formulas,
+  different summation order / FMA contraction;
+* PCG step vs the oracle's direct sparse Cholesky: relative 1e-6 in the
+  2-norm at pcg_relative_tol 1e-10 (the PCG stops on the preconditioned
+  residual, so the step error is bounded by cond(H) x tol);
+* optimiser result vs oracle/golden: same accepted-iteration count, final
+  error rtol 1e-8, poses within 1e-6 m / 1e-7 rad (KAT graphs: ground truth
+  to 1e-9).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from graphslam_amd import datasets
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def angdiff(a, b):
+    return np.abs(np.angle(np.exp(1j * (np.asarray(a) - np.asarray(b)))))
+
+
+def assert_poses(a, b, tol_xy, tol_th):
+    a, b = np.asarray(a), np.asarray(b)
+    dxy = np.abs(a[:, :2] - b[:, :2]).max() if len(a) else 0.0
+    dth = angdiff(a[:, 2], b[:, 2]).max() if len(a) else 0.0
+    assert dxy <= tol_xy and dth <= tol_th, (dxy, dth)
+
+
+@pytest.fixture(scope="module")
+def pg_cls(pgo_lib):
+    from graphslam_amd.pose_graph import PoseGraph
+    return PoseGraph
+
+
+def load(name):
+    if name == "square":
+        return datasets.square_loop()
+    if name == "chain":
+        return datasets.straight_chain()
+    return datasets.make(name)
+
+
+# ------------------------------------------------------------ linearisation
+@pytest.mark.parametrize("name", ["square", "C1", "C1-nn", "C2"])
+def test_linearize_parity(pg_cls, oracle_lib, name):
+    g = load(name)
+    pg = pg_cls.from_dataset(g)
+    hd, ho, grad, err = pg.debug_linearize(g.num_edges)
+    o = oracle_lib.Oracle(g)
+    hd0, ho0, g0, err0 = o.linearize()
+    scale_h = np.abs(hd0).max()
+    assert np.abs(hd - hd0).max() <= 1e-10 * scale_h
+    assert np.abs(ho - ho0).max() <= 1e-10 * scale_h
+    assert np.abs(grad - g0).max() <= 1e-10 * max(np.abs(g0).max(), 1.0)
+    assert abs(err - err0) <= 1e-10 * max(err0, 1e-30)
+    assert abs(pg.error() - o.error()) <= 1e-10 * max(err0, 1e-30)
+
+
+def test_linearize_nondiagonal_covariance(pg_cls, oracle_lib):
+    g = datasets.make("C1")
+    rng = np.random.default_rng(5)
+    L = np.tril(rng.normal(size=(g.num_edges, 3, 3)) * 0.02) + np.eye(3) * 0.05
+    cov = L @ np.transpose(L, (0, 2, 1))
+    g.edge_cov = cov.reshape(-1, 9)
+    pg = pg_cls.from_dataset(g)
+    hd, ho, grad, err = pg.debug_linearize(g.num_edges)
+    hd0, ho0, g0, err0 = oracle_lib.Oracle(g).linearize()
+    assert np.allclose(hd, hd0, rtol=1e-10, atol=1e-10 * np.abs(hd0).max())
+    assert np.allclose(ho, ho0, rtol=1e-10, atol=1e-10 * np.abs(hd0).max())
+    assert abs(err - err0) <= 1e-10 * err0
+
+
+def test_spmv_parity(pg_cls, oracle_lib):
+    from oracle import pgo_numpy as tw
+    g = datasets.make("C1-nn")
+    pg = pg_cls.from_dataset(g)
+    x = np.random.default_rng(1).normal(size=(g.num_poses, 3))
+    y = pg.debug_spmv(x, lam=0.37)
+    lin = tw.linearize(tw.problem_from_graph(g), tw.from_xyt(g.initial))
+    ref = (lin.H @ x.ravel() + 0.37 * x.ravel()).reshape(-1, 3)
+    assert np.abs(y - ref).max() <= 1e-10 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("name,lam", [("C1", 1e-5), ("C1-nn", 1e-3), ("C2", 1e-5)])
+def test_pcg_step_vs_direct_cholesky(pg_cls, oracle_lib, name, lam):
+    g = load(name)
+    pg = pg_cls.from_dataset(g)
+    d, it = pg.debug_solve(lam, pcg_relative_tol=1e-12, pcg_max_iterations=200000)
+    rc, d0 = oracle_lib.Oracle(g).solve(lam)
+    assert rc == 0 and it > 0
+    rel = np.linalg.norm(d - d0) / np.linalg.norm(d0)
+    assert rel <= 1e-6, rel
+
+
+# ------------------------------------------------------------ full optimiser
+@pytest.mark.parametrize("name", ["square", "chain"])
+def test_kat_ground_truth(pg_cls, name):
+    g = load(name)
+    pg = pg_cls.from_dataset(g)
+    st = pg.optimize()
+    assert st["final_error"] < 1e-18
+    assert_poses(pg.poses(), g.ground_truth, 1e-9, 1e-9)
+
+
+@pytest.mark.parametrize("name", ["square", "C1", "C1-nn", "C2"])
+def test_lm_parity_with_golden(pg_cls, name):
+    gold = np.load(os.path.join(GOLDEN, f"golden_{name}.npz"), allow_pickle=False)
+    g = load(name)
+    pg = pg_cls.from_dataset(g)
+    st = pg.optimize()
+    assert st["iterations"] == int(gold["iterations"])
+    fe = float(gold["final_error"])
+    assert abs(st["final_error"] - fe) <= 1e-8 * fe + 1e-18
+    assert_poses(pg.poses(), gold["final"], 1e-6, 1e-7)
+
+
+def test_lm_trace_matches_oracle_c1nn(pg_cls, oracle_lib):
+    g = datasets.make("C1-nn")
+    o = oracle_lib.Oracle(g).optimize()
+    pg = pg_cls.from_dataset(g)
+    st = pg.optimize()
+    assert st["iterations"] == o.stats["iterations"]
+    assert st["inner_iterations"] == o.stats["inner_iterations"]
+    assert st["linearizations"] == o.stats["linearizations"]
+    assert abs(st["initial_error"] - o.stats["initial_error"]) <= 1e-12 * o.stats["initial_error"]
+
+
+def test_gauss_newton_parity(pg_cls, oracle_lib):
+    g = datasets.make("C1")
+    o = oracle_lib.Oracle(g).optimize(algorithm=1)
+    pg = pg_cls.from_dataset(g)
+    st = pg.optimize(algorithm=1)
+    assert st["iterations"] == o.stats["iterations"]
+    assert abs(st["final_error"] - o.stats["final_error"]) <= 1e-8 * o.stats["final_error"]
+    assert_poses(pg.poses(), o.poses, 1e-6, 1e-7)
+
+
+def test_warm_start_write_back(pg_cls):
+    """graph.cpp:130 `initial = poses_opti`: a second optimize starts at the optimum."""
+    g = datasets.make("C1")
+    pg = pg_cls.from_dataset(g)
+    st1 = pg.optimize()
+    st2 = pg.optimize()
+    assert abs(st2["initial_error"] - st1["final_error"]) <= 1e-9 * st1["final_error"]
+    assert st2["final_error"] <= st2["initial_error"]
+
+
+def test_save_restore_and_determinism(pg_cls):
+    g = datasets.make("C2")
+    pg = pg_cls.from_dataset(g)
+    pg.save_values()
+    st1 = pg.optimize()
+    p1 = pg.poses()
+    pg.restore_values()
+    assert abs(pg.error() - st1["initial_error"]) == 0.0
+    st2 = pg.optimize()
+    assert st2["final_error"] == st1["final_error"]          # bitwise reproducible
+    assert np.array_equal(pg.poses(), p1)
+
+
+# ------------------------------------------------------------ headline size
+def test_c3_full_size_against_golden(pg_cls):
+    """C3 (100k poses / 500k edges): the oracle's trajectory -- LM gives up at
+    lambda >= 1e5 after 7 accepted steps from the dead-reckoned start -- and
+    its final error, plus a 1000-pose sample of the final values."""
+    gold = np.load(os.path.join(GOLDEN, "golden_C3.npz"), allow_pickle=False)
+    g = datasets.make("C3")
+    pg = pg_cls.from_dataset(g)
+    st = pg.optimize()
+    assert abs(st["initial_error"] - float(gold["initial_error"])) <= 1e-10 * float(gold["initial_error"])
+    assert st["iterations"] == int(gold["iterations"])
+    assert abs(st["final_error"] - float(gold["final_error"])) <= 1e-6 * float(gold["final_error"])
+    idx = gold["sample_index"]
+    assert_poses(pg.poses()[idx], gold["final_sample"], 1e-4, 1e-5)
+
+
+# ------------------------------------------------------------ edge cases
+def test_empty_graph(pg_cls):
+    pg = pg_cls()
+    st = pg.optimize()
+    assert st["final_error"] == 0.0 and st["iterations"] == 0
+
+
+def test_single_vertex_prior(pg_cls):
+    pg = pg_cls()
+    pg.add_vertex(1, 0.3, -0.2, 0.4)
+    pg.add_prior(1, [1.0, 2.0, 0.5], np.diag([0.01, 0.01, 0.01]))
+    pg.optimize()
+    assert_poses(pg.poses(), [[1.0, 2.0, 0.5]], 1e-9, 1e-9)
+
+
+def test_no_prior_gauge_freedom_lm(pg_cls, oracle_lib):
+    """No prior: H is singular; LM's damping keeps the system solvable."""
+    g = datasets.square_loop()
+    g.prior_keys = g.prior_keys[:0]
+    g.prior_pose = g.prior_pose[:0]
+    g.prior_cov = g.prior_cov[:0]
+    pg = pg_cls.from_dataset(g)
+    st = pg.optimize()
+    assert st["final_error"] < 1e-12
+
+
+def test_gauss_newton_singular_raises(pg_cls):
+    from graphslam_amd.pose_graph import IndeterminantLinearSystemException
+    pg = pg_cls()
+    pg.add_vertex(1, 0, 0, 0)
+    pg.add_vertex(2, 1.1, 0, 0)
+    pg.add_edge(1, 2, [1, 0, 0], np.diag([0.01, 0.01, 0.01]))   # no prior: gauge freedom
+    with pytest.raises(IndeterminantLinearSystemException):
+        pg.optimize(algorithm=1)
+
+
+def test_unknown_key_at_optimize(pg_cls):
+    from graphslam_amd.pose_graph import ValuesKeyDoesNotExist
+    pg = pg_cls()
+    pg.add_vertex(1, 0, 0, 0)
+    pg.add_edge(1, 5, [1, 0, 0], np.diag([0.01, 0.01, 0.01]))
+    with pytest.raises(ValuesKeyDoesNotExist):
+        pg.optimize()
+
+
+def test_duplicate_and_parallel_edges(pg_cls, oracle_lib):
+    """Two factors between the same pair (both orientations) are summed."""
+    g = datasets.square_loop()
+    i, j = g.edge_index()
+    extra_z = datasets.between_xyt(g.ground_truth[j[:3]], g.ground_truth[i[:3]]) + 0.01
+    g.edge_k1 = np.concatenate([g.edge_k1, g.edge_k2[:3], g.edge_k1[:2]])
+    g.edge_k2 = np.concatenate([g.edge_k2, g.edge_k1[:3], g.edge_k2[:2]])
+    g.edge_z = np.concatenate([g.edge_z, extra_z, g.edge_z[:2] - 0.02])
+    g.edge_cov = np.concatenate([g.edge_cov, g.edge_cov[:5]])
+    pg = pg_cls.from_dataset(g)
+    st = pg.optimize()
+    o = oracle_lib.Oracle(g).optimize()
+    assert abs(st["final_error"] - o.stats["final_error"]) <= 1e-9 * o.stats["final_error"]
+    assert_poses(pg.poses(), o.poses, 1e-7, 1e-8)
+
+
+def test_arbitrary_keys_and_insertion_order(pg_cls, oracle_lib):
+    g = datasets.make("C1")
+    perm = np.random.default_rng(2).permutation(g.num_poses)
+    keys = (np.arange(g.num_poses, dtype=np.uint64) * 7919 + 2 ** 33)
+    pg = pg_cls()
+    pg.add_vertices(keys[perm], g.initial[perm])
+    pg.add_prior(int(keys[0]), g.prior_pose[0], g.prior_cov[0])
+    i, j = g.edge_index()
+    pg.add_edges(keys[i], keys[j], g.edge_z, g.edge_cov)
+    pg.optimize()
+    gold = np.load(os.path.join(GOLDEN, "golden_C1.npz"), allow_pickle=False)
+    assert_poses(pg.poses(keys), gold["final"], 1e-6, 1e-7)
+
+
+def test_gtsam_mirror_end_to_end(pgo_lib):
+    """The graph.cpp call sequence, verbatim in the mirror's names."""
+    from graphslam_amd import gtsam as gt
+    g = datasets.square_loop()
+    graph = gt.NonlinearFactorGraph()
+    initial = gt.Values()
+    for k, p in zip(g.keys, g.initial):
+        initial.insert(int(k), gt.Pose2(*p))
+    graph.add(gt.PriorFactorPose2(1, gt.Pose2(0, 0, 0), gt.noiseModel.Gaussian.Covariance(np.diag([0.01] * 3))))
+    for k1, k2, z, c in zip(g.edge_k1, g.edge_k2, g.edge_z, g.edge_cov):
+        graph.add(gt.BetweenFactorPose2(int(k1), int(k2), gt.Pose2(*z),
+                                        gt.noiseModel.Gaussian.Covariance(c.reshape(3, 3))))
+    poses_opti = gt.LevenbergMarquardtOptimizer(graph, initial).optimize()
+    for k, p in zip(g.keys, g.ground_truth):
+        q = poses_opti.atPose2(int(k))
+        assert abs(q.x() - p[0]) < 1e-9 and abs(q.y() - p[1]) < 1e-9
+    assert graph.error(poses_opti) < 1e-18
