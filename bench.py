@@ -73,59 +73,32 @@ def main():
     ap.add_argument("--profile-every", type=int, default=16)
     ap.add_argument("--cpu-outer", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--max-outer", type=int, default=0,
+                    help="profiling runs only: stop each optimize after this many linearisations")
     args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from graphslam_amd import datasets
     from graphslam_amd.pose_graph import PoseGraph, default_params
+    from graphslam_amd.replicas import init_from_env, timed_steps
 
+    r = init_from_env()
+    world, rank = r.world, r.rank
     g = datasets.make(args.config)
-    pg = PoseGraph.from_dataset(g, device=local_rank)
+    pg = PoseGraph.from_dataset(g, device=r.local_rank)
     pg.save_values()                     # upload graph + values once; snapshot the initial values
-    params = default_params(profile_every=args.profile_every)
+    params = default_params(profile_every=args.profile_every, max_outer=args.max_outer)
 
-    for _ in range(args.warmup):
+    def step():
         pg.restore_values()
-        pg.optimize(params)
+        st = pg.optimize(params)         # returns after the handle's stream has drained
+        return st["linearizations"], st
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    totals = dict(linearizations=0, inner=0, pcg=0, spmv_ms=0.0, spmv_n=0, lin_ms=0.0, lin_n=0)
-    last = None
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        pg.restore_values()
-        st = pg.optimize(params)
-        totals["linearizations"] += st["linearizations"]
-        totals["inner"] += st["inner_iterations"]
-        totals["pcg"] += st["pcg_iterations"]
-        totals["spmv_ms"] += st["kernel_spmv_ms"]
-        totals["spmv_n"] += st["kernel_spmv_count"]
-        totals["lin_ms"] += st["kernel_linearize_ms"]
-        totals["lin_n"] += st["kernel_linearize_count"]
-        last = st
-    barrier()
-    elapsed = time.perf_counter() - t0
-
-    lin_total = totals["linearizations"]
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([float(lin_total)], dtype=torch.float64)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        lin_total = int(c.item())
+    elapsed, lin_total, results = timed_steps(r, step, args.steps, args.warmup)
+    stats = [s for _, s in results]
+    last = stats[-1]
+    totals = dict(spmv_ms=sum(s["kernel_spmv_ms"] for s in stats), spmv_n=sum(s["kernel_spmv_count"] for s in stats),
+                  lin_ms=sum(s["kernel_linearize_ms"] for s in stats),
+                  lin_n=sum(s["kernel_linearize_count"] for s in stats))
 
     if rank == 0:
         n, ne = g.num_poses, g.num_edges
@@ -188,8 +161,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(g, args.cpu_outer)
         print(json.dumps(out))
     pg.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    r.close()
 
 
 if __name__ == "__main__":

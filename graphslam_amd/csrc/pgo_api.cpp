@@ -41,6 +41,7 @@ struct pgo_graph {
   bool host_values = true;                  // host xyt == device pose
   DevGraph d;
   std::vector<int> edge_slot0;              // side-0 slot of every between factor
+  bool gauge_free = false;                  // some connected component has no prior
   double* h_scal = nullptr;                 // pinned
   int* h_ctrl = nullptr;                    // pinned
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -236,6 +237,26 @@ int upload_structure(pgo_graph* g) {
       slot_edge[k] = tmp[k - b].second;
     }
   }
+  // connected components without a prior leave H singular (3-dof gauge):
+  // GTSAM's Cholesky throws IndeterminantLinearSystemException there (GN);
+  // LM's damping keeps it solvable.
+  {
+    std::vector<int> uf(n);
+    for (int i = 0; i < n; i++) uf[i] = i;
+    auto find = [&](int x) {
+      while (uf[x] != x) x = uf[x] = uf[uf[x]];
+      return x;
+    };
+    for (int e = 0; e < ne; e++) {
+      const int a = find(eij[e].x), b = find(eij[e].y);
+      if (a != b) uf[a] = b;
+    }
+    std::vector<char> anchored(n, 0);
+    for (int q = 0; q < np; q++) anchored[find(pv[q])] = 1;
+    g->gauge_free = false;
+    for (int i = 0; i < n; i++)
+      if (!anchored[find(i)]) g->gauge_free = true;
+  }
   g->edge_slot0.assign(ne, -1);
   for (int k = 0; k < ns; k++)
     if ((slot_edge[k] & 1) == 0) g->edge_slot0[slot_edge[k] >> 1] = k;
@@ -362,11 +383,11 @@ int pcg_solve(pgo_graph* g, const pgo_params& p, double lam, PcgResult* out, pgo
     int npairs = 0;
     for (; k < stop; k++) {
       const bool timed = prof > 0 && (k % prof) == 0 && npairs < pgo_graph::kProfPairs;
-      if (timed) HIP_TRY(g, hipEventRecord(g->pev[2 * npairs], d.stream));
-      HIP_TRY(g, pgo::launch_pcg_spmv(d, lam));
       if (timed) {
-        HIP_TRY(g, hipEventRecord(g->pev[2 * npairs + 1], d.stream));
+        HIP_TRY(g, pgo::launch_pcg_spmv(d, lam, g->pev[2 * npairs], g->pev[2 * npairs + 1]));
         g->pk_iter[npairs++] = k;
+      } else {
+        HIP_TRY(g, pgo::launch_pcg_spmv(d, lam));
       }
       HIP_TRY(g, pgo::launch_pcg_vec(d, k, tol2));
     }
@@ -630,14 +651,18 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   double lam = p.lambda_initial, factor = p.lambda_factor;
   int iters = 0, inner = 0;
   int status = PGO_OK;
+  if (p.algorithm == PGO_ALG_GN && g->gauge_free && d.n > 0 && !(err <= p.error_tol)) {
+    st.status = PGO_E_INDETERMINANT;
+    if (stats) *stats = st;
+    return fail(g, PGO_E_INDETERMINANT,
+                "Gauss-Newton: a connected component has no prior, the linear system is singular");
+  }
   hipEvent_t* ev = g->ev;
   if (!(err <= p.error_tol) && iters < p.max_iterations && d.n > 0) {
     double new_err = err;
     for (;;) {
       const double cur_err = new_err;
-      HIP_TRY(g, hipEventRecord(ev[0], d.stream));
-      HIP_TRY(g, pgo::launch_linearize(d));
-      HIP_TRY(g, hipEventRecord(ev[1], d.stream));
+      HIP_TRY(g, pgo::launch_linearize(d, ev[0], ev[1]));
       st.linearizations++;
       bool first_try = true;
       for (;;) {  // tryLambda (GN: one plain step)
@@ -645,6 +670,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
         PcgResult pr;
         RC_TRY(pcg_solve(g, p, lam_try, &pr, &st));
         HIP_TRY(g, hipEventRecord(ev[2], d.stream));
+        HIP_TRY(g, hipEventSynchronize(ev[2]));
         if (first_try) {
           const double lin_ms = ms_between(ev[0], ev[1]);
           st.ms_linearize += lin_ms;

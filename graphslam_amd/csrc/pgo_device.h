@@ -61,11 +61,11 @@ constexpr int kRunning = 0, kConverged = 1, kBreakdown = 2;
 int grid_rows(const DevGraph& d);
 int grid_for(int work);
 
-hipError_t launch_linearize(const DevGraph& d);
+hipError_t launch_linearize(const DevGraph& d, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 hipError_t launch_error(const DevGraph& d, const double4* pose, double* out_scalar);
 hipError_t launch_retract(const DevGraph& d, const double* delta);
 hipError_t launch_pcg_init(const DevGraph& d, double lambda);
-hipError_t launch_pcg_spmv(const DevGraph& d, double lambda);
+hipError_t launch_pcg_spmv(const DevGraph& d, double lambda, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 hipError_t launch_pcg_vec(const DevGraph& d, int k, double tol2);
 hipError_t launch_model_decrease(const DevGraph& d, const double* delta, double* out2);
 hipError_t launch_spmv(const DevGraph& d, double lambda, const double* x, double* y);

@@ -12,6 +12,7 @@
 // Every reduction is a fixed-order tree (xor butterflies inside a wave, LDS
 // across waves, fixed-order partial sums across blocks): results are bitwise
 // reproducible run to run; no floating-point atomics anywhere.
+#include <hip/hip_ext.h>
 #include <math.h>
 
 #include "pgo_device.h"
@@ -431,9 +432,15 @@ int grid_rows(const DevGraph& d) {
     default: KERNEL<32><<<grid_rows(d), kThreads, 0, d.stream>>>(__VA_ARGS__); break; \
   }
 
-hipError_t launch_linearize(const DevGraph& d) {
+hipError_t launch_linearize(const DevGraph& d, hipEvent_t start, hipEvent_t stop) {
   if (d.n == 0) return hipSuccess;
-  PGO_DISPATCH_G(d.G, k_linearize, d);
+  const dim3 grid(grid_rows(d)), block(kThreads);
+  switch (d.G) {
+    case 4: hipExtLaunchKernelGGL(k_linearize<4>, grid, block, 0, d.stream, start, stop, 0, d); break;
+    case 8: hipExtLaunchKernelGGL(k_linearize<8>, grid, block, 0, d.stream, start, stop, 0, d); break;
+    case 16: hipExtLaunchKernelGGL(k_linearize<16>, grid, block, 0, d.stream, start, stop, 0, d); break;
+    default: hipExtLaunchKernelGGL(k_linearize<32>, grid, block, 0, d.stream, start, stop, 0, d); break;
+  }
   return hipGetLastError();
 }
 
@@ -457,8 +464,17 @@ hipError_t launch_pcg_init(const DevGraph& d, double lambda) {
   return hipGetLastError();
 }
 
-hipError_t launch_pcg_spmv(const DevGraph& d, double lambda) {
-  PGO_DISPATCH_G(d.G, k_pcg_spmv, d, lambda);
+// start/stop (optional): events written by the dispatch itself
+// (hipExtLaunchKernelGGL), i.e. the kernel's own begin/end like rocprofv3's
+// kernel trace -- no extra marker packets around the launch.
+hipError_t launch_pcg_spmv(const DevGraph& d, double lambda, hipEvent_t start, hipEvent_t stop) {
+  const dim3 grid(grid_rows(d)), block(kThreads);
+  switch (d.G) {
+    case 4: hipExtLaunchKernelGGL(k_pcg_spmv<4>, grid, block, 0, d.stream, start, stop, 0, d, lambda); break;
+    case 8: hipExtLaunchKernelGGL(k_pcg_spmv<8>, grid, block, 0, d.stream, start, stop, 0, d, lambda); break;
+    case 16: hipExtLaunchKernelGGL(k_pcg_spmv<16>, grid, block, 0, d.stream, start, stop, 0, d, lambda); break;
+    default: hipExtLaunchKernelGGL(k_pcg_spmv<32>, grid, block, 0, d.stream, start, stop, 0, d, lambda); break;
+  }
   return hipGetLastError();
 }
 
