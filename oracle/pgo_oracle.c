@@ -1285,6 +1285,19 @@ int orc_solve(void *h, const double *poses, double lambda, double *delta) {
   return rc;
 }
 
+int orc_supernodes(void *h, int *m, int *w, int *parent) {
+  orc *o = (orc *)h;
+  chol_sym *S = o->S;
+  if (m)
+    for (int s = 0; s < S->ns; s++) {
+      int wp = S->sfirst[s + 1] - S->sfirst[s];
+      m[s] = 3 * (wp + S->rptr[s + 1] - S->rptr[s]);
+      w[s] = 3 * wp;
+      parent[s] = S->sparent[s];
+    }
+  return S->ns;
+}
+
 double orc_error(void *h, const double *poses) {
   orc *o = (orc *)h;
   size_t Nn = o->n > 0 ? o->n : 1;

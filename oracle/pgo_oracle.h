@@ -81,6 +81,9 @@ int orc_linearize(void *h, const double *poses, double *hdiag, double *hoff, dou
 /* Solve (H + lambda I) delta = -g at poses with the sparse Cholesky. */
 int orc_solve(void *h, const double *poses, double lambda, double *delta);
 
+/* Supernode front sizes (scalar rows m, columns w) and supernodal parents; returns count. */
+int orc_supernodes(void *h, int *m, int *w, int *parent);
+
 /* 0.5 sum e^T Omega e at poses. */
 double orc_error(void *h, const double *poses);
 
