@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_MFMA_PEAK_TFS = 78.6  # MI355X datasheet: FP64 matrix (and vector) 78.6 TFLOP/s dense
 
 
 def spmv_bytes(n, slots):
@@ -73,6 +74,9 @@ def main():
     ap.add_argument("--profile-every", type=int, default=16)
     ap.add_argument("--cpu-outer", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--solver", choices=["cholesky", "pcg"], default="cholesky")
+    ap.add_argument("--no-graphs", action="store_true",
+                    help="eager launches instead of the captured factor+solve hipGraph (rocprofv3 runs)")
     ap.add_argument("--max-outer", type=int, default=0,
                     help="profiling runs only: stop each optimize after this many linearisations")
     args = ap.parse_args()
@@ -86,7 +90,9 @@ def main():
     g = datasets.make(args.config)
     pg = PoseGraph.from_dataset(g, device=r.local_rank)
     pg.save_values()                     # upload graph + values once; snapshot the initial values
-    params = default_params(profile_every=args.profile_every, max_outer=args.max_outer)
+    params = default_params(profile_every=args.profile_every, max_outer=args.max_outer,
+                            linear_solver=1 if args.solver == "cholesky" else 0,
+                            use_graphs=0 if args.no_graphs else 1)
 
     def step():
         pg.restore_values()
@@ -98,7 +104,9 @@ def main():
     last = stats[-1]
     totals = dict(spmv_ms=sum(s["kernel_spmv_ms"] for s in stats), spmv_n=sum(s["kernel_spmv_count"] for s in stats),
                   lin_ms=sum(s["kernel_linearize_ms"] for s in stats),
-                  lin_n=sum(s["kernel_linearize_count"] for s in stats))
+                  lin_n=sum(s["kernel_linearize_count"] for s in stats),
+                  syrk_ms=sum(s["kernel_syrk_ms"] for s in stats),
+                  syrk_n=sum(s["kernel_syrk_count"] for s in stats))
 
     if rank == 0:
         n, ne = g.num_poses, g.num_edges
@@ -106,11 +114,30 @@ def main():
         spmv_avg_ms = totals["spmv_ms"] / max(totals["spmv_n"], 1)
         achieved = spmv_bytes(n, slots) / (spmv_avg_ms * 1e-3) / 1e9 if totals["spmv_n"] else None
         lin_avg_ms = totals["lin_ms"] / max(totals["lin_n"], 1)
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                traffic = json.load(f).get(args.config, {}).get("k_pcg_spmv_bytes_per_launch")
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        pmc = json.load(open(pmc_path)).get(args.config, {}) if os.path.exists(pmc_path) else {}
+        if args.solver == "pcg":
+            roofline = {
+                "kernel": "k_pcg_spmv", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS if achieved else None,
+                "traffic": pmc.get("k_pcg_spmv_bytes_per_launch"),
+                "bytes_per_launch": spmv_bytes(n, slots), "avg_launch_ms": spmv_avg_ms,
+                "timed_launches": totals["spmv_n"],
+            }
+        else:
+            # Schur updates of one factorisation, all k_panel_syrk launches of the
+            # profiled factorisations timed by dispatch events
+            syrk_tfs = (last["syrk_flops"] * totals["syrk_n"] / (totals["syrk_ms"] * 1e-3) / 1e12
+                        if totals["syrk_n"] and totals["syrk_ms"] > 0 else None)
+            roofline = {
+                "kernel": "k_panel_syrk", "bound": "mfma", "achieved": syrk_tfs, "peak": FP64_MFMA_PEAK_TFS,
+                "unit": "TFLOP/s", "frac": syrk_tfs / FP64_MFMA_PEAK_TFS if syrk_tfs else None,
+                "traffic": pmc.get("k_panel_syrk_bytes_per_factorization"),
+                "flops_per_factorization": last["syrk_flops"],
+                "ms_per_factorization": totals["syrk_ms"] / totals["syrk_n"] if totals["syrk_n"] else None,
+                "profiled_factorizations": totals["syrk_n"],
+                "factor_flops": last["factor_flops"],
+            }
         out = {
             "metric": "GN iterations/sec + ms-to-chi2 convergence, 100k-pose Manhattan graph",
             "value": lin_total / elapsed,
@@ -129,7 +156,9 @@ def main():
                 "workload": f"{args.config}: {n} poses / {ne} between factors + 1 prior, Manhattan walk "
                             f"(seed {g.meta.get('seed')}), GTSAM-default LM from dead-reckoned values",
                 "poses": n, "edges": ne, "parallelism": f"replicas{world}",
-                "solver": "block-Jacobi PCG, rel tol %.0e" % params.pcg_relative_tol,
+                "solver": ("GPU supernodal multifrontal Cholesky (AMD ordering, fp64 MFMA Schur updates)"
+                           if args.solver == "cholesky" else
+                           "block-Jacobi PCG, rel tol %.0e" % params.pcg_relative_tol),
             },
             "per_step": {
                 "linearizations": last["linearizations"], "lm_tries": last["inner_iterations"],
@@ -137,18 +166,7 @@ def main():
                 "initial_error": last["initial_error"], "final_error": last["final_error"],
                 "ms_linearize": last["ms_linearize"], "ms_solve": last["ms_solve"], "ms_update": last["ms_update"],
             },
-            "roofline": {
-                "kernel": "k_pcg_spmv",
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS if achieved else None,
-                "traffic": traffic,
-                "bytes_per_launch": spmv_bytes(n, slots),
-                "avg_launch_ms": spmv_avg_ms,
-                "timed_launches": totals["spmv_n"],
-            },
+            "roofline": roofline,
             "linearize_kernel": {
                 "kernel": "k_linearize",
                 "avg_launch_ms": lin_avg_ms,

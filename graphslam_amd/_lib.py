@@ -28,6 +28,8 @@ PGO_E_BAD_EDGE = -10
 PGO_W_MAXITER = 1
 PGO_ALG_LM = 0
 PGO_ALG_GN = 1
+PGO_SOLVER_PCG = 0
+PGO_SOLVER_CHOLESKY = 1
 
 
 class PgoOpts(C.Structure):
@@ -42,7 +44,7 @@ class PgoParams(C.Structure):
                 ("min_model_fidelity", C.c_double), ("use_fixed_lambda_factor", C.c_int),
                 ("algorithm", C.c_int), ("linear_solver", C.c_int), ("pcg_relative_tol", C.c_double),
                 ("pcg_max_iterations", C.c_int), ("pcg_check_interval", C.c_int), ("max_outer", C.c_int),
-                ("profile_every", C.c_int)]
+                ("profile_every", C.c_int), ("use_graphs", C.c_int)]
 
 
 class PgoStats(C.Structure):
@@ -52,7 +54,8 @@ class PgoStats(C.Structure):
                 ("ms_linearize", C.c_double), ("ms_solve", C.c_double), ("ms_update", C.c_double),
                 ("kernel_spmv_ms", C.c_double), ("kernel_spmv_count", C.c_longlong),
                 ("kernel_linearize_ms", C.c_double), ("kernel_linearize_count", C.c_longlong),
-                ("reserved", C.c_double * 4)]
+                ("kernel_syrk_ms", C.c_double), ("kernel_syrk_count", C.c_longlong),
+                ("syrk_flops", C.c_double), ("factor_flops", C.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
@@ -105,6 +108,7 @@ def lib():
         "pgo_debug_linearize": (C.c_int, [vp, dp, dp, dp, dp]),
         "pgo_debug_spmv": (C.c_int, [vp, C.c_double, dp, dp]),
         "pgo_debug_solve": (C.c_int, [vp, C.c_double, C.POINTER(PgoParams), dp, C.POINTER(C.c_int)]),
+        "pgo_debug_plan": (C.c_int, [vp, dp, C.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "pgo.h"
+#include "pgo_chol.h"
 #include "pgo_device.h"
 
 using pgo::DevGraph;
@@ -44,10 +45,19 @@ struct pgo_graph {
   bool gauge_free = false;                  // some connected component has no prior
   double* h_scal = nullptr;                 // pinned
   int* h_ctrl = nullptr;                    // pinned
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[6] = {};
   static constexpr int kProfPairs = 64;     // sampled SpMV timings per read-back
   hipEvent_t pev[2 * kProfPairs] = {};
   int pk_iter[kProfPairs] = {};
+  // ---- supernodal Cholesky (built on first use; structure-dependent) ----
+  std::vector<int> h_row_ptr, h_slot_col;   // block-CSR pattern (old indices)
+  pgo::CholPlan chol;
+  bool chol_ready = false;
+  std::vector<hipEvent_t> sev;              // syrk profiling event pairs
+  std::vector<double> sev_flops;
+  long long factorizations = 0;
+  hipGraphExec_t chol_exec = nullptr;       // captured factor + solve (static per structure)
+  double* h_lam = nullptr;                  // pinned lambda staging
 };
 
 namespace {
@@ -112,6 +122,10 @@ void free_device(pgo_graph* g) {
   d.stream = s;
   g->dev_structure = false;
   g->dev_values = false;
+  if (g->chol_exec) (void)hipGraphExecDestroy(g->chol_exec);
+  g->chol_exec = nullptr;
+  if (g->chol_ready) pgo::chol_free(g->chol);
+  g->chol_ready = false;
 }
 
 int ensure_hip(pgo_graph* g) {
@@ -124,8 +138,12 @@ int ensure_hip(pgo_graph* g) {
   HIP_TRY(g, hipStreamCreateWithFlags(&g->d.stream, hipStreamNonBlocking));
   HIP_TRY(g, hipHostMalloc((void**)&g->h_scal, 16 * sizeof(double), hipHostMallocDefault));
   HIP_TRY(g, hipHostMalloc((void**)&g->h_ctrl, 4 * sizeof(int), hipHostMallocDefault));
+  HIP_TRY(g, hipHostMalloc((void**)&g->h_lam, sizeof(double), hipHostMallocDefault));
   for (auto& e : g->ev) HIP_TRY(g, hipEventCreate(&e));
   for (auto& e : g->pev) HIP_TRY(g, hipEventCreate(&e));
+  g->sev.resize(2 * 512);
+  g->sev_flops.resize(512);
+  for (auto& e : g->sev) HIP_TRY(g, hipEventCreate(&e));
   g->hip_ready = true;
   return PGO_OK;
 }
@@ -183,9 +201,15 @@ int download_values(pgo_graph* g) {
 
 // Build the device graph: resolve keys (GTSAM raises ValuesKeyDoesNotExist at
 // optimize time for a factor on an unknown key), block-CSR slots, priors.
-int upload_structure(pgo_graph* g) {
-  RC_TRY(ensure_hip(g));
-  RC_TRY(download_values(g));
+// Host-side structure of the graph (no HIP): resolved factor endpoints,
+// block-CSR slots, priors by vertex, gauge freedom.
+struct HostStructure {
+  std::vector<int2> eij;
+  std::vector<int> pv, row_ptr, slot_edge, slot_col, prior_ptr, porder;
+  bool gauge_free = false;
+};
+
+int build_structure(pgo_graph* g, HostStructure& H) {
   const int n = (int)g->keys.size();
   const int ne = (int)g->ek1.size();
   const int np = (int)g->pk.size();
@@ -257,9 +281,6 @@ int upload_structure(pgo_graph* g) {
     for (int i = 0; i < n; i++)
       if (!anchored[find(i)]) g->gauge_free = true;
   }
-  g->edge_slot0.assign(ne, -1);
-  for (int k = 0; k < ns; k++)
-    if ((slot_edge[k] & 1) == 0) g->edge_slot0[slot_edge[k] >> 1] = k;
   // priors CSR by vertex
   std::vector<int> prior_ptr(n + 1, 0);
   for (int q = 0; q < np; q++) prior_ptr[pv[q] + 1]++;
@@ -269,6 +290,38 @@ int upload_structure(pgo_graph* g) {
     std::vector<int> f(prior_ptr.begin(), prior_ptr.end() - 1);
     for (int q = 0; q < np; q++) porder[f[pv[q]]++] = q;
   }
+  H.gauge_free = g->gauge_free;
+  H.eij = std::move(eij);
+  H.pv = std::move(pv);
+  H.row_ptr = std::move(row_ptr);
+  H.slot_edge = std::move(slot_edge);
+  H.slot_col = std::move(slot_col);
+  H.prior_ptr = std::move(prior_ptr);
+  H.porder = std::move(porder);
+  return PGO_OK;
+}
+
+int upload_structure(pgo_graph* g) {
+  RC_TRY(ensure_hip(g));
+  RC_TRY(download_values(g));
+  HostStructure H;
+  RC_TRY(build_structure(g, H));
+  const int n = (int)g->keys.size();
+  const int ne = (int)g->ek1.size();
+  const int np = (int)g->pk.size();
+  const int ns = 2 * ne;
+  const auto& eij = H.eij;
+  const auto& pv = H.pv;
+  const auto& row_ptr = H.row_ptr;
+  const auto& slot_edge = H.slot_edge;
+  const auto& slot_col = H.slot_col;
+  const auto& prior_ptr = H.prior_ptr;
+  const auto& porder = H.porder;
+  g->h_row_ptr = row_ptr;
+  g->h_slot_col = slot_col;
+  g->edge_slot0.assign(ne, -1);
+  for (int k = 0; k < ns; k++)
+    if ((slot_edge[k] & 1) == 0) g->edge_slot0[slot_edge[k] >> 1] = k;
   std::vector<double4> hz(ne), hpz(np);
   std::vector<double2> hom(3 * (size_t)ne), hpom(3 * (size_t)np);
   for (int e = 0; e < ne; e++) {
@@ -366,6 +419,19 @@ struct PcgResult {
 
 double ms_between(hipEvent_t a, hipEvent_t b);
 
+int ensure_chol(pgo_graph* g) {
+  if (g->chol_ready) return PGO_OK;
+  pgo::chol_analyze(g->chol, g->d.n, g->h_row_ptr, g->h_slot_col);
+  const hipError_t e = pgo::chol_upload(g->chol, g->d.stream);
+  if (e != hipSuccess) {
+    pgo::chol_free(g->chol);
+    return fail(g, e == hipErrorOutOfMemory ? PGO_E_NOMEM : PGO_E_HIP,
+                std::string("Cholesky plan upload: ") + hipGetErrorString(e));
+  }
+  g->chol_ready = true;
+  return PGO_OK;
+}
+
 // PCG solve of (H + lambda I) x = -g at the current linearisation.  With
 // profile_every = k > 0, every k-th SpMV launch is bracketed by HIP events on
 // the handle's stream; launches that ran after convergence (early-exit no-ops)
@@ -402,6 +468,77 @@ int pcg_solve(pgo_graph* g, const pgo_params& p, double lam, PcgResult* out, pgo
   }
   out->flag = g->h_ctrl[0];
   out->iterations = g->h_ctrl[1];
+  return PGO_OK;
+}
+
+// (H + lambda I) x = -g.  PCG runs to completion here (its convergence reads
+// sync); the Cholesky path is only enqueued and its pivot flag is read back with
+// the next scalars (*known = false).
+struct SolveState {
+  bool known = true, solved = true;
+  bool profiled = false;
+  pgo::SyrkProfile prof;
+};
+
+int linear_solve(pgo_graph* g, const pgo_params& p, double lam, pgo_stats* st, SolveState* ss) {
+  if (p.linear_solver == PGO_SOLVER_PCG) {
+    PcgResult pr;
+    RC_TRY(pcg_solve(g, p, lam, &pr, st));
+    if (st) st->pcg_iterations += pr.iterations;
+    ss->known = true;
+    ss->solved = pr.flag != pgo::kBreakdown;
+    return PGO_OK;
+  }
+  RC_TRY(ensure_chol(g));
+  const DevGraph& d = g->d;
+  ss->profiled = st && p.profile_every > 0 && (g->factorizations % p.profile_every) == 0;
+  g->factorizations++;
+  pgo::SyrkProfile* prof = nullptr;
+  if (ss->profiled) {
+    ss->prof.ev = g->sev.data();
+    ss->prof.cap = (int)g->sev_flops.size();
+    ss->prof.used = 0;
+    ss->prof.flops = g->sev_flops.data();
+    prof = &ss->prof;
+  }
+  *g->h_lam = lam;
+  HIP_TRY(g, hipMemcpyAsync(g->chol.d_lambda, g->h_lam, sizeof(double), hipMemcpyHostToDevice, d.stream));
+  if (prof || !p.use_graphs) {  // eager: profiled factorisations time their Schur-update launches
+    HIP_TRY(g, pgo::chol_factor(g->chol, d.D, d.V, d.stream, prof));
+    HIP_TRY(g, pgo::chol_solve(g->chol, d.g, d.x, -1.0, d.stream));
+  } else {
+    if (!g->chol_exec) {  // capture once per structure: ~1e3 launches -> one graph launch
+      hipGraph_t graph = nullptr;
+      HIP_TRY(g, hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal));
+      const hipError_t e1 = pgo::chol_factor(g->chol, d.D, d.V, d.stream, nullptr);
+      const hipError_t e2 = pgo::chol_solve(g->chol, d.g, d.x, -1.0, d.stream);
+      HIP_TRY(g, hipStreamEndCapture(d.stream, &graph));
+      HIP_TRY(g, e1);
+      HIP_TRY(g, e2);
+      HIP_TRY(g, hipGraphInstantiate(&g->chol_exec, graph, nullptr, nullptr, 0));
+      HIP_TRY(g, hipGraphDestroy(graph));
+    }
+    HIP_TRY(g, hipGraphLaunch(g->chol_exec, d.stream));
+  }
+  ss->known = false;
+  return PGO_OK;
+}
+
+// after the stream has drained: pivot flag and profile of an enqueued Cholesky solve
+int finish_solve(pgo_graph* g, pgo_stats* st, SolveState* ss) {
+  if (ss->known) return PGO_OK;
+  int flag = 0;
+  HIP_TRY(g, hipMemcpy(&flag, g->chol.d_flag, sizeof(int), hipMemcpyDeviceToHost));
+  ss->solved = flag == 0;
+  ss->known = true;
+  if (st) st->factor_flops = g->chol.flops;
+  if (ss->profiled && st) {
+    double ms = 0.0;
+    for (int u = 0; u < ss->prof.used; u++) ms += ms_between(ss->prof.ev[2 * u], ss->prof.ev[2 * u + 1]);
+    st->kernel_syrk_ms += ms;
+    st->kernel_syrk_count++;
+    st->syrk_flops = g->chol.syrk_flops;
+  }
   return PGO_OK;
 }
 
@@ -457,12 +594,13 @@ void pgo_default_params(pgo_params* p) {
   p->min_model_fidelity = 1e-3;
   p->use_fixed_lambda_factor = 1;
   p->algorithm = PGO_ALG_LM;
-  p->linear_solver = PGO_SOLVER_PCG;
+  p->linear_solver = PGO_SOLVER_CHOLESKY;
   p->pcg_relative_tol = 1e-10;
   p->pcg_max_iterations = 20000;
   p->pcg_check_interval = 32;
   p->max_outer = 0;
   p->profile_every = 0;
+  p->use_graphs = 1;
 }
 
 pgo_graph* pgo_create(const pgo_opts* opts) {
@@ -482,6 +620,7 @@ void pgo_destroy(pgo_graph* g) {
       if (e) (void)hipEventDestroy(e);
     if (g->h_scal) (void)hipHostFree(g->h_scal);
     if (g->h_ctrl) (void)hipHostFree(g->h_ctrl);
+    if (g->h_lam) (void)hipHostFree(g->h_lam);
     for (auto& e : g->pev)
       if (e) (void)hipEventDestroy(e);
     if (g->d.stream) (void)hipStreamDestroy(g->d.stream);
@@ -667,10 +806,21 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
       bool first_try = true;
       for (;;) {  // tryLambda (GN: one plain step)
         const double lam_try = p.algorithm == PGO_ALG_GN ? 0.0 : lam;
-        PcgResult pr;
-        RC_TRY(pcg_solve(g, p, lam_try, &pr, &st));
+        SolveState ss;
         HIP_TRY(g, hipEventRecord(ev[2], d.stream));
-        HIP_TRY(g, hipEventSynchronize(ev[2]));
+        RC_TRY(linear_solve(g, p, lam_try, &st, &ss));
+        HIP_TRY(g, hipEventRecord(ev[3], d.stream));
+        const bool run_update = !ss.known || ss.solved;
+        if (run_update) {
+          // linear model decrease = -(g'delta + 0.5 delta'H delta) (LM only), retract,
+          // new error: one read-back for every scalar of this try
+          if (p.algorithm != PGO_ALG_GN) HIP_TRY(g, pgo::launch_model_decrease(d, d.x, d.scal + 1));
+          HIP_TRY(g, pgo::launch_retract(d, d.x));
+          HIP_TRY(g, pgo::launch_error(d, d.pose_cand, d.scal));
+        }
+        HIP_TRY(g, hipEventRecord(ev[4], d.stream));
+        RC_TRY(sync_scalars(g, 3));
+        RC_TRY(finish_solve(g, &st, &ss));
         if (first_try) {
           const double lin_ms = ms_between(ev[0], ev[1]);
           st.ms_linearize += lin_ms;
@@ -678,23 +828,16 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
             st.kernel_linearize_ms += lin_ms;
             st.kernel_linearize_count++;
           }
-          st.ms_solve += ms_between(ev[1], ev[2]);
           first_try = false;
-        } else {
-          st.ms_solve += ms_between(ev[3], ev[2]);
         }
-        st.pcg_iterations += pr.iterations;
-        const bool solved = pr.flag != pgo::kBreakdown;
+        st.ms_solve += ms_between(ev[2], ev[3]);
+        st.ms_update += ms_between(ev[3], ev[4]);
+        const bool solved = ss.solved;
         if (p.algorithm == PGO_ALG_GN) {
           if (!solved) {
             status = PGO_E_INDETERMINANT;
             break;
           }
-          HIP_TRY(g, pgo::launch_retract(d, d.x));
-          HIP_TRY(g, pgo::launch_error(d, d.pose_cand, d.scal));
-          HIP_TRY(g, hipEventRecord(ev[3], d.stream));
-          RC_TRY(sync_scalars(g, 1));
-          st.ms_update += ms_between(ev[2], ev[3]);
           std::swap(d.pose, d.pose_cand);
           err = g->h_scal[0];
           iters++;
@@ -704,14 +847,6 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
         double fidelity = 0.0, new_e = INFINITY;
         bool success = false, stop = false;
         if (solved) {
-          // linear model decrease = -(g'delta + 0.5 delta'H delta), retract, new error:
-          // one read-back for all three scalars
-          HIP_TRY(g, pgo::launch_model_decrease(d, d.x, d.scal + 1));
-          HIP_TRY(g, pgo::launch_retract(d, d.x));
-          HIP_TRY(g, pgo::launch_error(d, d.pose_cand, d.scal));
-          HIP_TRY(g, hipEventRecord(ev[3], d.stream));
-          RC_TRY(sync_scalars(g, 3));
-          st.ms_update += ms_between(ev[2], ev[3]);
           const double xhx = g->h_scal[1], gx = g->h_scal[2];
           const double lin_change = -(gx + 0.5 * xhx);
           if (lin_change >= 0) {
@@ -723,8 +858,6 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
             }
             if (std::fabs(cost_change) < p.relative_error_tol * err) stop = true;
           }
-        } else {
-          HIP_TRY(g, hipEventRecord(ev[3], d.stream));
         }
         if (success) {  // decreaseLambda
           if (p.use_fixed_lambda_factor) {
@@ -766,6 +899,54 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   if (stats) *stats = st;
   if (status < 0) return fail(g, status, pgo_status_string(status));
   return status;
+}
+
+int pgo_debug_plan(pgo_graph* g, double* out, int cap) {
+  if (!g || !out || cap < 16) return PGO_E_ARG;
+  RC_TRY(download_values(g));
+  HostStructure H;
+  RC_TRY(build_structure(g, H));
+  pgo::CholPlan P;
+  pgo::chol_analyze(P, (int)g->keys.size(), H.row_ptr, H.slot_col);
+  long long lf = 2, ls = 2, trsm = 0, syrk = 0;   // launches: memsets/assembly, perm in/out
+  int maxm = 0;
+  for (int s = 0; s < P.ns; s++) maxm = std::max(maxm, P.m[s]);
+  for (const auto& lv : P.levels) {
+    lf += (long long)lv.ea_off.size() + lv.small.size() + 3 * lv.panels.size();
+    ls += 2 + (long long)lv.fwd.size() + (long long)lv.bwd.size() - 1;
+    for (const auto& ps : lv.panels) {
+      trsm += ps.trsm_cnt;
+      syrk += ps.syrk_cnt;
+    }
+  }
+  for (int i = 0; i < cap; i++) out[i] = 0.0;
+  out[0] = P.ns;
+  out[1] = (double)P.levels.size();
+  out[2] = P.nnzl;
+  out[3] = P.flops;
+  out[4] = P.syrk_flops;
+  out[5] = (double)P.ftotal;
+  out[6] = (double)lf;
+  out[7] = (double)ls;
+  out[8] = maxm;
+  out[9] = (double)trsm;
+  out[10] = (double)syrk;
+  out[11] = (double)P.small_list.size();
+  int o = 16;
+  for (const auto& lv : P.levels) {   // per level: fronts, max m, max blocks, panels, small fronts, syrk tiles
+    if (o + 6 > cap) break;
+    long long tiles = 0;
+    int small = 0;
+    for (const auto& ps : lv.panels) tiles += ps.syrk_cnt;
+    for (const auto& sc : lv.small) small += sc.cnt;
+    out[o++] = lv.front_cnt;
+    out[o++] = lv.maxm;
+    out[o++] = lv.maxblk;
+    out[o++] = (double)lv.panels.size();
+    out[o++] = small;
+    out[o++] = (double)tiles;
+  }
+  return PGO_OK;
 }
 
 int pgo_debug_linearize(pgo_graph* g, double* hdiag, double* hoff, double* grad, double* err) {
@@ -816,12 +997,16 @@ int pgo_debug_solve(pgo_graph* g, double lambda, const pgo_params* params, doubl
   RC_TRY(ensure_device(g));
   DevGraph& d = g->d;
   HIP_TRY(g, pgo::launch_linearize(d));
-  PcgResult pr;
-  RC_TRY(pcg_solve(g, p, lambda, &pr, nullptr));
+  pgo_stats st;
+  std::memset(&st, 0, sizeof(st));
+  SolveState ss;
+  RC_TRY(linear_solve(g, p, lambda, &st, &ss));
+  HIP_TRY(g, hipStreamSynchronize(d.stream));
+  RC_TRY(finish_solve(g, nullptr, &ss));
   if (d.n) HIP_TRY(g, hipMemcpyAsync(delta, d.x, 3 * (size_t)d.n * 8, hipMemcpyDeviceToHost, d.stream));
   HIP_TRY(g, hipStreamSynchronize(d.stream));
-  if (pcg_iterations) *pcg_iterations = pr.iterations;
-  if (pr.flag == pgo::kBreakdown) return fail(g, PGO_E_INDETERMINANT, "PCG breakdown");
+  if (pcg_iterations) *pcg_iterations = (int)st.pcg_iterations;
+  if (!ss.solved) return fail(g, PGO_E_INDETERMINANT, "linear system not positive definite");
   return PGO_OK;
 }
 

@@ -1,0 +1,120 @@
+// Supernodal multifrontal Cholesky of H + lambda I on the GPU (internal).
+//
+// Replaces GTSAM's per-solve COLAMD ordering + multifrontal Cholesky
+// (GaussianFactorGraph::optimize inside LevenbergMarquardtOptimizer, graph.cpp:119)
+// with: a symbolic analysis done once per graph structure on the host
+// (approximate-minimum-degree ordering of the pose graph, elimination tree,
+// relaxed supernodes, front row structures, level schedule, task lists), and a
+// numeric factorisation + triangular solves on the device, level by level
+// (leaves first), every front of a level in flight at once.
+//
+// Fronts: supernode s has w_s = 3 * (its poses) pivot columns and
+// m_s = w_s + 3 * (its below-diagonal pose rows) rows; its m_s x m_s frontal
+// matrix lives column-major at F + foff[s] for the whole factorisation, so the
+// L panel (first w_s columns) stays in place for the solves and the update
+// matrix (trailing block) stays in place until the parent pulls it.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace pgo {
+
+constexpr int kSmallFront = 128;   // m <= this: whole front factorised in LDS by one workgroup
+constexpr int kNB = 64;            // panel width of the blocked path
+constexpr int kTile = 64;          // Schur-update output tile
+
+struct PanelStep {                 // one panel of the blocked path, all big fronts of a level
+  int kb;
+  int potrf_off, potrf_cnt;        // fronts whose diagonal tile is factored (potrf_list)
+  int trsm_off, trsm_cnt;          // tasks (front, row chunk) in trsm_tasks
+  int syrk_off, syrk_cnt;          // tasks (front, tile) in syrk_tasks
+  double syrk_flops;               // algorithmic flops of this step's Schur updates (lower triangles)
+};
+
+struct SolveStep {                 // one launch of the blocked triangular solves
+  int off, cnt;                    // int4 tasks (front, begin, end, owner-block or -1)
+};
+
+struct SmallClass {                // small fronts of one level with m <= mmax
+  int off, cnt, mmax;
+};
+
+struct CholLevel {
+  std::vector<SmallClass> small;   // fronts in small_list, by size class
+  std::vector<PanelStep> panels;   // blocked path
+  std::vector<int> ea_off, ea_cnt; // per child rank: children in ea_children (their parents are in this level)
+  std::vector<int> ea_cols_off;    // per child rank: offset into ea_colpref
+  int front_off, front_cnt;        // all fronts of the level in level_fronts (solves)
+  int small_maxm = 0, maxm = 0;    // LDS sizing
+  int maxblk = 0;                  // max 64-column blocks of a front's pivot columns
+  std::vector<SolveStep> fwd;      // forward step b = 0 .. maxblk-1 (rows below block b)
+  std::vector<SolveStep> bwd;      // backward: [0] = init (all columns), then steps b = maxblk-1 .. 1
+};
+
+struct CholPlan {
+  // ---- host symbolic result ----
+  int n = 0, ns = 0;
+  std::vector<int> perm, iperm;    // pose level: new -> old, old -> new
+  std::vector<int> sfirst;         // [ns+1] first pose (new index) of each supernode
+  std::vector<int> m, w;           // scalar front rows / pivot columns
+  std::vector<long long> foff;     // [ns+1] front offsets (doubles)
+  std::vector<int> voff;           // [ns+1] frontal-vector offsets (doubles)
+  std::vector<int> rptr, rows;     // front row poses (new index): own poses, then below rows
+  std::vector<int> parent, height;
+  std::vector<int> cptr, children; // children of each supernode, increasing order
+  std::vector<int> ea_rel;         // per supernode: local pose index in the parent of each below row
+  std::vector<int> ea_ptr;         // [ns+1] into ea_rel
+  // assembly of H: target blocks (front, local row pose, local col pose) and their slots
+  std::vector<int> asm_front, asm_li, asm_lj, asm_ptr, asm_src;
+  std::vector<int> dg_front, dg_loc;   // per new pose: front and local index (diagonal block)
+  // schedules
+  std::vector<CholLevel> levels;
+  std::vector<int> small_list, level_fronts, potrf_list;
+  std::vector<int2> trsm_tasks, syrk_tasks;
+  std::vector<int4> fwd_tasks, bwd_tasks;
+  std::vector<int> ea_children;    // child front ids grouped per (level, rank)
+  std::vector<long long> ea_colpref; // per group: prefix of update-matrix columns (3*below rows)
+  double flops = 0, nnzl = 0, syrk_flops = 0;
+  long long ftotal = 0;
+  int vtotal = 0;
+
+  // ---- device copies ----
+  double* F = nullptr;             // fronts
+  double* fv = nullptr;            // frontal vectors (solve)
+  double* xv = nullptr;            // permuted rhs / solution, 3n
+  int *d_m = nullptr, *d_w = nullptr, *d_voff = nullptr, *d_rptr = nullptr, *d_rows = nullptr;
+  long long* d_foff = nullptr;
+  int *d_cptr = nullptr, *d_children = nullptr, *d_ea_rel = nullptr, *d_ea_ptr = nullptr, *d_parent = nullptr;
+  int *d_asm_front = nullptr, *d_asm_li = nullptr, *d_asm_lj = nullptr, *d_asm_ptr = nullptr, *d_asm_src = nullptr;
+  int *d_dg_front = nullptr, *d_dg_loc = nullptr, *d_perm = nullptr;
+  int *d_small = nullptr, *d_level_fronts = nullptr, *d_potrf = nullptr;
+  int2 *d_trsm = nullptr, *d_syrk = nullptr;
+  int4 *d_fwd = nullptr, *d_bwd = nullptr;
+  int* d_ea_children = nullptr;
+  long long* d_ea_colpref = nullptr;
+  int* d_flag = nullptr;           // non-positive pivot seen
+  double* d_lambda = nullptr;      // damping read by the assembly (graph-replay friendly)
+};
+
+// host: symbolic analysis from the block-CSR pattern (old pose indices)
+void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
+hipError_t chol_upload(CholPlan& P, hipStream_t s);
+void chol_free(CholPlan& P);
+
+// device: factor H + lambda I (D: 6 doubles/pose upper, V: slot blocks, old indexing)
+// prof (optional): timing of the Schur-update launches with dispatch events;
+// pairs of events, capacity cap; *used pairs recorded, flops[i] per pair.
+struct SyrkProfile {
+  hipEvent_t* ev = nullptr;
+  int cap = 0, used = 0;
+  double* flops = nullptr;
+};
+// lambda is read from P.d_lambda (set it with a stream-ordered copy first)
+hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, hipStream_t s,
+                       SyrkProfile* prof = nullptr);
+// x = (L L^T)^{-1} b, b and x indexed by old pose (3 per pose); may alias
+hipError_t chol_solve(const CholPlan& P, const double* b, double* x, double scale_b, hipStream_t s);
+
+}  // namespace pgo

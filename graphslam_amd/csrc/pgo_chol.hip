@@ -1,0 +1,627 @@
+// GPU supernodal multifrontal Cholesky of H + lambda I and its triangular
+// solves (gfx950).  Host plan: pgo_symbolic.cpp; layout: pgo_chol.h.
+//
+// Factorisation, per level of the supernodal tree (leaves first):
+//   k_extend_add   children's update matrices -> parent fronts, one launch per
+//                  child rank (each parent receives from one child per launch:
+//                  no atomics, fixed order, bitwise reproducible)
+//   k_front_small  fronts with m <= 128: whole front in LDS, one workgroup each
+//   k_panel_trsm   blocked path, per 64-column panel: the diagonal tile is
+//                  factored in LDS (redundantly by every workgroup of the front)
+//                  and the rows below are solved against it
+//   k_panel_syrk   Schur update of the trailing matrix, 64x64 output tiles on
+//                  v_mfma_f64_16x16x4_f64 (4 waves x 2x2 MFMA tiles), panels
+//                  staged in LDS
+// Solves: multifrontal forward (frontal vectors pulled from children in fixed
+// order) bottom-up, then backward top-down, one workgroup per front.
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "pgo_chol.h"
+
+namespace pgo {
+
+struct CholDev {
+  double* F;
+  double* fv;
+  double* xv;
+  const int *m, *w, *voff, *rptr, *rows;
+  const long long* foff;
+  const int *cptr, *children, *ea_rel, *ea_ptr, *parent;
+  const int *asm_front, *asm_li, *asm_lj, *asm_ptr, *asm_src;
+  const int *dg_front, *dg_loc, *perm;
+  int* flag;
+};
+
+static CholDev dev_view(const CholPlan& P) {
+  CholDev c;
+  c.F = P.F; c.fv = P.fv; c.xv = P.xv;
+  c.m = P.d_m; c.w = P.d_w; c.voff = P.d_voff; c.rptr = P.d_rptr; c.rows = P.d_rows; c.foff = P.d_foff;
+  c.cptr = P.d_cptr; c.children = P.d_children; c.ea_rel = P.d_ea_rel; c.ea_ptr = P.d_ea_ptr;
+  c.parent = P.d_parent;
+  c.asm_front = P.d_asm_front; c.asm_li = P.d_asm_li; c.asm_lj = P.d_asm_lj; c.asm_ptr = P.d_asm_ptr;
+  c.asm_src = P.d_asm_src; c.dg_front = P.d_dg_front; c.dg_loc = P.d_dg_loc; c.perm = P.d_perm;
+  c.flag = P.d_flag;
+  return c;
+}
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------ assembly
+// off-diagonal lower blocks H_{i,j} (i > j) of a front: sum of their slots
+__global__ __launch_bounds__(256) void k_asm_offdiag(CholDev c, const double* __restrict__ V, int ntargets) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= ntargets) return;
+  const int s = c.asm_front[t];
+  const int m = c.m[s];
+  double* Fs = c.F + c.foff[s];
+  double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int q = c.asm_ptr[t]; q < c.asm_ptr[t + 1]; q++) {
+    const double* v = V + 9 * (size_t)c.asm_src[q];
+#pragma unroll
+    for (int e = 0; e < 9; e++) acc[e] += v[e];
+  }
+  const int r0 = 3 * c.asm_li[t], c0 = 3 * c.asm_lj[t];
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int b = 0; b < 3; b++) Fs[(r0 + a) + (size_t)(c0 + b) * m] = acc[3 * a + b];
+}
+
+// diagonal blocks H_jj + lambda I (lower part)
+__global__ __launch_bounds__(256) void k_asm_diag(CholDev c, const double* __restrict__ D,
+                                                 const double* __restrict__ lam_p, int n) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const double lam = *lam_p;
+  const int s = c.dg_front[j];
+  const int m = c.m[s];
+  double* Fs = c.F + c.foff[s];
+  const double* d = D + 6 * (size_t)c.perm[j];
+  const int o = 3 * c.dg_loc[j];
+  Fs[(o + 0) + (size_t)(o + 0) * m] = d[0] + lam;
+  Fs[(o + 1) + (size_t)(o + 0) * m] = d[1];
+  Fs[(o + 2) + (size_t)(o + 0) * m] = d[2];
+  Fs[(o + 1) + (size_t)(o + 1) * m] = d[3] + lam;
+  Fs[(o + 2) + (size_t)(o + 1) * m] = d[4];
+  Fs[(o + 2) + (size_t)(o + 2) * m] = d[5] + lam;
+}
+
+// ------------------------------------------------------------ extend-add
+// One wave per update-matrix column of one child; lanes walk the column's
+// lower part and add into the parent's front.
+__global__ __launch_bounds__(256) void k_extend_add(CholDev c, const int* __restrict__ kids,
+                                                   const long long* __restrict__ colpref, int cnt) {
+  const long long gw = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (gw >= colpref[cnt]) return;
+  int lo = 0, hi = cnt;  // largest q with colpref[q] <= gw
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (colpref[mid] <= gw) lo = mid; else hi = mid;
+  }
+  const int ch = kids[lo];
+  const int b = (int)(gw - colpref[lo]);
+  const int mc = c.m[ch], wc = c.w[ch], u = mc - wc;
+  const int p = c.parent[ch];
+  const int mp = c.m[p];
+  const int* __restrict__ rel = c.ea_rel + c.ea_ptr[ch];
+  const double* __restrict__ U = c.F + c.foff[ch] + wc + (size_t)(wc + b) * mc;
+  double* __restrict__ Fp = c.F + c.foff[p] + (size_t)(3 * rel[b / 3] + b % 3) * mp;
+  // 4 rows in flight per lane: loads first, then the scattered adds
+  int a = b + lane;
+  for (; a + 192 < u; a += 256) {
+    const double u0 = U[a], u1 = U[a + 64], u2 = U[a + 128], u3 = U[a + 192];
+    const int p0 = 3 * rel[a / 3] + a % 3, p1 = 3 * rel[(a + 64) / 3] + (a + 64) % 3;
+    const int p2 = 3 * rel[(a + 128) / 3] + (a + 128) % 3, p3 = 3 * rel[(a + 192) / 3] + (a + 192) % 3;
+    const double f0 = Fp[p0], f1 = Fp[p1], f2 = Fp[p2], f3 = Fp[p3];
+    Fp[p0] = f0 + u0;
+    Fp[p1] = f1 + u1;
+    Fp[p2] = f2 + u2;
+    Fp[p3] = f3 + u3;
+  }
+  for (; a < u; a += 64) Fp[3 * rel[a / 3] + a % 3] += U[a];
+}
+
+// ------------------------------------------------------------ small fronts (LDS)
+// m <= 128: the whole front in LDS; right-looking, two threads per row (the
+// row's columns split even/odd) so LDS accesses of a wave are consecutive rows.
+__global__ __launch_bounds__(256) void k_front_small(CholDev c, const int* __restrict__ list) {
+  extern __shared__ __attribute__((aligned(16))) double A[];
+  const int s = list[blockIdx.x];
+  const int m = c.m[s], w = c.w[s];
+  double* Fs = c.F + c.foff[s];
+  const int tid = threadIdx.x;
+  for (int j = 0; j < m; j++)
+    for (int i = j + tid; i < m; i += 256) A[i + j * m] = Fs[i + (size_t)j * m];
+  __syncthreads();
+  const int half = tid >> 7, rsub = tid & 127;
+  for (int k = 0; k < w; k++) {
+    double d = A[k + k * m];
+    if (!(d > 0.0) || !isfinite(d)) {
+      *c.flag = 1;
+      d = 1.0;
+    }
+    const double piv = sqrt(d);
+    __syncthreads();  // every thread has read the pivot before it is overwritten
+    if (tid == 0) A[k + k * m] = piv;
+    const double inv = 1.0 / piv;
+    for (int i = k + 1 + tid; i < m; i += 256) A[i + k * m] *= inv;
+    __syncthreads();
+    for (int i = k + 1 + rsub; i < m; i += 128) {
+      const double lik = A[i + k * m];
+      for (int j = k + 1 + half; j <= i; j += 2) A[i + j * m] -= lik * A[j + k * m];
+    }
+    __syncthreads();
+  }
+  for (int j = 0; j < m; j++)
+    for (int i = j + tid; i < m; i += 256) Fs[i + (size_t)j * m] = A[i + j * m];
+}
+
+// ------------------------------------------------------------ blocked path
+// Diagonal tile (nb x nb at kb) of each listed front, factored in place by ONE
+// wave: lane i keeps row i in registers; column j is broadcast through LDS.
+__global__ __launch_bounds__(64) void k_panel_potrf(CholDev c, const int* __restrict__ list, int kb) {
+  __shared__ double col[kNB];
+  const int s = list[blockIdx.x];
+  const int m = c.m[s], w = c.w[s];
+  const int nb = min(kNB, w - kb);
+  double* Fs = c.F + c.foff[s] + kb + (size_t)kb * m;
+  const int i = threadIdx.x;
+  double a[kNB];
+#pragma unroll
+  for (int k = 0; k < kNB; k++) a[k] = (k <= i && i < nb && k < nb) ? Fs[i + (size_t)k * m] : 0.0;
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < kNB; j++) {
+    if (j < nb) {
+      double d = __shfl(a[j], j);
+      if (!(d > 0.0) || !isfinite(d)) {
+        bad = true;
+        d = 1.0;
+      }
+      const double piv = sqrt(d), inv = 1.0 / piv;
+      const double l = i > j ? a[j] * inv : (i == j ? piv : 0.0);
+      a[j] = l;
+      col[i] = l;
+      __syncthreads();
+#pragma unroll
+      for (int k = j + 1; k < kNB; k++) a[k] -= l * col[k];
+      __syncthreads();
+    }
+  }
+  if (bad && i == 0) *c.flag = 1;
+#pragma unroll
+  for (int k = 0; k < kNB; k++)
+    if (k <= i && i < nb && k < nb) Fs[i + (size_t)k * m] = a[k];
+}
+
+// Rows [r0, r0+256) below the factored diagonal tile: X = B L^-T, one row per
+// thread in registers, right-looking (the FMAs of a step are independent).
+__global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __restrict__ tasks, int kb) {
+  __shared__ double T[kNB * (kNB + 1)];
+  __shared__ double dinv[kNB];
+  const int2 task = tasks[blockIdx.x];
+  const int s = task.x, chunk = task.y;
+  const int m = c.m[s], w = c.w[s];
+  const int nb = min(kNB, w - kb);
+  double* Fs = c.F + c.foff[s];
+  const int tid = threadIdx.x;
+  const int ld = kNB + 1;
+  for (int idx = tid; idx < nb * nb; idx += 256) {
+    const int i = idx % nb, j = idx / nb;
+    T[i + j * ld] = i >= j ? Fs[(kb + i) + (size_t)(kb + j) * m] : 0.0;
+  }
+  __syncthreads();
+  if (tid < nb) dinv[tid] = 1.0 / T[tid + tid * ld];
+  __syncthreads();
+  const int row = kb + nb + chunk * 256 + tid;
+  if (row >= m) return;
+  double x[kNB];
+#pragma unroll
+  for (int k = 0; k < kNB; k++) x[k] = k < nb ? Fs[row + (size_t)(kb + k) * m] : 0.0;
+#pragma unroll
+  for (int k = 0; k < kNB; k++) {
+    if (k < nb) {
+      x[k] *= dinv[k];
+#pragma unroll
+      for (int t = k + 1; t < kNB; t++) x[t] -= x[k] * T[t + k * ld];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kNB; k++)
+    if (k < nb) Fs[row + (size_t)(kb + k) * m] = x[k];
+}
+
+// Schur update of one 64x64 lower tile of the trailing matrix:
+// C[ti,tj] -= P_i P_j^T, P = F[r0:, kb:kb+nb], r0 = kb + nb.
+__global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int2* __restrict__ tasks, int kb) {
+  constexpr int LD = kTile + 16;  // [k][r] with an 80-double row: lanes l and l+16 on different banks
+  __shared__ __attribute__((aligned(16))) double Pi[kNB * LD];
+  __shared__ __attribute__((aligned(16))) double Pj[kNB * LD];
+  const int2 task = tasks[blockIdx.x];
+  const int s = task.x, ti = task.y >> 16, tj = task.y & 0xffff;
+  const int m = c.m[s], w = c.w[s];
+  const int nb = min(kNB, w - kb);
+  const int r0 = kb + nb;
+  const int ri = r0 + ti * kTile, rj = r0 + tj * kTile;
+  const double* Fs = c.F + c.foff[s];
+  const int tid = threadIdx.x;
+  const int K = (nb + 3) & ~3;
+  for (int idx = tid; idx < K * kTile; idx += 256) {
+    const int k = idx / kTile, r = idx % kTile;
+    const bool kin = k < nb;
+    Pi[k * LD + r] = (kin && ri + r < m) ? Fs[(ri + r) + (size_t)(kb + k) * m] : 0.0;
+    Pj[k * LD + r] = (kin && rj + r < m) ? Fs[(rj + r) + (size_t)(kb + k) * m] : 0.0;
+  }
+  __syncthreads();
+  const int wv = tid >> 6, lane = tid & 63;
+  const int qi = 32 * (wv >> 1), qj = 32 * (wv & 1);
+  const int kl = lane >> 4, rl = lane & 15;
+  d4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    const double* pa = Pi + (k0 + kl) * LD + qi + rl;
+    const double* pb = Pj + (k0 + kl) * LD + qj + rl;
+    const double a0 = pa[0], a1 = pa[16], b0 = pb[0], b1 = pb[16];
+    acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc00, 0, 0, 0);
+    acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc01, 0, 0, 0);
+    acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc10, 0, 0, 0);
+    acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc11, 0, 0, 0);
+  }
+  // D layout (f64 16x16x4): lane l, reg r -> row (l>>4) + 4r, col l&15
+  double* Fw = c.F + c.foff[s];
+  const int col0 = rj + qj + rl;
+#pragma unroll
+  for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+    for (int mj = 0; mj < 2; mj++) {
+      const d4 a = mi == 0 ? (mj == 0 ? acc00 : acc01) : (mj == 0 ? acc10 : acc11);
+      const int col = col0 + 16 * mj;
+      if (col >= m) continue;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = ri + qi + 16 * mi + kl + 4 * r;
+        if (row < m && row >= col) Fw[row + (size_t)col * m] -= a[r];
+      }
+    }
+}
+
+// ------------------------------------------------------------ solves
+__global__ __launch_bounds__(256) void k_perm_in(CholDev c, const double* __restrict__ b, double scale, int n) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const int o = c.perm[j];
+#pragma unroll
+  for (int a = 0; a < 3; a++) c.xv[3 * j + a] = scale * b[3 * o + a];
+}
+
+__global__ __launch_bounds__(256) void k_perm_out(CholDev c, double* __restrict__ x, int n) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const int o = c.perm[j];
+#pragma unroll
+  for (int a = 0; a < 3; a++) x[3 * o + a] = c.xv[3 * j + a];
+}
+
+// Diagonal-block solves by wave 0 of a workgroup, the 64x64 block staged in
+// LDS (Ld[i + k*65]); v holds the right-hand side (lane i <-> row i).
+__device__ __forceinline__ void stage_diag(const double* L, int m, int jb, int nbk, double* Ld) {
+  for (int idx = threadIdx.x; idx < nbk * nbk; idx += blockDim.x) {
+    const int i = idx % nbk, k = idx / nbk;
+    Ld[i + k * 65] = i >= k ? L[(jb + i) + (size_t)(jb + k) * m] : 0.0;
+  }
+}
+
+__device__ __forceinline__ double diag_fwd(double v, const double* Ld, int nbk) {  // wave 0 only
+  const int i = threadIdx.x;
+  for (int k = 0; k < nbk; k++) {
+    const double xk = __shfl(v, k) / Ld[k + k * 65];
+    if (i == k) v = xk;
+    else if (i > k) v -= Ld[i + k * 65] * xk;
+  }
+  return v;
+}
+
+__device__ __forceinline__ double diag_bwd(double v, const double* Ld, int nbk) {  // wave 0 only
+  const int i = threadIdx.x;
+  for (int k = nbk - 1; k >= 0; k--) {
+    const double xk = __shfl(v, k) / Ld[k + k * 65];
+    if (i == k) v = xk;
+    else if (i < k) v -= Ld[k + i * 65] * xk;
+  }
+  return v;
+}
+
+// Forward, launch 1 of a level: frontal vector = (own rhs, 0) + children's update
+// vectors (fixed order), then block 0 solved.  One workgroup per front.
+__global__ __launch_bounds__(256) void k_fwd_assemble(CholDev c, const int* __restrict__ list) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* Ld = sm;                 // 64 x 65
+  double* v = sm + 64 * 65;        // m
+  const int s = list[blockIdx.x];
+  const int m = c.m[s], w = c.w[s];
+  const double* L = c.F + c.foff[s];
+  const int* rows = c.rows + c.rptr[s];
+  const int tid = threadIdx.x;
+  for (int r = tid; r < m; r += 256) v[r] = r < w ? c.xv[3 * rows[r / 3] + r % 3] : 0.0;
+  const int nbk = min(64, w);
+  stage_diag(L, m, 0, nbk, Ld);
+  __syncthreads();
+  for (int q = c.cptr[s]; q < c.cptr[s + 1]; q++) {
+    const int ch = c.children[q];
+    const int uc = c.m[ch] - c.w[ch];
+    const double* uv = c.fv + c.voff[ch] + c.w[ch];
+    const int* rel = c.ea_rel + c.ea_ptr[ch];
+    for (int t = tid; t < uc; t += 256) v[3 * rel[t / 3] + t % 3] += uv[t];
+    __syncthreads();
+  }
+  if (tid < 64) {
+    const double y = diag_fwd(tid < nbk ? v[tid] : 0.0, Ld, nbk);
+    if (tid < nbk) v[tid] = y;
+  }
+  __syncthreads();
+  double* fv = c.fv + c.voff[s];
+  for (int r = tid; r < m; r += 256) fv[r] = v[r];
+}
+
+// Forward step b: rows [r0, r1) -= L[r, block b] y_b; the task owning the next
+// diagonal block (rows of block b+1) then solves it.
+__global__ __launch_bounds__(256) void k_fwd_step(CholDev c, const int4* __restrict__ tasks, int b) {
+  __shared__ double Ld[64 * 65];
+  __shared__ double y[64];
+  __shared__ double vn[64];
+  const int4 t = tasks[blockIdx.x];
+  const int s = t.x, r0 = t.y, r1 = t.z, owner = t.w;
+  const int m = c.m[s], w = c.w[s];
+  const double* L = c.F + c.foff[s];
+  double* fv = c.fv + c.voff[s];
+  const int tid = threadIdx.x;
+  const int jb = b * 64, nbk = min(64, w - jb);
+  if (tid < nbk) y[tid] = fv[jb + tid];
+  if (owner >= 0) stage_diag(L, m, owner * 64, r1 - r0, Ld);
+  __syncthreads();
+  const int r = r0 + tid;
+  if (r < r1) {
+    double acc = 0.0;
+    for (int k = 0; k < nbk; k++) acc += L[r + (size_t)(jb + k) * m] * y[k];
+    const double nv = fv[r] - acc;
+    if (owner >= 0) vn[tid] = nv;
+    else fv[r] = nv;
+  }
+  if (owner < 0) return;
+  __syncthreads();
+  if (tid < 64) {
+    const int n2 = r1 - r0;
+    const double yy = diag_fwd(tid < n2 ? vn[tid] : 0.0, Ld, n2);
+    if (tid < n2) fv[r0 + tid] = yy;
+  }
+}
+
+// Backward init of a level: z_j = y_j - L21[:, j]' x_below for the task's
+// columns (one wave per column); the owner of the last block solves it.
+__global__ __launch_bounds__(256) void k_bwd_init(CholDev c, const int4* __restrict__ tasks) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* Ld = sm;                 // 64 x 65
+  double* z = sm + 64 * 65;        // 64
+  double* xb = z + 64;             // m - w
+  const int4 t = tasks[blockIdx.x];
+  const int s = t.x, c0 = t.y, c1 = t.z, owner = t.w;
+  const int m = c.m[s], w = c.w[s];
+  const double* L = c.F + c.foff[s];
+  double* fv = c.fv + c.voff[s];
+  const int* rows = c.rows + c.rptr[s];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int r = w + tid; r < m; r += 256) xb[r - w] = c.xv[3 * rows[r / 3] + r % 3];
+  if (owner >= 0) stage_diag(L, m, c0, c1 - c0, Ld);
+  __syncthreads();
+  // L21[:, c0:c1]' x_below: thread (wave wv, lane) owns rows w + lane + 64 (wv + 4 t),
+  // keeps one partial per column (<= 64), loads of a row chunk all in flight
+  const int ncol = c1 - c0;
+  double acc[64];
+#pragma unroll
+  for (int q = 0; q < 64; q++) acc[q] = 0.0;
+  for (int r = w + lane + 64 * wv; r < m; r += 256) {
+    const double xr = xb[r - w];
+    const double* Lr = L + r + (size_t)c0 * m;
+#pragma unroll
+    for (int q = 0; q < 64; q++)
+      if (q < ncol) acc[q] += Lr[(size_t)q * m] * xr;
+  }
+  // reduce each column over the 256 threads: wave butterflies, then 4 waves via LDS
+  double* red = xb;  // reuse after the loop (m - w >= 0 doubles; need 4*64)
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 64; q++) {
+    double v = acc[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) red[wv * 64 + q] = v;
+  }
+  __syncthreads();
+  if (tid < ncol) z[tid] = fv[c0 + tid] - (red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid]);
+  __syncthreads();
+  if (owner < 0) {
+    for (int j = c0 + tid; j < c1; j += 256) fv[j] = z[j - c0];
+    return;
+  }
+  if (tid < 64) {
+    const int n2 = c1 - c0;
+    const double x = diag_bwd(tid < n2 ? z[tid] : 0.0, Ld, n2);
+    if (tid < n2) {
+      fv[c0 + tid] = x;
+      c.xv[3 * rows[(c0 + tid) / 3] + (c0 + tid) % 3] = x;
+    }
+  }
+}
+
+// Backward step b: z_j -= L[block b, j]' x_b for the task's columns (< 64 b);
+// the owner of block b-1 then solves it.
+__global__ __launch_bounds__(256) void k_bwd_step(CholDev c, const int4* __restrict__ tasks, int b) {
+  __shared__ double Ld[64 * 65];
+  __shared__ double xbk[64];
+  __shared__ double z[64];
+  const int4 t = tasks[blockIdx.x];
+  const int s = t.x, c0 = t.y, c1 = t.z, owner = t.w;
+  const int m = c.m[s], w = c.w[s];
+  const double* L = c.F + c.foff[s];
+  double* fv = c.fv + c.voff[s];
+  const int* rows = c.rows + c.rptr[s];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int jb = b * 64, nbk = min(64, w - jb);
+  if (tid < nbk) xbk[tid] = fv[jb + tid];
+  if (owner >= 0) stage_diag(L, m, c0, c1 - c0, Ld);
+  __syncthreads();
+  // wave wv: columns c0 + wv + 4q, q < 16; all 16 loads issued before the reductions
+  double part[16];
+  const double xl = lane < nbk ? xbk[lane] : 0.0;
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    const int j = c0 + wv + 4 * q;
+    part[q] = (j < c1 && lane < nbk) ? L[(jb + lane) + (size_t)j * m] * xl : 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    double acc = part[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    const int j = c0 + wv + 4 * q;
+    if (lane == 0 && j < c1) z[j - c0] = fv[j] - acc;
+  }
+  __syncthreads();
+  if (owner < 0) {
+    for (int j = c0 + tid; j < c1; j += 256) fv[j] = z[j - c0];
+    return;
+  }
+  if (tid < 64) {
+    const int n2 = c1 - c0;
+    const double x = diag_bwd(tid < n2 ? z[tid] : 0.0, Ld, n2);
+    if (tid < n2) {
+      fv[c0 + tid] = x;
+      c.xv[3 * rows[(c0 + tid) / 3] + (c0 + tid) % 3] = x;
+    }
+  }
+}
+
+// ------------------------------------------------------------ host drivers
+template <class T>
+static hipError_t up(T** d, const std::vector<T>& h, hipStream_t s) {
+  hipError_t e = hipMalloc((void**)d, std::max<size_t>(h.size(), 1) * sizeof(T));
+  if (e != hipSuccess) return e;
+  if (!h.empty()) e = hipMemcpyAsync(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s);
+  return e;
+}
+
+#define CH_TRY(x)                       \
+  do {                                  \
+    hipError_t e_ = (x);                \
+    if (e_ != hipSuccess) return e_;    \
+  } while (0)
+
+hipError_t chol_upload(CholPlan& P, hipStream_t s) {
+  CH_TRY(hipMalloc((void**)&P.F, std::max<long long>(P.ftotal, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.fv, std::max(P.vtotal, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.xv, std::max(3 * P.n, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.d_flag, sizeof(int)));
+  CH_TRY(hipMalloc((void**)&P.d_lambda, sizeof(double)));
+  CH_TRY(up(&P.d_m, P.m, s));
+  CH_TRY(up(&P.d_w, P.w, s));
+  CH_TRY(up(&P.d_voff, P.voff, s));
+  CH_TRY(up(&P.d_rptr, P.rptr, s));
+  CH_TRY(up(&P.d_rows, P.rows, s));
+  CH_TRY(up(&P.d_foff, P.foff, s));
+  CH_TRY(up(&P.d_cptr, P.cptr, s));
+  CH_TRY(up(&P.d_children, P.children, s));
+  CH_TRY(up(&P.d_ea_rel, P.ea_rel, s));
+  CH_TRY(up(&P.d_ea_ptr, P.ea_ptr, s));
+  CH_TRY(up(&P.d_parent, P.parent, s));
+  CH_TRY(up(&P.d_asm_front, P.asm_front, s));
+  CH_TRY(up(&P.d_asm_li, P.asm_li, s));
+  CH_TRY(up(&P.d_asm_lj, P.asm_lj, s));
+  CH_TRY(up(&P.d_asm_ptr, P.asm_ptr, s));
+  CH_TRY(up(&P.d_asm_src, P.asm_src, s));
+  CH_TRY(up(&P.d_dg_front, P.dg_front, s));
+  CH_TRY(up(&P.d_dg_loc, P.dg_loc, s));
+  CH_TRY(up(&P.d_perm, P.perm, s));
+  CH_TRY(up(&P.d_small, P.small_list, s));
+  CH_TRY(up(&P.d_level_fronts, P.level_fronts, s));
+  CH_TRY(up(&P.d_trsm, P.trsm_tasks, s));
+  CH_TRY(up(&P.d_potrf, P.potrf_list, s));
+  CH_TRY(up(&P.d_fwd, P.fwd_tasks, s));
+  CH_TRY(up(&P.d_bwd, P.bwd_tasks, s));
+  CH_TRY(up(&P.d_syrk, P.syrk_tasks, s));
+  CH_TRY(up(&P.d_ea_children, P.ea_children, s));
+  CH_TRY(up(&P.d_ea_colpref, P.ea_colpref, s));
+  return hipStreamSynchronize(s);
+}
+
+void chol_free(CholPlan& P) {
+  void* ptrs[] = {P.F, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
+                  P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
+                  P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
+                  P.d_trsm, P.d_syrk, P.d_ea_children, P.d_ea_colpref, P.d_potrf, P.d_fwd, P.d_bwd};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  P = CholPlan();
+}
+
+hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, hipStream_t s, SyrkProfile* prof) {
+  if (P.n == 0) return hipSuccess;
+  const CholDev c = dev_view(P);
+  CH_TRY(hipMemsetAsync(P.F, 0, P.ftotal * sizeof(double), s));
+  CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int), s));
+  const int nt = (int)P.asm_front.size();
+  if (nt) k_asm_offdiag<<<(nt + 255) / 256, 256, 0, s>>>(c, V, nt);
+  k_asm_diag<<<(P.n + 255) / 256, 256, 0, s>>>(c, D, P.d_lambda, P.n);
+  for (const CholLevel& lv : P.levels) {
+    for (size_t r = 0; r < lv.ea_off.size(); r++) {
+      const long long cols = P.ea_colpref[lv.ea_cols_off[r] + lv.ea_cnt[r]];
+      if (!cols) continue;
+      const long long blocks = (cols * 64 + 255) / 256;
+      k_extend_add<<<(unsigned)blocks, 256, 0, s>>>(c, P.d_ea_children + lv.ea_off[r],
+                                                    P.d_ea_colpref + lv.ea_cols_off[r], lv.ea_cnt[r]);
+    }
+    for (const SmallClass& sc : lv.small)
+      k_front_small<<<sc.cnt, 256, (size_t)sc.mmax * sc.mmax * sizeof(double), s>>>(c, P.d_small + sc.off);
+    for (const PanelStep& ps : lv.panels) {
+      k_panel_potrf<<<ps.potrf_cnt, 64, 0, s>>>(c, P.d_potrf + ps.potrf_off, ps.kb);
+      if (ps.trsm_cnt) k_panel_trsm<<<ps.trsm_cnt, 256, 0, s>>>(c, P.d_trsm + ps.trsm_off, ps.kb);
+      if (!ps.syrk_cnt) continue;
+      if (prof && prof->used < prof->cap) {
+        const int u = prof->used++;
+        prof->flops[u] = ps.syrk_flops;
+        hipExtLaunchKernelGGL(k_panel_syrk, dim3(ps.syrk_cnt), dim3(256), 0, s, prof->ev[2 * u], prof->ev[2 * u + 1], 0,
+                              c, (const int2*)(P.d_syrk + ps.syrk_off), ps.kb);
+      } else {
+        k_panel_syrk<<<ps.syrk_cnt, 256, 0, s>>>(c, P.d_syrk + ps.syrk_off, ps.kb);
+      }
+    }
+  }
+  return hipGetLastError();
+}
+
+hipError_t chol_solve(const CholPlan& P, const double* b, double* x, double scale_b, hipStream_t s) {
+  if (P.n == 0) return hipSuccess;
+  const CholDev c = dev_view(P);
+  const int g = (P.n + 255) / 256;
+  k_perm_in<<<g, 256, 0, s>>>(c, b, scale_b, P.n);
+  for (const CholLevel& lv : P.levels) {
+    k_fwd_assemble<<<lv.front_cnt, 256, (size_t)(64 * 65 + lv.maxm) * sizeof(double), s>>>(
+        c, P.d_level_fronts + lv.front_off);
+    for (int bb = 0; bb < (int)lv.fwd.size(); bb++)
+      if (lv.fwd[bb].cnt) k_fwd_step<<<lv.fwd[bb].cnt, 256, 0, s>>>(c, P.d_fwd + lv.fwd[bb].off, bb);
+  }
+  for (auto it = P.levels.rbegin(); it != P.levels.rend(); ++it) {
+    const CholLevel& lv = *it;
+    k_bwd_init<<<lv.bwd[0].cnt, 256, (size_t)(64 * 65 + 64 + std::max(lv.maxm, 256)) * sizeof(double), s>>>(
+        c, P.d_bwd + lv.bwd[0].off);
+    for (size_t q = 1; q < lv.bwd.size(); q++) {
+      const int bb = lv.maxblk - (int)q;   // step b = maxblk-1 .. 1
+      if (lv.bwd[q].cnt) k_bwd_step<<<lv.bwd[q].cnt, 256, 0, s>>>(c, P.d_bwd + lv.bwd[q].off, bb);
+    }
+  }
+  k_perm_out<<<g, 256, 0, s>>>(c, x, P.n);
+  return hipGetLastError();
+}
+
+}  // namespace pgo

@@ -1,0 +1,514 @@
+// Host-side symbolic analysis for the GPU supernodal Cholesky (pgo_chol.h).
+// Runs once per graph structure (GTSAM recomputes COLAMD every solve).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "pgo_chol.h"
+
+namespace pgo {
+namespace {
+
+// Approximate minimum degree on the quotient graph (Amestoy, Davis & Duff):
+// eliminated pivots become elements that absorb their adjacent elements;
+// external degrees are bounded by |A_i| + |L_p \ i| + sum_e |L_e \ L_p|,
+// with |L_e \ L_p| from the w(e) counters; aggressive element absorption.
+std::vector<int> amd(int n, const std::vector<int>& xadj, const std::vector<int>& adj) {
+  std::vector<std::vector<int>> var(n), elem(n), members(n);
+  std::vector<char> state(n, 0);  // 0 variable, 1 element, 2 absorbed
+  std::vector<int> deg(n), w(n, 0), wstamp(n, -1), mark(n, -1);
+  std::vector<int> head(n + 1, -1), nxt(n, -1), prv(n, -1);
+  auto unlink = [&](int i) {
+    if (prv[i] >= 0) nxt[prv[i]] = nxt[i];
+    else head[deg[i]] = nxt[i];
+    if (nxt[i] >= 0) prv[nxt[i]] = prv[i];
+  };
+  auto link = [&](int i) {
+    nxt[i] = head[deg[i]];
+    prv[i] = -1;
+    if (head[deg[i]] >= 0) prv[head[deg[i]]] = i;
+    head[deg[i]] = i;
+  };
+  for (int i = 0; i < n; i++) {
+    for (int k = xadj[i]; k < xadj[i + 1]; k++)
+      if (adj[k] != i) var[i].push_back(adj[k]);
+    deg[i] = (int)var[i].size();
+  }
+  for (int i = n - 1; i >= 0; i--) link(i);
+  std::vector<int> order(n);
+  int mindeg = 0;
+  for (int k = 0; k < n; k++) {
+    while (head[mindeg] < 0) mindeg++;
+    const int p = head[mindeg];
+    unlink(p);
+    order[k] = p;
+    std::vector<int> Lp;
+    mark[p] = k;
+    for (int j : var[p])
+      if (state[j] == 0 && mark[j] != k) {
+        mark[j] = k;
+        Lp.push_back(j);
+      }
+    for (int e : elem[p]) {
+      if (state[e] != 1) continue;
+      for (int j : members[e])
+        if (state[j] == 0 && mark[j] != k) {
+          mark[j] = k;
+          Lp.push_back(j);
+        }
+      state[e] = 2;
+      std::vector<int>().swap(members[e]);
+    }
+    state[p] = 1;
+    std::vector<int>().swap(var[p]);
+    std::vector<int>().swap(elem[p]);
+    for (int i : Lp) unlink(i);
+    for (int i : Lp)
+      for (int e : elem[i]) {
+        if (state[e] != 1) continue;
+        if (wstamp[e] != k) {
+          wstamp[e] = k;
+          w[e] = (int)members[e].size();
+        }
+        w[e]--;
+      }
+    const int left = n - k - 1;
+    const int lp = (int)Lp.size();
+    for (int i : Lp) {
+      long ext = 0;
+      auto& ei = elem[i];
+      size_t m = 0;
+      for (int e : ei) {
+        if (state[e] != 1) continue;
+        if (w[e] == 0) {  // aggressive absorption: L_e inside L_p
+          state[e] = 2;
+          std::vector<int>().swap(members[e]);
+          continue;
+        }
+        ei[m++] = e;
+        ext += w[e];
+      }
+      ei.resize(m);
+      ei.push_back(p);
+      auto& vi = var[i];
+      m = 0;
+      for (int j : vi)
+        if (state[j] == 0 && mark[j] != k) vi[m++] = j;
+      vi.resize(m);
+      long d = (long)vi.size() + (lp - 1) + ext;
+      d = std::min<long>(d, (long)deg[i] + lp - 1);
+      d = std::min<long>(d, left - 1);
+      deg[i] = (int)std::max<long>(d, 0);
+      link(i);
+      mindeg = std::min(mindeg, deg[i]);
+    }
+    members[p] = std::move(Lp);
+  }
+  return order;
+}
+
+}  // namespace
+
+void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
+  P.n = n;
+  // ---- pose adjacency (old index), unique, no self loops
+  std::vector<int> xadj(n + 1, 0), adj;
+  adj.reserve(slot_col.size());
+  {
+    std::vector<int> stamp(n, -1);
+    for (int i = 0; i < n; i++) {
+      stamp[i] = i;
+      for (int k = row_ptr[i]; k < row_ptr[i + 1]; k++) {
+        const int j = slot_col[k];
+        if (stamp[j] != i) {
+          stamp[j] = i;
+          adj.push_back(j);
+        }
+      }
+      xadj[i + 1] = (int)adj.size();
+    }
+  }
+  const std::vector<int> order0 = amd(n, xadj, adj);
+  std::vector<int> ip0(n);
+  for (int k = 0; k < n; k++) ip0[order0[k]] = k;
+  // ---- elimination tree of the permuted pattern (Liu, path compression)
+  std::vector<int> et(n, -1), anc(n, -1);
+  for (int j = 0; j < n; j++) {
+    const int oj = order0[j];
+    for (int k = xadj[oj]; k < xadj[oj + 1]; k++) {
+      int r = ip0[adj[k]];
+      if (r >= j) continue;
+      while (anc[r] != -1 && anc[r] != j) {
+        const int t = anc[r];
+        anc[r] = j;
+        r = t;
+      }
+      if (anc[r] == -1) {
+        anc[r] = j;
+        et[r] = j;
+      }
+    }
+  }
+  // ---- postorder (children in increasing order)
+  std::vector<int> chead(n, -1), cnext(n, -1), post;
+  post.reserve(n);
+  for (int j = n - 1; j >= 0; j--)
+    if (et[j] >= 0) {
+      cnext[j] = chead[et[j]];
+      chead[et[j]] = j;
+    }
+  {
+    std::vector<int> stack;
+    for (int r = 0; r < n; r++) {
+      if (et[r] != -1) continue;
+      stack.push_back(r);
+      while (!stack.empty()) {
+        const int j = stack.back();
+        const int c = chead[j];
+        if (c == -1) {
+          stack.pop_back();
+          post.push_back(j);
+        } else {
+          chead[j] = cnext[c];
+          stack.push_back(c);
+        }
+      }
+    }
+  }
+  P.perm.resize(n);
+  P.iperm.resize(n);
+  std::vector<int> pos(n), par(n);
+  for (int k = 0; k < n; k++) {
+    P.perm[k] = order0[post[k]];
+    pos[post[k]] = k;
+  }
+  for (int k = 0; k < n; k++) P.iperm[P.perm[k]] = k;
+  for (int k = 0; k < n; k++) par[k] = et[post[k]] >= 0 ? pos[et[post[k]]] : -1;
+  // ---- column counts (off-diagonal pose rows) via row subtrees
+  std::vector<int> cc(n, 0), mark(n, -1), nch(n, 0);
+  for (int i = 0; i < n; i++) {
+    mark[i] = i;
+    const int oi = P.perm[i];
+    for (int k = xadj[oi]; k < xadj[oi + 1]; k++) {
+      int j = P.iperm[adj[k]];
+      if (j >= i) continue;
+      while (mark[j] != i) {
+        cc[j]++;
+        mark[j] = i;
+        j = par[j];
+      }
+    }
+  }
+  for (int j = 0; j < n; j++)
+    if (par[j] >= 0) nch[par[j]]++;
+  // ---- fundamental supernodes, then relaxed amalgamation of a child that
+  // immediately precedes its parent when it adds few explicit zeros
+  std::vector<int> fs;
+  for (int j = 0; j < n; j++) {
+    if (j > 0 && par[j - 1] == j && nch[j] == 1 && cc[j - 1] == cc[j] + 1) continue;
+    fs.push_back(j);
+  }
+  fs.push_back(n);
+  std::vector<int> of, ol;
+  std::vector<double> onz;
+  for (size_t s = 0; s + 1 < fs.size(); s++) {
+    int f = fs[s];
+    const int l = fs[s + 1];
+    const int wd = l - f, nb = cc[l - 1];
+    double nz = 0.5 * wd * (wd + 1.0) + (double)wd * nb;
+    while (!of.empty()) {
+      const size_t t = of.size() - 1;
+      if (ol[t] != f) break;
+      const int lastc = ol[t] - 1;
+      if (par[lastc] < f || par[lastc] >= l) break;
+      const int W = l - of[t];
+      const double tot = 0.5 * W * (W + 1.0) + (double)W * nb;
+      const double tnz = nz + onz[t];
+      const double z = (tot - tnz) / tot;
+      const bool ok = (W <= 2) || (W <= 6 && z < 0.8) || (W <= 16 && z < 0.1) || (z < 0.05);
+      if (!ok) break;
+      f = of[t];
+      nz = tnz;
+      of.pop_back();
+      ol.pop_back();
+      onz.pop_back();
+    }
+    of.push_back(f);
+    ol.push_back(l);
+    onz.push_back(nz);
+  }
+  const int ns = (int)of.size();
+  P.ns = ns;
+  P.sfirst.assign(of.begin(), of.end());
+  P.sfirst.push_back(n);
+  std::vector<int> snode(n);
+  for (int s = 0; s < ns; s++)
+    for (int j = P.sfirst[s]; j < P.sfirst[s + 1]; j++) snode[j] = s;
+  P.parent.assign(ns, -1);
+  for (int s = 0; s < ns; s++) {
+    const int lc = P.sfirst[s + 1] - 1;
+    P.parent[s] = par[lc] >= 0 ? snode[par[lc]] : -1;
+  }
+  P.cptr.assign(ns + 1, 0);
+  for (int s = 0; s < ns; s++)
+    if (P.parent[s] >= 0) P.cptr[P.parent[s] + 1]++;
+  for (int s = 0; s < ns; s++) P.cptr[s + 1] += P.cptr[s];
+  P.children.assign(P.cptr[ns], 0);
+  {
+    std::vector<int> f(P.cptr.begin(), P.cptr.end() - 1);
+    for (int s = 0; s < ns; s++)
+      if (P.parent[s] >= 0) P.children[f[P.parent[s]]++] = s;
+  }
+  // ---- front rows: own poses then sorted below rows (A's pattern + children's rows)
+  std::vector<std::vector<int>> below(ns);
+  std::fill(mark.begin(), mark.end(), -1);
+  for (int s = 0; s < ns; s++) {
+    const int f = P.sfirst[s], l = P.sfirst[s + 1];
+    auto& b = below[s];
+    for (int j = f; j < l; j++) {
+      const int oj = P.perm[j];
+      for (int k = xadj[oj]; k < xadj[oj + 1]; k++) {
+        const int i = P.iperm[adj[k]];
+        if (i >= l && mark[i] != s) {
+          mark[i] = s;
+          b.push_back(i);
+        }
+      }
+    }
+    for (int q = P.cptr[s]; q < P.cptr[s + 1]; q++)
+      for (int i : below[P.children[q]])
+        if (i >= l && mark[i] != s) {
+          mark[i] = s;
+          b.push_back(i);
+        }
+    std::sort(b.begin(), b.end());
+  }
+  P.rptr.assign(ns + 1, 0);
+  P.m.resize(ns);
+  P.w.resize(ns);
+  P.foff.assign(ns + 1, 0);
+  P.voff.assign(ns + 1, 0);
+  P.flops = 0;
+  P.nnzl = 0;
+  for (int s = 0; s < ns; s++) {
+    const int wp = P.sfirst[s + 1] - P.sfirst[s];
+    P.w[s] = 3 * wp;
+    P.m[s] = 3 * (wp + (int)below[s].size());
+    P.rptr[s + 1] = P.rptr[s] + wp + (int)below[s].size();
+    const long long mm = P.m[s];
+    P.foff[s + 1] = P.foff[s] + ((mm * mm + 7) / 8) * 8;   // 64-byte aligned fronts
+    P.voff[s + 1] = P.voff[s] + ((P.m[s] + 7) / 8) * 8;
+    for (int k = 0; k < P.w[s]; k++) {
+      const double r = P.m[s] - k - 1;
+      P.flops += 1 + r + r * (r + 1);
+      P.nnzl += r + 1;
+    }
+  }
+  P.ftotal = P.foff[ns];
+  P.vtotal = P.voff[ns];
+  P.rows.resize(P.rptr[ns]);
+  for (int s = 0; s < ns; s++) {
+    int q = P.rptr[s];
+    for (int j = P.sfirst[s]; j < P.sfirst[s + 1]; j++) P.rows[q++] = j;
+    for (int i : below[s]) P.rows[q++] = i;
+  }
+  auto local_of = [&](int s, int i) {  // local pose index of new pose i in front s
+    const int f = P.sfirst[s], l = P.sfirst[s + 1];
+    if (i < l) return i - f;
+    const auto& b = below[s];
+    return (l - f) + (int)(std::lower_bound(b.begin(), b.end(), i) - b.begin());
+  };
+  // ---- extend-add maps: each below row of s -> local pose index in parent's front
+  P.ea_ptr.assign(ns + 1, 0);
+  for (int s = 0; s < ns; s++) P.ea_ptr[s + 1] = P.ea_ptr[s] + (int)below[s].size();
+  P.ea_rel.resize(P.ea_ptr[ns]);
+  for (int s = 0; s < ns; s++) {
+    const int p = P.parent[s];
+    for (size_t t = 0; t < below[s].size(); t++)
+      P.ea_rel[P.ea_ptr[s] + t] = p >= 0 ? local_of(p, below[s][t]) : -1;
+  }
+  // ---- assembly of H's lower blocks: block H_{i,j} (i > j, new) lives in the
+  // slots of block-CSR row perm[i] whose column is perm[j]; parallel factors
+  // between the same pair are summed in slot order.
+  struct Ent {
+    int j, i, k;
+  };
+  std::vector<Ent> ents;
+  ents.reserve(slot_col.size() / 2 + 1);
+  for (int r = 0; r < n; r++) {
+    const int i = P.iperm[r];
+    for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) {
+      const int j = P.iperm[slot_col[k]];
+      if (i > j) ents.push_back({j, i, k});
+    }
+  }
+  std::sort(ents.begin(), ents.end(), [](const Ent& a, const Ent& b) {
+    return a.j != b.j ? a.j < b.j : (a.i != b.i ? a.i < b.i : a.k < b.k);
+  });
+  P.asm_front.clear();
+  P.asm_li.clear();
+  P.asm_lj.clear();
+  P.asm_ptr.assign(1, 0);
+  P.asm_src.clear();
+  for (size_t t = 0; t < ents.size(); t++) {
+    if (t == 0 || ents[t].i != ents[t - 1].i || ents[t].j != ents[t - 1].j) {
+      if (t) P.asm_ptr.push_back((int)P.asm_src.size());
+      const int s = snode[ents[t].j];
+      P.asm_front.push_back(s);
+      P.asm_lj.push_back(ents[t].j - P.sfirst[s]);
+      P.asm_li.push_back(local_of(s, ents[t].i));
+    }
+    P.asm_src.push_back(ents[t].k);
+  }
+  P.asm_ptr.push_back((int)P.asm_src.size());
+  if (ents.empty()) P.asm_ptr.assign(1, 0);
+  P.dg_front.resize(n);
+  P.dg_loc.resize(n);
+  for (int j = 0; j < n; j++) {
+    P.dg_front[j] = snode[j];
+    P.dg_loc[j] = j - P.sfirst[snode[j]];
+  }
+  // ---- heights (leaves 0) and level schedules
+  P.height.assign(ns, 0);
+  for (int s = 0; s < ns; s++)  // children precede parents (postorder)
+    if (P.parent[s] >= 0) P.height[P.parent[s]] = std::max(P.height[P.parent[s]], P.height[s] + 1);
+  const int nl = ns ? *std::max_element(P.height.begin(), P.height.end()) + 1 : 0;
+  std::vector<std::vector<int>> bylevel(nl);
+  for (int s = 0; s < ns; s++) bylevel[P.height[s]].push_back(s);
+  P.levels.assign(nl, CholLevel());
+  P.small_list.clear();
+  P.level_fronts.clear();
+  P.trsm_tasks.clear();
+  P.syrk_tasks.clear();
+  P.potrf_list.clear();
+  P.fwd_tasks.clear();
+  P.bwd_tasks.clear();
+  P.ea_children.clear();
+  P.ea_colpref.clear();
+  for (int L = 0; L < nl; L++) {
+    CholLevel& lv = P.levels[L];
+    lv.front_off = (int)P.level_fronts.size();
+    lv.front_cnt = (int)bylevel[L].size();
+    for (int s : bylevel[L]) {
+      P.level_fronts.push_back(s);
+      lv.maxm = std::max(lv.maxm, P.m[s]);
+      if (P.m[s] <= kSmallFront) lv.small_maxm = std::max(lv.small_maxm, P.m[s]);
+    }
+    // blocked triangular solves (64-column blocks of each front's pivot columns)
+    for (int s : bylevel[L]) lv.maxblk = std::max(lv.maxblk, (P.w[s] + 63) / 64);
+    for (int b = 0; b < lv.maxblk; b++) {        // forward step b: rows below block b
+      SolveStep st{(int)P.fwd_tasks.size(), 0};
+      for (int s : bylevel[L]) {
+        const int w = P.w[s], m = P.m[s], nblk = (w + 63) / 64;
+        if (b >= nblk) continue;
+        int rest = w;
+        if (b + 1 < nblk) {                      // owner of the next diagonal block
+          const int e = std::min((b + 2) * 64, w);
+          P.fwd_tasks.push_back(make_int4(s, (b + 1) * 64, e, b + 1));
+          rest = e;
+        }
+        for (int r = rest; r < m; r += 256) P.fwd_tasks.push_back(make_int4(s, r, std::min(r + 256, m), -1));
+      }
+      st.cnt = (int)P.fwd_tasks.size() - st.off;
+      lv.fwd.push_back(st);
+    }
+    {                                            // backward init: all columns vs the rows below w
+      SolveStep st{(int)P.bwd_tasks.size(), 0};
+      for (int s : bylevel[L]) {
+        const int w = P.w[s], nblk = (w + 63) / 64;
+        for (int b = 0; b < nblk; b++)
+          P.bwd_tasks.push_back(make_int4(s, b * 64, std::min(b * 64 + 64, w), b == nblk - 1 ? b : -1));
+      }
+      st.cnt = (int)P.bwd_tasks.size() - st.off;
+      lv.bwd.push_back(st);
+    }
+    for (int b = lv.maxblk - 1; b >= 1; b--) {   // backward step b: columns left of block b
+      SolveStep st{(int)P.bwd_tasks.size(), 0};
+      for (int s : bylevel[L]) {
+        const int w = P.w[s], nblk = (w + 63) / 64;
+        if (b >= nblk) continue;
+        for (int c = 0; c < b; c++)
+          P.bwd_tasks.push_back(make_int4(s, c * 64, c * 64 + 64, c == b - 1 ? c : -1));
+      }
+      st.cnt = (int)P.bwd_tasks.size() - st.off;
+      lv.bwd.push_back(st);
+    }
+    // extend-add groups: children of this level's fronts, grouped by rank
+    int maxc = 0;
+    for (int s : bylevel[L]) maxc = std::max(maxc, P.cptr[s + 1] - P.cptr[s]);
+    for (int r = 0; r < maxc; r++) {
+      lv.ea_off.push_back((int)P.ea_children.size());
+      lv.ea_cols_off.push_back((int)P.ea_colpref.size());
+      long long cols = 0;
+      int cnt = 0;
+      for (int s : bylevel[L]) {
+        if (P.cptr[s] + r >= P.cptr[s + 1]) continue;
+        const int c = P.children[P.cptr[s] + r];
+        P.ea_children.push_back(c);
+        P.ea_colpref.push_back(cols);
+        cols += P.m[c] - P.w[c];
+        cnt++;
+      }
+      P.ea_colpref.push_back(cols);
+      lv.ea_cnt.push_back(cnt);
+    }
+    // small fronts: one workgroup each, in LDS; launched per size class so the
+    // LDS request (m^2 doubles) does not cap the occupancy of the tiny ones
+    std::vector<int> big;
+    {
+      const int classes[4] = {32, 64, 96, kSmallFront};
+      std::vector<int> bucket[4];
+      for (int s : bylevel[L]) {
+        if (P.m[s] > kSmallFront) {
+          big.push_back(s);
+          continue;
+        }
+        int q = 0;
+        while (P.m[s] > classes[q]) q++;
+        bucket[q].push_back(s);
+      }
+      for (int q = 0; q < 4; q++) {
+        if (bucket[q].empty()) continue;
+        SmallClass sc{(int)P.small_list.size(), (int)bucket[q].size(), 0};
+        for (int s : bucket[q]) {
+          P.small_list.push_back(s);
+          sc.mmax = std::max(sc.mmax, P.m[s]);
+        }
+        lv.small.push_back(sc);
+      }
+    }
+    int maxw = 0;
+    for (int s : big) maxw = std::max(maxw, P.w[s]);
+    for (int kb = 0; kb < maxw; kb += kNB) {
+      PanelStep ps;
+      ps.kb = kb;
+      ps.syrk_flops = 0;
+      ps.trsm_off = (int)P.trsm_tasks.size();
+      ps.syrk_off = (int)P.syrk_tasks.size();
+      ps.potrf_off = (int)P.potrf_list.size();
+      for (int s : big) {
+        if (P.w[s] <= kb) continue;
+        P.potrf_list.push_back(s);
+        const int nb = std::min(kNB, P.w[s] - kb);
+        const int below_rows = P.m[s] - kb - nb;
+        const int chunks = (below_rows + 255) / 256;
+        for (int c = 0; c < chunks; c++) P.trsm_tasks.push_back(make_int2(s, c));
+        if (below_rows > 0) {
+          ps.syrk_flops += (double)below_rows * (below_rows + 1.0) * nb;
+          const int nt = (below_rows + kTile - 1) / kTile;
+          for (int ti = 0; ti < nt; ti++)
+            for (int tj = 0; tj <= ti; tj++) P.syrk_tasks.push_back(make_int2(s, (ti << 16) | tj));
+        }
+      }
+      ps.potrf_cnt = (int)P.potrf_list.size() - ps.potrf_off;
+      ps.trsm_cnt = (int)P.trsm_tasks.size() - ps.trsm_off;
+      ps.syrk_cnt = (int)P.syrk_tasks.size() - ps.syrk_off;
+      P.syrk_flops += ps.syrk_flops;
+      lv.panels.push_back(ps);
+    }
+  }
+}
+
+}  // namespace pgo

@@ -198,6 +198,18 @@ class PoseGraph:
         self._check(self._L.pgo_debug_spmv(self._h, float(lam), L.dptr(x), L.dptr(y)))
         return y
 
+    def debug_plan(self, cap=4096):
+        """Host-only symbolic analysis summary of the supernodal Cholesky plan."""
+        out = np.zeros(cap)
+        self._check(self._L.pgo_debug_plan(self._h, L.dptr(out), cap))
+        keys = ["supernodes", "levels", "nnz_l", "factor_flops", "syrk_flops", "front_doubles",
+                "launches_factor", "launches_solve", "max_front", "trsm_tasks", "syrk_tiles", "small_fronts"]
+        summary = {k: out[i] for i, k in enumerate(keys)}
+        nl = int(out[1])
+        lv = out[16:16 + 6 * nl].reshape(-1, 6)
+        summary["levels_table"] = lv
+        return summary
+
     def debug_solve(self, lam, params=None, **kw):
         p = params if params is not None else default_params(**kw)
         d = np.zeros((self.num_vertices, 3))

@@ -54,6 +54,8 @@ extern "C" {
 #define PGO_ALG_LM 0             /* gtsam::LevenbergMarquardtOptimizer (graph.cpp:119) */
 #define PGO_ALG_GN 1             /* gtsam::GaussNewtonOptimizer                      */
 #define PGO_SOLVER_PCG 0         /* block-Jacobi preconditioned CG on the 3x3 BSR H  */
+#define PGO_SOLVER_CHOLESKY 1    /* supernodal multifrontal Cholesky on the GPU (exact,
+                                    like GTSAM's multifrontal elimination)          */
 
 typedef struct pgo_graph pgo_graph;
 
@@ -77,7 +79,7 @@ typedef struct {
   int use_fixed_lambda_factor;  /* [1]    */
   int algorithm;                /* [PGO_ALG_LM] */
   /* linear solver (the GPU replacement for GTSAM's multifrontal Cholesky) */
-  int linear_solver;            /* [PGO_SOLVER_PCG] */
+  int linear_solver;            /* [PGO_SOLVER_CHOLESKY] */
   double pcg_relative_tol;      /* stop when r'M^-1 r <= tol^2 * r0'M^-1 r0 [1e-10] */
   int pcg_max_iterations;       /* [20000] */
   int pcg_check_interval;       /* iterations enqueued between convergence reads [32] */
@@ -85,6 +87,7 @@ typedef struct {
   int profile_every;            /* >0: time every k-th PCG SpMV launch and every
                                    linearisation with HIP events on the handle's
                                    stream (pgo_stats.kernel_*) [0] */
+  int use_graphs;               /* replay the captured factor+solve hipGraph [1] */
 } pgo_params;
 
 typedef struct {
@@ -104,7 +107,11 @@ typedef struct {
   long long kernel_spmv_count;  /* number of timed SpMV launches                   */
   double kernel_linearize_ms;   /* summed device time of the linearisation kernel  */
   long long kernel_linearize_count;
-  double reserved[4];
+  double kernel_syrk_ms;        /* summed device time of Schur-update (MFMA) launches
+                                   of the profiled factorisations                  */
+  long long kernel_syrk_count;  /* profiled factorisations                         */
+  double syrk_flops;            /* Schur-update flops of one factorisation         */
+  double factor_flops;          /* flops of one numeric factorisation              */
 } pgo_stats;
 
 /* ---- lifetime ------------------------------------------------------------ */
@@ -158,6 +165,12 @@ int pgo_debug_spmv(pgo_graph *g, double lambda, const double *x, double *y);
 /* delta = PCG solve of (H + lambda I) delta = -g at the current values */
 int pgo_debug_solve(pgo_graph *g, double lambda, const pgo_params *params, double *delta,
                     int *pcg_iterations);
+/* Host-only symbolic analysis of the current graph (no device needed):
+ * out[0..11] = supernodes, levels, nnz(L), factor flops, Schur-update flops,
+ * front doubles, launches per factorisation, launches per solve, max front,
+ * trsm tasks, syrk tiles, small fronts; from out[16], 6 per level (leaves first):
+ * fronts, max m, max 64-blocks, panel steps, small fronts, syrk tiles. */
+int pgo_debug_plan(pgo_graph *g, double *out, int cap);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,8 @@
+#!/bin/bash
+# Development loop on the GPU box: selected parity tests, then a kernel-trace of one bench step.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -x -k "${PYTEST_K:-cholesky or lm_parity or c3 or smoke}" > gpurun_out/pytest_dev.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_dev.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+TAG=${TAG:-dev} bash scripts/gpu_trace.sh
