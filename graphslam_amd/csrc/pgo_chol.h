@@ -24,12 +24,13 @@ namespace pgo {
 constexpr int kSmallFront = 128;   // m <= this: whole front factorised in LDS by one workgroup
 constexpr int kNB = 64;            // panel width of the blocked path
 constexpr int kTile = 64;          // Schur-update output tile
+constexpr int kKB = 256;           // Schur-update depth: trailing matrix updated once per kKB columns
 
 struct PanelStep {                 // one panel of the blocked path, all big fronts of a level
   int kb;
   int potrf_off, potrf_cnt;        // fronts whose diagonal tile is factored (potrf_list)
   int trsm_off, trsm_cnt;          // tasks (front, row chunk) in trsm_tasks
-  int syrk_off, syrk_cnt;          // tasks (front, tile) in syrk_tasks
+  int syrk_off, syrk_cnt;          // tasks in syrk_tasks: (front, row0, col0, k0 | inner<<31)
   double syrk_flops;               // algorithmic flops of this step's Schur updates (lower triangles)
 };
 
@@ -60,6 +61,7 @@ struct CholPlan {
   std::vector<int> sfirst;         // [ns+1] first pose (new index) of each supernode
   std::vector<int> m, w;           // scalar front rows / pivot columns
   std::vector<long long> foff;     // [ns+1] front offsets (doubles)
+  std::vector<long long> toff;     // [ns+1] offsets of the inverted 64x64 diagonal blocks (doubles)
   std::vector<int> voff;           // [ns+1] frontal-vector offsets (doubles)
   std::vector<int> rptr, rows;     // front row poses (new index): own poses, then below rows
   std::vector<int> parent, height;
@@ -72,25 +74,29 @@ struct CholPlan {
   // schedules
   std::vector<CholLevel> levels;
   std::vector<int> small_list, level_fronts, potrf_list;
-  std::vector<int2> trsm_tasks, syrk_tasks;
+  std::vector<int2> trsm_tasks;
+  std::vector<int4> syrk_tasks;
   std::vector<int4> fwd_tasks, bwd_tasks;
   std::vector<int> ea_children;    // child front ids grouped per (level, rank)
   std::vector<long long> ea_colpref; // per group: prefix of update-matrix columns (3*below rows)
   double flops = 0, nnzl = 0, syrk_flops = 0;
-  long long ftotal = 0;
+  long long ftotal = 0, ttotal = 0;
   int vtotal = 0;
 
   // ---- device copies ----
   double* F = nullptr;             // fronts
+  double* Tinv = nullptr;          // inverses of the diagonal 64-blocks, column-major 64x64 each
   double* fv = nullptr;            // frontal vectors (solve)
   double* xv = nullptr;            // permuted rhs / solution, 3n
   int *d_m = nullptr, *d_w = nullptr, *d_voff = nullptr, *d_rptr = nullptr, *d_rows = nullptr;
   long long* d_foff = nullptr;
+  long long* d_toff = nullptr;
   int *d_cptr = nullptr, *d_children = nullptr, *d_ea_rel = nullptr, *d_ea_ptr = nullptr, *d_parent = nullptr;
   int *d_asm_front = nullptr, *d_asm_li = nullptr, *d_asm_lj = nullptr, *d_asm_ptr = nullptr, *d_asm_src = nullptr;
   int *d_dg_front = nullptr, *d_dg_loc = nullptr, *d_perm = nullptr;
   int *d_small = nullptr, *d_level_fronts = nullptr, *d_potrf = nullptr;
-  int2 *d_trsm = nullptr, *d_syrk = nullptr;
+  int2* d_trsm = nullptr;
+  int4* d_syrk = nullptr;
   int4 *d_fwd = nullptr, *d_bwd = nullptr;
   int* d_ea_children = nullptr;
   long long* d_ea_colpref = nullptr;

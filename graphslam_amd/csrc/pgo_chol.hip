@@ -24,6 +24,8 @@ namespace pgo {
 
 struct CholDev {
   double* F;
+  double* Tinv;
+  const long long* toff;
   double* fv;
   double* xv;
   const int *m, *w, *voff, *rptr, *rows;
@@ -36,7 +38,7 @@ struct CholDev {
 
 static CholDev dev_view(const CholPlan& P) {
   CholDev c;
-  c.F = P.F; c.fv = P.fv; c.xv = P.xv;
+  c.F = P.F; c.fv = P.fv; c.xv = P.xv; c.Tinv = P.Tinv; c.toff = P.d_toff;
   c.m = P.d_m; c.w = P.d_w; c.voff = P.d_voff; c.rptr = P.d_rptr; c.rows = P.d_rows; c.foff = P.d_foff;
   c.cptr = P.d_cptr; c.children = P.d_children; c.ea_rel = P.d_ea_rel; c.ea_ptr = P.d_ea_ptr;
   c.parent = P.d_parent;
@@ -124,6 +126,45 @@ __global__ __launch_bounds__(256) void k_extend_add(CholDev c, const int* __rest
   for (; a < u; a += 64) Fp[3 * rel[a / 3] + a % 3] += U[a];
 }
 
+// ------------------------------------------------------------ triangular inverse
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// X = L^-1 of an LDS-resident lower-triangular nbk x nbk block (element (r,c) at
+// L[r + c*ld]), by the 4 waves of a workgroup: wave wv owns columns 16wv..16wv+15,
+// lane i row i; column-oriented substitution, row k broadcast with v_readlane
+// (no LDS round trip on the dependency chain).  dinv: LDS scratch of 64.
+// Written column-major to M (M[a*64 + b] = X[b][a]), zero outside nbk x nbk.
+__device__ __forceinline__ void tri_inverse_wg(const double* L, int ld, int nbk, double* __restrict__ M,
+                                               double* dinv) {
+  const int tid = threadIdx.x;
+  if (tid < 64) dinv[tid] = tid < nbk ? 1.0 / L[tid + tid * ld] : 1.0;
+  __syncthreads();
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), i = tid & 63;
+  const int j0 = 16 * wv;
+  double xr[16];
+#pragma unroll
+  for (int q = 0; q < 16; q++) xr[q] = (i == j0 + q) ? 1.0 : 0.0;
+#pragma unroll
+  for (int k = 0; k < 64; k++) {
+    if (k < j0 || k >= nbk) continue;     // wave-uniform
+    const double dk = dinv[k];
+    const double lik = (i > k && i < nbk) ? L[i + k * ld] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      const double b = readlane_f64(xr[q], k) * dk;
+      xr[q] = (i == k) ? b : fma(-lik, b, xr[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 16; q++) M[(j0 + q) * 64 + i] = (i < nbk && j0 + q < nbk) ? xr[q] : 0.0;
+  __syncthreads();  // dinv reusable
+}
+
 // ------------------------------------------------------------ small fronts (LDS)
 // m <= 128: the whole front in LDS; right-looking, two threads per row (the
 // row's columns split even/odd) so LDS accesses of a wave are consecutive rows.
@@ -157,132 +198,178 @@ __global__ __launch_bounds__(256) void k_front_small(CholDev c, const int* __res
   }
   for (int j = 0; j < m; j++)
     for (int i = j + tid; i < m; i += 256) Fs[i + (size_t)j * m] = A[i + j * m];
+  // inverses of the 64-column diagonal blocks (used by the solves)
+  double* scratch = A + m * m;
+  for (int jb = 0; jb < w; jb += 64)
+    tri_inverse_wg(A + jb + jb * m, m, min(64, w - jb), c.Tinv + c.toff[s] + (jb / 64) * 4096, scratch);
 }
 
 // ------------------------------------------------------------ blocked path
-// Diagonal tile (nb x nb at kb) of each listed front, factored in place by ONE
-// wave: lane i keeps row i in registers; column j is broadcast through LDS.
-__global__ __launch_bounds__(64) void k_panel_potrf(CholDev c, const int* __restrict__ list, int kb) {
-  __shared__ double col[kNB];
+// Diagonal tile of each listed front at panel kb: factored in place by the 4
+// waves (thread (wave cg, lane i) keeps T[i][4q+cg], q < 16, in registers;
+// column j is finished by its owning wave and broadcast through a double-
+// buffered LDS column; the tile is padded with the identity beyond nb so every
+// step is unconditional), then inverted into Tinv for the TRSM GEMM and solves.
+__global__ __launch_bounds__(256) void k_panel_diag(CholDev c, const int* __restrict__ list, int kb) {
+  __shared__ double Ts[64 * 65];
+  __shared__ double colb[2][64];
+  __shared__ double dinv[64];
   const int s = list[blockIdx.x];
   const int m = c.m[s], w = c.w[s];
   const int nb = min(kNB, w - kb);
   double* Fs = c.F + c.foff[s] + kb + (size_t)kb * m;
-  const int i = threadIdx.x;
-  double a[kNB];
+  const int tid = threadIdx.x;
+  const int i = tid & 63, cg = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double a[16];
 #pragma unroll
-  for (int k = 0; k < kNB; k++) a[k] = (k <= i && i < nb && k < nb) ? Fs[i + (size_t)k * m] : 0.0;
+  for (int q = 0; q < 16; q++) {
+    const int k = 4 * q + cg;
+    a[q] = (i < nb && k < nb) ? (k <= i ? Fs[i + (size_t)k * m] : 0.0) : (i == k ? 1.0 : 0.0);
+  }
   bool bad = false;
 #pragma unroll
-  for (int j = 0; j < kNB; j++) {
-    if (j < nb) {
-      double d = __shfl(a[j], j);
+  for (int j = 0; j < 64; j++) {
+    const int qj = j >> 2;
+    double* cb = colb[j & 1];
+    if (cg == (j & 3)) {
+      double d = readlane_f64(a[qj], j);
       if (!(d > 0.0) || !isfinite(d)) {
         bad = true;
         d = 1.0;
       }
       const double piv = sqrt(d), inv = 1.0 / piv;
-      const double l = i > j ? a[j] * inv : (i == j ? piv : 0.0);
-      a[j] = l;
-      col[i] = l;
-      __syncthreads();
-#pragma unroll
-      for (int k = j + 1; k < kNB; k++) a[k] -= l * col[k];
-      __syncthreads();
+      const double l = i > j ? a[qj] * inv : (i == j ? piv : 0.0);
+      a[qj] = l;
+      cb[i] = l;
     }
+    __syncthreads();
+    const double li = cb[i];
+#pragma unroll
+    for (int q = 0; q < 16; q++)
+      if (4 * q + cg > j) a[q] -= li * cb[4 * q + cg];
   }
   if (bad && i == 0) *c.flag = 1;
 #pragma unroll
-  for (int k = 0; k < kNB; k++)
-    if (k <= i && i < nb && k < nb) Fs[i + (size_t)k * m] = a[k];
+  for (int q = 0; q < 16; q++) Ts[i + (4 * q + cg) * 65] = a[q];
+  __syncthreads();
+  tri_inverse_wg(Ts, 65, nb, c.Tinv + c.toff[s] + (kb / 64) * 4096, dinv);
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    const int k = 4 * q + cg;
+    if (i < nb && k < nb && k <= i) Fs[i + (size_t)k * m] = a[q];
+  }
 }
 
-// Rows [r0, r0+256) below the factored diagonal tile: X = B L^-T, one row per
-// thread in registers, right-looking (the FMAs of a step are independent).
+// Rows below the diagonal tile, 64 per workgroup (16 per wave): X = B L^-T as a
+// GEMM with the inverted tile, v_mfma_f64_16x16x4_f64, B fragments from global.
 __global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __restrict__ tasks, int kb) {
-  __shared__ double T[kNB * (kNB + 1)];
-  __shared__ double dinv[kNB];
+  constexpr int LDB = 80;
+  __shared__ __attribute__((aligned(16))) double Tb[64 * LDB];  // Tb[k*LDB + j] = Tinv[j][k]
   const int2 task = tasks[blockIdx.x];
   const int s = task.x, chunk = task.y;
   const int m = c.m[s], w = c.w[s];
   const int nb = min(kNB, w - kb);
-  double* Fs = c.F + c.foff[s];
+  const double* M = c.Tinv + c.toff[s] + (kb / 64) * 4096;
   const int tid = threadIdx.x;
-  const int ld = kNB + 1;
-  for (int idx = tid; idx < nb * nb; idx += 256) {
-    const int i = idx % nb, j = idx / nb;
-    T[i + j * ld] = i >= j ? Fs[(kb + i) + (size_t)(kb + j) * m] : 0.0;
+  for (int idx = tid; idx < 4096; idx += 256) Tb[(idx >> 6) * LDB + (idx & 63)] = M[idx];
+  __syncthreads();
+  const int wv = tid >> 6, l = tid & 63;
+  const int r0 = kb + nb + chunk * 64 + wv * 16;
+  if (r0 >= m) return;
+  double* Fc = c.F + c.foff[s] + (size_t)kb * m;   // column kb of the front
+  const int arow = r0 + (l & 15), kl = l >> 4;
+  double a[16];
+#pragma unroll
+  for (int ks = 0; ks < 16; ks++) {
+    const int k = 4 * ks + kl;
+    a[ks] = (arow < m && k < nb) ? Fc[arow + (size_t)k * m] : 0.0;
   }
-  __syncthreads();
-  if (tid < nb) dinv[tid] = 1.0 / T[tid + tid * ld];
-  __syncthreads();
-  const int row = kb + nb + chunk * 256 + tid;
-  if (row >= m) return;
-  double x[kNB];
+  d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0}, acc3 = {0, 0, 0, 0};
 #pragma unroll
-  for (int k = 0; k < kNB; k++) x[k] = k < nb ? Fs[row + (size_t)(kb + k) * m] : 0.0;
+  for (int ks = 0; ks < 16; ks++) {
+    const double* tb = Tb + (4 * ks + kl) * LDB + (l & 15);
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[0], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[16], acc1, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[32], acc2, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[48], acc3, 0, 0, 0);
+  }
 #pragma unroll
-  for (int k = 0; k < kNB; k++) {
-    if (k < nb) {
-      x[k] *= dinv[k];
+  for (int ct = 0; ct < 4; ct++) {
+    const d4 v = ct == 0 ? acc0 : (ct == 1 ? acc1 : (ct == 2 ? acc2 : acc3));
+    const int col = 16 * ct + (l & 15);
+    if (col >= nb) continue;
 #pragma unroll
-      for (int t = k + 1; t < kNB; t++) x[t] -= x[k] * T[t + k * ld];
+    for (int r = 0; r < 4; r++) {
+      const int row = r0 + kl + 4 * r;
+      if (row < m) Fc[row + (size_t)col * m] = v[r];
     }
   }
-#pragma unroll
-  for (int k = 0; k < kNB; k++)
-    if (k < nb) Fs[row + (size_t)(kb + k) * m] = x[k];
 }
 
-// Schur update of one 64x64 lower tile of the trailing matrix:
-// C[ti,tj] -= P_i P_j^T, P = F[r0:, kb:kb+nb], r0 = kb + nb.
-__global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int2* __restrict__ tasks, int kb) {
-  constexpr int LD = kTile + 16;  // [k][r] with an 80-double row: lanes l and l+16 on different banks
-  __shared__ __attribute__((aligned(16))) double Pi[kNB * LD];
-  __shared__ __attribute__((aligned(16))) double Pj[kNB * LD];
-  const int2 task = tasks[blockIdx.x];
-  const int s = task.x, ti = task.y >> 16, tj = task.y & 0xffff;
+// Schur update of one 64x64 lower tile: C[r0:r0+64, c0:c0+64] -= P_r P_c^T with
+// P = F[:, k0:kend), kend = end of the current panel (depth <= kKB).  Each wave
+// owns 32x32 of the tile as 2x2 v_mfma_f64_16x16x4_f64 blocks, operands straight
+// from global (the panel columns are L2-resident); the product is formed
+// transposed (A = column-side rows) so each store covers 16 consecutive rows.
+// Inner tasks (bit 31 of k0) clip columns at the end of the current kKB block.
+__global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int4* __restrict__ tasks, int kb) {
+  const int4 t = tasks[blockIdx.x];
+  const int s = t.x, row0 = t.y, col0 = t.z;
+  const bool inner = t.w < 0;
+  const int k0 = t.w & 0x7fffffff;
   const int m = c.m[s], w = c.w[s];
-  const int nb = min(kNB, w - kb);
-  const int r0 = kb + nb;
-  const int ri = r0 + ti * kTile, rj = r0 + tj * kTile;
-  const double* Fs = c.F + c.foff[s];
-  const int tid = threadIdx.x;
-  const int K = (nb + 3) & ~3;
-  for (int idx = tid; idx < K * kTile; idx += 256) {
-    const int k = idx / kTile, r = idx % kTile;
-    const bool kin = k < nb;
-    Pi[k * LD + r] = (kin && ri + r < m) ? Fs[(ri + r) + (size_t)(kb + k) * m] : 0.0;
-    Pj[k * LD + r] = (kin && rj + r < m) ? Fs[(rj + r) + (size_t)(kb + k) * m] : 0.0;
-  }
-  __syncthreads();
-  const int wv = tid >> 6, lane = tid & 63;
+  const int kend = min(kb + kNB, w);
+  const int colend = inner ? min((kb & ~(kKB - 1)) + kKB, w) : m;
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int qi = 32 * (wv >> 1), qj = 32 * (wv & 1);
-  const int kl = lane >> 4, rl = lane & 15;
+  if (row0 == col0 && qi < qj) return;       // strictly upper quarter of a diagonal tile
+  const int li = l & 15, lk = l >> 4;
+  double* Fs = c.F + c.foff[s];
+  const int rA = row0 + qi + li, rB = rA + 16;          // C rows (B operand rows)
+  const int cA = col0 + qj + li, cB = cA + 16;          // C columns (A operand rows)
+  // C prefetch (output layout: lane l, reg r -> column col0+qj+16mj+lk+4r, row row0+qi+16mi+li)
+  double cold[2][2][4];
+#pragma unroll
+  for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+    for (int mj = 0; mj < 2; mj++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = row0 + qi + 16 * mi + li, col = col0 + qj + 16 * mj + lk + 4 * r;
+        cold[mi][mj][r] = (row < m && col < colend && row >= col) ? Fs[row + (size_t)col * m] : 0.0;
+      }
+  const bool vrA = rA < m, vrB = rB < m, vcA = cA < m, vcB = cB < m;
+  const double* P = Fs + (size_t)(k0 + lk) * m;
   d4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
-  for (int k0 = 0; k0 < K; k0 += 4) {
-    const double* pa = Pi + (k0 + kl) * LD + qi + rl;
-    const double* pb = Pj + (k0 + kl) * LD + qj + rl;
-    const double a0 = pa[0], a1 = pa[16], b0 = pb[0], b1 = pb[16];
-    acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc00, 0, 0, 0);
-    acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc01, 0, 0, 0);
-    acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc10, 0, 0, 0);
-    acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc11, 0, 0, 0);
+  const int K = kend - k0;
+  for (int kk = 0; kk < K; kk += 16) {       // 16 operand loads in flight, then 16 MFMAs
+    double ra[4], rb[4], ca[4], cb[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const bool kin = kk + 4 * u + lk < K;
+      const double* pk = P + (size_t)(kk + 4 * u) * m;
+      ra[u] = (kin && vrA) ? pk[rA] : 0.0;
+      rb[u] = (kin && vrB) ? pk[rB] : 0.0;
+      ca[u] = (kin && vcA) ? pk[cA] : 0.0;
+      cb[u] = (kin && vcB) ? pk[cB] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[u], ra[u], acc00, 0, 0, 0);  // [mj=0][mi=0]
+      acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[u], rb[u], acc01, 0, 0, 0);  // [mj=0][mi=1]
+      acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(cb[u], ra[u], acc10, 0, 0, 0);  // [mj=1][mi=0]
+      acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(cb[u], rb[u], acc11, 0, 0, 0);  // [mj=1][mi=1]
+    }
   }
-  // D layout (f64 16x16x4): lane l, reg r -> row (l>>4) + 4r, col l&15
-  double* Fw = c.F + c.foff[s];
-  const int col0 = rj + qj + rl;
 #pragma unroll
   for (int mi = 0; mi < 2; mi++)
 #pragma unroll
     for (int mj = 0; mj < 2; mj++) {
-      const d4 a = mi == 0 ? (mj == 0 ? acc00 : acc01) : (mj == 0 ? acc10 : acc11);
-      const int col = col0 + 16 * mj;
-      if (col >= m) continue;
+      const d4 a = mj == 0 ? (mi == 0 ? acc00 : acc01) : (mi == 0 ? acc10 : acc11);
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        const int row = ri + qi + 16 * mi + kl + 4 * r;
-        if (row < m && row >= col) Fw[row + (size_t)col * m] -= a[r];
+        const int row = row0 + qi + 16 * mi + li, col = col0 + qj + 16 * mj + lk + 4 * r;
+        if (row < m && col < colend && row >= col) Fs[row + (size_t)col * m] = cold[mi][mj][r] - a[r];
       }
     }
 }
@@ -304,33 +391,24 @@ __global__ __launch_bounds__(256) void k_perm_out(CholDev c, double* __restrict_
   for (int a = 0; a < 3; a++) x[3 * o + a] = c.xv[3 * j + a];
 }
 
-// Diagonal-block solves by wave 0 of a workgroup, the 64x64 block staged in
-// LDS (Ld[i + k*65]); v holds the right-hand side (lane i <-> row i).
-__device__ __forceinline__ void stage_diag(const double* L, int m, int jb, int nbk, double* Ld) {
-  for (int idx = threadIdx.x; idx < nbk * nbk; idx += blockDim.x) {
-    const int i = idx % nbk, k = idx / nbk;
-    Ld[i + k * 65] = i >= k ? L[(jb + i) + (size_t)(jb + k) * m] : 0.0;
-  }
+// Diagonal-block solves with the inverted blocks: wave 0, lane i <-> row i.
+// y = X v (forward, X = L_bb^-1) and x = X' z (backward); v / z in LDS.
+__device__ __forceinline__ double tinv_fwd(const double* __restrict__ M, const double* v, int nbk) {
+  const int i = threadIdx.x;
+  double acc = 0.0;
+  for (int k = 0; k < nbk; k++) acc += M[k * 64 + i] * v[k];  // column k of X: coalesced
+  return acc;
 }
 
-__device__ __forceinline__ double diag_fwd(double v, const double* Ld, int nbk) {  // wave 0 only
+__device__ __forceinline__ double tinv_bwd(const double* Ms, const double* z, int nbk) {  // Ms: LDS, Ms[a*65+b]
   const int i = threadIdx.x;
-  for (int k = 0; k < nbk; k++) {
-    const double xk = __shfl(v, k) / Ld[k + k * 65];
-    if (i == k) v = xk;
-    else if (i > k) v -= Ld[i + k * 65] * xk;
-  }
-  return v;
+  double acc = 0.0;
+  for (int k = 0; k < nbk; k++) acc += Ms[i * 65 + k] * z[k];
+  return acc;
 }
 
-__device__ __forceinline__ double diag_bwd(double v, const double* Ld, int nbk) {  // wave 0 only
-  const int i = threadIdx.x;
-  for (int k = nbk - 1; k >= 0; k--) {
-    const double xk = __shfl(v, k) / Ld[k + k * 65];
-    if (i == k) v = xk;
-    else if (i < k) v -= Ld[k + i * 65] * xk;
-  }
-  return v;
+__device__ __forceinline__ void stage_tinv(const double* __restrict__ M, double* Ms) {
+  for (int idx = threadIdx.x; idx < 4096; idx += blockDim.x) Ms[(idx >> 6) * 65 + (idx & 63)] = M[idx];
 }
 
 // Forward, launch 1 of a level: frontal vector = (own rhs, 0) + children's update
@@ -341,12 +419,10 @@ __global__ __launch_bounds__(256) void k_fwd_assemble(CholDev c, const int* __re
   double* v = sm + 64 * 65;        // m
   const int s = list[blockIdx.x];
   const int m = c.m[s], w = c.w[s];
-  const double* L = c.F + c.foff[s];
   const int* rows = c.rows + c.rptr[s];
   const int tid = threadIdx.x;
   for (int r = tid; r < m; r += 256) v[r] = r < w ? c.xv[3 * rows[r / 3] + r % 3] : 0.0;
   const int nbk = min(64, w);
-  stage_diag(L, m, 0, nbk, Ld);
   __syncthreads();
   for (int q = c.cptr[s]; q < c.cptr[s + 1]; q++) {
     const int ch = c.children[q];
@@ -357,9 +433,11 @@ __global__ __launch_bounds__(256) void k_fwd_assemble(CholDev c, const int* __re
     __syncthreads();
   }
   if (tid < 64) {
-    const double y = diag_fwd(tid < nbk ? v[tid] : 0.0, Ld, nbk);
-    if (tid < nbk) v[tid] = y;
+    const double y = tinv_fwd(c.Tinv + c.toff[s], v, nbk);
+    Ld[tid] = y;
   }
+  __syncthreads();
+  if (tid < nbk) v[tid] = Ld[tid];
   __syncthreads();
   double* fv = c.fv + c.voff[s];
   for (int r = tid; r < m; r += 256) fv[r] = v[r];
@@ -368,7 +446,6 @@ __global__ __launch_bounds__(256) void k_fwd_assemble(CholDev c, const int* __re
 // Forward step b: rows [r0, r1) -= L[r, block b] y_b; the task owning the next
 // diagonal block (rows of block b+1) then solves it.
 __global__ __launch_bounds__(256) void k_fwd_step(CholDev c, const int4* __restrict__ tasks, int b) {
-  __shared__ double Ld[64 * 65];
   __shared__ double y[64];
   __shared__ double vn[64];
   const int4 t = tasks[blockIdx.x];
@@ -379,7 +456,6 @@ __global__ __launch_bounds__(256) void k_fwd_step(CholDev c, const int4* __restr
   const int tid = threadIdx.x;
   const int jb = b * 64, nbk = min(64, w - jb);
   if (tid < nbk) y[tid] = fv[jb + tid];
-  if (owner >= 0) stage_diag(L, m, owner * 64, r1 - r0, Ld);
   __syncthreads();
   const int r = r0 + tid;
   if (r < r1) {
@@ -393,7 +469,8 @@ __global__ __launch_bounds__(256) void k_fwd_step(CholDev c, const int4* __restr
   __syncthreads();
   if (tid < 64) {
     const int n2 = r1 - r0;
-    const double yy = diag_fwd(tid < n2 ? vn[tid] : 0.0, Ld, n2);
+    if (tid >= n2) vn[tid] = 0.0;
+    const double yy = tinv_fwd(c.Tinv + c.toff[s] + owner * 4096, vn, n2);
     if (tid < n2) fv[r0 + tid] = yy;
   }
 }
@@ -413,7 +490,7 @@ __global__ __launch_bounds__(256) void k_bwd_init(CholDev c, const int4* __restr
   const int* rows = c.rows + c.rptr[s];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int r = w + tid; r < m; r += 256) xb[r - w] = c.xv[3 * rows[r / 3] + r % 3];
-  if (owner >= 0) stage_diag(L, m, c0, c1 - c0, Ld);
+  if (owner >= 0) stage_tinv(c.Tinv + c.toff[s] + owner * 4096, Ld);
   __syncthreads();
   // L21[:, c0:c1]' x_below: thread (wave wv, lane) owns rows w + lane + 64 (wv + 4 t),
   // keeps one partial per column (<= 64), loads of a row chunk all in flight
@@ -447,7 +524,7 @@ __global__ __launch_bounds__(256) void k_bwd_init(CholDev c, const int4* __restr
   }
   if (tid < 64) {
     const int n2 = c1 - c0;
-    const double x = diag_bwd(tid < n2 ? z[tid] : 0.0, Ld, n2);
+    const double x = tinv_bwd(Ld, z, n2);
     if (tid < n2) {
       fv[c0 + tid] = x;
       c.xv[3 * rows[(c0 + tid) / 3] + (c0 + tid) % 3] = x;
@@ -470,7 +547,7 @@ __global__ __launch_bounds__(256) void k_bwd_step(CholDev c, const int4* __restr
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int jb = b * 64, nbk = min(64, w - jb);
   if (tid < nbk) xbk[tid] = fv[jb + tid];
-  if (owner >= 0) stage_diag(L, m, c0, c1 - c0, Ld);
+  if (owner >= 0) stage_tinv(c.Tinv + c.toff[s] + owner * 4096, Ld);
   __syncthreads();
   // wave wv: columns c0 + wv + 4q, q < 16; all 16 loads issued before the reductions
   double part[16];
@@ -495,7 +572,7 @@ __global__ __launch_bounds__(256) void k_bwd_step(CholDev c, const int4* __restr
   }
   if (tid < 64) {
     const int n2 = c1 - c0;
-    const double x = diag_bwd(tid < n2 ? z[tid] : 0.0, Ld, n2);
+    const double x = tinv_bwd(Ld, z, n2);
     if (tid < n2) {
       fv[c0 + tid] = x;
       c.xv[3 * rows[(c0 + tid) / 3] + (c0 + tid) % 3] = x;
@@ -520,6 +597,8 @@ static hipError_t up(T** d, const std::vector<T>& h, hipStream_t s) {
 
 hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(hipMalloc((void**)&P.F, std::max<long long>(P.ftotal, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.Tinv, std::max<long long>(P.ttotal, 1) * sizeof(double)));
+  CH_TRY(up(&P.d_toff, P.toff, s));
   CH_TRY(hipMalloc((void**)&P.fv, std::max(P.vtotal, 1) * sizeof(double)));
   CH_TRY(hipMalloc((void**)&P.xv, std::max(3 * P.n, 1) * sizeof(double)));
   CH_TRY(hipMalloc((void**)&P.d_flag, sizeof(int)));
@@ -556,7 +635,7 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
 }
 
 void chol_free(CholPlan& P) {
-  void* ptrs[] = {P.F, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
+  void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
                   P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
                   P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
                   P.d_trsm, P.d_syrk, P.d_ea_children, P.d_ea_colpref, P.d_potrf, P.d_fwd, P.d_bwd};
@@ -582,16 +661,16 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, hipS
                                                     P.d_ea_colpref + lv.ea_cols_off[r], lv.ea_cnt[r]);
     }
     for (const SmallClass& sc : lv.small)
-      k_front_small<<<sc.cnt, 256, (size_t)sc.mmax * sc.mmax * sizeof(double), s>>>(c, P.d_small + sc.off);
+      k_front_small<<<sc.cnt, 256, (size_t)(sc.mmax * sc.mmax + 64) * sizeof(double), s>>>(c, P.d_small + sc.off);
     for (const PanelStep& ps : lv.panels) {
-      k_panel_potrf<<<ps.potrf_cnt, 64, 0, s>>>(c, P.d_potrf + ps.potrf_off, ps.kb);
+      k_panel_diag<<<ps.potrf_cnt, 256, 0, s>>>(c, P.d_potrf + ps.potrf_off, ps.kb);
       if (ps.trsm_cnt) k_panel_trsm<<<ps.trsm_cnt, 256, 0, s>>>(c, P.d_trsm + ps.trsm_off, ps.kb);
       if (!ps.syrk_cnt) continue;
       if (prof && prof->used < prof->cap) {
         const int u = prof->used++;
         prof->flops[u] = ps.syrk_flops;
         hipExtLaunchKernelGGL(k_panel_syrk, dim3(ps.syrk_cnt), dim3(256), 0, s, prof->ev[2 * u], prof->ev[2 * u + 1], 0,
-                              c, (const int2*)(P.d_syrk + ps.syrk_off), ps.kb);
+                              c, (const int4*)(P.d_syrk + ps.syrk_off), ps.kb);
       } else {
         k_panel_syrk<<<ps.syrk_cnt, 256, 0, s>>>(c, P.d_syrk + ps.syrk_off, ps.kb);
       }

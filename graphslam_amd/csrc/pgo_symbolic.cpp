@@ -289,6 +289,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.m.resize(ns);
   P.w.resize(ns);
   P.foff.assign(ns + 1, 0);
+  P.toff.assign(ns + 1, 0);
   P.voff.assign(ns + 1, 0);
   P.flops = 0;
   P.nnzl = 0;
@@ -300,6 +301,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     const long long mm = P.m[s];
     P.foff[s + 1] = P.foff[s] + ((mm * mm + 7) / 8) * 8;   // 64-byte aligned fronts
     P.voff[s + 1] = P.voff[s] + ((P.m[s] + 7) / 8) * 8;
+    P.toff[s + 1] = P.toff[s] + (long long)((P.w[s] + 63) / 64) * 4096;
     for (int k = 0; k < P.w[s]; k++) {
       const double r = P.m[s] - k - 1;
       P.flops += 1 + r + r * (r + 1);
@@ -307,6 +309,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     }
   }
   P.ftotal = P.foff[ns];
+  P.ttotal = P.toff[ns];
   P.vtotal = P.voff[ns];
   P.rows.resize(P.rptr[ns]);
   for (int s = 0; s < ns; s++) {
@@ -493,13 +496,23 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
         P.potrf_list.push_back(s);
         const int nb = std::min(kNB, P.w[s] - kb);
         const int below_rows = P.m[s] - kb - nb;
-        const int chunks = (below_rows + 255) / 256;
+        const int chunks = (below_rows + 63) / 64;
         for (int c = 0; c < chunks; c++) P.trsm_tasks.push_back(make_int2(s, c));
-        if (below_rows > 0) {
-          ps.syrk_flops += (double)below_rows * (below_rows + 1.0) * nb;
-          const int nt = (below_rows + kTile - 1) / kTile;
-          for (int ti = 0; ti < nt; ti++)
-            for (int tj = 0; tj <= ti; tj++) P.syrk_tasks.push_back(make_int2(s, (ti << 16) | tj));
+        // Schur updates, blocked by kKB columns: within a block only the block's
+        // remaining columns are updated per 64-column panel ("inner"); after the
+        // block's last panel the trailing matrix gets one update of depth <= kKB
+        const int bs = kb & ~(kKB - 1), be = std::min(bs + kKB, P.w[s]);
+        const int m = P.m[s];
+        if (kb + nb < be) {
+          for (int c0 = kb + nb; c0 < be; c0 += kTile) {
+            for (int cc = c0; cc < std::min(c0 + kTile, be); cc++) ps.syrk_flops += 2.0 * nb * (m - cc);
+            for (int r0 = c0; r0 < m; r0 += kTile) P.syrk_tasks.push_back(make_int4(s, r0, c0, kb | (int)0x80000000));
+          }
+        } else if (be < m) {
+          const double K = kb + nb - bs, t = m - be;
+          ps.syrk_flops += K * t * (t + 1.0);
+          for (int c0 = be; c0 < m; c0 += kTile)
+            for (int r0 = c0; r0 < m; r0 += kTile) P.syrk_tasks.push_back(make_int4(s, r0, c0, bs));
         }
       }
       ps.potrf_cnt = (int)P.potrf_list.size() - ps.potrf_off;
