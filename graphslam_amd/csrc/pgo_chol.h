@@ -24,7 +24,8 @@ namespace pgo {
 constexpr int kSmallFront = 128;   // m <= this: whole front factorised in LDS by one workgroup
 constexpr int kNB = 64;            // panel width of the blocked path
 constexpr int kTile = 64;          // Schur-update output tile
-constexpr int kKB = 256;           // Schur-update depth: trailing matrix updated once per kKB columns
+constexpr int kKB = 256;
+constexpr int kBwdRows = 512;      // rows per partial product of the backward solve           // Schur-update depth: trailing matrix updated once per kKB columns
 
 struct PanelStep {                 // one panel of the blocked path, all big fronts of a level
   int kb;
@@ -52,6 +53,7 @@ struct CholLevel {
   int maxblk = 0;                  // max 64-column blocks of a front's pivot columns
   std::vector<SolveStep> fwd;      // forward step b = 0 .. maxblk-1 (rows below block b)
   std::vector<SolveStep> bwd;      // backward: [0] = init (all columns), then steps b = maxblk-1 .. 1
+  SolveStep bwd_part{0, 0};        // partial products feeding the init tasks
 };
 
 struct CholPlan {
@@ -77,6 +79,9 @@ struct CholPlan {
   std::vector<int2> trsm_tasks;
   std::vector<int4> syrk_tasks;
   std::vector<int4> fwd_tasks, bwd_tasks;
+  std::vector<int2> bwd_pref;      // per bwd task: first partial, partial count (init tasks)
+  std::vector<int4> bwd_part_tasks;  // (front, c0, r0, partial slot)
+  int npart = 0;
   std::vector<int> ea_children;    // child front ids grouped per (level, rank)
   std::vector<long long> ea_colpref; // per group: prefix of update-matrix columns (3*below rows)
   double flops = 0, nnzl = 0, syrk_flops = 0;
@@ -97,7 +102,9 @@ struct CholPlan {
   int *d_small = nullptr, *d_level_fronts = nullptr, *d_potrf = nullptr;
   int2* d_trsm = nullptr;
   int4* d_syrk = nullptr;
-  int4 *d_fwd = nullptr, *d_bwd = nullptr;
+  int4 *d_fwd = nullptr, *d_bwd = nullptr, *d_bwd_part = nullptr;
+  int2* d_bwd_pref = nullptr;
+  double* d_partial = nullptr;
   int* d_ea_children = nullptr;
   long long* d_ea_colpref = nullptr;
   int* d_flag = nullptr;           // non-positive pivot seen

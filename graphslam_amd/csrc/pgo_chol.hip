@@ -205,58 +205,202 @@ __global__ __launch_bounds__(256) void k_front_small(CholDev c, const int* __res
 }
 
 // ------------------------------------------------------------ blocked path
-// Diagonal tile of each listed front at panel kb: factored in place by the 4
-// waves (thread (wave cg, lane i) keeps T[i][4q+cg], q < 16, in registers;
-// column j is finished by its owning wave and broadcast through a double-
-// buffered LDS column; the tile is padded with the identity beyond nb so every
-// step is unconditional), then inverted into Tinv for the TRSM GEMM and solves.
+// ------------------------------------------------------------ diagonal tile
+__device__ __forceinline__ double rsqrt_nr(double d) {   // 1/sqrt(d), two Newton steps from v_rsq_f64
+  double y = __builtin_amdgcn_rsq(d);
+  y = y * fma(-0.5 * d * y, y, 1.5);
+  y = y * fma(-0.5 * d * y, y, 1.5);
+  return y;
+}
+
+// 16x16x16 product on one wave from LDS: D(i,j) = sum_k A(i,k) B(k,j),
+// A(i,k) = A[i*ars + k*acs], B(k,j) = B[k*brs + j*bcs]; D in the f64 MFMA
+// layout (lane l, reg r -> row (l>>4)+4r, col l&15).
+__device__ __forceinline__ d4 mm16(const double* A, int ars, int acs, const double* B, int brs, int bcs) {
+  const int l = threadIdx.x & 63, i = l & 15, kq = l >> 4;
+  double a[4], b[4];
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    a[t] = A[i * ars + (4 * t + kq) * acs];
+    b[t] = B[(4 * t + kq) * brs + i * bcs];
+  }
+  d4 acc = {0, 0, 0, 0};
+#pragma unroll
+  for (int t = 0; t < 4; t++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t], b[t], acc, 0, 0, 0);
+  return acc;
+}
+
+// C(16x16, ld 65) op= D
+__device__ __forceinline__ void st16(double* C, d4 v, bool sub) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    double* p = C + ((l >> 4) + 4 * r) + (l & 15) * 65;
+    *p = sub ? *p - v[r] : v[r];
+  }
+}
+
+// Cholesky factor L and inverse X = L^-1 of the 64x64 SPD tile T (LDS,
+// column-major, ld 65, lower part valid, identity beyond the live size), by the
+// 4 waves of the workgroup: right-looking over 16-column blocks J; the 16x16
+// diagonal block is factored and inverted by wave 0 (lane (r, g): row r,
+// columns g, g+4, g+8, g+12; column j and row j of the inverse broadcast
+// through LDS), the rest are 16x16x16 MFMA products:
+//   L_IJ = A_IJ X_JJ^T,  X_JK = X_JJ W_JK (K < J),
+//   A_IK -= L_IJ L_KJ^T (K > J),  W_IK -= L_IJ X_JK (K <= J)
+// where W (LDS, ld 65) must hold zeros below the diagonal blocks on entry
+// (the diagonal blocks are written here) and ends as X.
+// Returns (wave 0) whether a pivot was not positive and finite.
+#ifdef PGO_DIAG_CLOCKS
+__device__ long long g_diag_clk[16];
+#define DIAG_CLK(q) if (threadIdx.x == 0 && blockIdx.x == 0) g_diag_clk[q] = clock64()
+#else
+#define DIAG_CLK(q)
+#endif
+__device__ bool diag_factor_invert(double* T, double* W, double* bc) {
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  DIAG_CLK(0);
+  bool bad = false;
+  for (int J = 0; J < 4; J++) {
+    const int o = 16 * J;
+    double* TJ = T + o + o * 65;
+    if (wv == 0) {
+      const int r = l & 15, g = l >> 4;
+      double a[4], x[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int cu = 4 * u + g;
+        a[u] = cu <= r ? TJ[r + cu * 65] : 0.0;
+        x[u] = r == cu ? 1.0 : 0.0;
+      }
+      // pivot chain one step ahead in scalars: d_{j+1} = a(j+1,j+1) - l_{j+1}^2 from
+      // lane values before step j's broadcast, so the rsqrt overlaps the LDS round trip
+      double d = readlane_f64(a[0], 0);
+      if (!(d > 0.0) || !isfinite(d)) {
+        bad = true;
+        d = 1.0;
+      }
+      double inv = rsqrt_nr(d);
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int gj = j & 3, uj = j >> 2;
+        double dn = 1.0, invn = 1.0;
+        if (j < 15) {
+          const int j1 = j + 1, g1 = j1 & 3, u1 = j1 >> 2;
+          const double l1 = readlane_f64(a[uj], j1 + 16 * gj) * inv;
+          dn = fma(-l1, l1, readlane_f64(a[u1], j1 + 16 * g1));
+          if (!(dn > 0.0) || !isfinite(dn)) {
+            bad = true;
+            dn = 1.0;
+          }
+          invn = rsqrt_nr(dn);
+        }
+        if (g == gj) {
+          const double lv = r > j ? a[uj] * inv : 0.0;
+          a[uj] = r == j ? d * inv : lv;
+          bc[r] = lv;
+        }
+        if (r == j) {
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            x[u] *= inv;
+            bc[16 + 4 * u + g] = x[u];
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const double lr = bc[r];
+        double lk[4], xj[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          lk[u] = bc[4 * u + g];
+          xj[u] = bc[16 + 4 * u + g];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          a[u] = fma(-lr, lk[u], a[u]);
+          x[u] = fma(-lr, xj[u], x[u]);
+        }
+        __builtin_amdgcn_wave_barrier();
+        d = dn;
+        inv = invn;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int cu = 4 * u + g;
+        if (cu <= r) TJ[r + cu * 65] = a[u];
+        W[(o + r) + (o + cu) * 65] = cu <= r ? x[u] : 0.0;
+      }
+    }
+    __syncthreads();
+    DIAG_CLK(1 + 3 * J);
+    // phase B: 3 independent products (3-J panel blocks, J blocks of X's row J)
+    if (wv < 3) {
+      if (wv < 3 - J) {
+        const int oi = o + 16 * (wv + 1);
+        const d4 v = mm16(T + oi + o * 65, 1, 65, W + o + o * 65, 65, 1);
+        st16(T + oi + o * 65, v, false);
+      } else {
+        const int ok = 16 * (wv - (3 - J));
+        const d4 v = mm16(W + o + o * 65, 1, 65, W + o + ok * 65, 1, 65);
+        st16(W + o + ok * 65, v, false);
+      }
+    }
+    if (J == 3) break;
+    __syncthreads();
+    DIAG_CLK(2 + 3 * J);
+    // phase C: trailing updates of T and W
+    const int nA = (3 - J) * (4 - J) / 2, nW = (3 - J) * (J + 1);
+    for (int t = wv; t < nA + nW; t += 4) {
+      if (t < nA) {
+        int I = J + 1, q = t;                 // t-th pair J < K <= I
+        while (q >= I - J) {
+          q -= I - J;
+          I++;
+        }
+        const int K = J + 1 + q;
+        const int oi = 16 * I, ok = 16 * K;
+        const d4 v = mm16(T + oi + o * 65, 1, 65, T + ok + o * 65, 65, 1);
+        st16(T + oi + ok * 65, v, true);
+      } else {
+        const int q = t - nA, I = J + 1 + q / (J + 1), K = q % (J + 1);
+        const int oi = 16 * I, ok = 16 * K;
+        const d4 v = mm16(T + oi + o * 65, 1, 65, W + o + ok * 65, 1, 65);
+        st16(W + oi + ok * 65, v, true);
+      }
+    }
+    __syncthreads();
+    DIAG_CLK(3 + 3 * J);
+  }
+  __syncthreads();
+  DIAG_CLK(12);
+  return bad;
+}
+
+// Diagonal tile of each listed front at panel kb: factored and inverted in LDS
+// (diag_factor_invert); L back into the front, L^-1 into Tinv for the TRSM GEMM
+// and the solves.
 __global__ __launch_bounds__(256) void k_panel_diag(CholDev c, const int* __restrict__ list, int kb) {
   __shared__ double Ts[64 * 65];
-  __shared__ double colb[2][64];
-  __shared__ double dinv[64];
+  __shared__ double Ws[64 * 65];
+  __shared__ double bc[32];
   const int s = list[blockIdx.x];
   const int m = c.m[s], w = c.w[s];
   const int nb = min(kNB, w - kb);
   double* Fs = c.F + c.foff[s] + kb + (size_t)kb * m;
   const int tid = threadIdx.x;
-  const int i = tid & 63, cg = __builtin_amdgcn_readfirstlane(tid >> 6);
-  double a[16];
-#pragma unroll
-  for (int q = 0; q < 16; q++) {
-    const int k = 4 * q + cg;
-    a[q] = (i < nb && k < nb) ? (k <= i ? Fs[i + (size_t)k * m] : 0.0) : (i == k ? 1.0 : 0.0);
+  for (int idx = tid; idx < 4096; idx += 256) {
+    const int i = idx & 63, j = idx >> 6;
+    Ts[i + j * 65] = (i < nb && j < nb) ? (i >= j ? Fs[i + (size_t)j * m] : 0.0) : (i == j ? 1.0 : 0.0);
+    Ws[i + j * 65] = 0.0;
   }
-  bool bad = false;
-#pragma unroll
-  for (int j = 0; j < 64; j++) {
-    const int qj = j >> 2;
-    double* cb = colb[j & 1];
-    if (cg == (j & 3)) {
-      double d = readlane_f64(a[qj], j);
-      if (!(d > 0.0) || !isfinite(d)) {
-        bad = true;
-        d = 1.0;
-      }
-      const double piv = sqrt(d), inv = 1.0 / piv;
-      const double l = i > j ? a[qj] * inv : (i == j ? piv : 0.0);
-      a[qj] = l;
-      cb[i] = l;
-    }
-    __syncthreads();
-    const double li = cb[i];
-#pragma unroll
-    for (int q = 0; q < 16; q++)
-      if (4 * q + cg > j) a[q] -= li * cb[4 * q + cg];
-  }
-  if (bad && i == 0) *c.flag = 1;
-#pragma unroll
-  for (int q = 0; q < 16; q++) Ts[i + (4 * q + cg) * 65] = a[q];
   __syncthreads();
-  tri_inverse_wg(Ts, 65, nb, c.Tinv + c.toff[s] + (kb / 64) * 4096, dinv);
-#pragma unroll
-  for (int q = 0; q < 16; q++) {
-    const int k = 4 * q + cg;
-    if (i < nb && k < nb && k <= i) Fs[i + (size_t)k * m] = a[q];
+  if (diag_factor_invert(Ts, Ws, bc)) *c.flag = 1;
+  double* M = c.Tinv + c.toff[s] + (kb / 64) * 4096;
+  for (int idx = tid; idx < 4096; idx += 256) {
+    const int i = idx & 63, j = idx >> 6;
+    const bool live = i < nb && j < nb && i >= j;
+    if (live) Fs[i + (size_t)j * m] = Ts[i + j * 65];
+    M[j * 64 + i] = live ? Ws[i + j * 65] : 0.0;
   }
 }
 
@@ -407,8 +551,9 @@ __device__ __forceinline__ double tinv_bwd(const double* Ms, const double* z, in
   return acc;
 }
 
-__device__ __forceinline__ void stage_tinv(const double* __restrict__ M, double* Ms) {
-  for (int idx = threadIdx.x; idx < 4096; idx += blockDim.x) Ms[(idx >> 6) * 65 + (idx & 63)] = M[idx];
+__device__ __forceinline__ void stage_tinv(const double* __restrict__ M, double* Ms, int n) {  // live n x n
+  for (int idx = threadIdx.x; idx < n * 64; idx += blockDim.x)
+    if ((idx & 63) < n) Ms[(idx >> 6) * 65 + (idx & 63)] = M[idx];
 }
 
 // Forward, launch 1 of a level: frontal vector = (own rhs, 0) + children's update
@@ -475,51 +620,74 @@ __global__ __launch_bounds__(256) void k_fwd_step(CholDev c, const int4* __restr
   }
 }
 
-// Backward init of a level: z_j = y_j - L21[:, j]' x_below for the task's
-// columns (one wave per column); the owner of the last block solves it.
-__global__ __launch_bounds__(256) void k_bwd_init(CholDev c, const int4* __restrict__ tasks) {
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* Ld = sm;                 // 64 x 65
-  double* z = sm + 64 * 65;        // 64
-  double* xb = z + 64;             // m - w
+// acc[0..N) of each lane -> acc[0..N/2): lanes with bit N/2 set keep the upper
+// half, the other half goes to the partner lane (recursive halving).  After
+// halve<64> ... halve<2>, acc[0] of lane q is the wave sum of column q.
+template <int N>
+__device__ __forceinline__ void halve(double* acc, int lane) {
+  const bool up = lane & (N / 2);
+#pragma unroll
+  for (int i = 0; i < N / 2; i++) {
+    const double send = up ? acc[i] : acc[i + N / 2];
+    const double keep = up ? acc[i + N / 2] : acc[i];
+    acc[i] = keep + __shfl_xor(send, N / 2);
+  }
+}
+
+// Backward partial product: part[slot][j] = sum over rows [r0, r0+kBwdRows) of
+// L[r, c0+j] x_r (rows below the pivot columns; x gathered from xv).
+__global__ __launch_bounds__(256) void k_bwd_part(CholDev c, const int4* __restrict__ tasks,
+                                                  double* __restrict__ part) {
+  __shared__ double red[4][64];
   const int4 t = tasks[blockIdx.x];
-  const int s = t.x, c0 = t.y, c1 = t.z, owner = t.w;
+  const int s = t.x, c0 = t.y, r0 = t.z, slot = t.w;
   const int m = c.m[s], w = c.w[s];
-  const double* L = c.F + c.foff[s];
-  double* fv = c.fv + c.voff[s];
+  const int ncol = min(64, w - c0), r1 = min(r0 + kBwdRows, m);
+  const double* L = c.F + c.foff[s] + (size_t)c0 * m;
   const int* rows = c.rows + c.rptr[s];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int r = w + tid; r < m; r += 256) xb[r - w] = c.xv[3 * rows[r / 3] + r % 3];
-  if (owner >= 0) stage_tinv(c.Tinv + c.toff[s] + owner * 4096, Ld);
-  __syncthreads();
-  // L21[:, c0:c1]' x_below: thread (wave wv, lane) owns rows w + lane + 64 (wv + 4 t),
-  // keeps one partial per column (<= 64), loads of a row chunk all in flight
-  const int ncol = c1 - c0;
   double acc[64];
 #pragma unroll
   for (int q = 0; q < 64; q++) acc[q] = 0.0;
-  for (int r = w + lane + 64 * wv; r < m; r += 256) {
-    const double xr = xb[r - w];
-    const double* Lr = L + r + (size_t)c0 * m;
+  for (int r = r0 + tid; r < r1; r += 256) {
+    const double xr = c.xv[3 * rows[r / 3] + r % 3];
+    const double* Lr = L + r;
 #pragma unroll
     for (int q = 0; q < 64; q++)
       if (q < ncol) acc[q] += Lr[(size_t)q * m] * xr;
   }
-  // reduce each column over the 256 threads: wave butterflies, then 4 waves via LDS
-  double* red = xb;  // reuse after the loop (m - w >= 0 doubles; need 4*64)
+  halve<64>(acc, lane);
+  halve<32>(acc, lane);
+  halve<16>(acc, lane);
+  halve<8>(acc, lane);
+  halve<4>(acc, lane);
+  halve<2>(acc, lane);
+  red[wv][lane] = acc[0];
   __syncthreads();
-#pragma unroll
-  for (int q = 0; q < 64; q++) {
-    double v = acc[q];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if (lane == 0) red[wv * 64 + q] = v;
+  if (tid < 64) part[(size_t)slot * 64 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+}
+
+// Backward init of a level: z_j = y_j - sum of the block's partials (fixed
+// order); the owner of the last block then solves it.
+__global__ __launch_bounds__(256) void k_bwd_init(CholDev c, const int4* __restrict__ tasks,
+                                                  const int2* __restrict__ pref, const double* __restrict__ part) {
+  __shared__ double Ld[64 * 65];
+  __shared__ double z[64];
+  const int4 t = tasks[blockIdx.x];
+  const int s = t.x, c0 = t.y, c1 = t.z, owner = t.w;
+  const int2 pr = pref[blockIdx.x];
+  double* fv = c.fv + c.voff[s];
+  const int* rows = c.rows + c.rptr[s];
+  const int tid = threadIdx.x;
+  if (owner >= 0) stage_tinv(c.Tinv + c.toff[s] + owner * 4096, Ld, c1 - c0);
+  if (tid < c1 - c0) {
+    double acc = 0.0;
+    for (int p = 0; p < pr.y; p++) acc += part[(size_t)(pr.x + p) * 64 + tid];
+    z[tid] = fv[c0 + tid] - acc;
   }
   __syncthreads();
-  if (tid < ncol) z[tid] = fv[c0 + tid] - (red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid]);
-  __syncthreads();
   if (owner < 0) {
-    for (int j = c0 + tid; j < c1; j += 256) fv[j] = z[j - c0];
+    if (tid < c1 - c0) fv[c0 + tid] = z[tid];
     return;
   }
   if (tid < 64) {
@@ -547,7 +715,7 @@ __global__ __launch_bounds__(256) void k_bwd_step(CholDev c, const int4* __restr
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int jb = b * 64, nbk = min(64, w - jb);
   if (tid < nbk) xbk[tid] = fv[jb + tid];
-  if (owner >= 0) stage_tinv(c.Tinv + c.toff[s] + owner * 4096, Ld);
+  if (owner >= 0) stage_tinv(c.Tinv + c.toff[s] + owner * 4096, Ld, c1 - c0);
   __syncthreads();
   // wave wv: columns c0 + wv + 4q, q < 16; all 16 loads issued before the reductions
   double part[16];
@@ -628,6 +796,9 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(up(&P.d_potrf, P.potrf_list, s));
   CH_TRY(up(&P.d_fwd, P.fwd_tasks, s));
   CH_TRY(up(&P.d_bwd, P.bwd_tasks, s));
+  CH_TRY(up(&P.d_bwd_pref, P.bwd_pref, s));
+  CH_TRY(up(&P.d_bwd_part, P.bwd_part_tasks, s));
+  CH_TRY(hipMalloc((void**)&P.d_partial, std::max(P.npart, 1) * 64 * sizeof(double)));
   CH_TRY(up(&P.d_syrk, P.syrk_tasks, s));
   CH_TRY(up(&P.d_ea_children, P.ea_children, s));
   CH_TRY(up(&P.d_ea_colpref, P.ea_colpref, s));
@@ -638,7 +809,7 @@ void chol_free(CholPlan& P) {
   void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
                   P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
                   P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
-                  P.d_trsm, P.d_syrk, P.d_ea_children, P.d_ea_colpref, P.d_potrf, P.d_fwd, P.d_bwd};
+                  P.d_trsm, P.d_syrk, P.d_ea_children, P.d_ea_colpref, P.d_potrf, P.d_fwd, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   P = CholPlan();
@@ -692,8 +863,9 @@ hipError_t chol_solve(const CholPlan& P, const double* b, double* x, double scal
   }
   for (auto it = P.levels.rbegin(); it != P.levels.rend(); ++it) {
     const CholLevel& lv = *it;
-    k_bwd_init<<<lv.bwd[0].cnt, 256, (size_t)(64 * 65 + 64 + std::max(lv.maxm, 256)) * sizeof(double), s>>>(
-        c, P.d_bwd + lv.bwd[0].off);
+    if (lv.bwd_part.cnt)
+      k_bwd_part<<<lv.bwd_part.cnt, 256, 0, s>>>(c, P.d_bwd_part + lv.bwd_part.off, P.d_partial);
+    k_bwd_init<<<lv.bwd[0].cnt, 256, 0, s>>>(c, P.d_bwd + lv.bwd[0].off, P.d_bwd_pref + lv.bwd[0].off, P.d_partial);
     for (size_t q = 1; q < lv.bwd.size(); q++) {
       const int bb = lv.maxblk - (int)q;   // step b = maxblk-1 .. 1
       if (lv.bwd[q].cnt) k_bwd_step<<<lv.bwd[q].cnt, 256, 0, s>>>(c, P.d_bwd + lv.bwd[q].off, bb);

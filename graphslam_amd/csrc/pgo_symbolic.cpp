@@ -388,6 +388,9 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.potrf_list.clear();
   P.fwd_tasks.clear();
   P.bwd_tasks.clear();
+  P.bwd_pref.clear();
+  P.bwd_part_tasks.clear();
+  P.npart = 0;
   P.ea_children.clear();
   P.ea_colpref.clear();
   for (int L = 0; L < nl; L++) {
@@ -418,13 +421,22 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       lv.fwd.push_back(st);
     }
     {                                            // backward init: all columns vs the rows below w
+      // partial products L21[r0:r0+kBwdRows, block]' x_below, one task each,
+      // reduced in fixed order by the init task of the block
+      SolveStep sp{(int)P.bwd_part_tasks.size(), 0};
       SolveStep st{(int)P.bwd_tasks.size(), 0};
       for (int s : bylevel[L]) {
-        const int w = P.w[s], nblk = (w + 63) / 64;
-        for (int b = 0; b < nblk; b++)
+        const int w = P.w[s], m = P.m[s], nblk = (w + 63) / 64;
+        for (int b = 0; b < nblk; b++) {
+          const int p0 = P.npart;
+          for (int r0 = w; r0 < m; r0 += kBwdRows) P.bwd_part_tasks.push_back(make_int4(s, b * 64, r0, P.npart++));
           P.bwd_tasks.push_back(make_int4(s, b * 64, std::min(b * 64 + 64, w), b == nblk - 1 ? b : -1));
+          P.bwd_pref.push_back(make_int2(p0, P.npart - p0));
+        }
       }
+      sp.cnt = (int)P.bwd_part_tasks.size() - sp.off;
       st.cnt = (int)P.bwd_tasks.size() - st.off;
+      lv.bwd_part = sp;
       lv.bwd.push_back(st);
     }
     for (int b = lv.maxblk - 1; b >= 1; b--) {   // backward step b: columns left of block b
@@ -433,7 +445,10 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
         const int w = P.w[s], nblk = (w + 63) / 64;
         if (b >= nblk) continue;
         for (int c = 0; c < b; c++)
+        {
           P.bwd_tasks.push_back(make_int4(s, c * 64, c * 64 + 64, c == b - 1 ? c : -1));
+          P.bwd_pref.push_back(make_int2(0, 0));
+        }
       }
       st.cnt = (int)P.bwd_tasks.size() - st.off;
       lv.bwd.push_back(st);

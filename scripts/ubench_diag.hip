@@ -1,0 +1,352 @@
+// Microbenchmark of the per-panel diagonal-tile kernel (k_panel_diag) and its
+// phases, for latency work on the Cholesky critical path.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include scripts/ubench_diag.hip -o graphslam_amd/build/ubench_diag
+//   ./graphslam_amd/build/ubench_diag [fronts] [m]
+#define PGO_DIAG_CLOCKS 1
+#include "../graphslam_amd/csrc/pgo_chol.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+using namespace pgo;
+
+// phase kernels ------------------------------------------------------------
+__global__ __launch_bounds__(256) void u_load_store(CholDev c, const int* list) {
+  const int s = list[blockIdx.x];
+  const int m = c.m[s];
+  double* Fs = c.F + c.foff[s];
+  const int i = threadIdx.x & 63, cg = threadIdx.x >> 6;
+  double a[16];
+#pragma unroll
+  for (int q = 0; q < 16; q++) a[q] = Fs[i + (size_t)(4 * q + cg) * m];
+#pragma unroll
+  for (int q = 0; q < 16; q++) Fs[i + (size_t)(4 * q + cg) * m] = a[q] * 1.0000001;
+}
+
+__global__ __launch_bounds__(256) void u_inverse(CholDev c, const int* list) {
+  __shared__ double Ts[64 * 65];
+  __shared__ double dinv[64];
+  const int s = list[blockIdx.x];
+  for (int idx = threadIdx.x; idx < 4096; idx += 256) {
+    const int i = idx & 63, j = idx >> 6;
+    Ts[i + j * 65] = i == j ? 2.0 : (i > j ? 0.01 : 0.0);
+  }
+  __syncthreads();
+  tri_inverse_wg(Ts, 65, 64, c.Tinv + c.toff[s], dinv);
+}
+
+// single-wave right-looking potrf, column broadcast by v_readlane
+__global__ __launch_bounds__(64) void u_potrf1(CholDev c, const int* list) {
+  const int s = list[blockIdx.x];
+  const int m = c.m[s];
+  double* Fs = c.F + c.foff[s];
+  const int i = threadIdx.x;
+  double a[64];
+#pragma unroll
+  for (int k = 0; k < 64; k++) a[k] = k <= i ? Fs[i + (size_t)k * m] : 0.0;
+#pragma unroll
+  for (int j = 0; j < 64; j++) {
+    const double d = readlane_f64(a[j], j);
+    const double piv = sqrt(d), inv = 1.0 / piv;
+    const double l = i > j ? a[j] * inv : (i == j ? piv : 0.0);
+    a[j] = l;
+#pragma unroll
+    for (int k = j + 1; k < 64; k++) a[k] -= l * readlane_f64(l, k);
+  }
+#pragma unroll
+  for (int k = 0; k < 64; k++)
+    if (k <= i) Fs[i + (size_t)k * m] = a[k];
+}
+
+
+
+__device__ long long g_clk[4];
+// single wave potrf, lane i = row i, column j broadcast through LDS (wave-ordered)
+__global__ __launch_bounds__(64) void u_potrf_lds(CholDev c, const int* list) {
+  __shared__ double colb[64];
+  const int s = list[blockIdx.x];
+  const int m = c.m[s], w = c.w[s];
+  const int nb = min(64, w);
+  double* Fs = c.F + c.foff[s];
+  const int i = threadIdx.x;
+  double a[64];
+#pragma unroll
+  for (int k = 0; k < 64; k++)
+    a[k] = (i < nb && k < nb) ? (k <= i ? Fs[i + (size_t)k * m] : 0.0) : (i == k ? 1.0 : 0.0);
+  bool bad = false;
+  double acc0 = 0;
+#pragma unroll
+  for (int k = 0; k < 64; k++) acc0 += a[k];
+  if (acc0 == 12345.0) *c.flag = 7;
+  const long long t0 = clock64(), w0 = wall_clock64();
+#pragma unroll
+  for (int j = 0; j < 64; j++) {
+    double d = readlane_f64(a[j], j);
+    if (!(d > 0.0) || !isfinite(d)) {
+      bad = true;
+      d = 1.0;
+    }
+    const double inv = rsqrt_nr(d);
+    const double l = i > j ? a[j] * inv : 0.0;
+    a[j] = i == j ? d * inv : l;
+    colb[i] = l;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = j + 1; k < 64; k++) a[k] -= l * colb[k];
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (bad && i == 0) *c.flag = 1;
+  double acc1 = 0;
+#pragma unroll
+  for (int k = 0; k < 64; k++) acc1 += a[k];
+  if (acc1 == 12345.0) *c.flag = 7;
+  const long long t1 = clock64(), w1 = wall_clock64();
+  if (i == 0 && blockIdx.x == 0) { g_clk[0] = t1 - t0; g_clk[1] = w1 - w0; }
+#pragma unroll
+  for (int k = 0; k < 64; k++)
+    if (k <= i && i < nb && k < nb) Fs[i + (size_t)k * m] = a[k];
+}
+
+// 4-wave inverse, LDS broadcast of row k (lane k writes 16 values), reciprocals precomputed
+__global__ __launch_bounds__(256) void u_inv_lds(CholDev c, const int* list) {
+  __shared__ double Ts[64 * 65];
+  __shared__ double dinv[64];
+  __shared__ double sc[4][16];
+  const int s = list[blockIdx.x];
+  for (int idx = threadIdx.x; idx < 4096; idx += 256) {
+    const int i = idx & 63, j = idx >> 6;
+    Ts[i + j * 65] = i == j ? 2.0 : (i > j ? 0.01 : 0.0);
+  }
+  __syncthreads();
+  const int tid = threadIdx.x, nbk = 64, ld = 65;
+  const double* L = Ts;
+  if (tid < 64) dinv[tid] = 1.0 / L[tid + tid * ld];
+  __syncthreads();
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), i = tid & 63;
+  const int j0 = 16 * wv;
+  double xr[16];
+#pragma unroll
+  for (int q = 0; q < 16; q++) xr[q] = (i == j0 + q) ? 1.0 : 0.0;
+  double* scw = sc[wv];
+  for (int k = j0; k < nbk; k++) {
+    if (i == k) {
+      const double dk = dinv[k];
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        xr[q] *= dk;
+        scw[q] = xr[q];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const double lik = (i > k) ? L[i + k * ld] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) xr[q] -= lik * scw[q];
+    __builtin_amdgcn_wave_barrier();
+  }
+  double* M = c.Tinv + c.toff[s];
+#pragma unroll
+  for (int q = 0; q < 16; q++) M[(j0 + q) * 64 + i] = xr[q];
+}
+
+
+__device__ long long g_lat[8];
+__global__ __launch_bounds__(64) void u_latency(double* out) {
+  __shared__ double bc[64];
+  const int l = threadIdx.x;
+  double v = l * 0.001 + 1.0;
+  long long t0 = clock64();
+  for (int it = 0; it < 256; it++) {
+    bc[l] = v;
+    __builtin_amdgcn_wave_barrier();
+    v = bc[(l + 1) & 63] * 0.999 + 0.001;
+    __builtin_amdgcn_wave_barrier();
+  }
+  long long t1 = clock64();
+  double d = v + 1.0;
+  for (int it = 0; it < 256; it++) d = rsqrt_nr(d) * 1.5 + 0.25;
+  long long t2 = clock64();
+  double e = d;
+  for (int it = 0; it < 256; it++) e = readlane_f64(e, it & 63) * 0.999 + 0.5;
+  long long t3 = clock64();
+  double f = e;
+  for (int it = 0; it < 256; it++) f = fma(f, 0.999, 0.5);
+  long long t4 = clock64();
+  out[l] = v + d + e + f;
+  if (l == 0) {
+    g_lat[0] = (t1 - t0) / 256;
+    g_lat[1] = (t2 - t1) / 256;
+    g_lat[2] = (t3 - t2) / 256;
+    g_lat[3] = (t4 - t3) / 256;
+  }
+}
+
+static double time_launches(void (*launch)(hipStream_t), hipStream_t st, int reps) {
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  for (int r = 0; r < 5; r++) launch(st);
+  hipEventRecord(a, st);
+  for (int r = 0; r < reps; r++) launch(st);
+  hipEventRecord(b, st);
+  hipEventSynchronize(b);
+  float ms = 0;
+  hipEventElapsedTime(&ms, a, b);
+  return 1e3 * ms / reps;
+}
+
+static CholDev g_c;
+static int* g_list;
+static int g_n;
+static std::vector<double> g_host;
+static double* g_F;
+static double* g_P;
+static size_t g_bytes;
+static void reset(hipStream_t st) { hipMemcpyAsync(g_F, g_P, g_bytes, hipMemcpyDeviceToDevice, st); }
+
+int main(int argc, char** argv) {
+  const int N = argc > 1 ? atoi(argv[1]) : 1;
+  const int M = argc > 2 ? atoi(argv[2]) : 64;
+  hipStream_t st;
+  hipStreamCreate(&st);
+  std::vector<int> hm(N, M), hw(N, 64), list(N);
+  std::vector<long long> foff(N + 1), toff(N + 1);
+  for (int s = 0; s < N; s++) {
+    list[s] = s;
+    foff[s + 1] = foff[s] + (long long)M * M;
+    toff[s + 1] = toff[s] + 4096;
+  }
+  // SPD tiles: A = 64 I + small symmetric noise
+  g_host.assign(foff[N], 0.0);
+  srand(7);
+  for (int s = 0; s < N; s++)
+    for (int j = 0; j < 64; j++)
+      for (int i = j; i < M; i++) {
+        const double v = (i == j) ? 64.0 + (rand() % 100) / 100.0 : ((rand() % 2001) - 1000) / 2000.0;
+        g_host[foff[s] + i + (size_t)j * M] = v;
+      }
+  g_bytes = g_host.size() * sizeof(double);
+  int *d_m, *d_w, *d_flag;
+  long long *d_foff, *d_toff;
+  double* d_T;
+  hipMalloc(&g_F, g_bytes);
+  hipMalloc(&g_P, g_bytes);
+  hipMemcpy(g_P, g_host.data(), g_bytes, hipMemcpyHostToDevice);
+  hipMalloc(&d_T, toff[N] * sizeof(double));
+  hipMalloc(&d_m, N * 4);
+  hipMalloc(&d_w, N * 4);
+  hipMalloc(&g_list, N * 4);
+  hipMalloc(&d_flag, 4);
+  hipMalloc(&d_foff, (N + 1) * 8);
+  hipMalloc(&d_toff, (N + 1) * 8);
+  hipMemcpy(d_m, hm.data(), N * 4, hipMemcpyHostToDevice);
+  hipMemcpy(d_w, hw.data(), N * 4, hipMemcpyHostToDevice);
+  hipMemcpy(g_list, list.data(), N * 4, hipMemcpyHostToDevice);
+  hipMemcpy(d_foff, foff.data(), (N + 1) * 8, hipMemcpyHostToDevice);
+  hipMemcpy(d_toff, toff.data(), (N + 1) * 8, hipMemcpyHostToDevice);
+  hipMemset(d_flag, 0, 4);
+  g_c = CholDev{};
+  g_c.F = g_F;
+  g_c.Tinv = d_T;
+  g_c.toff = d_toff;
+  g_c.m = d_m;
+  g_c.w = d_w;
+  g_c.foff = d_foff;
+  g_c.flag = d_flag;
+  g_n = N;
+  const int reps = 200;
+  auto empty = [](hipStream_t s) { u_load_store<<<1, 64, 0, s>>>(g_c, g_list); };
+  printf("fronts %d m %d\n", N, M);
+  {
+    double* o;
+    hipMalloc(&o, 64 * 8);
+    u_latency<<<1, 64, 0, st>>>(o);
+    hipStreamSynchronize(st);
+    long long lat[8];
+    hipMemcpyFromSymbol(lat, HIP_SYMBOL(g_lat), sizeof(lat));
+    printf("  latency (clocks): lds write->read step %lld, rsqrt_nr %lld, readlane+fma %lld, fma %lld\n", lat[0],
+           lat[1], lat[2], lat[3]);
+  }
+  printf("  load_store(1 wg,64 thr)  %8.2f us\n", time_launches(empty, st, reps));
+  printf("  load_store               %8.2f us\n",
+         time_launches([](hipStream_t s) { u_load_store<<<g_n, 256, 0, s>>>(g_c, g_list); }, st, reps));
+  printf("  inverse                  %8.2f us\n",
+         time_launches([](hipStream_t s) { u_inverse<<<g_n, 256, 0, s>>>(g_c, g_list); }, st, reps));
+  // full kernel and single-wave potrf need fresh SPD input each launch: time with a reset copy
+  const double t_reset = time_launches(reset, st, reps);
+  printf("  reset copy               %8.2f us\n", t_reset);
+  printf("  k_panel_diag (+reset)    %8.2f us\n", time_launches([](hipStream_t s) {
+           reset(s);
+           k_panel_diag<<<g_n, 256, 0, s>>>(g_c, g_list, 0);
+         }, st, reps) - t_reset);
+  printf("  potrf1 (+reset)          %8.2f us\n", time_launches([](hipStream_t s) {
+           reset(s);
+           u_potrf1<<<g_n, 64, 0, s>>>(g_c, g_list);
+         }, st, reps) - t_reset);
+  printf("  potrf_lds (+reset)       %8.2f us\n", time_launches([](hipStream_t s) {
+           reset(s);
+           u_potrf_lds<<<g_n, 64, 0, s>>>(g_c, g_list);
+         }, st, reps) - t_reset);
+  printf("  inv_lds                  %8.2f us\n",
+         time_launches([](hipStream_t s) { u_inv_lds<<<g_n, 256, 0, s>>>(g_c, g_list); }, st, reps));
+  {
+    reset(st);
+    u_potrf1<<<N, 64, 0, st>>>(g_c, g_list);
+    std::vector<double> f1(g_host.size()), f2(g_host.size());
+    hipMemcpyAsync(f1.data(), g_F, g_bytes, hipMemcpyDeviceToHost, st);
+    reset(st);
+    u_potrf_lds<<<N, 64, 0, st>>>(g_c, g_list);
+    hipMemcpyAsync(f2.data(), g_F, g_bytes, hipMemcpyDeviceToHost, st);
+    hipStreamSynchronize(st);
+    double mf = 0;
+    for (size_t q = 0; q < f1.size(); q++) mf = std::max(mf, fabs(f1[q] - f2[q]));
+    printf("  potrf_lds vs potrf1: max |dL| %.3e\n", mf);
+    long long clk[4];
+    hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_clk), sizeof(clk));
+    printf("  potrf_lds loop: %lld shader clocks, %lld wall ticks (100 MHz) -> %.2f us, %.2f GHz\n", clk[0], clk[1],
+           clk[1] / 100.0, clk[0] / (clk[1] * 10.0));
+  }
+  {
+    // k_panel_diag: X L = I on the live block
+    reset(st);
+    k_panel_diag<<<N, 256, 0, st>>>(g_c, g_list, 0);
+    std::vector<double> f1(g_host.size()), t1(toff[N]);
+    hipMemcpyAsync(f1.data(), g_F, g_bytes, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(t1.data(), d_T, toff[N] * 8, hipMemcpyDeviceToHost, st);
+    hipStreamSynchronize(st);
+    double me = 0;
+    for (int s = 0; s < N; s++)
+      for (int i = 0; i < 64; i++)
+        for (int j = 0; j < 64; j++) {
+          double acc = 0;
+          for (int k = 0; k < 64; k++) {
+            const double x = t1[toff[s] + k * 64 + i];                         // X(i,k)
+            const double L = k >= j ? f1[foff[s] + k + (size_t)j * M] : 0.0;   // L(k,j)
+            acc += x * L;
+          }
+          me = std::max(me, fabs(acc - (i == j ? 1.0 : 0.0)));
+        }
+    printf("  k_panel_diag: max |X L - I| = %.3e\n", me);
+    long long dc[16];
+    hipMemcpyFromSymbol(dc, HIP_SYMBOL(g_diag_clk), sizeof(dc));
+    printf("  diag phases (clocks from start):");
+    for (int q = 1; q <= 12; q++) printf(" %lld", dc[q] - dc[0]);
+    printf("\n");
+  }
+  // correctness: potrf1 vs k_panel_diag on the same input
+  reset(st);
+  k_panel_diag<<<N, 256, 0, st>>>(g_c, g_list, 0);
+  std::vector<double> r1(g_host.size()), r2(g_host.size());
+  hipMemcpyAsync(r1.data(), g_F, g_bytes, hipMemcpyDeviceToHost, st);
+  reset(st);
+  u_potrf1<<<N, 64, 0, st>>>(g_c, g_list);
+  hipMemcpyAsync(r2.data(), g_F, g_bytes, hipMemcpyDeviceToHost, st);
+  hipStreamSynchronize(st);
+  double md = 0;
+  for (size_t q = 0; q < r1.size(); q++) md = std::max(md, fabs(r1[q] - r2[q]));
+  int flag = 0;
+  hipMemcpy(&flag, d_flag, 4, hipMemcpyDeviceToHost);
+  printf("  max |diag - potrf1| = %.3e  flag %d\n", md, flag);
+  return 0;
+}
