@@ -24,6 +24,7 @@ namespace pgo {
 constexpr int kSmallFront = 128;   // m <= this: whole front factorised in LDS by one workgroup
 constexpr int kNB = 64;            // panel width of the blocked path
 constexpr int kTile = 64;          // Schur-update output tile
+constexpr int kBigTile = 128;      // Schur-update output tile of the LDS-pipelined kernel
 constexpr int kKB = 256;
 constexpr int kBwdRows = 512;      // rows per partial product of the backward solve           // Schur-update depth: trailing matrix updated once per kKB columns
 
@@ -33,6 +34,8 @@ struct PanelStep {                 // one panel of the blocked path, all big fro
   int trsm_off, trsm_cnt;          // tasks (front, row chunk) in trsm_tasks
   int syrk_off, syrk_cnt;          // tasks in syrk_tasks: (front, row0, col0, k0 | inner<<31)
   double syrk_flops;               // algorithmic flops of this step's Schur updates (lower triangles)
+  int syrk_tile;                   // kTile or kBigTile
+  int sdiag_off, sdiag_cnt;        // look-ahead tasks in sdiag_tasks (next panel's diagonal tile)
 };
 
 struct SolveStep {                 // one launch of the blocked triangular solves
@@ -77,7 +80,7 @@ struct CholPlan {
   std::vector<CholLevel> levels;
   std::vector<int> small_list, level_fronts, potrf_list;
   std::vector<int2> trsm_tasks;
-  std::vector<int4> syrk_tasks;
+  std::vector<int4> syrk_tasks, sdiag_tasks;
   std::vector<int4> fwd_tasks, bwd_tasks;
   std::vector<int2> bwd_pref;      // per bwd task: first partial, partial count (init tasks)
   std::vector<int4> bwd_part_tasks;  // (front, c0, r0, partial slot)
@@ -101,7 +104,10 @@ struct CholPlan {
   int *d_dg_front = nullptr, *d_dg_loc = nullptr, *d_perm = nullptr;
   int *d_small = nullptr, *d_level_fronts = nullptr, *d_potrf = nullptr;
   int2* d_trsm = nullptr;
-  int4* d_syrk = nullptr;
+  int4 *d_syrk = nullptr, *d_sdiag = nullptr;
+  hipStream_t side = nullptr;      // look-ahead diagonal tiles
+  hipStream_t side2 = nullptr;     // small fronts beside the blocked path
+  hipEvent_t evs[4] = {nullptr, nullptr, nullptr, nullptr};
   int4 *d_fwd = nullptr, *d_bwd = nullptr, *d_bwd_part = nullptr;
   int2* d_bwd_pref = nullptr;
   double* d_partial = nullptr;

@@ -257,7 +257,7 @@ __device__ long long g_diag_clk[16];
 #else
 #define DIAG_CLK(q)
 #endif
-__device__ bool diag_factor_invert(double* T, double* W, double* bc) {
+__device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double* bc) {
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   DIAG_CLK(0);
   bool bad = false;
@@ -456,8 +456,8 @@ __global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __res
 // from global (the panel columns are L2-resident); the product is formed
 // transposed (A = column-side rows) so each store covers 16 consecutive rows.
 // Inner tasks (bit 31 of k0) clip columns at the end of the current kKB block.
-__global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int4* __restrict__ tasks, int kb) {
-  const int4 t = tasks[blockIdx.x];
+template <bool kToLds>
+__device__ __forceinline__ void syrk_tile64(const CholDev& c, const int4 t, int kb, double* Ts) {
   const int s = t.x, row0 = t.y, col0 = t.z;
   const bool inner = t.w < 0;
   const int k0 = t.w & 0x7fffffff;
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int4* __res
   const int colend = inner ? min((kb & ~(kKB - 1)) + kKB, w) : m;
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int qi = 32 * (wv >> 1), qj = 32 * (wv & 1);
-  if (row0 == col0 && qi < qj) return;       // strictly upper quarter of a diagonal tile
+  if (row0 == col0 && qi < qj) return;       // strictly upper quarter of a diagonal tile (caller syncs)
   const int li = l & 15, lk = l >> 4;
   double* Fs = c.F + c.foff[s];
   const int rA = row0 + qi + li, rB = rA + 16;          // C rows (B operand rows)
@@ -513,9 +513,146 @@ __global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int4* __res
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int row = row0 + qi + 16 * mi + li, col = col0 + qj + 16 * mj + lk + 4 * r;
-        if (row < m && col < colend && row >= col) Fs[row + (size_t)col * m] = cold[mi][mj][r] - a[r];
+        if (row < m && col < colend && row >= col) {
+          const double v = cold[mi][mj][r] - a[r];
+          Fs[row + (size_t)col * m] = v;
+          if (kToLds) Ts[(row - row0) + (col - col0) * 65] = v;
+        }
       }
     }
+}
+
+__global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int4* __restrict__ tasks, int kb) {
+  syrk_tile64<false>(c, tasks[blockIdx.x], kb, nullptr);
+}
+
+// The Schur-update tile that is the next panel's diagonal tile (row0 = col0 =
+// kb + nb < w), then that tile factored and inverted in place (look-ahead: runs
+// on a second stream beside the rest of the panel's Schur update, so the next
+// panel starts without a separate diagonal step).
+__global__ __launch_bounds__(256) void k_syrk_diag(CholDev c, const int4* __restrict__ tasks, int kb) {
+  __shared__ double Ts[64 * 65];
+  __shared__ double Ws[64 * 65];
+  __shared__ double bc[32];
+  const int4 t = tasks[blockIdx.x];
+  const int s = t.x, kn = t.y;
+  const int m = c.m[s], w = c.w[s];
+  const int nb = min(kNB, w - kn);
+  const int tid = threadIdx.x;
+  syrk_tile64<true>(c, t, kb, Ts);
+  __syncthreads();
+  for (int idx = tid; idx < 4096; idx += 256) {
+    const int i = idx & 63, j = idx >> 6;
+    if (!(i < nb && j < nb)) Ts[i + j * 65] = i == j ? 1.0 : 0.0;
+    Ws[i + j * 65] = 0.0;
+  }
+  __syncthreads();
+  if (diag_factor_invert(Ts, Ws, bc)) *c.flag = 1;
+  double* Fs = c.F + c.foff[s] + kn + (size_t)kn * m;
+  double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;
+  for (int idx = tid; idx < 4096; idx += 256) {
+    const int i = idx & 63, j = idx >> 6;
+    const bool live = i < nb && j < nb && i >= j;
+    if (live) Fs[i + (size_t)j * m] = Ts[i + j * 65];
+    M[j * 64 + i] = live ? Ws[i + j * 65] : 0.0;
+  }
+}
+
+// Schur update of one 128x128 lower tile (same task format and semantics as
+// k_panel_syrk).  The panel rows/columns are staged through LDS in chunks of
+// 16 k (double-buffered: the global loads of chunk c+1 are in flight while the
+// MFMAs of chunk c run); each wave owns 64x64 of the tile as 4x4
+// v_mfma_f64_16x16x4_f64 blocks.
+__global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __restrict__ tasks, int kb) {
+  constexpr int LD = 144;   // [k][row] rows of 128 + pad
+  __shared__ __attribute__((aligned(16))) double Sr[2][16 * LD];
+  __shared__ __attribute__((aligned(16))) double Sc[2][16 * LD];
+  const int4 t = tasks[blockIdx.x];
+  const int s = t.x, row0 = t.y, col0 = t.z;
+  const bool inner = t.w < 0;
+  const int k0 = t.w & 0x7fffffff;
+  const int m = c.m[s], w = c.w[s];
+  const int kend = min(kb + kNB, w);
+  const int colend = inner ? min((kb & ~(kKB - 1)) + kKB, w) : m;
+  const int K = kend - k0, nchunk = (K + 15) >> 4;
+  double* Fs = c.F + c.foff[s];
+  const double* P = Fs + (size_t)k0 * m;
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int wi = wv >> 1, wj = wv & 1;
+  const bool active = !(row0 == col0 && wi < wj) && row0 + 64 * wi < m && col0 + 64 * wj < colend;
+  // staging: thread covers (k = idx >> 7, r = idx & 127), idx = tid + 256 q, q < 8
+  double st[16];
+  auto load = [&](int ch) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int idx = tid + 256 * q, k = 16 * ch + (idx >> 7), r = idx & 127;
+      const bool kin = k < K;
+      const double* pk = P + (size_t)k * m;
+      st[q] = (kin && row0 + r < m) ? pk[row0 + r] : 0.0;
+      st[8 + q] = (kin && col0 + r < m) ? pk[col0 + r] : 0.0;
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int idx = tid + 256 * q, k = idx >> 7, r = idx & 127;
+      Sr[buf][k * LD + r] = st[q];
+      Sc[buf][k * LD + r] = st[8 + q];
+    }
+  };
+  d4 acc[4][4];
+#pragma unroll
+  for (int bj = 0; bj < 4; bj++)
+#pragma unroll
+    for (int bi = 0; bi < 4; bi++) acc[bj][bi] = d4{0, 0, 0, 0};
+  load(0);
+  stash(0);
+  __syncthreads();
+  for (int ch = 0; ch < nchunk; ch++) {
+    const int buf = ch & 1;
+    if (ch + 1 < nchunk) load(ch + 1);
+    if (active) {
+      const double* sr = Sr[buf] + 64 * wi + (l & 15);
+      const double* sc = Sc[buf] + 64 * wj + (l & 15);
+#pragma unroll
+      for (int kk = 0; kk < 4; kk++) {
+        const int ko = (4 * kk + (l >> 4)) * LD;
+        double ra[4], ca[4];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          ra[b] = sr[ko + 16 * b];
+          ca[b] = sc[ko + 16 * b];
+        }
+#pragma unroll
+        for (int bj = 0; bj < 4; bj++)
+#pragma unroll
+          for (int bi = 0; bi < 4; bi++)
+            acc[bj][bi] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[bj], ra[bi], acc[bj][bi], 0, 0, 0);
+      }
+    }
+    if (ch + 1 < nchunk) stash(buf ^ 1);
+    __syncthreads();
+  }
+  if (!active) return;
+  // lane l, reg r of acc[bj][bi] -> row row0+64wi+16bi+(l&15), col col0+64wj+16bj+(l>>4)+4r
+#pragma unroll
+  for (int bj = 0; bj < 4; bj++) {
+    double cold[4][4];
+#pragma unroll
+    for (int bi = 0; bi < 4; bi++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = row0 + 64 * wi + 16 * bi + (l & 15), col = col0 + 64 * wj + 16 * bj + (l >> 4) + 4 * r;
+        cold[bi][r] = (row < m && col < colend && row >= col) ? Fs[row + (size_t)col * m] : 0.0;
+      }
+#pragma unroll
+    for (int bi = 0; bi < 4; bi++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = row0 + 64 * wi + 16 * bi + (l & 15), col = col0 + 64 * wj + 16 * bj + (l >> 4) + 4 * r;
+        if (row < m && col < colend && row >= col) Fs[row + (size_t)col * m] = cold[bi][r] - acc[bj][bi][r];
+      }
+  }
 }
 
 // ------------------------------------------------------------ solves
@@ -800,6 +937,10 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(up(&P.d_bwd_part, P.bwd_part_tasks, s));
   CH_TRY(hipMalloc((void**)&P.d_partial, std::max(P.npart, 1) * 64 * sizeof(double)));
   CH_TRY(up(&P.d_syrk, P.syrk_tasks, s));
+  CH_TRY(up(&P.d_sdiag, P.sdiag_tasks, s));
+  CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
+  CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
+  for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   CH_TRY(up(&P.d_ea_children, P.ea_children, s));
   CH_TRY(up(&P.d_ea_colpref, P.ea_colpref, s));
   return hipStreamSynchronize(s);
@@ -809,9 +950,13 @@ void chol_free(CholPlan& P) {
   void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
                   P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
                   P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
-                  P.d_trsm, P.d_syrk, P.d_ea_children, P.d_ea_colpref, P.d_potrf, P.d_fwd, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial};
+                  P.d_trsm, P.d_syrk, P.d_ea_children, P.d_ea_colpref, P.d_potrf, P.d_fwd, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (hipEvent_t e : P.evs)
+    if (e) (void)hipEventDestroy(e);
+  if (P.side) (void)hipStreamDestroy(P.side);
+  if (P.side2) (void)hipStreamDestroy(P.side2);
   P = CholPlan();
 }
 
@@ -831,20 +976,43 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, hipS
       k_extend_add<<<(unsigned)blocks, 256, 0, s>>>(c, P.d_ea_children + lv.ea_off[r],
                                                     P.d_ea_colpref + lv.ea_cols_off[r], lv.ea_cnt[r]);
     }
+    // small fronts on the second side stream, beside the blocked path of the
+    // same level (disjoint fronts); joined before the next level
+    const bool fork_small = !lv.small.empty() && !lv.panels.empty();
+    hipStream_t ss = s;
+    if (fork_small) {
+      CH_TRY(hipEventRecord(P.evs[0], s));
+      CH_TRY(hipStreamWaitEvent(P.side2, P.evs[0], 0));
+      ss = P.side2;
+    }
     for (const SmallClass& sc : lv.small)
-      k_front_small<<<sc.cnt, 256, (size_t)(sc.mmax * sc.mmax + 64) * sizeof(double), s>>>(c, P.d_small + sc.off);
+      k_front_small<<<sc.cnt, 256, (size_t)(sc.mmax * sc.mmax + 64) * sizeof(double), ss>>>(c, P.d_small + sc.off);
     for (const PanelStep& ps : lv.panels) {
-      k_panel_diag<<<ps.potrf_cnt, 256, 0, s>>>(c, P.d_potrf + ps.potrf_off, ps.kb);
+      if (ps.potrf_cnt) k_panel_diag<<<ps.potrf_cnt, 256, 0, s>>>(c, P.d_potrf + ps.potrf_off, ps.kb);
       if (ps.trsm_cnt) k_panel_trsm<<<ps.trsm_cnt, 256, 0, s>>>(c, P.d_trsm + ps.trsm_off, ps.kb);
-      if (!ps.syrk_cnt) continue;
-      if (prof && prof->used < prof->cap) {
-        const int u = prof->used++;
-        prof->flops[u] = ps.syrk_flops;
-        hipExtLaunchKernelGGL(k_panel_syrk, dim3(ps.syrk_cnt), dim3(256), 0, s, prof->ev[2 * u], prof->ev[2 * u + 1], 0,
-                              c, (const int4*)(P.d_syrk + ps.syrk_off), ps.kb);
-      } else {
-        k_panel_syrk<<<ps.syrk_cnt, 256, 0, s>>>(c, P.d_syrk + ps.syrk_off, ps.kb);
+      if (ps.sdiag_cnt) {   // look-ahead: next panel's diagonal tiles on the side stream
+        CH_TRY(hipEventRecord(P.evs[2], s));
+        CH_TRY(hipStreamWaitEvent(P.side, P.evs[2], 0));
+        k_syrk_diag<<<ps.sdiag_cnt, 256, 0, P.side>>>(c, P.d_sdiag + ps.sdiag_off, ps.kb);
+        CH_TRY(hipEventRecord(P.evs[3], P.side));
       }
+      if (ps.syrk_cnt) {
+        const int4* tasks = (const int4*)(P.d_syrk + ps.syrk_off);
+        auto kern = ps.syrk_tile == kBigTile ? k_panel_syrk128 : k_panel_syrk;
+        if (prof && prof->used < prof->cap) {
+          const int u = prof->used++;
+          prof->flops[u] = ps.syrk_flops;
+          hipExtLaunchKernelGGL(kern, dim3(ps.syrk_cnt), dim3(256), 0, s, prof->ev[2 * u], prof->ev[2 * u + 1], 0, c,
+                                tasks, ps.kb);
+        } else {
+          kern<<<ps.syrk_cnt, 256, 0, s>>>(c, tasks, ps.kb);
+        }
+      }
+      if (ps.sdiag_cnt) CH_TRY(hipStreamWaitEvent(s, P.evs[3], 0));
+    }
+    if (fork_small) {
+      CH_TRY(hipEventRecord(P.evs[1], P.side2));
+      CH_TRY(hipStreamWaitEvent(s, P.evs[1], 0));
     }
   }
   return hipGetLastError();

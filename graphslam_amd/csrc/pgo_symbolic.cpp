@@ -385,6 +385,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.level_fronts.clear();
   P.trsm_tasks.clear();
   P.syrk_tasks.clear();
+  P.sdiag_tasks.clear();
   P.potrf_list.clear();
   P.fwd_tasks.clear();
   P.bwd_tasks.clear();
@@ -499,6 +500,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     }
     int maxw = 0;
     for (int s : big) maxw = std::max(maxw, P.w[s]);
+    std::vector<char> diag_ready(ns, 0);
     for (int kb = 0; kb < maxw; kb += kNB) {
       PanelStep ps;
       ps.kb = kb;
@@ -506,9 +508,16 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       ps.trsm_off = (int)P.trsm_tasks.size();
       ps.syrk_off = (int)P.syrk_tasks.size();
       ps.potrf_off = (int)P.potrf_list.size();
+      ps.sdiag_off = (int)P.sdiag_tasks.size();
+      struct Upd {
+        int s, c0, c1, k0;   // columns [c0, c1) of front s, rows c0..m, depth from k0 (bit 31: inner)
+        int next;            // next panel's first column (its diagonal tile is in this update), or -1
+      };
+      std::vector<Upd> upd;
       for (int s : big) {
         if (P.w[s] <= kb) continue;
-        P.potrf_list.push_back(s);
+        if (!diag_ready[s]) P.potrf_list.push_back(s);
+        diag_ready[s] = 0;
         const int nb = std::min(kNB, P.w[s] - kb);
         const int below_rows = P.m[s] - kb - nb;
         const int chunks = (below_rows + 63) / 64;
@@ -519,17 +528,37 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
         const int bs = kb & ~(kKB - 1), be = std::min(bs + kKB, P.w[s]);
         const int m = P.m[s];
         if (kb + nb < be) {
-          for (int c0 = kb + nb; c0 < be; c0 += kTile) {
-            for (int cc = c0; cc < std::min(c0 + kTile, be); cc++) ps.syrk_flops += 2.0 * nb * (m - cc);
-            for (int r0 = c0; r0 < m; r0 += kTile) P.syrk_tasks.push_back(make_int4(s, r0, c0, kb | (int)0x80000000));
-          }
+          for (int cc = kb + nb; cc < be; cc++) ps.syrk_flops += 2.0 * nb * (m - cc);
+          upd.push_back({s, kb + nb, be, kb | (int)0x80000000, kb + nb < P.w[s] ? kb + nb : -1});
         } else if (be < m) {
           const double K = kb + nb - bs, t = m - be;
           ps.syrk_flops += K * t * (t + 1.0);
-          for (int c0 = be; c0 < m; c0 += kTile)
-            for (int r0 = c0; r0 < m; r0 += kTile) P.syrk_tasks.push_back(make_int4(s, r0, c0, bs));
+          upd.push_back({s, be, m, bs, kb + nb < P.w[s] ? kb + nb : -1});
         }
       }
+      // output tiles: 128x128 (LDS-pipelined kernel) only when there are many
+      // rounds of them (measured: at <= ~500 tiles the 64x64 kernel's finer
+      // granularity wins, scripts/ubench_syrk.hip), else 64x64
+      auto ntiles = [&](int T) {
+        long long cnt = 0;
+        for (const Upd& u : upd)
+          for (int c0 = u.c0; c0 < u.c1; c0 += T) cnt += (P.m[u.s] - c0 + T - 1) / T;
+        return cnt;
+      };
+      ps.syrk_tile = ntiles(kBigTile) >= 4096 ? kBigTile : kTile;
+      // with 64-tiles, the tile holding the next panel's diagonal block goes to
+      // k_syrk_diag (look-ahead factorisation on the side stream)
+      for (const Upd& u : upd)
+        for (int c0 = u.c0; c0 < u.c1; c0 += ps.syrk_tile)
+          for (int r0 = c0; r0 < P.m[u.s]; r0 += ps.syrk_tile) {
+            if (ps.syrk_tile == kTile && r0 == c0 && c0 == u.next) {
+              P.sdiag_tasks.push_back(make_int4(u.s, r0, c0, u.k0));
+              diag_ready[u.s] = 1;
+            } else {
+              P.syrk_tasks.push_back(make_int4(u.s, r0, c0, u.k0));
+            }
+          }
+      ps.sdiag_cnt = (int)P.sdiag_tasks.size() - ps.sdiag_off;
       ps.potrf_cnt = (int)P.potrf_list.size() - ps.potrf_off;
       ps.trsm_cnt = (int)P.trsm_tasks.size() - ps.trsm_off;
       ps.syrk_cnt = (int)P.syrk_tasks.size() - ps.syrk_off;
