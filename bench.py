@@ -106,7 +106,8 @@ def main():
                   lin_ms=sum(s["kernel_linearize_ms"] for s in stats),
                   lin_n=sum(s["kernel_linearize_count"] for s in stats),
                   syrk_ms=sum(s["kernel_syrk_ms"] for s in stats),
-                  syrk_n=sum(s["kernel_syrk_count"] for s in stats))
+                  syrk_n=sum(s["kernel_syrk_count"] for s in stats),
+                  syrk_launches=sum(s["kernel_syrk_launches"] for s in stats))
 
     if rank == 0:
         n, ne = g.num_poses, g.num_edges
@@ -125,18 +126,20 @@ def main():
                 "timed_launches": totals["spmv_n"],
             }
         else:
-            # Schur updates of one factorisation, all k_panel_syrk launches of the
-            # profiled factorisations timed by dispatch events
-            syrk_tfs = (last["syrk_flops"] * totals["syrk_n"] / (totals["syrk_ms"] * 1e-3) / 1e12
-                        if totals["syrk_n"] and totals["syrk_ms"] > 0 else None)
+            # Schur updates (k_panel_syrk / k_panel_syrk128 launches) of the
+            # profiled factorisations (every --profile-every'th), each launch timed
+            # by dispatch events on the library's stream: achieved = algorithmic
+            # flops per launch / average launch duration
+            nl = last["kernel_syrk_count"] and totals["syrk_launches"] / totals["syrk_n"]
+            avg_ms = totals["syrk_ms"] / totals["syrk_launches"] if totals["syrk_launches"] else None
+            flops_launch = last["syrk_flops"] / nl if nl else None
+            syrk_tfs = flops_launch / (avg_ms * 1e-3) / 1e12 if avg_ms else None
             roofline = {
                 "kernel": "k_panel_syrk", "bound": "mfma", "achieved": syrk_tfs, "peak": FP64_MFMA_PEAK_TFS,
                 "unit": "TFLOP/s", "frac": syrk_tfs / FP64_MFMA_PEAK_TFS if syrk_tfs else None,
-                "traffic": pmc.get("k_panel_syrk_bytes_per_factorization"),
-                "flops_per_factorization": last["syrk_flops"],
-                "ms_per_factorization": totals["syrk_ms"] / totals["syrk_n"] if totals["syrk_n"] else None,
-                "profiled_factorizations": totals["syrk_n"],
-                "factor_flops": last["factor_flops"],
+                "traffic": pmc.get("k_panel_syrk_bytes_per_launch"),
+                "flops_per_launch": flops_launch, "avg_launch_ms": avg_ms, "launches_per_factorization": nl,
+                "profiled_factorizations": totals["syrk_n"], "factor_flops": last["factor_flops"],
             }
         out = {
             "metric": "GN iterations/sec + ms-to-chi2 convergence, 100k-pose Manhattan graph",

@@ -55,7 +55,8 @@ class PgoStats(C.Structure):
                 ("kernel_spmv_ms", C.c_double), ("kernel_spmv_count", C.c_longlong),
                 ("kernel_linearize_ms", C.c_double), ("kernel_linearize_count", C.c_longlong),
                 ("kernel_syrk_ms", C.c_double), ("kernel_syrk_count", C.c_longlong),
-                ("syrk_flops", C.c_double), ("factor_flops", C.c_double)]
+                ("syrk_flops", C.c_double), ("factor_flops", C.c_double),
+                ("kernel_syrk_launches", C.c_longlong)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
@@ -114,7 +115,7 @@ def lib():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.pgo_abi_version() != 1:
+    if L.pgo_abi_version() != 2:
         raise RuntimeError("libpgo.so ABI version mismatch")
     _lib = L
     return L

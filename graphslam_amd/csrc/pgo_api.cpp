@@ -537,6 +537,7 @@ int finish_solve(pgo_graph* g, pgo_stats* st, SolveState* ss) {
     for (int u = 0; u < ss->prof.used; u++) ms += ms_between(ss->prof.ev[2 * u], ss->prof.ev[2 * u + 1]);
     st->kernel_syrk_ms += ms;
     st->kernel_syrk_count++;
+    st->kernel_syrk_launches += ss->prof.used;
     st->syrk_flops = g->chol.syrk_flops;
   }
   return PGO_OK;

@@ -554,6 +554,10 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
             if (ps.syrk_tile == kTile && r0 == c0 && c0 == u.next) {
               P.sdiag_tasks.push_back(make_int4(u.s, r0, c0, u.k0));
               diag_ready[u.s] = 1;
+              // its flops leave the k_panel_syrk launch (profiled roofline)
+              const int m = P.m[u.s], depth = std::min(kb + kNB, P.w[u.s]) - (u.k0 & 0x7fffffff);
+              for (int cc = c0; cc < std::min({c0 + kTile, u.c1, m}); cc++)
+                ps.syrk_flops -= 2.0 * depth * (std::min(r0 + kTile, m) - cc);
             } else {
               P.syrk_tasks.push_back(make_int4(u.s, r0, c0, u.k0));
             }

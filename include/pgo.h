@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PGO_ABI_VERSION 1
+#define PGO_ABI_VERSION 2
 
 /* ---- status codes (GTSAM exception each one replaces) -------------------- */
 #define PGO_OK 0
@@ -112,6 +112,8 @@ typedef struct {
   long long kernel_syrk_count;  /* profiled factorisations                         */
   double syrk_flops;            /* Schur-update flops of one factorisation         */
   double factor_flops;          /* flops of one numeric factorisation              */
+  long long kernel_syrk_launches; /* timed Schur-update launches (all profiled
+                                   factorisations)                                  */
 } pgo_stats;
 
 /* ---- lifetime ------------------------------------------------------------ */

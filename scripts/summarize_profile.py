@@ -33,6 +33,12 @@ def counters(path):
             for k, v in per.items()}
 
 
+def short(name):
+    """'void pgo::k_panel_syrk<...>(pgo::CholDev, ...)' -> 'k_panel_syrk'."""
+    base = name.split("(")[0].split("<")[0]
+    return base.split("::")[-1].split(" ")[-1]
+
+
 def find(d, suffix):
     for base, _, files in os.walk(d):
         for f in files:
@@ -50,20 +56,29 @@ def main():
     shutil.copy(stats, os.path.join(out, f"{tag}_kernel_stats.csv"))
     fetch = counters(find(os.path.join(src, "pmc_FETCH_SIZE"), "counter_collection.csv.gz"))
     write = counters(find(os.path.join(src, "pmc_WRITE_SIZE"), "counter_collection.csv.gz"))
-    summary = {"tag": tag, "config": "C3", "formula": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024", "kernels": {}}
+    summary = {"tag": tag, "config": "C3", "formula": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024",
+               "note": "per launch: mean over the launches of the first linearisation (launch sizes vary "
+                       "for the Cholesky kernels), median also given", "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
-        f = fetch.get(k, {}).get("median_kib")
-        w = write.get(k, {}).get("median_kib")
-        summary["kernels"][k] = {"FETCH_SIZE_kib": f, "WRITE_SIZE_kib": w,
-                                 "hbm_bytes_per_launch": (2 * f + w) * 1024 if f is not None and w is not None else None,
-                                 "launches": fetch.get(k, {}).get("launches")}
+        f, w = fetch.get(k, {}), write.get(k, {})
+        ent = {"launches": f.get("launches"), "FETCH_SIZE_kib_mean": f.get("mean_kib"),
+               "WRITE_SIZE_kib_mean": w.get("mean_kib"), "FETCH_SIZE_kib_median": f.get("median_kib"),
+               "WRITE_SIZE_kib_median": w.get("median_kib")}
+        ok = f and w
+        ent["hbm_bytes_per_launch"] = (2 * f["mean_kib"] + w["mean_kib"]) * 1024 if ok else None
+        ent["hbm_bytes_per_launch_median"] = (2 * f["median_kib"] + w["median_kib"]) * 1024 if ok else None
+        summary["kernels"][short(k)] = ent
     with open(os.path.join(out, f"{tag}_pmc.json"), "w") as fh:
         json.dump(summary, fh, indent=1)
     traffic_path = os.path.join(out, "pmc_traffic.json")
     traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
-    traffic["C3"] = {"source": f"{tag}_pmc.json",
-                     "k_pcg_spmv_bytes_per_launch": summary["kernels"].get("k_pcg_spmv", {}).get("hbm_bytes_per_launch"),
-                     "k_linearize_bytes_per_launch": summary["kernels"].get("k_linearize", {}).get("hbm_bytes_per_launch")}
+    ent = traffic.get("C3", {})
+    ent["source"] = f"{tag}_pmc.json"
+    for k in ("k_panel_syrk", "k_linearize", "k_pcg_spmv"):
+        v = summary["kernels"].get(k, {}).get("hbm_bytes_per_launch")
+        if v is not None:
+            ent[f"{k}_bytes_per_launch"] = v
+    traffic["C3"] = ent
     with open(traffic_path, "w") as fh:
         json.dump(traffic, fh, indent=1)
     for logname in ("trace_bench.log",):
