@@ -41,7 +41,8 @@ struct pgo_graph {
   bool dev_values = false;                  // device pose == host xyt
   bool host_values = true;                  // host xyt == device pose
   DevGraph d;
-  std::vector<int> edge_slot0;              // side-0 slot of every between factor
+  std::vector<int> edge_slot0;              // side-0 slot of every between factor (user order)
+  std::vector<int> h_slot_edge;             // host copy of slot_edge (owner bits)
   bool gauge_free = false;                  // some connected component has no prior
   double* h_scal = nullptr;                 // pinned
   int* h_ctrl = nullptr;                    // pinned
@@ -204,7 +205,8 @@ int download_values(pgo_graph* g) {
 // Host-side structure of the graph (no HIP): resolved factor endpoints,
 // block-CSR slots, priors by vertex, gauge freedom.
 struct HostStructure {
-  std::vector<int2> eij;
+  std::vector<int2> eij;           // device order
+  std::vector<int> dorder;         // device factor -> user factor index
   std::vector<int> pv, row_ptr, slot_edge, slot_col, prior_ptr, porder;
   bool gauge_free = false;
 };
@@ -230,6 +232,18 @@ int build_structure(pgo_graph* g, HostStructure& H) {
       return fail(g, PGO_E_NO_KEY, "prior factor on key " + std::to_string(g->pk[q]) + " with no inserted value");
     pv[q] = a->second;
   }
+  // device order of the factors: sorted by (ei, ej), so that the side-0 slots
+  // of a row read consecutive factors (coalesced factor loads in k_linearize)
+  std::vector<int> dorder(ne);
+  for (int e = 0; e < ne; e++) dorder[e] = e;
+  std::stable_sort(dorder.begin(), dorder.end(), [&](int a, int b) {
+    return eij[a].x != eij[b].x ? eij[a].x < eij[b].x : eij[a].y < eij[b].y;
+  });
+  {
+    std::vector<int2> t(ne);
+    for (int e = 0; e < ne; e++) t[e] = eij[dorder[e]];
+    eij.swap(t);
+  }
   // block-CSR rows: every factor owns a slot in row ei (side 0) and row ej (side 1)
   const int ns = 2 * ne;
   std::vector<int> row_ptr(n + 1, 0);
@@ -240,12 +254,12 @@ int build_structure(pgo_graph* g, HostStructure& H) {
   for (int i = 0; i < n; i++) row_ptr[i + 1] += row_ptr[i];
   std::vector<int> fillp(row_ptr.begin(), row_ptr.end() - 1);
   std::vector<int> slot_edge(ns), slot_col(ns);
-  for (int e = 0; e < ne; e++) {
+  for (int e = 0; e < ne; e++) {   // owner: side 0 until a Cholesky plan re-assigns it
     int s0 = fillp[eij[e].x]++;
-    slot_edge[s0] = e << 1;
+    slot_edge[s0] = (e << 2) | 2;
     slot_col[s0] = eij[e].y;
     int s1 = fillp[eij[e].y]++;
-    slot_edge[s1] = (e << 1) | 1;
+    slot_edge[s1] = (e << 2) | 1;
     slot_col[s1] = eij[e].x;
   }
   // order each row by column (locality of the x gathers)
@@ -291,6 +305,7 @@ int build_structure(pgo_graph* g, HostStructure& H) {
     for (int q = 0; q < np; q++) porder[f[pv[q]]++] = q;
   }
   H.gauge_free = g->gauge_free;
+  H.dorder = std::move(dorder);
   H.eij = std::move(eij);
   H.pv = std::move(pv);
   H.row_ptr = std::move(row_ptr);
@@ -319,18 +334,20 @@ int upload_structure(pgo_graph* g) {
   const auto& porder = H.porder;
   g->h_row_ptr = row_ptr;
   g->h_slot_col = slot_col;
-  g->edge_slot0.assign(ne, -1);
+  g->h_slot_edge = slot_edge;
+  g->edge_slot0.assign(ne, -1);   // user factor -> its side-0 slot
   for (int k = 0; k < ns; k++)
-    if ((slot_edge[k] & 1) == 0) g->edge_slot0[slot_edge[k] >> 1] = k;
+    if ((slot_edge[k] & 1) == 0) g->edge_slot0[H.dorder[slot_edge[k] >> 2]] = k;
   std::vector<double4> hz(ne), hpz(np);
   std::vector<double2> hom(3 * (size_t)ne), hpom(3 * (size_t)np);
-  for (int e = 0; e < ne; e++) {
+  for (int de = 0; de < ne; de++) {
+    const int e = H.dorder[de];
     const double th = g->ez[3 * e + 2];
-    hz[e] = make_double4(g->ez[3 * e], g->ez[3 * e + 1], std::cos(th), std::sin(th));
+    hz[de] = make_double4(g->ez[3 * e], g->ez[3 * e + 1], std::cos(th), std::sin(th));
     const double* o = &g->eom[6 * (size_t)e];
-    hom[3 * e] = make_double2(o[0], o[1]);
-    hom[3 * e + 1] = make_double2(o[2], o[3]);
-    hom[3 * e + 2] = make_double2(o[4], o[5]);
+    hom[3 * de] = make_double2(o[0], o[1]);
+    hom[3 * de + 1] = make_double2(o[2], o[3]);
+    hom[3 * de + 2] = make_double2(o[4], o[5]);
   }
   for (int t = 0; t < np; t++) {
     const int q = porder[t];
@@ -427,6 +444,23 @@ int ensure_chol(pgo_graph* g) {
     pgo::chol_free(g->chol);
     return fail(g, e == hipErrorOutOfMemory ? PGO_E_NOMEM : PGO_E_HIP,
                 std::string("Cholesky plan upload: ") + hipGetErrorString(e));
+  }
+  // owner slot of every factor := its block in the lower triangle of the
+  // permuted matrix (the one the assembly reads); with write_all = 0 the
+  // linearisation writes only these
+  {
+    const int n = g->d.n;
+    std::vector<int> slot_edge = g->h_slot_edge;
+    for (int r = 0; r < n; r++)
+      for (int k = g->h_row_ptr[r]; k < g->h_row_ptr[r + 1]; k++) {
+        const bool own = g->chol.iperm[r] > g->chol.iperm[g->h_slot_col[k]];
+        slot_edge[k] = (slot_edge[k] & ~2) | (own ? 2 : 0);
+      }
+    g->h_slot_edge = slot_edge;
+    if (!slot_edge.empty())
+      HIP_TRY(g, hipMemcpyAsync(g->d.slot_edge, slot_edge.data(), slot_edge.size() * sizeof(int),
+                                hipMemcpyHostToDevice, g->d.stream));
+    HIP_TRY(g, hipStreamSynchronize(g->d.stream));
   }
   g->chol_ready = true;
   return PGO_OK;
@@ -798,6 +832,10 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
                 "Gauss-Newton: a connected component has no prior, the linear system is singular");
   }
   hipEvent_t* ev = g->ev;
+  // Cholesky: the plan (and the owner bits it assigns) first, then the
+  // linearisation writes only the blocks the assembly reads
+  if (p.linear_solver != PGO_SOLVER_PCG && d.n > 0) RC_TRY(ensure_chol(g));
+  d.write_all = p.linear_solver == PGO_SOLVER_PCG ? 1 : 0;
   if (!(err <= p.error_tol) && iters < p.max_iterations && d.n > 0) {
     double new_err = err;
     for (;;) {
@@ -954,6 +992,7 @@ int pgo_debug_linearize(pgo_graph* g, double* hdiag, double* hoff, double* grad,
   if (!g) return PGO_E_ARG;
   RC_TRY(ensure_device(g));
   DevGraph& d = g->d;
+  d.write_all = 1;   // diagnostics read every block
   HIP_TRY(g, pgo::launch_linearize(d));
   HIP_TRY(g, pgo::launch_error(d, d.pose, d.scal));  // overwrites partial slice A
   std::vector<double> V(9 * (size_t)d.nslots), D(6 * (size_t)d.n), G(3 * (size_t)d.n);
@@ -973,7 +1012,8 @@ int pgo_debug_linearize(pgo_graph* g, double* hdiag, double* hoff, double* grad,
       o[6] = s[2]; o[7] = s[4]; o[8] = s[5];
     }
   if (hoff)
-    for (int e = 0; e < d.ne; e++) std::memcpy(hoff + 9 * (size_t)e, &V[9 * (size_t)g->edge_slot0[e]], 72);
+    for (int e = 0; e < d.ne; e++)
+      for (int q = 0; q < 9; q++) hoff[9 * (size_t)e + q] = V[q * (size_t)d.nslots + g->edge_slot0[e]];
   if (grad) std::memcpy(grad, G.data(), G.size() * 8);
   return PGO_OK;
 }
@@ -982,6 +1022,7 @@ int pgo_debug_spmv(pgo_graph* g, double lambda, const double* x, double* y) {
   if (!g || !x || !y) return PGO_E_ARG;
   RC_TRY(ensure_device(g));
   DevGraph& d = g->d;
+  d.write_all = 1;   // diagnostics read every block
   HIP_TRY(g, pgo::launch_linearize(d));
   RC_TRY(h2d(g, d.p, x, 3 * (size_t)d.n));
   HIP_TRY(g, pgo::launch_spmv(d, lambda, d.p, d.q));
@@ -997,6 +1038,7 @@ int pgo_debug_solve(pgo_graph* g, double lambda, const pgo_params* params, doubl
   else pgo_default_params(&p);
   RC_TRY(ensure_device(g));
   DevGraph& d = g->d;
+  d.write_all = 1;   // diagnostics read every block
   HIP_TRY(g, pgo::launch_linearize(d));
   pgo_stats st;
   std::memset(&st, 0, sizeof(st));

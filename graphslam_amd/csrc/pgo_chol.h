@@ -62,6 +62,7 @@ struct CholLevel {
 struct CholPlan {
   // ---- host symbolic result ----
   int n = 0, ns = 0;
+  long long nslots = 0;            // block-CSR slots of the analysed pattern (stride of V)
   std::vector<int> perm, iperm;    // pose level: new -> old, old -> new
   std::vector<int> sfirst;         // [ns+1] first pose (new index) of each supernode
   std::vector<int> m, w;           // scalar front rows / pivot columns
@@ -122,7 +123,8 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
 hipError_t chol_upload(CholPlan& P, hipStream_t s);
 void chol_free(CholPlan& P);
 
-// device: factor H + lambda I (D: 6 doubles/pose upper, V: slot blocks, old indexing)
+// device: factor H + lambda I (D: 6 doubles/pose upper, V: slot blocks as structure of
+// arrays V[q * nslots + slot], old indexing; only the slots in asm_src are read)
 // prof (optional): timing of the Schur-update launches with dispatch events;
 // pairs of events, capacity cap; *used pairs recorded, flops[i] per pair.
 struct SyrkProfile {

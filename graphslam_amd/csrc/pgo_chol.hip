@@ -52,7 +52,8 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------ assembly
 // off-diagonal lower blocks H_{i,j} (i > j) of a front: sum of their slots
-__global__ __launch_bounds__(256) void k_asm_offdiag(CholDev c, const double* __restrict__ V, int ntargets) {
+__global__ __launch_bounds__(256) void k_asm_offdiag(CholDev c, const double* __restrict__ V, long long S,
+                                                     int ntargets) {
   const int t = blockIdx.x * 256 + threadIdx.x;
   if (t >= ntargets) return;
   const int s = c.asm_front[t];
@@ -60,9 +61,9 @@ __global__ __launch_bounds__(256) void k_asm_offdiag(CholDev c, const double* __
   double* Fs = c.F + c.foff[s];
   double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int q = c.asm_ptr[t]; q < c.asm_ptr[t + 1]; q++) {
-    const double* v = V + 9 * (size_t)c.asm_src[q];
+    const double* v = V + c.asm_src[q];   // structure of arrays: element e at v[e * S]
 #pragma unroll
-    for (int e = 0; e < 9; e++) acc[e] += v[e];
+    for (int e = 0; e < 9; e++) acc[e] += v[e * S];
   }
   const int r0 = 3 * c.asm_li[t], c0 = 3 * c.asm_lj[t];
 #pragma unroll
@@ -966,7 +967,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, hipS
   CH_TRY(hipMemsetAsync(P.F, 0, P.ftotal * sizeof(double), s));
   CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int), s));
   const int nt = (int)P.asm_front.size();
-  if (nt) k_asm_offdiag<<<(nt + 255) / 256, 256, 0, s>>>(c, V, nt);
+  if (nt) k_asm_offdiag<<<(nt + 255) / 256, 256, 0, s>>>(c, V, P.nslots, nt);
   k_asm_diag<<<(P.n + 255) / 256, 256, 0, s>>>(c, D, P.d_lambda, P.n);
   for (const CholLevel& lv : P.levels) {
     for (size_t r = 0; r < lv.ea_off.size(); r++) {

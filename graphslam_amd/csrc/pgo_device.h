@@ -5,12 +5,18 @@
 //                row_ptr int, prior_ptr int, D 6 doubles (upper of H_ii),
 //                g 3, Minv 6, PCG x/r/z/p/q 3 each
 //   per factor : eij int2, ez double4 (x, y, c, s), eom 3 x double2
-//                (O00,O01)(O02,O11)(O12,O22) -- Omega upper triangle
-//   per slot   : V 9 doubles (row-major 3x3 block H_{row,col}), slot_edge int
-//                (factor << 1 | side), slot_col int.  Slots of a row are
-//                contiguous (block-CSR over vertices, full symmetric storage),
-//                each between factor owns two slots: side 0 in row ei holds
-//                H_{ei,ej} = J1^T Omega, side 1 in row ej holds H_{ej,ei} = Omega J1.
+//                (O00,O01)(O02,O11)(O12,O22) -- Omega upper triangle.  Factors
+//                are stored in device order, sorted by (ei, ej), so the side-0
+//                slots of a row read consecutive factors.
+//   per slot   : V 9 doubles, structure of arrays: V[q * S + k] = element q
+//                (row-major) of the 3x3 block H_{row,col} of slot k (coalesced
+//                in slot order); slot_edge int (factor << 2 | owner << 1 | side),
+//                slot_col int.  Slots of a row are contiguous (block-CSR over
+//                vertices, full symmetric storage), each between factor owns two
+//                slots: side 0 in row ei holds H_{ei,ej} = J1^T Omega, side 1 in
+//                row ej holds H_{ej,ei} = Omega J1.  One of the two is the
+//                factor's owner slot (side 0, or with the Cholesky plan the
+//                block in the lower triangle of the permuted matrix).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -32,7 +38,9 @@ struct DevGraph {
   double2* pom = nullptr;
   // block-CSR rows
   int* row_ptr = nullptr;
-  int* slot_edge = nullptr;
+  int* slot_edge = nullptr;        // (device edge << 2) | (owner << 1) | side
+  int write_all = 1;                // 1: both blocks of every edge in V (PCG, diagnostics);
+                                    // 0: owner blocks only (the Cholesky assembly reads no others)
   int* slot_col = nullptr;
   double* V = nullptr;
   double* D = nullptr;

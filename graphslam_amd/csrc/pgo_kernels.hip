@@ -73,7 +73,8 @@ __global__ __launch_bounds__(kThreads) void k_linearize(DevGraph d) {
     const int beg = d.row_ptr[row], end = d.row_ptr[row + 1];
     for (int k = beg + lane; k < end; k += G) {
       const int se = d.slot_edge[k];
-      const int e = se >> 1;
+      const int e = se >> 2;
+      const bool put = d.write_all || (se & 2);   // owner blocks only for the Cholesky assembly
       const int2 ij = d.eij[e];
       const double4 p1 = d.pose[ij.x], p2 = d.pose[ij.y], z = d.ez[e];
       const double2 oA = d.eom[3 * e], oB = d.eom[3 * e + 1], oC = d.eom[3 * e + 2];
@@ -97,11 +98,14 @@ __global__ __launch_bounds__(kThreads) void k_linearize(DevGraph d) {
       const double w0 = o00 * e0 + o01 * e1 + o02 * e2;
       const double w1 = o01 * e0 + o11 * e1 + o12 * e2;
       const double w2 = o02 * e0 + o12 * e1 + o22 * e2;
-      double* v = d.V + 9 * (size_t)k;
+      double* v = d.V + k;
+      const size_t S = d.nslots;
       if ((se & 1) == 0) {  // row ei: H_ij = J1'Omega = M', H_ii += J1'M, g_i += J1'w
-        v[0] = m00; v[1] = m10; v[2] = m20;
-        v[3] = m01; v[4] = m11; v[5] = m21;
-        v[6] = m02; v[7] = m12; v[8] = m22;
+        if (put) {
+          v[0] = m00; v[S] = m10; v[2 * S] = m20;
+          v[3 * S] = m01; v[4 * S] = m11; v[5 * S] = m21;
+          v[6 * S] = m02; v[7 * S] = m12; v[8 * S] = m22;
+        }
         a00 += -hc * m00 + hs * m10;
         a01 += -hc * m01 + hs * m11;
         a02 += -hc * m02 + hs * m12;
@@ -113,9 +117,11 @@ __global__ __launch_bounds__(kThreads) void k_linearize(DevGraph d) {
         g2 += dt1 * w0 + dt2 * w1 - w2;
         chi += 0.5 * (e0 * w0 + e1 * w1 + e2 * w2);
       } else {              // row ej: H_ji = Omega J1 = M, H_jj += Omega, g_j += w
-        v[0] = m00; v[1] = m01; v[2] = m02;
-        v[3] = m10; v[4] = m11; v[5] = m12;
-        v[6] = m20; v[7] = m21; v[8] = m22;
+        if (put) {
+          v[0] = m00; v[S] = m01; v[2 * S] = m02;
+          v[3 * S] = m10; v[4 * S] = m11; v[5 * S] = m12;
+          v[6 * S] = m20; v[7 * S] = m21; v[8 * S] = m22;
+        }
         a00 += o00; a01 += o01; a02 += o02; a11 += o11; a12 += o12; a22 += o22;
         g0 += w0; g1 += w1; g2 += w2;
       }
@@ -260,11 +266,12 @@ __global__ __launch_bounds__(kThreads) void k_pcg_spmv(DevGraph d, double lam) {
     const int beg = d.row_ptr[row], end = d.row_ptr[row + 1];
     for (int k = beg + lane; k < end; k += G) {
       const int c = d.slot_col[k];
-      const double* v = d.V + 9 * (size_t)k;
+      const double* v = d.V + k;
+      const size_t S = d.nslots;
       const double x0 = P[3 * c], x1 = P[3 * c + 1], x2 = P[3 * c + 2];
-      y0 += v[0] * x0 + v[1] * x1 + v[2] * x2;
-      y1 += v[3] * x0 + v[4] * x1 + v[5] * x2;
-      y2 += v[6] * x0 + v[7] * x1 + v[8] * x2;
+      y0 += v[0] * x0 + v[S] * x1 + v[2 * S] * x2;
+      y1 += v[3 * S] * x0 + v[4 * S] * x1 + v[5 * S] * x2;
+      y2 += v[6 * S] * x0 + v[7 * S] * x1 + v[8 * S] * x2;
     }
     y0 = sg_sum<G>(y0);
     y1 = sg_sum<G>(y1);
@@ -341,35 +348,38 @@ __global__ __launch_bounds__(kThreads) void k_pcg_dir(DevGraph d, int nb_vec, in
   }
 }
 
-// y = H delta (no damping); partials delta'H delta (slice A) and g'delta (slice A+1)
+// Partials delta'H delta (slice A) and g'delta (slice A+1), H undamped:
+// delta'H delta = sum_i d_i'H_ii d_i + 2 sum over owner slots d_row'H_{row,col} d_col,
+// so it needs only the owner blocks (what the Cholesky-mode linearisation writes).
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_model_decrease(DevGraph d, const double* __restrict__ X) {
   __shared__ double lds[kThreads / 64];
   const int lane = threadIdx.x & (G - 1);
   const int nsg = gridDim.x * (kThreads / G);
+  const size_t S = d.nslots;
   double xhx = 0.0, gx = 0.0;
   for (int row = (blockIdx.x * kThreads + threadIdx.x) / G; row < d.n; row += nsg) {
-    double y0 = 0, y1 = 0, y2 = 0;
+    const double r0 = X[3 * row], r1 = X[3 * row + 1], r2 = X[3 * row + 2];
+    double t = 0.0;
     const int beg = d.row_ptr[row], end = d.row_ptr[row + 1];
     for (int k = beg + lane; k < end; k += G) {
+      if (!(d.slot_edge[k] & 2)) continue;
       const int c = d.slot_col[k];
-      const double* v = d.V + 9 * (size_t)k;
+      const double* v = d.V + k;
       const double x0 = X[3 * c], x1 = X[3 * c + 1], x2 = X[3 * c + 2];
-      y0 += v[0] * x0 + v[1] * x1 + v[2] * x2;
-      y1 += v[3] * x0 + v[4] * x1 + v[5] * x2;
-      y2 += v[6] * x0 + v[7] * x1 + v[8] * x2;
+      const double y0 = v[0] * x0 + v[S] * x1 + v[2 * S] * x2;
+      const double y1 = v[3 * S] * x0 + v[4 * S] * x1 + v[5 * S] * x2;
+      const double y2 = v[6 * S] * x0 + v[7 * S] * x1 + v[8 * S] * x2;
+      t += r0 * y0 + r1 * y1 + r2 * y2;
     }
-    y0 = sg_sum<G>(y0);
-    y1 = sg_sum<G>(y1);
-    y2 = sg_sum<G>(y2);
+    t = sg_sum<G>(t);
     if (lane == 0) {
       const double* D = d.D + 6 * (size_t)row;
-      const double x0 = X[3 * row], x1 = X[3 * row + 1], x2 = X[3 * row + 2];
-      y0 += D[0] * x0 + D[1] * x1 + D[2] * x2;
-      y1 += D[1] * x0 + D[3] * x1 + D[4] * x2;
-      y2 += D[2] * x0 + D[4] * x1 + D[5] * x2;
-      xhx += x0 * y0 + x1 * y1 + x2 * y2;
-      gx += d.g[3 * row] * x0 + d.g[3 * row + 1] * x1 + d.g[3 * row + 2] * x2;
+      const double y0 = D[0] * r0 + D[1] * r1 + D[2] * r2;
+      const double y1 = D[1] * r0 + D[3] * r1 + D[4] * r2;
+      const double y2 = D[2] * r0 + D[4] * r1 + D[5] * r2;
+      xhx += 2.0 * t + (r0 * y0 + r1 * y1 + r2 * y2);
+      gx += d.g[3 * row] * r0 + d.g[3 * row + 1] * r1 + d.g[3 * row + 2] * r2;
     }
   }
   xhx = block_sum(xhx, lds);
@@ -391,11 +401,12 @@ __global__ __launch_bounds__(kThreads) void k_spmv(DevGraph d, double lam, const
     const int beg = d.row_ptr[row], end = d.row_ptr[row + 1];
     for (int k = beg + lane; k < end; k += G) {
       const int c = d.slot_col[k];
-      const double* v = d.V + 9 * (size_t)k;
+      const double* v = d.V + k;
+      const size_t S = d.nslots;
       const double x0 = X[3 * c], x1 = X[3 * c + 1], x2 = X[3 * c + 2];
-      y0 += v[0] * x0 + v[1] * x1 + v[2] * x2;
-      y1 += v[3] * x0 + v[4] * x1 + v[5] * x2;
-      y2 += v[6] * x0 + v[7] * x1 + v[8] * x2;
+      y0 += v[0] * x0 + v[S] * x1 + v[2 * S] * x2;
+      y1 += v[3 * S] * x0 + v[4 * S] * x1 + v[5 * S] * x2;
+      y2 += v[6 * S] * x0 + v[7 * S] * x1 + v[8 * S] * x2;
     }
     y0 = sg_sum<G>(y0);
     y1 = sg_sum<G>(y1);

@@ -112,6 +112,7 @@ std::vector<int> amd(int n, const std::vector<int>& xadj, const std::vector<int>
 }  // namespace
 
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
+  P.nslots = (long long)slot_col.size();
   P.n = n;
   // ---- pose adjacency (old index), unique, no self loops
   std::vector<int> xadj(n + 1, 0), adj;
