@@ -538,14 +538,14 @@ int linear_solve(pgo_graph* g, const pgo_params& p, double lam, pgo_stats* st, S
   *g->h_lam = lam;
   HIP_TRY(g, hipMemcpyAsync(g->chol.d_lambda, g->h_lam, sizeof(double), hipMemcpyHostToDevice, d.stream));
   if (prof || !p.use_graphs) {  // eager: profiled factorisations time their Schur-update launches
-    HIP_TRY(g, pgo::chol_factor(g->chol, d.D, d.V, d.stream, prof));
-    HIP_TRY(g, pgo::chol_solve(g->chol, d.g, d.x, -1.0, d.stream));
+    HIP_TRY(g, pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, prof));
+    HIP_TRY(g, pgo::chol_solve(g->chol, d.x, d.stream));
   } else {
     if (!g->chol_exec) {  // capture once per structure: ~1e3 launches -> one graph launch
       hipGraph_t graph = nullptr;
       HIP_TRY(g, hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal));
-      const hipError_t e1 = pgo::chol_factor(g->chol, d.D, d.V, d.stream, nullptr);
-      const hipError_t e2 = pgo::chol_solve(g->chol, d.g, d.x, -1.0, d.stream);
+      const hipError_t e1 = pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr);
+      const hipError_t e2 = pgo::chol_solve(g->chol, d.x, d.stream);
       HIP_TRY(g, hipStreamEndCapture(d.stream, &graph));
       HIP_TRY(g, e1);
       HIP_TRY(g, e2);
@@ -947,12 +947,17 @@ int pgo_debug_plan(pgo_graph* g, double* out, int cap) {
   RC_TRY(build_structure(g, H));
   pgo::CholPlan P;
   pgo::chol_analyze(P, (int)g->keys.size(), H.row_ptr, H.slot_col);
-  long long lf = 2, ls = 2, trsm = 0, syrk = 0;   // launches: memsets/assembly, perm in/out
+  // launches: factor = memsets, assembly, rhs permutation, per level extend-add
+  // ranks + vector assembly + small classes + per panel diag/trsm/Schur (+look-ahead);
+  // solve (backward only) = per level partials + init + steps, perm out
+  long long lf = 5, ls = 1, trsm = 0, syrk = 0;
   int maxm = 0;
   for (int s = 0; s < P.ns; s++) maxm = std::max(maxm, P.m[s]);
   for (const auto& lv : P.levels) {
-    lf += (long long)lv.ea_off.size() + lv.small.size() + 3 * lv.panels.size();
-    ls += 2 + (long long)lv.fwd.size() + (long long)lv.bwd.size() - 1;
+    lf += (long long)lv.ea_off.size() + 1 + lv.small.size();
+    for (const auto& ps : lv.panels)
+      lf += (ps.potrf_cnt > 0) + (ps.trsm_cnt > 0) + (ps.syrk_cnt > 0) + (ps.sdiag_cnt > 0);
+    ls += (lv.bwd_part.cnt > 0) + (long long)lv.bwd.size();
     for (const auto& ps : lv.panels) {
       trsm += ps.trsm_cnt;
       syrk += ps.syrk_cnt;

@@ -54,7 +54,6 @@ struct CholLevel {
   int front_off, front_cnt;        // all fronts of the level in level_fronts (solves)
   int small_maxm = 0, maxm = 0;    // LDS sizing
   int maxblk = 0;                  // max 64-column blocks of a front's pivot columns
-  std::vector<SolveStep> fwd;      // forward step b = 0 .. maxblk-1 (rows below block b)
   std::vector<SolveStep> bwd;      // backward: [0] = init (all columns), then steps b = maxblk-1 .. 1
   SolveStep bwd_part{0, 0};        // partial products feeding the init tasks
 };
@@ -82,7 +81,7 @@ struct CholPlan {
   std::vector<int> small_list, level_fronts, potrf_list;
   std::vector<int2> trsm_tasks;
   std::vector<int4> syrk_tasks, sdiag_tasks;
-  std::vector<int4> fwd_tasks, bwd_tasks;
+  std::vector<int4> bwd_tasks;
   std::vector<int2> bwd_pref;      // per bwd task: first partial, partial count (init tasks)
   std::vector<int4> bwd_part_tasks;  // (front, c0, r0, partial slot)
   int npart = 0;
@@ -109,7 +108,7 @@ struct CholPlan {
   hipStream_t side = nullptr;      // look-ahead diagonal tiles
   hipStream_t side2 = nullptr;     // small fronts beside the blocked path
   hipEvent_t evs[4] = {nullptr, nullptr, nullptr, nullptr};
-  int4 *d_fwd = nullptr, *d_bwd = nullptr, *d_bwd_part = nullptr;
+  int4 *d_bwd = nullptr, *d_bwd_part = nullptr;
   int2* d_bwd_pref = nullptr;
   double* d_partial = nullptr;
   int* d_ea_children = nullptr;
@@ -132,10 +131,12 @@ struct SyrkProfile {
   int cap = 0, used = 0;
   double* flops = nullptr;
 };
-// lambda is read from P.d_lambda (set it with a stream-ordered copy first)
-hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, hipStream_t s,
-                       SyrkProfile* prof = nullptr);
-// x = (L L^T)^{-1} b, b and x indexed by old pose (3 per pose); may alias
-hipError_t chol_solve(const CholPlan& P, const double* b, double* x, double scale_b, hipStream_t s);
+// lambda is read from P.d_lambda (set it with a stream-ordered copy first).  The
+// right-hand side scale_b * b (old pose indexing) is carried through the
+// factorisation as an extra column: on return the frontal vectors hold y = L^-1 b.
+hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
+                       hipStream_t s, SyrkProfile* prof = nullptr);
+// after chol_factor: x = L^-T y = (L L^T)^{-1} scale_b b, indexed by old pose
+hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s);
 
 }  // namespace pgo

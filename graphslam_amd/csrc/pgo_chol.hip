@@ -170,14 +170,19 @@ __device__ __forceinline__ void tri_inverse_wg(const double* L, int ld, int nbk,
 // m <= 128: the whole front in LDS; right-looking, two threads per row (the
 // row's columns split even/odd) so LDS accesses of a wave are consecutive rows.
 __global__ __launch_bounds__(256) void k_front_small(CholDev c, const int* __restrict__ list) {
-  extern __shared__ __attribute__((aligned(16))) double A[];
+  extern __shared__ __attribute__((aligned(16))) double A[];   // m*m front, 64 scratch, m frontal vector
   const int s = list[blockIdx.x];
   const int m = c.m[s], w = c.w[s];
   double* Fs = c.F + c.foff[s];
+  double* fv = c.fv + c.voff[s];
+  double* v = A + m * m + 64;
   const int tid = threadIdx.x;
   for (int j = 0; j < m; j++)
     for (int i = j + tid; i < m; i += 256) A[i + j * m] = Fs[i + (size_t)j * m];
+  for (int i = tid; i < m; i += 256) v[i] = fv[i];
   __syncthreads();
+  // the frontal vector is carried as an extra column: forward substitution
+  // L y = v for the pivot rows and v_below -= L21 y, in the same sweep
   const int half = tid >> 7, rsub = tid & 127;
   for (int k = 0; k < w; k++) {
     double d = A[k + k * m];
@@ -187,19 +192,25 @@ __global__ __launch_bounds__(256) void k_front_small(CholDev c, const int* __res
     }
     const double piv = sqrt(d);
     __syncthreads();  // every thread has read the pivot before it is overwritten
-    if (tid == 0) A[k + k * m] = piv;
     const double inv = 1.0 / piv;
+    if (tid == 0) {
+      A[k + k * m] = piv;
+      v[k] *= inv;
+    }
     for (int i = k + 1 + tid; i < m; i += 256) A[i + k * m] *= inv;
     __syncthreads();
+    const double vk = v[k];
     for (int i = k + 1 + rsub; i < m; i += 128) {
       const double lik = A[i + k * m];
+      if (half == 0) v[i] -= lik * vk;
       for (int j = k + 1 + half; j <= i; j += 2) A[i + j * m] -= lik * A[j + k * m];
     }
     __syncthreads();
   }
   for (int j = 0; j < m; j++)
     for (int i = j + tid; i < m; i += 256) Fs[i + (size_t)j * m] = A[i + j * m];
-  // inverses of the 64-column diagonal blocks (used by the solves)
+  for (int i = tid; i < m; i += 256) fv[i] = v[i];
+  // inverses of the 64-column diagonal blocks (used by the backward solve)
   double* scratch = A + m * m;
   for (int jb = 0; jb < w; jb += 64)
     tri_inverse_wg(A + jb + jb * m, m, min(64, w - jb), c.Tinv + c.toff[s] + (jb / 64) * 4096, scratch);
@@ -377,13 +388,26 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
   return bad;
 }
 
+// Forward substitution of the panel's rows of the frontal vector: y = X v with
+// X = L_bb^-1 (LDS, ld 65); the rows below get v -= L y in k_panel_trsm.
+__device__ __forceinline__ void panel_rhs(double* v, const double* X, int nb, double* buf) {
+  const int tid = threadIdx.x;
+  if (tid < 64) buf[tid] = tid < nb ? v[tid] : 0.0;
+  __syncthreads();
+  if (tid < nb) {
+    double acc = 0.0;
+    for (int k = 0; k <= tid; k++) acc = fma(X[tid + k * 65], buf[k], acc);
+    v[tid] = acc;
+  }
+}
+
 // Diagonal tile of each listed front at panel kb: factored and inverted in LDS
 // (diag_factor_invert); L back into the front, L^-1 into Tinv for the TRSM GEMM
 // and the solves.
 __global__ __launch_bounds__(256) void k_panel_diag(CholDev c, const int* __restrict__ list, int kb) {
   __shared__ double Ts[64 * 65];
   __shared__ double Ws[64 * 65];
-  __shared__ double bc[32];
+  __shared__ double bc[64];
   const int s = list[blockIdx.x];
   const int m = c.m[s], w = c.w[s];
   const int nb = min(kNB, w - kb);
@@ -403,6 +427,7 @@ __global__ __launch_bounds__(256) void k_panel_diag(CholDev c, const int* __rest
     if (live) Fs[i + (size_t)j * m] = Ts[i + j * 65];
     M[j * 64 + i] = live ? Ws[i + j * 65] : 0.0;
   }
+  panel_rhs(c.fv + c.voff[s] + kb, Ws, nb, bc);
 }
 
 // Rows below the diagonal tile, 64 per workgroup (16 per wave): X = B L^-T as a
@@ -413,10 +438,13 @@ __global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __res
   const int2 task = tasks[blockIdx.x];
   const int s = task.x, chunk = task.y;
   const int m = c.m[s], w = c.w[s];
+  __shared__ double ys[64];
   const int nb = min(kNB, w - kb);
   const double* M = c.Tinv + c.toff[s] + (kb / 64) * 4096;
+  double* fv = c.fv + c.voff[s];
   const int tid = threadIdx.x;
   for (int idx = tid; idx < 4096; idx += 256) Tb[(idx >> 6) * LDB + (idx & 63)] = M[idx];
+  if (tid < 64) ys[tid] = tid < nb ? fv[kb + tid] : 0.0;   // y of the panel (diagonal step)
   __syncthreads();
   const int wv = tid >> 6, l = tid & 63;
   const int r0 = kb + nb + chunk * 64 + wv * 16;
@@ -438,16 +466,28 @@ __global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __res
     acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[32], acc2, 0, 0, 0);
     acc3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[48], acc3, 0, 0, 0);
   }
+  double part[4] = {0, 0, 0, 0};   // L[row, panel] y for the lane's 4 rows
 #pragma unroll
   for (int ct = 0; ct < 4; ct++) {
     const d4 v = ct == 0 ? acc0 : (ct == 1 ? acc1 : (ct == 2 ? acc2 : acc3));
     const int col = 16 * ct + (l & 15);
+    const double yc = ys[col];
+#pragma unroll
+    for (int r = 0; r < 4; r++) part[r] = fma(v[r], yc, part[r]);
     if (col >= nb) continue;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int row = r0 + kl + 4 * r;
       if (row < m) Fc[row + (size_t)col * m] = v[r];
     }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) {   // sum over the 16 lanes of the row group
+    double t = part[r];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o);
+    const int row = r0 + kl + 4 * r;
+    if ((l & 15) == 0 && row < m) fv[row] -= t;
   }
 }
 
@@ -534,7 +574,7 @@ __global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int4* __res
 __global__ __launch_bounds__(256) void k_syrk_diag(CholDev c, const int4* __restrict__ tasks, int kb) {
   __shared__ double Ts[64 * 65];
   __shared__ double Ws[64 * 65];
-  __shared__ double bc[32];
+  __shared__ double bc[64];
   const int4 t = tasks[blockIdx.x];
   const int s = t.x, kn = t.y;
   const int m = c.m[s], w = c.w[s];
@@ -557,6 +597,7 @@ __global__ __launch_bounds__(256) void k_syrk_diag(CholDev c, const int4* __rest
     if (live) Fs[i + (size_t)j * m] = Ts[i + j * 65];
     M[j * 64 + i] = live ? Ws[i + j * 65] : 0.0;
   }
+  panel_rhs(c.fv + c.voff[s] + kn, Ws, nb, bc);
 }
 
 // Schur update of one 128x128 lower tile (same task format and semantics as
@@ -675,12 +716,6 @@ __global__ __launch_bounds__(256) void k_perm_out(CholDev c, double* __restrict_
 
 // Diagonal-block solves with the inverted blocks: wave 0, lane i <-> row i.
 // y = X v (forward, X = L_bb^-1) and x = X' z (backward); v / z in LDS.
-__device__ __forceinline__ double tinv_fwd(const double* __restrict__ M, const double* v, int nbk) {
-  const int i = threadIdx.x;
-  double acc = 0.0;
-  for (int k = 0; k < nbk; k++) acc += M[k * 64 + i] * v[k];  // column k of X: coalesced
-  return acc;
-}
 
 __device__ __forceinline__ double tinv_bwd(const double* Ms, const double* z, int nbk) {  // Ms: LDS, Ms[a*65+b]
   const int i = threadIdx.x;
@@ -694,18 +729,18 @@ __device__ __forceinline__ void stage_tinv(const double* __restrict__ M, double*
     if ((idx & 63) < n) Ms[(idx >> 6) * 65 + (idx & 63)] = M[idx];
 }
 
-// Forward, launch 1 of a level: frontal vector = (own rhs, 0) + children's update
-// vectors (fixed order), then block 0 solved.  One workgroup per front.
-__global__ __launch_bounds__(256) void k_fwd_assemble(CholDev c, const int* __restrict__ list) {
+// Frontal vectors of a level before its factorisation: own rows from the
+// permuted right-hand side, below rows zero, plus the children's update
+// vectors (fixed order).  The factorisation then carries them as an extra
+// column (forward substitution fused into the panels).
+__global__ __launch_bounds__(256) void k_vec_assemble(CholDev c, const int* __restrict__ list) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* Ld = sm;                 // 64 x 65
-  double* v = sm + 64 * 65;        // m
+  double* v = sm;                  // m
   const int s = list[blockIdx.x];
   const int m = c.m[s], w = c.w[s];
   const int* rows = c.rows + c.rptr[s];
   const int tid = threadIdx.x;
   for (int r = tid; r < m; r += 256) v[r] = r < w ? c.xv[3 * rows[r / 3] + r % 3] : 0.0;
-  const int nbk = min(64, w);
   __syncthreads();
   for (int q = c.cptr[s]; q < c.cptr[s + 1]; q++) {
     const int ch = c.children[q];
@@ -715,47 +750,8 @@ __global__ __launch_bounds__(256) void k_fwd_assemble(CholDev c, const int* __re
     for (int t = tid; t < uc; t += 256) v[3 * rel[t / 3] + t % 3] += uv[t];
     __syncthreads();
   }
-  if (tid < 64) {
-    const double y = tinv_fwd(c.Tinv + c.toff[s], v, nbk);
-    Ld[tid] = y;
-  }
-  __syncthreads();
-  if (tid < nbk) v[tid] = Ld[tid];
-  __syncthreads();
   double* fv = c.fv + c.voff[s];
   for (int r = tid; r < m; r += 256) fv[r] = v[r];
-}
-
-// Forward step b: rows [r0, r1) -= L[r, block b] y_b; the task owning the next
-// diagonal block (rows of block b+1) then solves it.
-__global__ __launch_bounds__(256) void k_fwd_step(CholDev c, const int4* __restrict__ tasks, int b) {
-  __shared__ double y[64];
-  __shared__ double vn[64];
-  const int4 t = tasks[blockIdx.x];
-  const int s = t.x, r0 = t.y, r1 = t.z, owner = t.w;
-  const int m = c.m[s], w = c.w[s];
-  const double* L = c.F + c.foff[s];
-  double* fv = c.fv + c.voff[s];
-  const int tid = threadIdx.x;
-  const int jb = b * 64, nbk = min(64, w - jb);
-  if (tid < nbk) y[tid] = fv[jb + tid];
-  __syncthreads();
-  const int r = r0 + tid;
-  if (r < r1) {
-    double acc = 0.0;
-    for (int k = 0; k < nbk; k++) acc += L[r + (size_t)(jb + k) * m] * y[k];
-    const double nv = fv[r] - acc;
-    if (owner >= 0) vn[tid] = nv;
-    else fv[r] = nv;
-  }
-  if (owner < 0) return;
-  __syncthreads();
-  if (tid < 64) {
-    const int n2 = r1 - r0;
-    if (tid >= n2) vn[tid] = 0.0;
-    const double yy = tinv_fwd(c.Tinv + c.toff[s] + owner * 4096, vn, n2);
-    if (tid < n2) fv[r0 + tid] = yy;
-  }
 }
 
 // acc[0..N) of each lane -> acc[0..N/2): lanes with bit N/2 set keep the upper
@@ -932,7 +928,6 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(up(&P.d_level_fronts, P.level_fronts, s));
   CH_TRY(up(&P.d_trsm, P.trsm_tasks, s));
   CH_TRY(up(&P.d_potrf, P.potrf_list, s));
-  CH_TRY(up(&P.d_fwd, P.fwd_tasks, s));
   CH_TRY(up(&P.d_bwd, P.bwd_tasks, s));
   CH_TRY(up(&P.d_bwd_pref, P.bwd_pref, s));
   CH_TRY(up(&P.d_bwd_part, P.bwd_part_tasks, s));
@@ -951,7 +946,7 @@ void chol_free(CholPlan& P) {
   void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
                   P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
                   P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
-                  P.d_trsm, P.d_syrk, P.d_ea_children, P.d_ea_colpref, P.d_potrf, P.d_fwd, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag};
+                  P.d_trsm, P.d_syrk, P.d_ea_children, P.d_ea_colpref, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : P.evs)
@@ -961,9 +956,11 @@ void chol_free(CholPlan& P) {
   P = CholPlan();
 }
 
-hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, hipStream_t s, SyrkProfile* prof) {
+hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
+                       hipStream_t s, SyrkProfile* prof) {
   if (P.n == 0) return hipSuccess;
   const CholDev c = dev_view(P);
+  k_perm_in<<<(P.n + 255) / 256, 256, 0, s>>>(c, b, scale_b, P.n);
   CH_TRY(hipMemsetAsync(P.F, 0, P.ftotal * sizeof(double), s));
   CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int), s));
   const int nt = (int)P.asm_front.size();
@@ -977,6 +974,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, hipS
       k_extend_add<<<(unsigned)blocks, 256, 0, s>>>(c, P.d_ea_children + lv.ea_off[r],
                                                     P.d_ea_colpref + lv.ea_cols_off[r], lv.ea_cnt[r]);
     }
+    k_vec_assemble<<<lv.front_cnt, 256, (size_t)lv.maxm * sizeof(double), s>>>(c, P.d_level_fronts + lv.front_off);
     // small fronts on the second side stream, beside the blocked path of the
     // same level (disjoint fronts); joined before the next level
     const bool fork_small = !lv.small.empty() && !lv.panels.empty();
@@ -987,7 +985,8 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, hipS
       ss = P.side2;
     }
     for (const SmallClass& sc : lv.small)
-      k_front_small<<<sc.cnt, 256, (size_t)(sc.mmax * sc.mmax + 64) * sizeof(double), ss>>>(c, P.d_small + sc.off);
+      k_front_small<<<sc.cnt, 256, (size_t)(sc.mmax * sc.mmax + 64 + sc.mmax) * sizeof(double), ss>>>(
+          c, P.d_small + sc.off);
     for (const PanelStep& ps : lv.panels) {
       if (ps.potrf_cnt) k_panel_diag<<<ps.potrf_cnt, 256, 0, s>>>(c, P.d_potrf + ps.potrf_off, ps.kb);
       if (ps.trsm_cnt) k_panel_trsm<<<ps.trsm_cnt, 256, 0, s>>>(c, P.d_trsm + ps.trsm_off, ps.kb);
@@ -1019,17 +1018,10 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, hipS
   return hipGetLastError();
 }
 
-hipError_t chol_solve(const CholPlan& P, const double* b, double* x, double scale_b, hipStream_t s) {
+hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s) {
   if (P.n == 0) return hipSuccess;
   const CholDev c = dev_view(P);
   const int g = (P.n + 255) / 256;
-  k_perm_in<<<g, 256, 0, s>>>(c, b, scale_b, P.n);
-  for (const CholLevel& lv : P.levels) {
-    k_fwd_assemble<<<lv.front_cnt, 256, (size_t)(64 * 65 + lv.maxm) * sizeof(double), s>>>(
-        c, P.d_level_fronts + lv.front_off);
-    for (int bb = 0; bb < (int)lv.fwd.size(); bb++)
-      if (lv.fwd[bb].cnt) k_fwd_step<<<lv.fwd[bb].cnt, 256, 0, s>>>(c, P.d_fwd + lv.fwd[bb].off, bb);
-  }
   for (auto it = P.levels.rbegin(); it != P.levels.rend(); ++it) {
     const CholLevel& lv = *it;
     if (lv.bwd_part.cnt)

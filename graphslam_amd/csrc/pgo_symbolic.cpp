@@ -388,7 +388,6 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.syrk_tasks.clear();
   P.sdiag_tasks.clear();
   P.potrf_list.clear();
-  P.fwd_tasks.clear();
   P.bwd_tasks.clear();
   P.bwd_pref.clear();
   P.bwd_part_tasks.clear();
@@ -404,24 +403,9 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       lv.maxm = std::max(lv.maxm, P.m[s]);
       if (P.m[s] <= kSmallFront) lv.small_maxm = std::max(lv.small_maxm, P.m[s]);
     }
-    // blocked triangular solves (64-column blocks of each front's pivot columns)
+    // blocked backward solve (64-column blocks of each front's pivot columns);
+    // the forward substitution is carried by the factorisation
     for (int s : bylevel[L]) lv.maxblk = std::max(lv.maxblk, (P.w[s] + 63) / 64);
-    for (int b = 0; b < lv.maxblk; b++) {        // forward step b: rows below block b
-      SolveStep st{(int)P.fwd_tasks.size(), 0};
-      for (int s : bylevel[L]) {
-        const int w = P.w[s], m = P.m[s], nblk = (w + 63) / 64;
-        if (b >= nblk) continue;
-        int rest = w;
-        if (b + 1 < nblk) {                      // owner of the next diagonal block
-          const int e = std::min((b + 2) * 64, w);
-          P.fwd_tasks.push_back(make_int4(s, (b + 1) * 64, e, b + 1));
-          rest = e;
-        }
-        for (int r = rest; r < m; r += 256) P.fwd_tasks.push_back(make_int4(s, r, std::min(r + 256, m), -1));
-      }
-      st.cnt = (int)P.fwd_tasks.size() - st.off;
-      lv.fwd.push_back(st);
-    }
     {                                            // backward init: all columns vs the rows below w
       // partial products L21[r0:r0+kBwdRows, block]' x_below, one task each,
       // reduced in fixed order by the init task of the block
