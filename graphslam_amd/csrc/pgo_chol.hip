@@ -139,7 +139,7 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // L[r + c*ld]), by the 4 waves of a workgroup: wave wv owns columns 16wv..16wv+15,
 // lane i row i; column-oriented substitution, row k broadcast with v_readlane
 // (no LDS round trip on the dependency chain).  dinv: LDS scratch of 64.
-// Written column-major to M (M[a*64 + b] = X[b][a]), zero outside nbk x nbk.
+// Written row-major to M (M[a*64 + b] = X[a][b]), zero outside nbk x nbk.
 __device__ __forceinline__ void tri_inverse_wg(const double* L, int ld, int nbk, double* __restrict__ M,
                                                double* dinv) {
   const int tid = threadIdx.x;
@@ -162,7 +162,7 @@ __device__ __forceinline__ void tri_inverse_wg(const double* L, int ld, int nbk,
     }
   }
 #pragma unroll
-  for (int q = 0; q < 16; q++) M[(j0 + q) * 64 + i] = (i < nbk && j0 + q < nbk) ? xr[q] : 0.0;
+  for (int q = 0; q < 16; q++) M[i * 64 + j0 + q] = (i < nbk && j0 + q < nbk) ? xr[q] : 0.0;
   __syncthreads();  // dinv reusable
 }
 
@@ -420,12 +420,12 @@ __global__ __launch_bounds__(256) void k_panel_diag(CholDev c, const int* __rest
   }
   __syncthreads();
   if (diag_factor_invert(Ts, Ws, bc)) *c.flag = 1;
-  double* M = c.Tinv + c.toff[s] + (kb / 64) * 4096;
+  double* M = c.Tinv + c.toff[s] + (kb / 64) * 4096;   // row-major L^-1 of the tile
   for (int idx = tid; idx < 4096; idx += 256) {
     const int i = idx & 63, j = idx >> 6;
-    const bool live = i < nb && j < nb && i >= j;
-    if (live) Fs[i + (size_t)j * m] = Ts[i + j * 65];
-    M[j * 64 + i] = live ? Ws[i + j * 65] : 0.0;
+    if (i < nb && j < nb && i >= j) Fs[i + (size_t)j * m] = Ts[i + j * 65];
+    const int a = idx >> 6, b = idx & 63;
+    M[idx] = (a < nb && b < nb && a >= b) ? Ws[a + b * 65] : 0.0;
   }
   panel_rhs(c.fv + c.voff[s] + kb, Ws, nb, bc);
 }
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(256) void k_panel_diag(CholDev c, const int* __rest
 // Rows below the diagonal tile, 64 per workgroup (16 per wave): X = B L^-T as a
 // GEMM with the inverted tile, v_mfma_f64_16x16x4_f64, B fragments from global.
 __global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __restrict__ tasks, int kb) {
-  constexpr int LDB = 80;
+  constexpr int LDB = 81;
   __shared__ __attribute__((aligned(16))) double Tb[64 * LDB];  // Tb[k*LDB + j] = Tinv[j][k]
   const int2 task = tasks[blockIdx.x];
   const int s = task.x, chunk = task.y;
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __res
   const double* M = c.Tinv + c.toff[s] + (kb / 64) * 4096;
   double* fv = c.fv + c.voff[s];
   const int tid = threadIdx.x;
-  for (int idx = tid; idx < 4096; idx += 256) Tb[(idx >> 6) * LDB + (idx & 63)] = M[idx];
+  for (int idx = tid; idx < 4096; idx += 256) Tb[(idx & 63) * LDB + (idx >> 6)] = M[idx];   // M row-major
   if (tid < 64) ys[tid] = tid < nb ? fv[kb + tid] : 0.0;   // y of the panel (diagonal step)
   __syncthreads();
   const int wv = tid >> 6, l = tid & 63;
@@ -590,12 +590,12 @@ __global__ __launch_bounds__(256) void k_syrk_diag(CholDev c, const int4* __rest
   __syncthreads();
   if (diag_factor_invert(Ts, Ws, bc)) *c.flag = 1;
   double* Fs = c.F + c.foff[s] + kn + (size_t)kn * m;
-  double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;
+  double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;   // row-major L^-1 of the tile
   for (int idx = tid; idx < 4096; idx += 256) {
     const int i = idx & 63, j = idx >> 6;
-    const bool live = i < nb && j < nb && i >= j;
-    if (live) Fs[i + (size_t)j * m] = Ts[i + j * 65];
-    M[j * 64 + i] = live ? Ws[i + j * 65] : 0.0;
+    if (i < nb && j < nb && i >= j) Fs[i + (size_t)j * m] = Ts[i + j * 65];
+    const int a = idx >> 6, b = idx & 63;
+    M[idx] = (a < nb && b < nb && a >= b) ? Ws[a + b * 65] : 0.0;
   }
   panel_rhs(c.fv + c.voff[s] + kn, Ws, nb, bc);
 }
@@ -717,16 +717,22 @@ __global__ __launch_bounds__(256) void k_perm_out(CholDev c, double* __restrict_
 // Diagonal-block solves with the inverted blocks: wave 0, lane i <-> row i.
 // y = X v (forward, X = L_bb^-1) and x = X' z (backward); v / z in LDS.
 
-__device__ __forceinline__ double tinv_bwd(const double* Ms, const double* z, int nbk) {  // Ms: LDS, Ms[a*65+b]
-  const int i = threadIdx.x;
-  double acc = 0.0;
-  for (int k = 0; k < nbk; k++) acc += Ms[i * 65 + k] * z[k];
-  return acc;
+// Backward diagonal step: x = X' z for the owner block (X = L_bb^-1, row-major
+// in global memory: lane i reads column i of X' = X[k][i], coalesced over i).
+struct TinvCol {
+  double m[64];
+};
+__device__ __forceinline__ void tinv_col_load(TinvCol& t, const double* __restrict__ M, int n) {
+  const int i = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 64; k++) t.m[k] = k < n ? M[k * 64 + i] : 0.0;
 }
-
-__device__ __forceinline__ void stage_tinv(const double* __restrict__ M, double* Ms, int n) {  // live n x n
-  for (int idx = threadIdx.x; idx < n * 64; idx += blockDim.x)
-    if ((idx & 63) < n) Ms[(idx >> 6) * 65 + (idx & 63)] = M[idx];
+__device__ __forceinline__ double tinv_col_dot(const TinvCol& t, const double* z, int n) {
+  double acc = 0.0;
+#pragma unroll
+  for (int k = 0; k < 64; k++)
+    if (k < n) acc = fma(t.m[k], z[k], acc);
+  return acc;
 }
 
 // Frontal vectors of a level before its factorisation: own rows from the
@@ -805,28 +811,28 @@ __global__ __launch_bounds__(256) void k_bwd_part(CholDev c, const int4* __restr
 // order); the owner of the last block then solves it.
 __global__ __launch_bounds__(256) void k_bwd_init(CholDev c, const int4* __restrict__ tasks,
                                                   const int2* __restrict__ pref, const double* __restrict__ part) {
-  __shared__ double Ld[64 * 65];
   __shared__ double z[64];
   const int4 t = tasks[blockIdx.x];
   const int s = t.x, c0 = t.y, c1 = t.z, owner = t.w;
+  const int n2 = c1 - c0;
   const int2 pr = pref[blockIdx.x];
   double* fv = c.fv + c.voff[s];
   const int* rows = c.rows + c.rptr[s];
   const int tid = threadIdx.x;
-  if (owner >= 0) stage_tinv(c.Tinv + c.toff[s] + owner * 4096, Ld, c1 - c0);
-  if (tid < c1 - c0) {
+  TinvCol tc;
+  if (owner >= 0 && tid < 64) tinv_col_load(tc, c.Tinv + c.toff[s] + owner * 4096, n2);   // in flight
+  if (tid < n2) {
     double acc = 0.0;
     for (int p = 0; p < pr.y; p++) acc += part[(size_t)(pr.x + p) * 64 + tid];
     z[tid] = fv[c0 + tid] - acc;
   }
   __syncthreads();
   if (owner < 0) {
-    if (tid < c1 - c0) fv[c0 + tid] = z[tid];
+    if (tid < n2) fv[c0 + tid] = z[tid];
     return;
   }
   if (tid < 64) {
-    const int n2 = c1 - c0;
-    const double x = tinv_bwd(Ld, z, n2);
+    const double x = tinv_col_dot(tc, z, n2);
     if (tid < n2) {
       fv[c0 + tid] = x;
       c.xv[3 * rows[(c0 + tid) / 3] + (c0 + tid) % 3] = x;
@@ -837,44 +843,46 @@ __global__ __launch_bounds__(256) void k_bwd_init(CholDev c, const int4* __restr
 // Backward step b: z_j -= L[block b, j]' x_b for the task's columns (< 64 b);
 // the owner of block b-1 then solves it.
 __global__ __launch_bounds__(256) void k_bwd_step(CholDev c, const int4* __restrict__ tasks, int b) {
-  __shared__ double Ld[64 * 65];
   __shared__ double xbk[64];
   __shared__ double z[64];
   const int4 t = tasks[blockIdx.x];
   const int s = t.x, c0 = t.y, c1 = t.z, owner = t.w;
+  const int n2 = c1 - c0;
   const int m = c.m[s], w = c.w[s];
   const double* L = c.F + c.foff[s];
   double* fv = c.fv + c.voff[s];
   const int* rows = c.rows + c.rptr[s];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int jb = b * 64, nbk = min(64, w - jb);
-  if (tid < nbk) xbk[tid] = fv[jb + tid];
-  if (owner >= 0) stage_tinv(c.Tinv + c.toff[s] + owner * 4096, Ld, c1 - c0);
+  TinvCol tc;
+  if (owner >= 0 && tid < 64) tinv_col_load(tc, c.Tinv + c.toff[s] + owner * 4096, n2);   // in flight
+  // wave wv: columns c0 + 16 wv + q (q < 16), lane = row jb + lane of block b
+  double acc[16];
+  const bool rin = lane < nbk;
+  const double* Lr = L + (jb + lane) + (size_t)(c0 + 16 * wv) * m;
+#pragma unroll
+  for (int q = 0; q < 16; q++) acc[q] = (rin && c0 + 16 * wv + q < c1) ? Lr[(size_t)q * m] : 0.0;
+  if (tid < 64) xbk[tid] = tid < nbk ? fv[jb + tid] : 0.0;
   __syncthreads();
-  // wave wv: columns c0 + wv + 4q, q < 16; all 16 loads issued before the reductions
-  double part[16];
-  const double xl = lane < nbk ? xbk[lane] : 0.0;
+  const double xl = xbk[lane];
 #pragma unroll
-  for (int q = 0; q < 16; q++) {
-    const int j = c0 + wv + 4 * q;
-    part[q] = (j < c1 && lane < nbk) ? L[(jb + lane) + (size_t)j * m] * xl : 0.0;
-  }
-#pragma unroll
-  for (int q = 0; q < 16; q++) {
-    double acc = part[q];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-    const int j = c0 + wv + 4 * q;
-    if (lane == 0 && j < c1) z[j - c0] = fv[j] - acc;
-  }
+  for (int q = 0; q < 16; q++) acc[q] *= xl;
+  halve<16>(acc, lane);   // lane l: column (l & 15), summed over its 16-lane group
+  halve<8>(acc, lane);
+  halve<4>(acc, lane);
+  halve<2>(acc, lane);
+  double tsum = acc[0];
+  tsum += __shfl_xor(tsum, 16);
+  tsum += __shfl_xor(tsum, 32);
+  const int j = c0 + 16 * wv + lane;
+  if (lane < 16 && j < c1) z[j - c0] = fv[j] - tsum;
   __syncthreads();
   if (owner < 0) {
-    for (int j = c0 + tid; j < c1; j += 256) fv[j] = z[j - c0];
+    if (tid < n2) fv[c0 + tid] = z[tid];
     return;
   }
   if (tid < 64) {
-    const int n2 = c1 - c0;
-    const double x = tinv_bwd(Ld, z, n2);
+    const double x = tinv_col_dot(tc, z, n2);
     if (tid < n2) {
       fv[c0 + tid] = x;
       c.xv[3 * rows[(c0 + tid) / 3] + (c0 + tid) % 3] = x;

@@ -321,7 +321,7 @@ int main(int argc, char** argv) {
         for (int j = 0; j < 64; j++) {
           double acc = 0;
           for (int k = 0; k < 64; k++) {
-            const double x = t1[toff[s] + k * 64 + i];                         // X(i,k)
+            const double x = t1[toff[s] + i * 64 + k];                         // X(i,k), row-major
             const double L = k >= j ? f1[foff[s] + k + (size_t)j * M] : 0.0;   // L(k,j)
             acc += x * L;
           }
