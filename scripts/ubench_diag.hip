@@ -254,10 +254,26 @@ int main(int argc, char** argv) {
   g_c.w = d_w;
   g_c.foff = d_foff;
   g_c.flag = d_flag;
+  {   // frontal vectors (the diagonal step also does the panel's forward substitution)
+    std::vector<int> voff(N + 1);
+    for (int q = 0; q <= N; q++) voff[q] = 64 * q;
+    int* d_voff;
+    double* d_fv;
+    hipMalloc(&d_voff, (N + 1) * 4);
+    hipMalloc(&d_fv, (size_t)N * 64 * 8);
+    hipMemcpy(d_voff, voff.data(), (N + 1) * 4, hipMemcpyHostToDevice);
+    hipMemset(d_fv, 0, (size_t)N * 64 * 8);
+    g_c.voff = d_voff;
+    g_c.fv = d_fv;
+  }
   g_n = N;
   const int reps = 200;
   auto empty = [](hipStream_t s) { u_load_store<<<1, 64, 0, s>>>(g_c, g_list); };
   printf("fronts %d m %d\n", N, M);
+  if (!g_c.fv || !g_c.voff || !g_c.Tinv || !g_c.toff) {
+    printf("device view incomplete\n");
+    return 1;
+  }
   {
     double* o;
     hipMalloc(&o, 64 * 8);
