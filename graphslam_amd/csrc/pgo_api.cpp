@@ -940,6 +940,21 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   return status;
 }
 
+int pgo_debug_fronts(pgo_graph* g, int* w, int* m, int* level, int cap) {
+  if (!g || cap < 0 || (cap > 0 && (!w || !m || !level))) return PGO_E_ARG;
+  RC_TRY(download_values(g));
+  HostStructure H;
+  RC_TRY(build_structure(g, H));
+  pgo::CholPlan P;
+  pgo::chol_analyze(P, (int)g->keys.size(), H.row_ptr, H.slot_col);
+  for (int s = 0; s < P.ns && s < cap; s++) {
+    w[s] = P.w[s];
+    m[s] = P.m[s];
+    level[s] = P.height[s];
+  }
+  return P.ns;
+}
+
 int pgo_debug_plan(pgo_graph* g, double* out, int cap) {
   if (!g || !out || cap < 16) return PGO_E_ARG;
   RC_TRY(download_values(g));

@@ -22,6 +22,7 @@
 namespace pgo {
 
 constexpr int kSmallFront = 128;   // m <= this: whole front factorised in LDS by one workgroup
+constexpr int kWaveW = 32;         // ... and w <= this: by one wavefront (panel in LDS, Schur update streamed)
 constexpr int kNB = 64;            // panel width of the blocked path
 constexpr int kTile = 64;          // Schur-update output tile
 constexpr int kBigTile = 128;      // Schur-update output tile of the LDS-pipelined kernel
@@ -44,6 +45,7 @@ struct SolveStep {                 // one launch of the blocked triangular solve
 
 struct SmallClass {                // small fronts of one level with m <= mmax
   int off, cnt, mmax;
+  int wave;                        // 1: w <= kWaveW, one wavefront per front (k_front_wave)
 };
 
 struct CholLevel {

@@ -50,6 +50,14 @@ static CholDev dev_view(const CholPlan& P) {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+#ifdef PGO_DIAG_CLOCKS
+__device__ long long g_diag_clk[32];
+#define DIAG_CLK(q) if (threadIdx.x == 0 && blockIdx.x == 0) g_diag_clk[q] = clock64()
+#else
+#define DIAG_CLK(q)
+#endif
+
+
 // ------------------------------------------------------------ assembly
 // off-diagonal lower blocks H_{i,j} (i > j) of a front: sum of their slots
 __global__ __launch_bounds__(256) void k_asm_offdiag(CholDev c, const double* __restrict__ V, long long S,
@@ -135,6 +143,13 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+__device__ __forceinline__ double rsqrt_nr(double d) {   // 1/sqrt(d), two Newton steps from v_rsq_f64
+  double y = __builtin_amdgcn_rsq(d);
+  y = y * fma(-0.5 * d * y, y, 1.5);
+  y = y * fma(-0.5 * d * y, y, 1.5);
+  return y;
+}
+
 // X = L^-1 of an LDS-resident lower-triangular nbk x nbk block (element (r,c) at
 // L[r + c*ld]), by the 4 waves of a workgroup: wave wv owns columns 16wv..16wv+15,
 // lane i row i; column-oriented substitution, row k broadcast with v_readlane
@@ -166,6 +181,25 @@ __device__ __forceinline__ void tri_inverse_wg(const double* L, int ld, int nbk,
   __syncthreads();  // dinv reusable
 }
 
+// dst[0..n) = src[0..n) with 8 loads per thread in flight (a plain copy loop
+// would wait on every global load before its LDS store)
+__device__ __forceinline__ void copy_in(double* __restrict__ dst, const double* __restrict__ src, int n, int t,
+                                        int nt) {
+  for (int base = t; base < n; base += 8 * nt) {
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int idx = base + q * nt;
+      v[q] = idx < n ? src[idx] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int idx = base + q * nt;
+      if (idx < n) dst[idx] = v[q];
+    }
+  }
+}
+
 // ------------------------------------------------------------ small fronts (LDS)
 // m <= 128: the whole front in LDS; right-looking, two threads per row (the
 // row's columns split even/odd) so LDS accesses of a wave are consecutive rows.
@@ -177,9 +211,8 @@ __global__ __launch_bounds__(256) void k_front_small(CholDev c, const int* __res
   double* fv = c.fv + c.voff[s];
   double* v = A + m * m + 64;
   const int tid = threadIdx.x;
-  for (int j = 0; j < m; j++)
-    for (int i = j + tid; i < m; i += 256) A[i + j * m] = Fs[i + (size_t)j * m];
-  for (int i = tid; i < m; i += 256) v[i] = fv[i];
+  copy_in(A, Fs, m * m, tid, 256);   // (the upper triangle comes along; never read)
+  copy_in(v, fv, m, tid, 256);
   __syncthreads();
   // the frontal vector is carried as an extra column: forward substitution
   // L y = v for the pivot rows and v_below -= L21 y, in the same sweep
@@ -216,14 +249,131 @@ __global__ __launch_bounds__(256) void k_front_small(CholDev c, const int* __res
     tri_inverse_wg(A + jb + jb * m, m, min(64, w - jb), c.Tinv + c.toff[s] + (jb / 64) * 4096, scratch);
 }
 
+// Small front with w <= kWaveW pivot columns (and m <= 128), one wavefront:
+// lane l owns rows l and l + 64 of the m x w panel in registers; per pivot k the
+// panel's column k is published through LDS (one store per lane, broadcast
+// reads, no read-modify-write of LDS), so the pivot chain costs one LDS round
+// trip and one rsqrt.  The frontal vector rides along (forward substitution).
+// Then the rank-w Schur update of the trailing block is streamed through global
+// memory (rows of L from registers, columns broadcast from an LDS copy), and
+// the w x w inverse for the backward solve is formed lane = column.
+template <bool kTwoRows>   // m > 64: lane also owns row l + 64
+__global__ __launch_bounds__(64) void k_front_wave(CholDev c, const int* __restrict__ list) {
+  constexpr int W = kWaveW, LDP = kWaveW + 1;   // odd row stride: conflict-free per-lane rows
+  extern __shared__ __attribute__((aligned(16))) double S[];
+  const int s = list[blockIdx.x];
+  const int m = c.m[s], w = c.w[s];
+  double* PR = S;                 // m x W row-major copy of L (after the factorisation)
+  double* cb = S + m * LDP;       // 128 + 2: column k of the panel, then v[k]; then 1/L(k,k)
+  double* Fs = c.F + c.foff[s];
+  double* fv = c.fv + c.voff[s];
+  const int l = threadIdx.x, lb = l + 64;
+  const bool ra = l < m, rb = kTwoRows && lb < m;
+  DIAG_CLK(23);
+  double* invs = cb + 130;        // [W] 1 / L(k,k)
+  double pa[W], pb[W];
+#pragma unroll
+  for (int k = 0; k < W; k++) {
+    pa[k] = (ra && k < w && k <= l) ? Fs[l + (size_t)k * m] : 0.0;
+    pb[k] = (rb && k < w) ? Fs[lb + (size_t)k * m] : 0.0;
+  }
+  double va = ra ? fv[l] : 0.0, vb = rb ? fv[lb] : 0.0;
+  bool bad = false;
+  DIAG_CLK(24);
+#pragma unroll
+  for (int k = 0; k < W; k++) {
+    if (k < w) {                              // uniform
+      cb[l] = pa[k];
+      cb[64 + l] = pb[k];
+      if (l == k) cb[128] = va;
+      __builtin_amdgcn_wave_barrier();
+      double d = cb[k];
+      const double vk = cb[128];
+      if (!(d > 0.0) || !isfinite(d)) {
+        bad = true;
+        d = 1.0;
+      }
+      const double r = rsqrt_nr(d);
+      const double yk = vk * r;
+      const double la = l > k ? pa[k] * r : (l == k ? d * r : pa[k]);
+      const double lbv = pb[k] * r;
+#pragma unroll
+      for (int j = k + 1; j < W; j++) {   // branch-free: the LDS reads issue together
+        const double lj = j < w ? cb[j] * r : 0.0;
+        pa[j] = fma(l >= j ? -la : 0.0, lj, pa[j]);
+        pb[j] = fma(-lbv, lj, pb[j]);
+      }
+      pa[k] = la;
+      pb[k] = lbv;
+      va = l == k ? yk : (l > k ? fma(-la, yk, va) : va);
+      vb = fma(-lbv, yk, vb);
+      if (l == 0) invs[k] = r;
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (bad && l == 0) *c.flag = 1;
+  DIAG_CLK(25);
+  // L back to the front (and a row-major LDS copy), y to the frontal vector
+#pragma unroll
+  for (int k = 0; k < W; k++) {   // (columns k >= w of the LDS copy are zero)
+    if (k < w) {
+      if (ra && k <= l) Fs[l + (size_t)k * m] = pa[k];
+      if (rb) Fs[lb + (size_t)k * m] = pb[k];
+    }
+    if (ra) PR[l * LDP + k] = k <= l ? pa[k] : 0.0;
+    if (rb) PR[lb * LDP + k] = pb[k];
+  }
+  if (ra) fv[l] = va;
+  if (rb) fv[lb] = vb;
+  __builtin_amdgcn_wave_barrier();
+  DIAG_CLK(26);
+  // trailing update C[i][j] -= L[i,:] L[j,:]', w <= j <= i < m; lane rows l, l + 64;
+  // 16 columns per round so that their loads are in flight together
+  constexpr int JB = 16;
+  for (int j0 = w; j0 < m; j0 += JB) {
+    double ca[JB], cbv[JB];
+#pragma unroll
+    for (int q = 0; q < JB; q++) {
+      const int j = j0 + q;
+      ca[q] = (ra && l >= w && j < m && j <= l) ? Fs[l + (size_t)j * m] : 0.0;
+      cbv[q] = (rb && j < m && j <= lb) ? Fs[lb + (size_t)j * m] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < JB; q++) {
+      const int j = min(j0 + q, m - 1);
+      double sa = 0.0, sb = 0.0;
+#pragma unroll
+      for (int k = 0; k < W; k++) {   // branch-free (pa, pb, PR are zero beyond w)
+        const double ljk = PR[j * LDP + k];
+        sa = fma(pa[k], ljk, sa);
+        if (kTwoRows) sb = fma(pb[k], ljk, sb);
+      }
+      const int jj = j0 + q;
+      if (ra && l >= w && jj < m && jj <= l) Fs[l + (size_t)jj * m] = ca[q] - sa;
+      if (rb && jj < m && jj <= lb) Fs[lb + (size_t)jj * m] = cbv[q] - sb;
+    }
+  }
+  DIAG_CLK(27);
+  // X = L11^-1 (w x w), lane = column: forward substitution of e_l
+  if (l < w) {
+    double x[W];
+#pragma unroll
+    for (int r = 0; r < W; r++) {
+      double acc = r == l ? 1.0 : 0.0;
+#pragma unroll
+      for (int t = 0; t < r; t++) acc = fma(-PR[min(r, m - 1) * LDP + t], x[t], acc);
+      x[r] = r < w ? acc * invs[r] : 0.0;
+    }
+    double* M = c.Tinv + c.toff[s];   // row-major, live w x w
+#pragma unroll
+    for (int r = 0; r < W; r++)
+      if (r < w) M[r * 64 + l] = r >= l ? x[r] : 0.0;
+  }
+  DIAG_CLK(28);
+}
+
 // ------------------------------------------------------------ blocked path
 // ------------------------------------------------------------ diagonal tile
-__device__ __forceinline__ double rsqrt_nr(double d) {   // 1/sqrt(d), two Newton steps from v_rsq_f64
-  double y = __builtin_amdgcn_rsq(d);
-  y = y * fma(-0.5 * d * y, y, 1.5);
-  y = y * fma(-0.5 * d * y, y, 1.5);
-  return y;
-}
 
 // 16x16x16 product on one wave from LDS: D(i,j) = sum_k A(i,k) B(k,j),
 // A(i,k) = A[i*ars + k*acs], B(k,j) = B[k*brs + j*bcs]; D in the f64 MFMA
@@ -263,12 +413,6 @@ __device__ __forceinline__ void st16(double* C, d4 v, bool sub) {
 // where W (LDS, ld 65) must hold zeros below the diagonal blocks on entry
 // (the diagonal blocks are written here) and ends as X.
 // Returns (wave 0) whether a pivot was not positive and finite.
-#ifdef PGO_DIAG_CLOCKS
-__device__ long long g_diag_clk[16];
-#define DIAG_CLK(q) if (threadIdx.x == 0 && blockIdx.x == 0) g_diag_clk[q] = clock64()
-#else
-#define DIAG_CLK(q)
-#endif
 __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double* bc) {
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   DIAG_CLK(0);
@@ -992,9 +1136,16 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       CH_TRY(hipStreamWaitEvent(P.side2, P.evs[0], 0));
       ss = P.side2;
     }
-    for (const SmallClass& sc : lv.small)
-      k_front_small<<<sc.cnt, 256, (size_t)(sc.mmax * sc.mmax + 64 + sc.mmax) * sizeof(double), ss>>>(
-          c, P.d_small + sc.off);
+    for (const SmallClass& sc : lv.small) {
+      if (sc.wave) {
+        const size_t lds = (size_t)(sc.mmax * (kWaveW + 1) + 130 + kWaveW) * sizeof(double);
+        if (sc.mmax > 64) k_front_wave<true><<<sc.cnt, 64, lds, ss>>>(c, P.d_small + sc.off);
+        else k_front_wave<false><<<sc.cnt, 64, lds, ss>>>(c, P.d_small + sc.off);
+      }
+      else
+        k_front_small<<<sc.cnt, 256, (size_t)(sc.mmax * sc.mmax + 64 + sc.mmax) * sizeof(double), ss>>>(
+            c, P.d_small + sc.off);
+    }
     for (const PanelStep& ps : lv.panels) {
       if (ps.potrf_cnt) k_panel_diag<<<ps.potrf_cnt, 256, 0, s>>>(c, P.d_potrf + ps.potrf_off, ps.kb);
       if (ps.trsm_cnt) k_panel_trsm<<<ps.trsm_cnt, 256, 0, s>>>(c, P.d_trsm + ps.trsm_off, ps.kb);

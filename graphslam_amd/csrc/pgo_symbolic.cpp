@@ -458,24 +458,46 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       P.ea_colpref.push_back(cols);
       lv.ea_cnt.push_back(cnt);
     }
-    // small fronts: one workgroup each, in LDS; launched per size class so the
-    // LDS request (m^2 doubles) does not cap the occupancy of the tiny ones
+    // small fronts (m <= kSmallFront): with w <= kWaveW one wavefront each (the
+    // m x w panel in LDS, the rank-w Schur update streamed), largest first;
+    // else one workgroup each with the whole front in LDS, launched per size
+    // class so the LDS request (m^2 doubles) does not cap the occupancy
     std::vector<int> big;
     {
       const int classes[4] = {32, 64, 96, kSmallFront};
-      std::vector<int> bucket[4];
+      std::vector<int> bucket[4], wave;
       for (int s : bylevel[L]) {
         if (P.m[s] > kSmallFront) {
           big.push_back(s);
+          continue;
+        }
+        if (P.w[s] <= kWaveW) {
+          wave.push_back(s);
           continue;
         }
         int q = 0;
         while (P.m[s] > classes[q]) q++;
         bucket[q].push_back(s);
       }
+      for (int half = 0; half < 2; half++) {      // m <= 64 (one row per lane), m > 64
+        std::vector<int> part;
+        for (int s : wave)
+          if ((P.m[s] > 64) == (half == 1)) part.push_back(s);
+        if (part.empty()) continue;
+        std::stable_sort(part.begin(), part.end(), [&](int a, int b) {
+          const double wa = (double)P.m[a] * P.m[a] * P.w[a], wb = (double)P.m[b] * P.m[b] * P.w[b];
+          return wa > wb;
+        });
+        SmallClass sc{(int)P.small_list.size(), (int)part.size(), 0, 1};
+        for (int s : part) {
+          P.small_list.push_back(s);
+          sc.mmax = std::max(sc.mmax, P.m[s]);
+        }
+        lv.small.push_back(sc);
+      }
       for (int q = 0; q < 4; q++) {
         if (bucket[q].empty()) continue;
-        SmallClass sc{(int)P.small_list.size(), (int)bucket[q].size(), 0};
+        SmallClass sc{(int)P.small_list.size(), (int)bucket[q].size(), 0, 0};
         for (int s : bucket[q]) {
           P.small_list.push_back(s);
           sc.mmax = std::max(sc.mmax, P.m[s]);

@@ -210,6 +210,19 @@ class PoseGraph:
         summary["levels_table"] = lv
         return summary
 
+    def debug_fronts(self):
+        """Host-only: (w, m, level) of every supernode of the Cholesky plan."""
+        ns = self._L.pgo_debug_fronts(self._h, None, None, None, 0)
+        if ns < 0:
+            self._check(ns)
+        w = np.zeros(ns, np.int32)
+        m = np.zeros(ns, np.int32)
+        lv = np.zeros(ns, np.int32)
+        ip = C.POINTER(C.c_int)
+        self._check(min(0, self._L.pgo_debug_fronts(self._h, w.ctypes.data_as(ip), m.ctypes.data_as(ip),
+                                                     lv.ctypes.data_as(ip), ns)))
+        return w, m, lv
+
     def debug_solve(self, lam, params=None, **kw):
         p = params if params is not None else default_params(**kw)
         d = np.zeros((self.num_vertices, 3))

@@ -173,6 +173,10 @@ int pgo_debug_solve(pgo_graph *g, double lambda, const pgo_params *params, doubl
  * trsm tasks, syrk tiles, small fronts; from out[16], 6 per level (leaves first):
  * fronts, max m, max 64-blocks, panel steps, small fronts, syrk tiles. */
 int pgo_debug_plan(pgo_graph *g, double *out, int cap);
+/* per supernode of the same host-only plan: pivot columns w, rows m, level
+   (height in the elimination tree); returns the supernode count (arrays are
+   filled up to cap entries) or a negative status */
+int pgo_debug_fronts(pgo_graph *g, int *w, int *m, int *level, int cap);
 
 #ifdef __cplusplus
 }

@@ -344,7 +344,7 @@ int main(int argc, char** argv) {
           me = std::max(me, fabs(acc - (i == j ? 1.0 : 0.0)));
         }
     printf("  k_panel_diag: max |X L - I| = %.3e\n", me);
-    long long dc[16];
+    long long dc[32];
     hipMemcpyFromSymbol(dc, HIP_SYMBOL(g_diag_clk), sizeof(dc));
     printf("  diag phases (clocks from start):");
     for (int q = 1; q <= 12; q++) printf(" %lld", dc[q] - dc[0]);

@@ -1,0 +1,87 @@
+// Microbenchmark of the one-wavefront small-front kernel (k_front_wave) on
+// synthetic SPD fronts of one shape; per-phase clocks of front 0.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include scripts/ubench_wave.hip -o graphslam_amd/build/ubench_wave
+//   ./graphslam_amd/build/ubench_wave [fronts] [m] [w]
+#define PGO_DIAG_CLOCKS 1
+#include "../graphslam_amd/csrc/pgo_chol.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace pgo;
+
+int main(int argc, char** argv) {
+  const int N = argc > 1 ? atoi(argv[1]) : 4096;
+  const int M = argc > 2 ? atoi(argv[2]) : 80;
+  const int W = argc > 3 ? atoi(argv[3]) : 15;
+  if (W > kWaveW || M > kSmallFront || W > M) return 1;
+  hipStream_t st;
+  hipStreamCreate(&st);
+  std::vector<double> h((size_t)N * M * M, 0.0);
+  srand(5);
+  for (int s = 0; s < N; s++)
+    for (int j = 0; j < M; j++)
+      for (int i = j; i < M; i++)
+        h[(size_t)s * M * M + i + (size_t)j * M] = i == j ? 64.0 : ((rand() % 2001) - 1000) / 4000.0;
+  const size_t bytes = h.size() * 8;
+  double *F, *F0, *T, *fv;
+  hipMalloc(&F, bytes);
+  hipMalloc(&F0, bytes);
+  hipMalloc(&T, (size_t)N * 4096 * 8);
+  hipMalloc(&fv, (size_t)N * M * 8);
+  hipMemset(fv, 0, (size_t)N * M * 8);
+  hipMemcpy(F0, h.data(), bytes, hipMemcpyHostToDevice);
+  std::vector<int> hm(N, M), hw(N, W), list(N), voff(N + 1);
+  std::vector<long long> foff(N + 1), toff(N + 1);
+  for (int s = 0; s <= N; s++) {
+    foff[s] = (long long)s * M * M;
+    toff[s] = (long long)s * 4096;
+    voff[s] = s * M;
+    if (s < N) list[s] = s;
+  }
+  auto up = [](auto* hv, size_t n) {
+    void* d;
+    hipMalloc(&d, n);
+    hipMemcpy(d, hv, n, hipMemcpyHostToDevice);
+    return d;
+  };
+  CholDev c{};
+  c.F = F;
+  c.Tinv = T;
+  c.fv = fv;
+  c.m = (int*)up(hm.data(), N * 4);
+  c.w = (int*)up(hw.data(), N * 4);
+  c.voff = (int*)up(voff.data(), (N + 1) * 4);
+  c.foff = (long long*)up(foff.data(), (N + 1) * 8);
+  c.toff = (long long*)up(toff.data(), (N + 1) * 8);
+  int* flag;
+  hipMalloc(&flag, 4);
+  hipMemset(flag, 0, 4);
+  c.flag = flag;
+  int* dl = (int*)up(list.data(), N * 4);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  float best = 1e30f;
+  for (int r = 0; r < 5; r++) {
+    hipMemcpyAsync(F, F0, bytes, hipMemcpyDeviceToDevice, st);
+    hipEventRecord(a, st);
+    if (M > 64) k_front_wave<true><<<N, 64, (size_t)(M * (kWaveW + 1) + 130 + kWaveW) * 8, st>>>(c, dl);
+    else k_front_wave<false><<<N, 64, (size_t)(M * (kWaveW + 1) + 130 + kWaveW) * 8, st>>>(c, dl);
+    hipEventRecord(b, st);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    best = ms < best ? ms : best;
+  }
+  long long clk[32];
+  hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_diag_clk), sizeof(clk));
+  int fl = 0;
+  hipMemcpy(&fl, flag, 4, hipMemcpyDeviceToHost);
+  printf("fronts %d m %d w %d: %.1f us per launch (%.3f us per front), flag %d\n", N, M, W, best * 1e3,
+         best * 1e3 / N, fl);
+  printf("  front 0 clocks: start->loads %lld factor %lld store %lld trailing %lld inverse %lld\n", clk[24] - clk[23],
+         clk[25] - clk[24], clk[26] - clk[25], clk[27] - clk[26], clk[28] - clk[27]);
+  return 0;
+}
