@@ -29,6 +29,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_MFMA_PEAK_TFS = 78.6  # MI355X datasheet: FP64 matrix (and vector) 78.6 TFLOP/s dense
+# measured on the box (scripts/ubench_syrk.hip): a bare v_mfma_f64_16x16x4_f64 loop,
+# 8 independent chains per wave, 8-32 waves per CU, sustains 45-49 TFLOP/s
+FP64_MFMA_LOOP_TFS = 49.0
 
 
 def spmv_bytes(n, slots):
@@ -126,7 +129,7 @@ def main():
                 "timed_launches": totals["spmv_n"],
             }
         else:
-            # Schur updates (k_panel_syrk / k_panel_syrk128 launches) of the
+            # Schur updates (k_panel_syrk_lds / k_panel_syrk128 launches) of the
             # profiled factorisations (every --profile-every'th), each launch timed
             # by dispatch events on the library's stream: achieved = algorithmic
             # flops per launch / average launch duration
@@ -135,9 +138,10 @@ def main():
             flops_launch = last["syrk_flops"] / nl if nl else None
             syrk_tfs = flops_launch / (avg_ms * 1e-3) / 1e12 if avg_ms else None
             roofline = {
-                "kernel": "k_panel_syrk", "bound": "mfma", "achieved": syrk_tfs, "peak": FP64_MFMA_PEAK_TFS,
+                "kernel": "k_panel_syrk_lds", "bound": "mfma", "achieved": syrk_tfs, "peak": FP64_MFMA_PEAK_TFS,
                 "unit": "TFLOP/s", "frac": syrk_tfs / FP64_MFMA_PEAK_TFS if syrk_tfs else None,
-                "traffic": pmc.get("k_panel_syrk_bytes_per_launch"),
+                "traffic": pmc.get("k_panel_syrk_lds_bytes_per_launch"),
+                "measured_loop_peak_tfs": FP64_MFMA_LOOP_TFS,
                 "flops_per_launch": flops_launch, "avg_launch_ms": avg_ms, "launches_per_factorization": nl,
                 "profiled_factorizations": totals["syrk_n"], "factor_flops": last["factor_flops"],
             }

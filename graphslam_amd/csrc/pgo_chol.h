@@ -119,6 +119,12 @@ struct CholPlan {
   double* d_lambda = nullptr;      // damping read by the assembly (graph-replay friendly)
 };
 
+// host: XCD-aware order of Schur-update tile tasks (front, row0, col0, k0): tiles
+// are grouped into 8x8-tile blocks, blocks dealt round-robin to the 8 XCDs
+// (workgroup i runs on XCD i mod 8), so each XCD's L2 holds the panel rows and
+// columns of the blocks it works on
+void xcd_order(std::vector<int4>& tasks, int tile);
+
 // host: symbolic analysis from the block-CSR pattern (old pose indices)
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
 hipError_t chol_upload(CholPlan& P, hipStream_t s);

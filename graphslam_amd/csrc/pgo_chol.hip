@@ -707,8 +707,98 @@ __device__ __forceinline__ void syrk_tile64(const CholDev& c, const int4 t, int 
     }
 }
 
+// register-fragment variant (kept for the microbenchmark; k_panel_syrk_lds is launched)
 __global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int4* __restrict__ tasks, int kb) {
   syrk_tile64<false>(c, tasks[blockIdx.x], kb, nullptr);
+}
+
+// Same tile and semantics as k_panel_syrk, with the panel rows and columns of
+// the tile staged through LDS in chunks of 16 k (double-buffered, every operand
+// loaded once per workgroup instead of once per wave pair; 8 loads per thread
+// per chunk, issued one chunk ahead of the MFMAs).  Low register count, so
+// several workgroups per CU hide the load latency.
+__global__ __launch_bounds__(256) void k_panel_syrk_lds(CholDev c, const int4* __restrict__ tasks, int kb) {
+  constexpr int LD = 64 + 4;
+  __shared__ __attribute__((aligned(16))) double Sr[2][16 * LD];
+  __shared__ __attribute__((aligned(16))) double Sc[2][16 * LD];
+  const int4 t = tasks[blockIdx.x];
+  const int s = t.x, row0 = t.y, col0 = t.z;
+  const bool inner = t.w < 0;
+  const int k0 = t.w & 0x7fffffff;
+  const int m = c.m[s], w = c.w[s];
+  const int kend = min(kb + kNB, w);
+  const int colend = inner ? min((kb & ~(kKB - 1)) + kKB, w) : m;
+  const int K = kend - k0, nch = (K + 15) >> 4;
+  double* Fs = c.F + c.foff[s];
+  const double* P = Fs + (size_t)k0 * m;
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int qi = 32 * (wv >> 1), qj = 32 * (wv & 1);
+  const bool active = !(row0 == col0 && qi < qj);
+  const int li = l & 15, lk = l >> 4;
+  // staging map: thread -> (k = idx >> 6, r = idx & 63), idx = tid + 256 q, q < 4
+  double st[8];
+  auto load = [&](int ch) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int idx = tid + 256 * q, k = 16 * ch + (idx >> 6), r = idx & 63;
+      const double* pk = P + (size_t)k * m;
+      st[q] = (k < K && row0 + r < m) ? pk[row0 + r] : 0.0;
+      st[4 + q] = (k < K && col0 + r < m) ? pk[col0 + r] : 0.0;
+    }
+  };
+  auto stash = [&](int b) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int idx = tid + 256 * q;
+      Sr[b][(idx >> 6) * LD + (idx & 63)] = st[q];
+      Sc[b][(idx >> 6) * LD + (idx & 63)] = st[4 + q];
+    }
+  };
+  d4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
+  load(0);
+  stash(0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ch++) {
+    const int b = ch & 1;
+    if (ch + 1 < nch) load(ch + 1);
+    if (active) {
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const double* sr = Sr[b] + (4 * u + lk) * LD + qi + li;
+        const double* sc = Sc[b] + (4 * u + lk) * LD + qj + li;
+        const double ra = sr[0], rb = sr[16], ca = sc[0], cb = sc[16];
+        acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(ca, ra, acc00, 0, 0, 0);
+        acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(ca, rb, acc01, 0, 0, 0);
+        acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(cb, ra, acc10, 0, 0, 0);
+        acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(cb, rb, acc11, 0, 0, 0);
+      }
+    }
+    if (ch + 1 < nch) stash(b ^ 1);
+    __syncthreads();
+  }
+  if (!active) return;
+  // C read-modify-write (layout: lane l, reg r -> column col0+qj+16mj+lk+4r, row row0+qi+16mi+li)
+  double cold[2][2][4];
+#pragma unroll
+  for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+    for (int mj = 0; mj < 2; mj++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = row0 + qi + 16 * mi + li, col = col0 + qj + 16 * mj + lk + 4 * r;
+        cold[mi][mj][r] = (row < m && col < colend && row >= col) ? Fs[row + (size_t)col * m] : 0.0;
+      }
+#pragma unroll
+  for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+    for (int mj = 0; mj < 2; mj++) {
+      const d4 a = mj == 0 ? (mi == 0 ? acc00 : acc01) : (mi == 0 ? acc10 : acc11);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = row0 + qi + 16 * mi + li, col = col0 + qj + 16 * mj + lk + 4 * r;
+        if (row < m && col < colend && row >= col) Fs[row + (size_t)col * m] = cold[mi][mj][r] - a[r];
+      }
+    }
 }
 
 // The Schur-update tile that is the next panel's diagonal tile (row0 = col0 =
@@ -1157,7 +1247,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       }
       if (ps.syrk_cnt) {
         const int4* tasks = (const int4*)(P.d_syrk + ps.syrk_off);
-        auto kern = ps.syrk_tile == kBigTile ? k_panel_syrk128 : k_panel_syrk;
+        auto kern = ps.syrk_tile == kBigTile ? k_panel_syrk128 : k_panel_syrk_lds;
         if (prof && prof->used < prof->cap) {
           const int u = prof->used++;
           prof->flops[u] = ps.syrk_flops;

@@ -1,6 +1,7 @@
 // Host-side symbolic analysis for the GPU supernodal Cholesky (pgo_chol.h).
 // Runs once per graph structure (GTSAM recomputes COLAMD every solve).
 #include <algorithm>
+#include <tuple>
 #include <cmath>
 #include <cstring>
 #include <numeric>
@@ -110,6 +111,37 @@ std::vector<int> amd(int n, const std::vector<int>& xadj, const std::vector<int>
 }
 
 }  // namespace
+
+void xcd_order(std::vector<int4>& tasks, int tile) {
+  constexpr int kXcd = 8, kBlk = 8;
+  if ((int)tasks.size() < 4 * kXcd * kBlk) return;   // small launches: keep the natural order
+  const int span = tile * kBlk;
+  std::vector<int> idx(tasks.size());
+  for (size_t i = 0; i < idx.size(); i++) idx[i] = (int)i;
+  auto key = [&](const int4& t) { return std::make_tuple(t.x, t.z / span, t.y / span); };
+  std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return key(tasks[a]) < key(tasks[b]); });
+  std::vector<std::vector<int4>> q(kXcd);
+  int blk = -1;
+  std::tuple<int, int, int> prev{-1, -1, -1};
+  for (int i : idx) {
+    const auto k = key(tasks[i]);
+    if (k != prev) {
+      blk++;
+      prev = k;
+    }
+    q[blk % kXcd].push_back(tasks[i]);
+  }
+  std::vector<int4> out;
+  out.reserve(tasks.size());
+  std::vector<size_t> pos(kXcd, 0);
+  for (size_t left = tasks.size(); left;)
+    for (int x = 0; x < kXcd; x++)
+      if (pos[x] < q[x].size()) {
+        out.push_back(q[x][pos[x]++]);
+        left--;
+      }
+  tasks.swap(out);
+}
 
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
   P.nslots = (long long)slot_col.size();
@@ -569,6 +601,11 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
               P.syrk_tasks.push_back(make_int4(u.s, r0, c0, u.k0));
             }
           }
+      {   // XCD-aware order of this step's Schur-update tiles
+        std::vector<int4> mine(P.syrk_tasks.begin() + ps.syrk_off, P.syrk_tasks.end());
+        xcd_order(mine, ps.syrk_tile);
+        std::copy(mine.begin(), mine.end(), P.syrk_tasks.begin() + ps.syrk_off);
+      }
       ps.sdiag_cnt = (int)P.sdiag_tasks.size() - ps.sdiag_off;
       ps.potrf_cnt = (int)P.potrf_list.size() - ps.potrf_off;
       ps.trsm_cnt = (int)P.trsm_tasks.size() - ps.trsm_off;

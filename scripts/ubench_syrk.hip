@@ -4,6 +4,7 @@
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include scripts/ubench_syrk.hip -o graphslam_amd/build/ubench_syrk
 //   ./graphslam_amd/build/ubench_syrk [m] [w]
 #include "../graphslam_amd/csrc/pgo_chol.hip"
+#include "../graphslam_amd/csrc/pgo_symbolic.cpp"
 
 #include <cstdio>
 #include <cstdlib>
@@ -11,7 +12,93 @@
 
 using namespace pgo;
 
+__device__ long long g_mclk[4];
+template <int NC>
+__global__ __launch_bounds__(256) void u_mfma4_peak(double* out, int iters) {
+  double a[NC];
+#pragma unroll
+  for (int q = 0; q < NC; q++) a[q] = 0.0;
+  double x = threadIdx.x * 1e-3, y = 1.0 - x;
+  for (int i = 0; i < iters; i++) {
+#pragma unroll
+    for (int q = 0; q < NC; q++) a[q] = __builtin_amdgcn_mfma_f64_4x4x4f64(q & 1 ? x : y, q & 2 ? y : x, a[q], 0, 0, 0);
+  }
+  double acc = 0;
+#pragma unroll
+  for (int q = 0; q < NC; q++) acc += a[q];
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+template <int NC>
+__global__ __launch_bounds__(256) void u_mfma_peak(double* out, int iters) {
+  d4 a[NC];
+#pragma unroll
+  for (int q = 0; q < NC; q++) a[q] = d4{0, 0, 0, 0};
+  double x = threadIdx.x * 1e-3, y = 1.0 - x;
+  const long long t0 = clock64(), w0 = wall_clock64();
+  for (int i = 0; i < iters; i++) {
+#pragma unroll
+    for (int q = 0; q < NC; q++) a[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(q & 1 ? x : y, q & 2 ? y : x, a[q], 0, 0, 0);
+  }
+  const long long t1 = clock64(), w1 = wall_clock64();
+  double acc = 0;
+#pragma unroll
+  for (int q = 0; q < NC; q++) acc += a[q][q & 3];
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    g_mclk[0] = t1 - t0;
+    g_mclk[1] = w1 - w0;
+  }
+}
+
 int main(int argc, char** argv) {
+  for (int wpc : {16, 32}) {
+    double* o;
+    const int nb = 256 * (wpc / 4), iters = 8192;
+    hipMalloc(&o, (size_t)nb * 256 * 8);
+    u_mfma4_peak<16><<<nb, 256>>>(o, 16);
+    hipDeviceSynchronize();
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a);
+    u_mfma4_peak<16><<<nb, 256>>>(o, iters);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    const double flops = (double)nb * 4 * iters * 16 * 512.0;
+    printf("mfma f64 4x4x4_4b: 16 chains/wave, %d waves/CU: %.1f TFLOP/s\n", wpc, flops / (ms * 1e-3) / 1e12);
+    hipFree(o);
+  }
+  for (int NC : {8}) {
+    for (int wpc : {8, 16, 32}) {   // waves per CU requested (WGs of 4 waves)
+      double* o;
+      const int nb = 256 * (wpc / 4), iters = 2048;
+      hipMalloc(&o, (size_t)nb * 256 * 8);
+      auto run = [&](int it) {
+        if (NC == 4) u_mfma_peak<4><<<nb, 256>>>(o, it);
+        else if (NC == 8) u_mfma_peak<8><<<nb, 256>>>(o, it);
+        else u_mfma_peak<16><<<nb, 256>>>(o, it);
+      };
+      run(16);
+      hipDeviceSynchronize();
+      hipEvent_t a, b;
+      hipEventCreate(&a);
+      hipEventCreate(&b);
+      hipEventRecord(a);
+      run(iters);
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      long long mc[4];
+      hipMemcpyFromSymbol(mc, HIP_SYMBOL(g_mclk), sizeof(mc));
+      const double flops = (double)nb * 4 * iters * NC * 2048.0;
+      printf("mfma f64 16x16x4: %2d chains/wave, %d waves/CU: %.1f TFLOP/s, %.1f cycles per MFMA per wave, %.2f GHz\n",
+             NC, wpc, flops / (ms * 1e-3) / 1e12, (double)mc[0] / ((double)NC * iters), mc[0] / (mc[1] * 10.0));
+      hipFree(o);
+    }
+  }
   const int M = argc > 1 ? atoi(argv[1]) : 4096;
   const int W = argc > 2 ? atoi(argv[2]) : 512;
   hipStream_t st;
@@ -42,10 +129,12 @@ int main(int argc, char** argv) {
   // outer update after panel kb = 192 (block 0 = columns 0..255): trailing [256, M), k0 = 0
   const int kb = 192, be = 256;
   const double flops = 256.0 * (M - be) * (M - be + 1.0);
-  for (int T : {64, 128}) {
+  for (int T : {64, 65, 128}) {   // 65: the LDS-staged 64x64 kernel
+    const int TT = T == 65 ? 64 : T;
     std::vector<int4> tasks;
-    for (int c0 = be; c0 < M; c0 += T)
-      for (int r0 = c0; r0 < M; r0 += T) tasks.push_back(make_int4(0, r0, c0, 0));
+    for (int c0 = be; c0 < M; c0 += TT)
+      for (int r0 = c0; r0 < M; r0 += TT) tasks.push_back(make_int4(0, r0, c0, 0));
+    if (getenv("XCD")) xcd_order(tasks, TT);
     int4* dt;
     hipMalloc(&dt, tasks.size() * sizeof(int4));
     hipMemcpy(dt, tasks.data(), tasks.size() * sizeof(int4), hipMemcpyHostToDevice);
@@ -58,6 +147,7 @@ int main(int argc, char** argv) {
       hipMemcpyAsync(F, F0, n * 8, hipMemcpyDeviceToDevice, st);
       hipEventRecord(a, st);
       if (T == 64) k_panel_syrk<<<(int)tasks.size(), 256, 0, st>>>(c, dt, kb);
+      else if (T == 65) k_panel_syrk_lds<<<(int)tasks.size(), 256, 0, st>>>(c, dt, kb);
       else k_panel_syrk128<<<(int)tasks.size(), 256, 0, st>>>(c, dt, kb);
       hipEventRecord(b, st);
       hipEventSynchronize(b);
