@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void u_mfma_peak(double* out, int iters) {
 }
 
 int main(int argc, char** argv) {
-  for (int wpc : {16, 32}) {
+  for (int wpc : {32}) {
     double* o;
     const int nb = 256 * (wpc / 4), iters = 8192;
     hipMalloc(&o, (size_t)nb * 256 * 8);
@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
     hipFree(o);
   }
   for (int NC : {8}) {
-    for (int wpc : {8, 16, 32}) {   // waves per CU requested (WGs of 4 waves)
+    for (int wpc : {32}) {   // waves per CU requested (WGs of 4 waves)
       double* o;
       const int nb = 256 * (wpc / 4), iters = 2048;
       hipMalloc(&o, (size_t)nb * 256 * 8);
@@ -130,7 +130,7 @@ int main(int argc, char** argv) {
   const int kb = 192, be = 256;
   const double flops = 256.0 * (M - be) * (M - be + 1.0);
   for (int T : {64, 65, 128}) {   // 65: the LDS-staged 64x64 kernel
-    const int TT = T == 65 ? 64 : T;
+    const int TT = T >= 65 ? 64 : T;
     std::vector<int4> tasks;
     for (int c0 = be; c0 < M; c0 += TT)
       for (int r0 = c0; r0 < M; r0 += TT) tasks.push_back(make_int4(0, r0, c0, 0));
