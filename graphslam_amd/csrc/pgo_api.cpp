@@ -794,6 +794,37 @@ int pgo_restore_values(pgo_graph* g) {
   return PGO_OK;
 }
 
+int pgo_marginal_covariances(pgo_graph* g, size_t n, const uint64_t* keys, double* out) {
+  if (!g || (n && (!keys || !out))) return PGO_E_ARG;
+  if (n == 0) return PGO_OK;
+  std::vector<int> poses(n);
+  for (size_t i = 0; i < n; i++) {
+    auto it = g->index.find(keys[i]);
+    if (it == g->index.end()) return fail(g, PGO_E_NO_KEY, "marginal of key " + std::to_string(keys[i]) + " with no inserted value");
+    poses[i] = it->second;
+  }
+  RC_TRY(ensure_device(g));
+  HIP_TRY(g, hipSetDevice(g->device));
+  RC_TRY(ensure_chol(g));
+  DevGraph& d = g->d;
+  d.write_all = 0;
+  HIP_TRY(g, pgo::launch_linearize(d));
+  *g->h_lam = 0.0;
+  HIP_TRY(g, hipMemcpyAsync(g->chol.d_lambda, g->h_lam, sizeof(double), hipMemcpyHostToDevice, d.stream));
+  HIP_TRY(g, pgo::chol_factor(g->chol, d.D, d.V, d.g, 0.0, d.stream, nullptr));
+  int flag = 0;
+  HIP_TRY(g, hipMemcpyAsync(&flag, g->chol.d_flag, sizeof(int), hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(g, hipStreamSynchronize(d.stream));
+  if (flag) return fail(g, PGO_E_INDETERMINANT, "marginals: the linearised system is not positive definite");
+  // batches bound the per-workgroup scratch (6 x max front rows doubles each)
+  const size_t B = 256;
+  for (size_t b0 = 0; b0 < n; b0 += B) {
+    const int nb = (int)std::min(B, n - b0);
+    HIP_TRY(g, pgo::chol_marginals(g->chol, poses.data() + b0, nb, out + 9 * b0, d.stream));
+  }
+  return PGO_OK;
+}
+
 int pgo_error(pgo_graph* g, double* err) {
   if (!g || !err) return PGO_E_ARG;
   RC_TRY(ensure_device(g));

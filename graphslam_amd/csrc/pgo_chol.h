@@ -144,6 +144,9 @@ struct SyrkProfile {
 // factorisation as an extra column: on return the frontal vectors hold y = L^-1 b.
 hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
                        hipStream_t s, SyrkProfile* prof = nullptr);
+// after chol_factor: 3x3 blocks of (L L^T)^{-1} at the given poses (old index),
+// row-major 9 doubles each into host memory out (synchronises the stream)
+hipError_t chol_marginals(const CholPlan& P, const int* poses, int n, double* out, hipStream_t s);
 // after chol_factor: x = L^-T y = (L L^T)^{-1} scale_b b, indexed by old pose
 hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s);
 

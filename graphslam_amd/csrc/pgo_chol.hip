@@ -1124,6 +1124,106 @@ __global__ __launch_bounds__(256) void k_bwd_step(CholDev c, const int4* __restr
   }
 }
 
+// ------------------------------------------------------------ marginals
+// Marginal covariance of one pose (GTSAM Marginals::marginalCovariance): with
+// H_perm = L L', the 3x3 block of H^-1 at the pose is Y'Y, Y = L^-1 [e_a e_b e_c]
+// for the pose's three (permuted) columns.  Y is nonzero only on the fronts
+// from the pose's supernode up to the root, so one workgroup per pose walks
+// that path: per 64-column block y_b = X_bb v_b (X = inverted diagonal block),
+// the rows below get v -= L y_b, the Gram of the y blocks accumulates, and the
+// update vector moves to the parent front (extend-add of a single child).
+// v lives in a per-workgroup global scratch (two buffers of 3 x maxm).
+__global__ __launch_bounds__(256) void k_marginals(CholDev c, const int2* __restrict__ start, int maxm,
+                                                   double* __restrict__ scratch, double* __restrict__ out) {
+  __shared__ double ys[3][64];
+  __shared__ double red[6][4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int2 st = start[blockIdx.x];   // (supernode, local row of the pose's first column)
+  double* va = scratch + (size_t)blockIdx.x * 6 * maxm;
+  double* vb = va + 3 * (size_t)maxm;
+  int s = st.x;
+  {
+    const int m = c.m[s];
+    for (int r = 0; r < 3; r++)
+      for (int i = tid; i < m; i += 256) va[r * maxm + i] = i == st.y + r ? 1.0 : 0.0;
+  }
+  double g[6] = {0, 0, 0, 0, 0, 0};    // (aa, ab, ac, bb, bc, cc)
+  __syncthreads();
+  while (s >= 0) {
+    const int m = c.m[s], w = c.w[s];
+    const double* L = c.F + c.foff[s];
+    for (int c0 = 0; c0 < w; c0 += 64) {
+      const int n2 = min(64, w - c0);
+      if (tid < 64) {
+        const double* M = c.Tinv + c.toff[s] + (c0 / 64) * 4096;   // row-major X_bb
+        double y0 = 0, y1 = 0, y2 = 0;
+        if (tid < n2)
+          for (int k = 0; k <= tid; k++) {
+            const double x = M[tid * 64 + k];
+            y0 = fma(x, va[c0 + k], y0);
+            y1 = fma(x, va[maxm + c0 + k], y1);
+            y2 = fma(x, va[2 * maxm + c0 + k], y2);
+          }
+        ys[0][tid] = y0;
+        ys[1][tid] = y1;
+        ys[2][tid] = y2;
+        g[0] += y0 * y0;
+        g[1] += y0 * y1;
+        g[2] += y0 * y2;
+        g[3] += y1 * y1;
+        g[4] += y1 * y2;
+        g[5] += y2 * y2;
+      }
+      __syncthreads();
+      for (int r = c0 + n2 + tid; r < m; r += 256) {
+        double a0 = 0, a1 = 0, a2 = 0;
+        for (int k = 0; k < n2; k++) {
+          const double l = L[r + (size_t)(c0 + k) * m];
+          a0 = fma(l, ys[0][k], a0);
+          a1 = fma(l, ys[1][k], a1);
+          a2 = fma(l, ys[2][k], a2);
+        }
+        va[r] -= a0;
+        va[maxm + r] -= a1;
+        va[2 * maxm + r] -= a2;
+      }
+      __syncthreads();
+    }
+    const int p = c.parent[s];
+    if (p >= 0) {
+      const int mp = c.m[p];
+      for (int r = 0; r < 3; r++)
+        for (int i = tid; i < mp; i += 256) vb[r * maxm + i] = 0.0;
+      __syncthreads();
+      const int* rel = c.ea_rel + c.ea_ptr[s];
+      for (int t = tid; t < m - w; t += 256) {
+        const int q = 3 * rel[t / 3] + t % 3;
+        for (int r = 0; r < 3; r++) vb[r * maxm + q] = va[r * maxm + w + t];
+      }
+      __syncthreads();
+      double* tmp = va;
+      va = vb;
+      vb = tmp;
+    }
+    s = p;
+  }
+  // Gram reduction (wave butterflies, then the 4 waves)
+#pragma unroll
+  for (int q = 0; q < 6; q++) {
+    double v = g[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) red[q][wv] = v;
+  }
+  __syncthreads();
+  if (tid < 9) {
+    const int i = tid / 3, j = tid % 3;
+    const int a = i <= j ? i : j, b = i <= j ? j : i;
+    const int q = a == 0 ? b : (a == 1 ? 2 + b : 5);
+    out[(size_t)blockIdx.x * 9 + tid] = (red[q][0] + red[q][1]) + (red[q][2] + red[q][3]);
+  }
+}
+
 // ------------------------------------------------------------ host drivers
 template <class T>
 static hipError_t up(T** d, const std::vector<T>& h, hipStream_t s) {
@@ -1265,6 +1365,33 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
     }
   }
   return hipGetLastError();
+}
+
+hipError_t chol_marginals(const CholPlan& P, const int* poses, int n, double* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  int maxm = 1;
+  for (int q = 0; q < P.ns; q++) maxm = std::max(maxm, P.m[q]);
+  std::vector<int2> st(n);
+  for (int i = 0; i < n; i++) {
+    const int j = P.iperm[poses[i]];
+    st[i] = make_int2(P.dg_front[j], 3 * P.dg_loc[j]);
+  }
+  int2* d_st = nullptr;
+  double *d_scr = nullptr, *d_out = nullptr;
+  hipError_t e = hipMalloc((void**)&d_st, n * sizeof(int2));
+  if (e == hipSuccess) e = hipMalloc((void**)&d_scr, (size_t)n * 6 * maxm * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&d_out, (size_t)n * 9 * sizeof(double));
+  if (e == hipSuccess) e = hipMemcpyAsync(d_st, st.data(), n * sizeof(int2), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) {
+    k_marginals<<<n, 256, 0, s>>>(dev_view(P), d_st, maxm, d_scr, d_out);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, (size_t)n * 9 * sizeof(double), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (d_st) (void)hipFree(d_st);
+  if (d_scr) (void)hipFree(d_scr);
+  if (d_out) (void)hipFree(d_out);
+  return e;
 }
 
 hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s) {

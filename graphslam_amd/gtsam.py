@@ -179,6 +179,21 @@ def _build(graph: NonlinearFactorGraph, values: Values, device=0):
     return _Handle(pg)
 
 
+class Marginals:
+    """``gtsam::Marginals(graph, values)`` (graph.cpp:120, commented in the reference):
+    ``marginalCovariance(key)`` -> 3x3 numpy array (x, y, theta)."""
+
+    def __init__(self, graph: NonlinearFactorGraph, values: Values, device=0):
+        self.graph, self.values, self.device = graph, values, device
+
+    def marginalCovariance(self, key):
+        return self.marginalCovariances([key])[0]
+
+    def marginalCovariances(self, keys):
+        with _build(self.graph, self.values, self.device) as pg:
+            return pg.marginal_covariances(keys)
+
+
 class LevenbergMarquardtParams:
     """gtsam::LevenbergMarquardtParams with GTSAM 4.0 defaults (+ PCG knobs)."""
 

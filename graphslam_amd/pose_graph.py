@@ -163,6 +163,14 @@ class PoseGraph:
         self._check(self._L.pgo_get_poses(self._h, len(keys), L.u64ptr(keys), L.dptr(out)))
         return out
 
+    def marginal_covariances(self, keys):
+        """3x3 covariances (x, y, theta) of the poses at the current values:
+        gtsam::Marginals(graph, values).marginalCovariance(key) (graph.cpp:120,126-127)."""
+        keys = np.ascontiguousarray(np.atleast_1d(keys), dtype=np.uint64)
+        out = np.zeros((len(keys), 3, 3))
+        self._check(self._L.pgo_marginal_covariances(self._h, len(keys), L.u64ptr(keys), L.dptr(out)))
+        return out
+
     def set_poses(self, xyt, keys=None):
         xyt = np.ascontiguousarray(xyt, dtype=np.float64).reshape(-1, 3)
         kp = None

@@ -157,6 +157,15 @@ size_t pgo_num_vertices(const pgo_graph *g);  /* initial.size()    */
 /* graph.error(values) = 0.5 sum e^T Omega e at the current values (device). */
 int pgo_error(pgo_graph *g, double *err);
 
+/* ---- marginals ------------------------------------------
+   gtsam::Marginals(graph, values).marginalCovariance(key) (graph.cpp:120,
+   126-127, commented out in the reference; eigen_to_covariance graph.hpp:60-68):
+   the 3x3 covariance of each pose in its tangent space (x, y, theta), i.e. the
+   pose's block of H^-1 with H = J'Omega J linearised at the current values (no
+   damping).  out: n x 9 doubles, row-major.  A singular H (a component without
+   prior) returns PGO_E_INDETERMINANT, as GTSAM's Cholesky throws. */
+int pgo_marginal_covariances(pgo_graph *g, size_t n, const uint64_t *keys, double *out);
+
 /* ---- diagnostics (parity tests; device results at the current values) ---- */
 /* H diagonal blocks (9 doubles row-major per vertex, insertion order), the
  * off-diagonal block H_{k1,k2} = J1^T Omega of every between factor (9 per

@@ -245,6 +245,24 @@ def solve(H, rhs, lam):
 
 
 # ------------------------------------------------------------------ optimizers
+def marginal_covariances(prob: Problem, poses, idx):
+    """gtsam::Marginals(graph, values).marginalCovariance(key) (used, commented
+    out, at graph.cpp:120,126-127): the 3x3 block of H^-1 of each pose in idx, H =
+    J'Omega J at `poses` (no damping).  Columns of H^-1 by a sparse LU solve."""
+    import scipy.sparse.linalg as spla
+    lin = linearize(prob, poses)
+    lu = spla.splu(lin.H.tocsc(), permc_spec="COLAMD")
+    out = np.zeros((len(idx), 3, 3))
+    n3 = 3 * prob.n
+    for q, i in enumerate(idx):
+        E = np.zeros((n3, 3))
+        E[3 * i:3 * i + 3, :] = np.eye(3)
+        X = lu.solve(E)
+        blk = X[3 * i:3 * i + 3, :]
+        out[q] = 0.5 * (blk + blk.T)
+    return out
+
+
 @dataclass
 class LMParams:
     max_iterations: int = 100

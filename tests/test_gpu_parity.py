@@ -303,3 +303,61 @@ def test_gtsam_mirror_end_to_end(pgo_lib):
         q = poses_opti.atPose2(int(k))
         assert abs(q.x() - p[0]) < 1e-9 and abs(q.y() - p[1]) < 1e-9
     assert graph.error(poses_opti) < 1e-18
+
+
+# ------------------------------------------------------------ marginals
+@pytest.mark.parametrize("name,at", [("square", "initial"), ("C1", "initial"), ("C1", "optimum"),
+                                     ("C1-nn", "optimum"), ("C2", "initial")])
+def test_marginal_covariances(pg_cls, name, at):
+    """pgo_marginal_covariances vs the oracle's columns of H^-1 (sparse LU) at the
+    same values: both exact, agreement to rounding amplified by cond(H)."""
+    from oracle import pgo_numpy as pn
+    g = load(name)
+    pg = pg_cls.from_dataset(g)
+    if at == "optimum":
+        pg.optimize()
+    n = g.num_poses
+    idx = sorted(set([0, 1, n // 3, n // 2, n - 2, n - 1]))
+    keys = np.asarray(g.keys)[idx]
+    cov = pg.marginal_covariances(keys)
+    prob = pn.problem_from_graph(g)
+    ref = pn.marginal_covariances(prob, pn.from_xyt(pg.poses()), idx)
+    for q in range(len(idx)):
+        assert np.abs(cov[q] - cov[q].T).max() <= 1e-12 * np.abs(cov[q]).max()
+        assert np.abs(cov[q] - ref[q]).max() <= 1e-8 * np.abs(ref[q]).max(), (idx[q], cov[q], ref[q])
+
+
+def test_marginals_batch_and_errors(pg_cls):
+    """A batch larger than one launch (256 keys), repeated keys, an unknown key,
+    and a graph without a prior (singular H, GTSAM's Cholesky throws)."""
+    from graphslam_amd.pose_graph import IndeterminantLinearSystemException, PgoError
+    g = load("C1")
+    pg = pg_cls.from_dataset(g)
+    keys = np.asarray(g.keys)[np.arange(0, g.num_poses, 3)]
+    keys = np.concatenate([keys, keys[:5]])
+    cov = pg.marginal_covariances(keys)
+    assert cov.shape == (len(keys), 3, 3)
+    assert np.array_equal(cov[-5:], cov[:5])            # deterministic
+    with pytest.raises(PgoError):
+        pg.marginal_covariances([10 ** 12])
+    free = pg_cls()
+    free.add_vertices(np.array([1, 2], dtype=np.uint64), np.array([[0, 0, 0], [1, 0, 0]], float))
+    free.add_edge(1, 2, [1, 0, 0], np.diag([0.01, 0.01, 0.001]))
+    with pytest.raises(IndeterminantLinearSystemException):
+        free.marginal_covariances([1])
+
+
+def test_gtsam_mirror_marginals(pgo_lib):
+    from graphslam_amd import gtsam
+    graph, values = gtsam.NonlinearFactorGraph(), gtsam.Values()
+    cov = np.diag([0.01, 0.01, 0.01])
+    graph.add(gtsam.PriorFactorPose2(1, gtsam.Pose2(0, 0, 0), gtsam.noiseModel.Gaussian.Covariance(cov)))
+    for k in range(1, 6):
+        values.insert(k, gtsam.Pose2(k - 1.0, 0.0, 0.0))
+    for k in range(1, 5):
+        graph.add(gtsam.BetweenFactorPose2(k, k + 1, gtsam.Pose2(1, 0, 0),
+                                           gtsam.noiseModel.Gaussian.Covariance(np.diag([0.05 ** 2, 0.05 ** 2, 0.01]))))
+    m = gtsam.Marginals(graph, values)
+    c1, c5 = m.marginalCovariance(1), m.marginalCovariance(5)
+    assert np.allclose(c1, cov, rtol=1e-12, atol=1e-15)   # a chain leaves the prior pose at the prior
+    assert c5[0, 0] > c1[0, 0] and c5[1, 1] > c1[1, 1] and c5[2, 2] > c1[2, 2]   # uncertainty grows

@@ -190,3 +190,20 @@ def test_direct_solve_matches_scipy(oracle_lib):
     lin = tw.linearize(prob, tw.from_xyt(g.initial))
     ref = tw.solve(lin.H, -lin.g, 1e-3).reshape(-1, 3)
     assert np.allclose(d, ref, rtol=1e-8, atol=1e-9 * np.abs(ref).max())
+
+
+def test_marginals_twin_dense():
+    """The marginal restatement (sparse LU columns of H^-1) vs a dense inverse."""
+    from oracle import pgo_numpy as pn
+    g = datasets.make("C1")
+    prob = pn.problem_from_graph(g)
+    poses = pn.from_xyt(g.initial)
+    idx = [0, 1, 17, 500, g.num_poses - 1]
+    cov = pn.marginal_covariances(prob, poses, idx)
+    Hinv = np.linalg.inv(pn.linearize(prob, poses).H.toarray())
+    for q, i in enumerate(idx):
+        ref = Hinv[3 * i:3 * i + 3, 3 * i:3 * i + 3]
+        assert np.abs(cov[q] - ref).max() <= 1e-9 * np.abs(ref).max()
+        assert np.all(np.linalg.eigvalsh(cov[q]) > 0)
+    # the prior pins pose 0 (Sigma = diag(0.01)): its marginal is at most the prior
+    assert np.all(np.diag(cov[0]) <= 0.01 + 1e-12)
