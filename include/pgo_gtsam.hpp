@@ -177,4 +177,41 @@ class LevenbergMarquardtOptimizer {
   pgo_stats stats_{};
 };
 
+// gtsam::Marginals(graph, values) (graph.cpp:120, commented in the reference):
+// marginalCovariance(key) is the pose's 3x3 covariance (x, y, theta) at `values`,
+// row-major in Matrix3::m (what eigen_to_covariance, graph.hpp:60-68, copies).
+class Marginals {
+ public:
+  Marginals(const NonlinearFactorGraph& graph, const Values& values, int device = 0) {
+    pgo_opts o{};
+    o.device = device;
+    g_ = pgo_create(&o);
+    if (!g_) throw std::runtime_error("pgo_create failed");
+    for (size_t i = 0; i < values.size(); i++) {
+      const Pose2& p = values.poses()[i];
+      throw_status(pgo_add_vertex(g_, values.keys()[i], p.x(), p.y(), p.raw_theta()), g_);
+    }
+    for (const auto& f : graph.priors()) {
+      const double z[3] = {f.prior.x(), f.prior.y(), f.prior.raw_theta()};
+      throw_status(pgo_add_prior(g_, f.key, z, f.noise.cov.m), g_);
+    }
+    for (const auto& f : graph.betweens()) {
+      const double z[3] = {f.measured.x(), f.measured.y(), f.measured.raw_theta()};
+      throw_status(pgo_add_edge(g_, f.key1, f.key2, z, f.noise.cov.m), g_);
+    }
+  }
+  ~Marginals() { pgo_destroy(g_); }
+  Marginals(const Marginals&) = delete;
+  Marginals& operator=(const Marginals&) = delete;
+
+  Matrix3 marginalCovariance(Key key) const {
+    Matrix3 out;
+    throw_status(pgo_marginal_covariances(g_, 1, &key, out.m), g_);
+    return out;
+  }
+
+ private:
+  pgo_graph* g_ = nullptr;
+};
+
 }  // namespace pgo_gtsam

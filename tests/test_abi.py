@@ -157,6 +157,9 @@ int main() {
     for (Key k = 1; k <= 8; k++)
       std::printf("%llu %.9f %.9f %.9f\n", (unsigned long long)k, poses_opti.at<Pose2>(k).x(),
                   poses_opti.at<Pose2>(k).y(), poses_opti.at<Pose2>(k).theta());
+    Marginals marginals(graph, poses_opti);                                       // graph.cpp:120
+    const Matrix3 c = marginals.marginalCovariance(8);                            // graph.cpp:126
+    std::printf("cov8 %.6e %.6e %.6e\n", c(0, 0), c(1, 1), c(2, 2));
   } catch (const std::runtime_error& e) {
     std::printf("runtime_error %s\n", e.what());
   }
@@ -180,4 +183,4 @@ def test_cpp_adapter_compiles_and_runs_host_side(tmp_path, pgo_lib):
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("factors 9")
     # no GPU here: the optimiser reports it instead of falling back to the CPU
-    assert ("runtime_error" in r.stdout and "device" in r.stdout) or r.stdout.count("\n") == 9
+    assert ("runtime_error" in r.stdout and "device" in r.stdout) or r.stdout.count("\n") == 10

@@ -361,3 +361,18 @@ def test_gtsam_mirror_marginals(pgo_lib):
     c1, c5 = m.marginalCovariance(1), m.marginalCovariance(5)
     assert np.allclose(c1, cov, rtol=1e-12, atol=1e-15)   # a chain leaves the prior pose at the prior
     assert c5[0, 0] > c1[0, 0] and c5[1, 1] > c1[1, 1] and c5[2, 2] > c1[2, 2]   # uncertainty grows
+
+
+def test_cpp_adapter_on_gpu(tmp_path, pgo_lib):
+    """graph.cpp's call sequence through include/pgo_gtsam.hpp, optimize + Marginals, on the GPU."""
+    import subprocess
+    from test_abi import build_graph_cpp_style
+    exe = build_graph_cpp_style(tmp_path)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert lines[0] == "factors 9" and len(lines) == 10, r.stdout
+    xyt = np.array([[float(v) for v in ln.split()[1:]] for ln in lines[1:9]])
+    assert np.all(np.isfinite(xyt))
+    cov = [float(v) for v in lines[9].split()[1:]]
+    assert lines[9].startswith("cov8") and all(v > 0 for v in cov)
