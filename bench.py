@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--solver", choices=["cholesky", "pcg"], default="cholesky")
     ap.add_argument("--no-graphs", action="store_true",
                     help="eager launches instead of the captured factor+solve hipGraph (rocprofv3 runs)")
+    ap.add_argument("--marginals", type=int, default=64,
+                    help="after the timed steps: time marginal covariances of this many poses (0: skip)")
     ap.add_argument("--max-outer", type=int, default=0,
                     help="profiling runs only: stop each optimize after this many linearisations")
     args = ap.parse_args()
@@ -103,6 +105,17 @@ def main():
         return st["linearizations"], st
 
     elapsed, lin_total, results = timed_steps(r, step, args.steps, args.warmup)
+    marg = None
+    if args.marginals > 0 and rank == 0:
+        import numpy as np
+        keys = np.asarray(g.keys)[np.linspace(0, g.num_poses - 1, args.marginals).astype(np.int64)]
+        pg.marginal_covariances(keys[:1])            # plan + first factorisation warm
+        t0 = time.perf_counter()
+        pg.marginal_covariances(keys)
+        dt = time.perf_counter() - t0
+        marg = {"keys": int(len(keys)), "ms": 1e3 * dt,
+                "note": "gtsam::Marginals::marginalCovariance per pose at the optimum: one undamped "
+                        "factorisation + per-pose path solves (Y'Y, Y = L^-1 E)"}
     stats = [s for _, s in results]
     last = stats[-1]
     totals = dict(spmv_ms=sum(s["kernel_spmv_ms"] for s in stats), spmv_n=sum(s["kernel_spmv_count"] for s in stats),
@@ -181,6 +194,7 @@ def main():
                 "achieved_gbs": linearize_bytes(n, ne) / (lin_avg_ms * 1e-3) / 1e9 if totals["lin_n"] else None,
             },
             "cpu_baseline": None,
+            "marginals": marg,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(g, args.cpu_outer)
