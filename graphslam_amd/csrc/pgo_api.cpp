@@ -1002,7 +1002,7 @@ int pgo_debug_plan(pgo_graph* g, double* out, int cap) {
   for (const auto& lv : P.levels) {
     lf += (long long)lv.ea_off.size() + 1 + lv.small.size();
     for (const auto& ps : lv.panels)
-      lf += (ps.potrf_cnt > 0) + (ps.trsm_cnt > 0) + (ps.syrk_cnt > 0) + (ps.sdiag_cnt > 0);
+      lf += (ps.potrf_cnt > 0) + (ps.trsm_cnt > 0) + (ps.fused ? 1 : (ps.syrk_cnt > 0) + (ps.sdiag_cnt > 0));
     ls += (lv.bwd_part.cnt > 0) + (long long)lv.bwd.size();
     for (const auto& ps : lv.panels) {
       trsm += ps.trsm_cnt;

@@ -37,6 +37,7 @@ struct PanelStep {                 // one panel of the blocked path, all big fro
   double syrk_flops;               // algorithmic flops of this step's Schur updates (lower triangles)
   int syrk_tile;                   // kTile or kBigTile
   int sdiag_off, sdiag_cnt;        // look-ahead tasks in sdiag_tasks (next panel's diagonal tile)
+  int fused;                       // 1: look-ahead and update in one launch (k_step_fused) on the main stream
 };
 
 struct SolveStep {                 // one launch of the blocked triangular solves

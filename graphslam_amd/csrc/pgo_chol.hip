@@ -717,11 +717,11 @@ __global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int4* __res
 // loaded once per workgroup instead of once per wave pair; 8 loads per thread
 // per chunk, issued one chunk ahead of the MFMAs).  Low register count, so
 // several workgroups per CU hide the load latency.
-__global__ __launch_bounds__(256) void k_panel_syrk_lds(CholDev c, const int4* __restrict__ tasks, int kb) {
+// smem: 4 * 16 * 68 doubles (Sr[2], Sc[2])
+__device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, int kb, double* smem) {
   constexpr int LD = 64 + 4;
-  __shared__ __attribute__((aligned(16))) double Sr[2][16 * LD];
-  __shared__ __attribute__((aligned(16))) double Sc[2][16 * LD];
-  const int4 t = tasks[blockIdx.x];
+  double(*Sr)[16 * LD] = reinterpret_cast<double(*)[16 * LD]>(smem);
+  double(*Sc)[16 * LD] = reinterpret_cast<double(*)[16 * LD]>(smem + 2 * 16 * LD);
   const int s = t.x, row0 = t.y, col0 = t.z;
   const bool inner = t.w < 0;
   const int k0 = t.w & 0x7fffffff;
@@ -801,20 +801,100 @@ __global__ __launch_bounds__(256) void k_panel_syrk_lds(CholDev c, const int4* _
     }
 }
 
+__global__ __launch_bounds__(256) void k_panel_syrk_lds(CholDev c, const int4* __restrict__ tasks, int kb) {
+  __shared__ __attribute__((aligned(16))) double smem[4 * 16 * 68];
+  syrk_lds_body(c, tasks[blockIdx.x], kb, smem);
+}
+
+// Schur update of a diagonal 64x64 tile into LDS: Ts (ld 65, lower) = C - P P^T,
+// P = F[r0:r0+64, k0:kend).  C and the first 64-deep chunk of P are loaded
+// together (one memory latency for the usual inner depth of 64); P goes
+// through Sp (LDS, [k][row], ld 68) chunk by chunk, the next chunk's loads in
+// flight during the MFMAs; the 10 lower 16x16 blocks are dealt 3/3/2/2 to the
+// waves.  Elements outside the live nb x nb block (nb < 64 at a front's last
+// panel) are written back to F here; the caller factors the live block.
+__device__ __forceinline__ void diag_tile_update(const CholDev& c, const int4 t, int kb, double* Ts, double* Sp) {
+  constexpr int LD = 68;
+  const int s = t.x, r0 = t.y;
+  const bool inner = t.w < 0;
+  const int k0 = t.w & 0x7fffffff;
+  const int m = c.m[s], w = c.w[s];
+  const int kend = min(kb + kNB, w);
+  const int colend = inner ? min((kb & ~(kKB - 1)) + kKB, w) : m;
+  const int K = kend - k0, nch = (K + 63) >> 6;
+  const int nb = min(kNB, w - r0);
+  double* Fs = c.F + c.foff[s];
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int li = l & 15, lk = l >> 4;
+  double st[16];
+  auto load = [&](int ch) {
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      const int idx = tid + 256 * q, i = idx & 63, k = 64 * ch + (idx >> 6);
+      st[q] = (k < K && r0 + i < m) ? Fs[(r0 + i) + (size_t)(k0 + k) * m] : 0.0;
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < 16; q++) {   // C, lower part of the updated region
+    const int idx = tid + 256 * q, i = idx & 63, j = idx >> 6;
+    Ts[i + j * 65] = (i >= j && r0 + i < m && r0 + j < colend) ? Fs[(r0 + i) + (size_t)(r0 + j) * m] : 0.0;
+  }
+  load(0);
+  // lower 16x16 blocks (I, J) of this wave
+  const int nblk = wv < 2 ? 3 : 2;
+  const int bI0 = wv == 0 ? 0 : (wv == 1 ? 3 : 3), bJ0 = wv == 0 ? 0 : (wv == 1 ? 0 : (wv == 2 ? 1 : 2));
+  const int bI1 = wv == 0 ? 1 : (wv == 1 ? 1 : (wv == 2 ? 2 : 3)), bJ1 = wv == 0 ? 0 : (wv == 1 ? 1 : (wv == 2 ? 2 : 3));
+  const int bI2 = wv == 0 ? 2 : 2, bJ2 = wv == 0 ? 0 : 1;
+  d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0};
+  for (int ch = 0; ch < nch; ch++) {
+    if (ch) __syncthreads();   // previous chunk's MFMAs are done with Sp
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      const int idx = tid + 256 * q;
+      Sp[(idx >> 6) * LD + (idx & 63)] = st[q];
+    }
+    __syncthreads();
+    if (ch + 1 < nch) load(ch + 1);
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const double* sk = Sp + (4 * u + lk) * LD + li;
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(sk[16 * bJ0], sk[16 * bI0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(sk[16 * bJ1], sk[16 * bI1], acc1, 0, 0, 0);
+      if (nblk == 3) acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(sk[16 * bJ2], sk[16 * bI2], acc2, 0, 0, 0);
+    }
+  }
+  // lane l, reg r of block (I, J): row 16I + li, column 16J + lk + 4r
+#pragma unroll
+  for (int b = 0; b < 3; b++) {
+    if (b == 2 && nblk < 3) break;
+    const d4 a = b == 0 ? acc0 : (b == 1 ? acc1 : acc2);
+    const int I = b == 0 ? bI0 : (b == 1 ? bI1 : bI2), J = b == 0 ? bJ0 : (b == 1 ? bJ1 : bJ2);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int i = 16 * I + li, j = 16 * J + lk + 4 * r;
+      if (i >= j && r0 + i < m && r0 + j < colend) {
+        const double v = Ts[i + j * 65] - a[r];
+        Ts[i + j * 65] = v;
+        if (!(i < nb && j < nb)) Fs[(r0 + i) + (size_t)(r0 + j) * m] = v;
+      }
+    }
+  }
+}
+
 // The Schur-update tile that is the next panel's diagonal tile (row0 = col0 =
 // kb + nb < w), then that tile factored and inverted in place (look-ahead: runs
-// on a second stream beside the rest of the panel's Schur update, so the next
-// panel starts without a separate diagonal step).
-__global__ __launch_bounds__(256) void k_syrk_diag(CholDev c, const int4* __restrict__ tasks, int kb) {
-  __shared__ double Ts[64 * 65];
-  __shared__ double Ws[64 * 65];
-  __shared__ double bc[64];
-  const int4 t = tasks[blockIdx.x];
+// on a second stream beside the rest of the panel's Schur update, or as the
+// first workgroups of k_step_fused, so the next panel starts without a
+// separate diagonal step).  smem: 64*65 + 64*68 + 64 doubles.
+__device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, int kb, double* smem) {
+  double* Ts = smem;
+  double* Ws = smem + 64 * 65;
+  double* bc = Ws + 64 * 68;
   const int s = t.x, kn = t.y;
   const int m = c.m[s], w = c.w[s];
   const int nb = min(kNB, w - kn);
   const int tid = threadIdx.x;
-  syrk_tile64<true>(c, t, kb, Ts);
+  diag_tile_update(c, t, kb, Ts, Ws);
   __syncthreads();
   for (int idx = tid; idx < 4096; idx += 256) {
     const int i = idx & 63, j = idx >> 6;
@@ -832,6 +912,25 @@ __global__ __launch_bounds__(256) void k_syrk_diag(CholDev c, const int4* __rest
     M[idx] = (a < nb && b < nb && a >= b) ? Ws[a + b * 65] : 0.0;
   }
   panel_rhs(c.fv + c.voff[s] + kn, Ws, nb, bc);
+}
+
+constexpr int kDiagSmem = 64 * 65 + 64 * 68 + 64;
+
+__global__ __launch_bounds__(256) void k_syrk_diag(CholDev c, const int4* __restrict__ tasks, int kb) {
+  __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
+  syrk_diag_body(c, tasks[blockIdx.x], kb, smem);
+}
+
+// One panel step's Schur update in a single launch on the main stream (steps
+// whose update is small beside the look-ahead diagonal factorisation): the
+// first nsd workgroups are the look-ahead diagonal tiles (k_syrk_diag), the
+// rest the 64x64 update tiles (k_panel_syrk_lds).
+__global__ __launch_bounds__(256) void k_step_fused(CholDev c, const int4* __restrict__ sdiag, int nsd,
+                                                    const int4* __restrict__ tasks, int kb) {
+  __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
+  const int b = blockIdx.x;
+  if (b < nsd) syrk_diag_body(c, sdiag[b], kb, smem);
+  else syrk_lds_body(c, tasks[b - nsd], kb, smem);
 }
 
 // Schur update of one 128x128 lower tile (same task format and semantics as
@@ -1339,6 +1438,11 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
     for (const PanelStep& ps : lv.panels) {
       if (ps.potrf_cnt) k_panel_diag<<<ps.potrf_cnt, 256, 0, s>>>(c, P.d_potrf + ps.potrf_off, ps.kb);
       if (ps.trsm_cnt) k_panel_trsm<<<ps.trsm_cnt, 256, 0, s>>>(c, P.d_trsm + ps.trsm_off, ps.kb);
+      if (ps.fused) {
+        k_step_fused<<<ps.sdiag_cnt + ps.syrk_cnt, 256, 0, s>>>(c, P.d_sdiag + ps.sdiag_off, ps.sdiag_cnt,
+                                                                 (const int4*)(P.d_syrk + ps.syrk_off), ps.kb);
+        continue;
+      }
       if (ps.sdiag_cnt) {   // look-ahead: next panel's diagonal tiles on the side stream
         CH_TRY(hipEventRecord(P.evs[2], s));
         CH_TRY(hipStreamWaitEvent(P.side, P.evs[2], 0));

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <tuple>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -540,6 +541,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     int maxw = 0;
     for (int s : big) maxw = std::max(maxw, P.w[s]);
     std::vector<char> diag_ready(ns, 0);
+    static const double fuse_flops = getenv("PGO_FUSE_FLOPS") ? atof(getenv("PGO_FUSE_FLOPS")) : 2e9;
     for (int kb = 0; kb < maxw; kb += kNB) {
       PanelStep ps;
       ps.kb = kb;
@@ -610,7 +612,10 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       ps.potrf_cnt = (int)P.potrf_list.size() - ps.potrf_off;
       ps.trsm_cnt = (int)P.trsm_tasks.size() - ps.trsm_off;
       ps.syrk_cnt = (int)P.syrk_tasks.size() - ps.syrk_off;
-      P.syrk_flops += ps.syrk_flops;
+      // a small update runs in the look-ahead's launch (no second-stream
+      // hand-off); the profiled Schur-update flops count the separate launches only
+      ps.fused = ps.sdiag_cnt > 0 && ps.syrk_flops <= fuse_flops;
+      if (!ps.fused) P.syrk_flops += ps.syrk_flops;
       lv.panels.push_back(ps);
     }
   }
