@@ -79,11 +79,14 @@ struct CholPlan {
   // assembly of H: target blocks (front, local row pose, local col pose) and their slots
   std::vector<int> asm_front, asm_li, asm_lj, asm_ptr, asm_src;
   std::vector<int> dg_front, dg_loc;   // per new pose: front and local index (diagonal block)
+  std::vector<int> dg_order;       // new poses, those of leaf-level fronts first
+  int asm_split = 0, dg_split = 0, zero_split = 0;   // leaf-level prefixes of asm targets, dg_order, zero_tasks
   // schedules
   std::vector<CholLevel> levels;
   std::vector<int> small_list, level_fronts, potrf_list;
   std::vector<int2> trsm_tasks;
   std::vector<int4> syrk_tasks, sdiag_tasks;
+  std::vector<int4> zero_tasks;     // (front, first column, end column): lower triangles zeroed per factorisation
   std::vector<int4> bwd_tasks;
   std::vector<int2> bwd_pref;      // per bwd task: first partial, partial count (init tasks)
   std::vector<int4> bwd_part_tasks;  // (front, c0, r0, partial slot)
@@ -104,13 +107,14 @@ struct CholPlan {
   long long* d_toff = nullptr;
   int *d_cptr = nullptr, *d_children = nullptr, *d_ea_rel = nullptr, *d_ea_ptr = nullptr, *d_parent = nullptr;
   int *d_asm_front = nullptr, *d_asm_li = nullptr, *d_asm_lj = nullptr, *d_asm_ptr = nullptr, *d_asm_src = nullptr;
-  int *d_dg_front = nullptr, *d_dg_loc = nullptr, *d_perm = nullptr;
+  int *d_dg_front = nullptr, *d_dg_loc = nullptr, *d_perm = nullptr, *d_dg_order = nullptr;
   int *d_small = nullptr, *d_level_fronts = nullptr, *d_potrf = nullptr;
   int2* d_trsm = nullptr;
-  int4 *d_syrk = nullptr, *d_sdiag = nullptr;
+  int4 *d_syrk = nullptr, *d_sdiag = nullptr, *d_zero = nullptr;
   hipStream_t side = nullptr;      // look-ahead diagonal tiles
   hipStream_t side2 = nullptr;     // small fronts beside the blocked path
-  hipEvent_t evs[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipStream_t side3 = nullptr;     // zeroing + assembly of the non-leaf fronts beside the leaf level
+  hipEvent_t evs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int4 *d_bwd = nullptr, *d_bwd_part = nullptr;
   int2* d_bwd_pref = nullptr;
   double* d_partial = nullptr;

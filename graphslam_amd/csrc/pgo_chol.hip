@@ -32,7 +32,7 @@ struct CholDev {
   const long long* foff;
   const int *cptr, *children, *ea_rel, *ea_ptr, *parent;
   const int *asm_front, *asm_li, *asm_lj, *asm_ptr, *asm_src;
-  const int *dg_front, *dg_loc, *perm;
+  const int *dg_front, *dg_loc, *perm, *dg_order;
   int* flag;
 };
 
@@ -44,6 +44,7 @@ static CholDev dev_view(const CholPlan& P) {
   c.parent = P.d_parent;
   c.asm_front = P.d_asm_front; c.asm_li = P.d_asm_li; c.asm_lj = P.d_asm_lj; c.asm_ptr = P.d_asm_ptr;
   c.asm_src = P.d_asm_src; c.dg_front = P.d_dg_front; c.dg_loc = P.d_dg_loc; c.perm = P.d_perm;
+  c.dg_order = P.d_dg_order;
   c.flag = P.d_flag;
   return c;
 }
@@ -61,9 +62,9 @@ __device__ long long g_diag_clk[32];
 // ------------------------------------------------------------ assembly
 // off-diagonal lower blocks H_{i,j} (i > j) of a front: sum of their slots
 __global__ __launch_bounds__(256) void k_asm_offdiag(CholDev c, const double* __restrict__ V, long long S,
-                                                     int ntargets) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= ntargets) return;
+                                                     int t0, int t1) {
+  const int t = t0 + blockIdx.x * 256 + threadIdx.x;
+  if (t >= t1) return;
   const int s = c.asm_front[t];
   const int m = c.m[s];
   double* Fs = c.F + c.foff[s];
@@ -82,9 +83,10 @@ __global__ __launch_bounds__(256) void k_asm_offdiag(CholDev c, const double* __
 
 // diagonal blocks H_jj + lambda I (lower part)
 __global__ __launch_bounds__(256) void k_asm_diag(CholDev c, const double* __restrict__ D,
-                                                 const double* __restrict__ lam_p, int n) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= n) return;
+                                                 const double* __restrict__ lam_p, int t0, int t1) {
+  const int t = t0 + blockIdx.x * 256 + threadIdx.x;
+  if (t >= t1) return;
+  const int j = c.dg_order[t];
   const double lam = *lam_p;
   const int s = c.dg_front[j];
   const int m = c.m[s];
@@ -587,20 +589,20 @@ __global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __res
   const double* M = c.Tinv + c.toff[s] + (kb / 64) * 4096;
   double* fv = c.fv + c.voff[s];
   const int tid = threadIdx.x;
-  for (int idx = tid; idx < 4096; idx += 256) Tb[(idx & 63) * LDB + (idx >> 6)] = M[idx];   // M row-major
-  if (tid < 64) ys[tid] = tid < nb ? fv[kb + tid] : 0.0;   // y of the panel (diagonal step)
-  __syncthreads();
   const int wv = tid >> 6, l = tid & 63;
   const int r0 = kb + nb + chunk * 64 + wv * 16;
-  if (r0 >= m) return;
   double* Fc = c.F + c.foff[s] + (size_t)kb * m;   // column kb of the front
   const int arow = r0 + (l & 15), kl = l >> 4;
-  double a[16];
+  double a[16];   // B fragments, in flight with the staging of the inverse
 #pragma unroll
   for (int ks = 0; ks < 16; ks++) {
     const int k = 4 * ks + kl;
     a[ks] = (arow < m && k < nb) ? Fc[arow + (size_t)k * m] : 0.0;
   }
+  for (int idx = tid; idx < 4096; idx += 256) Tb[(idx & 63) * LDB + (idx >> 6)] = M[idx];   // M row-major
+  if (tid < 64) ys[tid] = tid < nb ? fv[kb + tid] : 0.0;   // y of the panel (diagonal step)
+  __syncthreads();
+  if (r0 >= m) return;
   d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0}, acc3 = {0, 0, 0, 0};
 #pragma unroll
   for (int ks = 0; ks < 16; ks++) {
@@ -1030,6 +1032,24 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
   }
 }
 
+// Lower triangles of the fronts (columns [j0, j1) of a front per workgroup)
+// zeroed before assembly; the upper triangles are never written.
+__global__ __launch_bounds__(256) void k_zero_lower(CholDev c, const int4* __restrict__ tasks) {
+  const int4 t = tasks[blockIdx.x];
+  const int m = c.m[t.x];
+  const long long base = c.foff[t.x];
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (int j = t.y + wv; j < t.z; j += 4) {   // a wave per column, 16-B stores
+    const long long g0 = base + (long long)j * m + j, g1 = base + (long long)j * m + m;
+    const long long a0 = (g0 + 1) & ~1LL;       // first 16-B aligned element
+    if (l == 0 && a0 != g0) c.F[g0] = 0.0;
+    double2* p = reinterpret_cast<double2*>(c.F + a0);
+    const long long np = (g1 - a0) >> 1;
+    for (long long q = l; q < np; q += 64) p[q] = make_double2(0.0, 0.0);
+    if (l == 0 && a0 + 2 * np < g1) c.F[g1 - 1] = 0.0;
+  }
+}
+
 // ------------------------------------------------------------ solves
 __global__ __launch_bounds__(256) void k_perm_in(CholDev c, const double* __restrict__ b, double scale, int n) {
   const int j = blockIdx.x * 256 + threadIdx.x;
@@ -1375,8 +1395,12 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(hipMalloc((void**)&P.d_partial, std::max(P.npart, 1) * 64 * sizeof(double)));
   CH_TRY(up(&P.d_syrk, P.syrk_tasks, s));
   CH_TRY(up(&P.d_sdiag, P.sdiag_tasks, s));
+  CH_TRY(up(&P.d_zero, P.zero_tasks, s));
+  CH_TRY(up(&P.d_dg_order, P.dg_order, s));
+  CH_TRY(hipMemsetAsync(P.F, 0, std::max<long long>(P.ftotal, 1) * sizeof(double), s));   // upper triangles stay zero
   CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
   CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
+  CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));
   for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   CH_TRY(up(&P.d_ea_children, P.ea_children, s));
   CH_TRY(up(&P.d_ea_colpref, P.ea_colpref, s));
@@ -1387,13 +1411,14 @@ void chol_free(CholPlan& P) {
   void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
                   P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
                   P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
-                  P.d_trsm, P.d_syrk, P.d_ea_children, P.d_ea_colpref, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag};
+                  P.d_trsm, P.d_syrk, P.d_ea_children, P.d_ea_colpref, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_zero, P.d_dg_order};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : P.evs)
     if (e) (void)hipEventDestroy(e);
   if (P.side) (void)hipStreamDestroy(P.side);
   if (P.side2) (void)hipStreamDestroy(P.side2);
+  if (P.side3) (void)hipStreamDestroy(P.side3);
   P = CholPlan();
 }
 
@@ -1402,12 +1427,26 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
   if (P.n == 0) return hipSuccess;
   const CholDev c = dev_view(P);
   k_perm_in<<<(P.n + 255) / 256, 256, 0, s>>>(c, b, scale_b, P.n);
-  CH_TRY(hipMemsetAsync(P.F, 0, P.ftotal * sizeof(double), s));
   CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int), s));
-  const int nt = (int)P.asm_front.size();
-  if (nt) k_asm_offdiag<<<(nt + 255) / 256, 256, 0, s>>>(c, V, P.nslots, nt);
-  k_asm_diag<<<(P.n + 255) / 256, 256, 0, s>>>(c, D, P.d_lambda, P.n);
-  for (const CholLevel& lv : P.levels) {
+  // zeroing + assembly: leaf-level fronts on the main stream, the others on
+  // side3 beside the leaf level (joined before level 1's extend-add)
+  const int nz = (int)P.zero_tasks.size(), nt = (int)P.asm_front.size();
+  auto assemble = [&](int z0, int z1, int a0, int a1, int d0, int d1, hipStream_t st) {
+    if (z1 > z0) k_zero_lower<<<z1 - z0, 256, 0, st>>>(c, P.d_zero + z0);
+    if (a1 > a0) k_asm_offdiag<<<(a1 - a0 + 255) / 256, 256, 0, st>>>(c, V, P.nslots, a0, a1);
+    if (d1 > d0) k_asm_diag<<<(d1 - d0 + 255) / 256, 256, 0, st>>>(c, D, P.d_lambda, d0, d1);
+  };
+  assemble(0, P.zero_split, 0, P.asm_split, 0, P.dg_split, s);
+  const bool fork_rest = P.zero_split < nz || P.asm_split < nt || P.dg_split < P.n;
+  if (fork_rest) {
+    CH_TRY(hipEventRecord(P.evs[4], s));
+    CH_TRY(hipStreamWaitEvent(P.side3, P.evs[4], 0));
+    assemble(P.zero_split, nz, P.asm_split, nt, P.dg_split, P.n, P.side3);
+    CH_TRY(hipEventRecord(P.evs[5], P.side3));
+  }
+  for (size_t li = 0; li < P.levels.size(); li++) {
+    const CholLevel& lv = P.levels[li];
+    if (li == 1 && fork_rest) CH_TRY(hipStreamWaitEvent(s, P.evs[5], 0));
     for (size_t r = 0; r < lv.ea_off.size(); r++) {
       const long long cols = P.ea_colpref[lv.ea_cols_off[r] + lv.ea_cnt[r]];
       if (!cols) continue;

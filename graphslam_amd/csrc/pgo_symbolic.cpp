@@ -366,6 +366,10 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     for (size_t t = 0; t < below[s].size(); t++)
       P.ea_rel[P.ea_ptr[s] + t] = p >= 0 ? local_of(p, below[s][t]) : -1;
   }
+  // ---- heights (leaves 0)
+  P.height.assign(ns, 0);
+  for (int s = 0; s < ns; s++)  // children precede parents (postorder)
+    if (P.parent[s] >= 0) P.height[P.parent[s]] = std::max(P.height[P.parent[s]], P.height[s] + 1);
   // ---- assembly of H's lower blocks: block H_{i,j} (i > j, new) lives in the
   // slots of block-CSR row perm[i] whose column is perm[j]; parallel factors
   // between the same pair are summed in slot order.
@@ -381,7 +385,11 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       if (i > j) ents.push_back({j, i, k});
     }
   }
-  std::sort(ents.begin(), ents.end(), [](const Ent& a, const Ent& b) {
+  // targets of leaf-level fronts first (assembled on the main stream, the rest
+  // beside the leaf level)
+  std::sort(ents.begin(), ents.end(), [&](const Ent& a, const Ent& b) {
+    const bool la = P.height[snode[a.j]] > 0, lb = P.height[snode[b.j]] > 0;
+    if (la != lb) return lb;
     return a.j != b.j ? a.j < b.j : (a.i != b.i ? a.i < b.i : a.k < b.k);
   });
   P.asm_front.clear();
@@ -401,16 +409,21 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   }
   P.asm_ptr.push_back((int)P.asm_src.size());
   if (ents.empty()) P.asm_ptr.assign(1, 0);
+  P.asm_split = 0;
+  while (P.asm_split < (int)P.asm_front.size() && P.height[P.asm_front[P.asm_split]] == 0) P.asm_split++;
   P.dg_front.resize(n);
   P.dg_loc.resize(n);
   for (int j = 0; j < n; j++) {
     P.dg_front[j] = snode[j];
     P.dg_loc[j] = j - P.sfirst[snode[j]];
   }
-  // ---- heights (leaves 0) and level schedules
-  P.height.assign(ns, 0);
-  for (int s = 0; s < ns; s++)  // children precede parents (postorder)
-    if (P.parent[s] >= 0) P.height[P.parent[s]] = std::max(P.height[P.parent[s]], P.height[s] + 1);
+  P.dg_order.clear();
+  for (int pass = 0; pass < 2; pass++)
+    for (int j = 0; j < n; j++)
+      if ((P.height[snode[j]] > 0) == (pass == 1)) P.dg_order.push_back(j);
+  P.dg_split = 0;
+  for (int j = 0; j < n; j++) P.dg_split += P.height[snode[j]] == 0;
+  // ---- level schedules
   const int nl = ns ? *std::max_element(P.height.begin(), P.height.end()) + 1 : 0;
   std::vector<std::vector<int>> bylevel(nl);
   for (int s = 0; s < ns; s++) bylevel[P.height[s]].push_back(s);
@@ -420,6 +433,24 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.trsm_tasks.clear();
   P.syrk_tasks.clear();
   P.sdiag_tasks.clear();
+  P.zero_tasks.clear();
+  P.zero_split = 0;
+  for (int qq = 0; qq < 2 * P.ns; qq++) {   // lower triangles in pieces of ~32k doubles, leaf level first
+    const int q = qq % P.ns;
+    if (qq == P.ns) P.zero_split = (int)P.zero_tasks.size();
+    if ((P.height[q] > 0) != (qq >= P.ns)) continue;
+    const int m = P.m[q];
+    int j0 = 0;
+    long long acc = 0;
+    for (int j = 0; j < m; j++) {
+      acc += m - j;
+      if (acc >= 32768 || j == m - 1) {
+        P.zero_tasks.push_back(make_int4(q, j0, j + 1, 0));
+        j0 = j + 1;
+        acc = 0;
+      }
+    }
+  }
   P.potrf_list.clear();
   P.bwd_tasks.clear();
   P.bwd_pref.clear();

@@ -1,0 +1,74 @@
+// Host-only statistics of the supernodal plan for an edge list (int32 pairs):
+// per level the fronts, panel steps and extend-add volume.
+//   hipcc -O2 -std=c++17 -I include scripts/plan_stats.cpp graphslam_amd/csrc/pgo_symbolic.cpp -o /tmp/plan_stats
+//   /tmp/plan_stats edges.bin n
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../graphslam_amd/csrc/pgo_chol.h"
+
+int main(int argc, char** argv) {
+  if (argc < 3) return 2;
+  FILE* f = fopen(argv[1], "rb");
+  if (!f) return 1;
+  const int n = atoi(argv[2]);
+  std::vector<int> e;
+  int buf[2];
+  while (fread(buf, 4, 2, f) == 2) {
+    e.push_back(buf[0]);
+    e.push_back(buf[1]);
+  }
+  fclose(f);
+  const int ne = (int)e.size() / 2;
+  std::vector<int> row_ptr(n + 1, 0);
+  for (int q = 0; q < ne; q++) {
+    row_ptr[e[2 * q] + 1]++;
+    row_ptr[e[2 * q + 1] + 1]++;
+  }
+  for (int i = 0; i < n; i++) row_ptr[i + 1] += row_ptr[i];
+  std::vector<int> fill(row_ptr.begin(), row_ptr.end() - 1), col(row_ptr[n]);
+  for (int q = 0; q < ne; q++) {
+    col[fill[e[2 * q]]++] = e[2 * q + 1];
+    col[fill[e[2 * q + 1]]++] = e[2 * q];
+  }
+  pgo::CholPlan P;
+  pgo::chol_analyze(P, n, row_ptr, col);
+  double tri = 0, ftot = 0;
+  for (int s = 0; s < P.ns; s++) {
+    tri += 0.5 * P.m[s] * (P.m[s] + 1.0);
+    ftot += (double)P.m[s] * P.m[s];
+  }
+  printf("fronts %d, F %.0fM doubles, lower triangles %.0fM, flops %.3g, syrk_flops %.3g\n", P.ns, ftot / 1e6, tri / 1e6,
+         P.flops, P.syrk_flops);
+  double inv = 0, uel = 0;
+  for (int s2 = 0; s2 < P.ns; s2++)
+    if (P.parent[s2] >= 0) {
+      inv += P.m[P.parent[s2]];
+      const double u = P.m[s2] - P.w[s2];
+      uel += 0.5 * u * (u + 1);
+    }
+  printf("inverse maps %.1fM ints, update-matrix elements %.1fM\n", inv / 1e6, uel / 1e6);
+  int li = 0;
+  for (const auto& lv : P.levels) {
+    int nsmall = 0;
+    for (const auto& sc : lv.small) nsmall += sc.cnt;
+    double ea = 0;   // update matrices extended into this level (lower triangles, doubles)
+    for (size_t r = 0; r < lv.ea_off.size(); r++)
+      for (int q = 0; q < lv.ea_cnt[r]; q++) {
+        const int ch = P.ea_children[lv.ea_off[r] + q];
+        const double u = P.m[ch] - P.w[ch];
+        ea += 0.5 * u * (u + 1);
+      }
+    int nfused = 0, ntr = 0, nsy = 0, npotrf = 0;
+    for (const auto& ps : lv.panels) {
+      nfused += ps.fused;
+      ntr += ps.trsm_cnt;
+      nsy += ps.syrk_cnt;
+      npotrf += ps.potrf_cnt;
+    }
+    printf("level %2d: fronts %6d (small %6d) maxm %5d ranks %zu ea %6.1fM dbl, steps %3zu (fused %3d) potrf %5d trsm %6d syrk %7d\n",
+           li++, lv.front_cnt, nsmall, lv.maxm, lv.ea_off.size(), ea / 1e6, lv.panels.size(), nfused, npotrf, ntr, nsy);
+  }
+  return 0;
+}

@@ -7,9 +7,9 @@ import sys
 
 rows = list(csv.DictReader(gzip.open(sys.argv[1], "rt")))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("k_asm_offdiag")]
+idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("k_perm_in")]
 k = int(sys.argv[2]) if len(sys.argv) > 2 else len(idx) // 2
-w = rows[idx[k] - 2:idx[k + 1] - 2]
+w = rows[idx[k]:idx[k + 1]]
 t0 = int(w[0]["Start_Timestamp"])
 S = lambda r: (int(r["Start_Timestamp"]) - t0) / 1e3
 E = lambda r: (int(r["End_Timestamp"]) - t0) / 1e3
