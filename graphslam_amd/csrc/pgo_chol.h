@@ -27,6 +27,7 @@ constexpr int kNB = 64;            // panel width of the blocked path
 constexpr int kTile = 64;          // Schur-update output tile
 constexpr int kBigTile = 128;      // Schur-update output tile of the LDS-pipelined kernel
 constexpr int kKB = 256;
+constexpr int kEaPiece = 4096;   // update-matrix elements per extend-add workgroup
 constexpr int kBwdRows = 512;      // rows per partial product of the backward solve           // Schur-update depth: trailing matrix updated once per kKB columns
 
 struct PanelStep {                 // one panel of the blocked path, all big fronts of a level
@@ -52,8 +53,7 @@ struct SmallClass {                // small fronts of one level with m <= mmax
 struct CholLevel {
   std::vector<SmallClass> small;   // fronts in small_list, by size class
   std::vector<PanelStep> panels;   // blocked path
-  std::vector<int> ea_off, ea_cnt; // per child rank: children in ea_children (their parents are in this level)
-  std::vector<int> ea_cols_off;    // per child rank: offset into ea_colpref
+  std::vector<int> ea_off, ea_cnt; // per child rank: tasks in ea_tasks (children whose parents are in this level)
   int front_off, front_cnt;        // all fronts of the level in level_fronts (solves)
   int small_maxm = 0, maxm = 0;    // LDS sizing
   int maxblk = 0;                  // max 64-column blocks of a front's pivot columns
@@ -91,8 +91,8 @@ struct CholPlan {
   std::vector<int2> bwd_pref;      // per bwd task: first partial, partial count (init tasks)
   std::vector<int4> bwd_part_tasks;  // (front, c0, r0, partial slot)
   int npart = 0;
-  std::vector<int> ea_children;    // child front ids grouped per (level, rank)
-  std::vector<long long> ea_colpref; // per group: prefix of update-matrix columns (3*below rows)
+  std::vector<int4> ea_tasks;      // (child, first, end): pieces of a child's update-matrix lower triangle
+                                   // (column-major element order), grouped per (level, child rank)
   double flops = 0, nnzl = 0, syrk_flops = 0;
   long long ftotal = 0, ttotal = 0;
   int vtotal = 0;
@@ -118,8 +118,7 @@ struct CholPlan {
   int4 *d_bwd = nullptr, *d_bwd_part = nullptr;
   int2* d_bwd_pref = nullptr;
   double* d_partial = nullptr;
-  int* d_ea_children = nullptr;
-  long long* d_ea_colpref = nullptr;
+  int4* d_ea_tasks = nullptr;
   int* d_flag = nullptr;           // non-positive pivot seen
   double* d_lambda = nullptr;      // damping read by the assembly (graph-replay friendly)
 };

@@ -102,39 +102,55 @@ __global__ __launch_bounds__(256) void k_asm_diag(CholDev c, const double* __res
 }
 
 // ------------------------------------------------------------ extend-add
-// One wave per update-matrix column of one child; lanes walk the column's
-// lower part and add into the parent's front.
-__global__ __launch_bounds__(256) void k_extend_add(CholDev c, const int* __restrict__ kids,
-                                                   const long long* __restrict__ colpref, int cnt) {
-  const long long gw = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (gw >= colpref[cnt]) return;
-  int lo = 0, hi = cnt;  // largest q with colpref[q] <= gw
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (colpref[mid] <= gw) lo = mid; else hi = mid;
-  }
-  const int ch = kids[lo];
-  const int b = (int)(gw - colpref[lo]);
+// A piece of a child's update-matrix lower triangle (elements [e0, e1) in
+// column-major order) added into the parent front, 16 elements per thread,
+// loads first.  One launch per child rank: a parent receives from one child
+// per launch (no atomics, fixed order, bitwise reproducible).
+__device__ __forceinline__ int tri_col(long long e, int u) {   // column b of element e: b*u - b(b-1)/2 <= e
+  const double q = 2.0 * u + 1.0;
+  int b = (int)((q - sqrt(fmax(q * q - 8.0 * (double)e, 0.0))) * 0.5);
+  b = max(0, min(b, u - 1));
+  while (b > 0 && (long long)b * u - (long long)b * (b - 1) / 2 > e) b--;
+  while (b + 1 < u && (long long)(b + 1) * u - (long long)(b + 1) * b / 2 <= e) b++;
+  return b;
+}
+__global__ __launch_bounds__(256) void k_extend_add(CholDev c, const int4* __restrict__ tasks) {
+  const int4 t = tasks[blockIdx.x];
+  const int ch = t.x;
   const int mc = c.m[ch], wc = c.w[ch], u = mc - wc;
   const int p = c.parent[ch];
   const int mp = c.m[p];
   const int* __restrict__ rel = c.ea_rel + c.ea_ptr[ch];
-  const double* __restrict__ U = c.F + c.foff[ch] + wc + (size_t)(wc + b) * mc;
-  double* __restrict__ Fp = c.F + c.foff[p] + (size_t)(3 * rel[b / 3] + b % 3) * mp;
-  // 4 rows in flight per lane: loads first, then the scattered adds
-  int a = b + lane;
-  for (; a + 192 < u; a += 256) {
-    const double u0 = U[a], u1 = U[a + 64], u2 = U[a + 128], u3 = U[a + 192];
-    const int p0 = 3 * rel[a / 3] + a % 3, p1 = 3 * rel[(a + 64) / 3] + (a + 64) % 3;
-    const int p2 = 3 * rel[(a + 128) / 3] + (a + 128) % 3, p3 = 3 * rel[(a + 192) / 3] + (a + 192) % 3;
-    const double f0 = Fp[p0], f1 = Fp[p1], f2 = Fp[p2], f3 = Fp[p3];
-    Fp[p0] = f0 + u0;
-    Fp[p1] = f1 + u1;
-    Fp[p2] = f2 + u2;
-    Fp[p3] = f3 + u3;
+  const double* __restrict__ U = c.F + c.foff[ch] + wc + (size_t)wc * mc;
+  double* __restrict__ Fp = c.F + c.foff[p];
+  constexpr int R = kEaPiece / 256;
+  const int e0 = t.y + threadIdx.x, e1 = t.z;
+  // element e0 + 256 q: walk the columns from the first one
+  int b = e0 < e1 ? tri_col(e0, u) : 0;
+  long long cs = (long long)b * u - (long long)b * (b - 1) / 2;   // first element of column b
+  int src[R], dst[R];
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const int e = e0 + 256 * q;
+    src[q] = -1;
+    if (e < e1) {
+      while (e - cs >= u - b) {   // next column
+        cs += u - b;
+        b++;
+      }
+      const int a = b + (int)(e - cs);
+      src[q] = a + b * mc;
+      dst[q] = (3 * rel[a / 3] + a % 3) + (3 * rel[b / 3] + b % 3) * mp;
+    }
   }
-  for (; a < u; a += 64) Fp[3 * rel[a / 3] + a % 3] += U[a];
+  double v[R], f[R];
+#pragma unroll
+  for (int q = 0; q < R; q++) v[q] = src[q] >= 0 ? U[src[q]] : 0.0;
+#pragma unroll
+  for (int q = 0; q < R; q++) f[q] = src[q] >= 0 ? Fp[dst[q]] : 0.0;
+#pragma unroll
+  for (int q = 0; q < R; q++)
+    if (src[q] >= 0) Fp[dst[q]] = f[q] + v[q];
 }
 
 // ------------------------------------------------------------ triangular inverse
@@ -1400,10 +1416,9 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(hipMemsetAsync(P.F, 0, std::max<long long>(P.ftotal, 1) * sizeof(double), s));   // upper triangles stay zero
   CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
   CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
-  CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));
+  CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));   // (a non-default priority measured 1.5x slower)
   for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  CH_TRY(up(&P.d_ea_children, P.ea_children, s));
-  CH_TRY(up(&P.d_ea_colpref, P.ea_colpref, s));
+  CH_TRY(up(&P.d_ea_tasks, P.ea_tasks, s));
   return hipStreamSynchronize(s);
 }
 
@@ -1411,7 +1426,7 @@ void chol_free(CholPlan& P) {
   void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
                   P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
                   P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
-                  P.d_trsm, P.d_syrk, P.d_ea_children, P.d_ea_colpref, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_zero, P.d_dg_order};
+                  P.d_trsm, P.d_syrk, P.d_ea_tasks, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_zero, P.d_dg_order};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : P.evs)
@@ -1447,13 +1462,8 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
   for (size_t li = 0; li < P.levels.size(); li++) {
     const CholLevel& lv = P.levels[li];
     if (li == 1 && fork_rest) CH_TRY(hipStreamWaitEvent(s, P.evs[5], 0));
-    for (size_t r = 0; r < lv.ea_off.size(); r++) {
-      const long long cols = P.ea_colpref[lv.ea_cols_off[r] + lv.ea_cnt[r]];
-      if (!cols) continue;
-      const long long blocks = (cols * 64 + 255) / 256;
-      k_extend_add<<<(unsigned)blocks, 256, 0, s>>>(c, P.d_ea_children + lv.ea_off[r],
-                                                    P.d_ea_colpref + lv.ea_cols_off[r], lv.ea_cnt[r]);
-    }
+    for (size_t r = 0; r < lv.ea_off.size(); r++)
+      if (lv.ea_cnt[r]) k_extend_add<<<lv.ea_cnt[r], 256, 0, s>>>(c, P.d_ea_tasks + lv.ea_off[r]);
     k_vec_assemble<<<lv.front_cnt, 256, (size_t)lv.maxm * sizeof(double), s>>>(c, P.d_level_fronts + lv.front_off);
     // small fronts on the second side stream, beside the blocked path of the
     // same level (disjoint fronts); joined before the next level

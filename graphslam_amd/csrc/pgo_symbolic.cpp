@@ -456,8 +456,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.bwd_pref.clear();
   P.bwd_part_tasks.clear();
   P.npart = 0;
-  P.ea_children.clear();
-  P.ea_colpref.clear();
+  P.ea_tasks.clear();
   for (int L = 0; L < nl; L++) {
     CholLevel& lv = P.levels[L];
     lv.front_off = (int)P.level_fronts.size();
@@ -507,20 +506,14 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     int maxc = 0;
     for (int s : bylevel[L]) maxc = std::max(maxc, P.cptr[s + 1] - P.cptr[s]);
     for (int r = 0; r < maxc; r++) {
-      lv.ea_off.push_back((int)P.ea_children.size());
-      lv.ea_cols_off.push_back((int)P.ea_colpref.size());
-      long long cols = 0;
-      int cnt = 0;
+      lv.ea_off.push_back((int)P.ea_tasks.size());
       for (int s : bylevel[L]) {
         if (P.cptr[s] + r >= P.cptr[s + 1]) continue;
         const int c = P.children[P.cptr[s] + r];
-        P.ea_children.push_back(c);
-        P.ea_colpref.push_back(cols);
-        cols += P.m[c] - P.w[c];
-        cnt++;
+        const int u = P.m[c] - P.w[c], tri = u * (u + 1) / 2;
+        for (int e0 = 0; e0 < tri; e0 += kEaPiece) P.ea_tasks.push_back(make_int4(c, e0, std::min(e0 + kEaPiece, tri), 0));
       }
-      P.ea_colpref.push_back(cols);
-      lv.ea_cnt.push_back(cnt);
+      lv.ea_cnt.push_back((int)P.ea_tasks.size() - lv.ea_off.back());
     }
     // small fronts (m <= kSmallFront): with w <= kWaveW one wavefront each (the
     // m x w panel in LDS, the rank-w Schur update streamed), largest first;

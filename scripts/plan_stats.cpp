@@ -56,9 +56,8 @@ int main(int argc, char** argv) {
     double ea = 0;   // update matrices extended into this level (lower triangles, doubles)
     for (size_t r = 0; r < lv.ea_off.size(); r++)
       for (int q = 0; q < lv.ea_cnt[r]; q++) {
-        const int ch = P.ea_children[lv.ea_off[r] + q];
-        const double u = P.m[ch] - P.w[ch];
-        ea += 0.5 * u * (u + 1);
+        const int4 t = P.ea_tasks[lv.ea_off[r] + q];
+        ea += t.z - t.y;
       }
     int nfused = 0, ntr = 0, nsy = 0, npotrf = 0;
     for (const auto& ps : lv.panels) {
