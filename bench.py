@@ -8,11 +8,16 @@ after its HIP stream has drained (it reads the final error back), so the host
 clock brackets all device work.
 
 value = linearisations ("GN iterations": linearise + solve(s) + retract + chi^2)
-summed over all ranks / max-over-ranks wall time of the K timed steps.
+of the job (replicas: summed over ranks) / max-over-ranks wall time of the K
+timed steps.
 
-Multi-GPU: the path runs as independent replicas (one process per GPU, each
-optimising its own copy of the graph; no data-path collective) -> "weak"
-scaling.  The RCCL-sharded solve is future work.
+Multi-GPU (--gpus N, one process per GPU via torch.distributed.run): the
+default is the speculative lambda search: every rank holds the
+graph, the ranks solve consecutive lambda tries of GTSAM's sequence at once and
+exchange the outcomes and the accepted values over RCCL (xGMI).  One job,
+bitwise the one-GPU trajectory -> value = that job's linearisations / wall
+time, "strong" scaling.  --multi replicas runs N independent copies instead
+("weak").
 
     python bench.py [--gpus N --steps K --warmup W --config C3 --no-cpu-baseline]
 """
@@ -82,6 +87,10 @@ def main():
                     help="eager launches instead of the captured factor+solve hipGraph (rocprofv3 runs)")
     ap.add_argument("--marginals", type=int, default=64,
                     help="after the timed steps: time marginal covariances of this many poses (0: skip)")
+    ap.add_argument("--multi", choices=["spec", "replicas"], default="spec",
+                    help="N>1: speculative lambda search over RCCL (one job) or independent replicas")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a one-GPU box: every rank on device 0, host (gloo) transport")
     ap.add_argument("--max-outer", type=int, default=0,
                     help="profiling runs only: stop each optimize after this many linearisations")
     args = ap.parse_args()
@@ -93,7 +102,15 @@ def main():
     r = init_from_env()
     world, rank = r.world, r.rank
     g = datasets.make(args.config)
-    pg = PoseGraph.from_dataset(g, device=r.local_rank)
+    pg = PoseGraph.from_dataset(g, device=0 if args.same_device else r.local_rank)
+    spec = world > 1 and args.multi == "spec"
+    hc = None
+    if spec:
+        from graphslam_amd import multi_gpu
+        if args.same_device:
+            hc = multi_gpu.attach_host(pg, r.dist, rank, world)
+        else:
+            multi_gpu.attach_rccl(pg, r.dist, rank, world)
     pg.save_values()                     # upload graph + values once; snapshot the initial values
     params = default_params(profile_every=args.profile_every, max_outer=args.max_outer,
                             linear_solver=1 if args.solver == "cholesky" else 0,
@@ -105,6 +122,8 @@ def main():
         return st["linearizations"], st
 
     elapsed, lin_total, results = timed_steps(r, step, args.steps, args.warmup)
+    if spec:   # one job: every rank walked the same linearisations
+        lin_total /= world
     marg = None
     if args.marginals > 0 and rank == 0:
         import numpy as np
@@ -168,14 +187,15 @@ def main():
             "ms_per_step": 1e3 * elapsed / args.steps,
             "ms_to_convergence": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if spec else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {
                 "workload": f"{args.config}: {n} poses / {ne} between factors + 1 prior, Manhattan walk "
                             f"(seed {g.meta.get('seed')}), GTSAM-default LM from dead-reckoned values",
-                "poses": n, "edges": ne, "parallelism": f"replicas{world}",
+                "poses": n, "edges": ne, "parallelism": (f"spec-lambda{world}" + ("-host" if args.same_device else "-rccl")) if spec
+                else f"replicas{world}",
                 "solver": ("GPU supernodal multifrontal Cholesky (AMD ordering, fp64 MFMA Schur updates)"
                            if args.solver == "cholesky" else
                            "block-Jacobi PCG, rel tol %.0e" % params.pcg_relative_tol),
@@ -185,6 +205,7 @@ def main():
                 "accepted": last["iterations"], "pcg_iterations": last["pcg_iterations"],
                 "initial_error": last["initial_error"], "final_error": last["final_error"],
                 "ms_linearize": last["ms_linearize"], "ms_solve": last["ms_solve"], "ms_update": last["ms_update"],
+                "lambda_rounds": last["lambda_rounds"], "solves_rank0": last["solves"], "ms_comm": last["ms_comm"],
             },
             "roofline": roofline,
             "linearize_kernel": {
@@ -199,7 +220,10 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(g, args.cpu_outer)
         print(json.dumps(out))
+    if spec:
+        pg.comm_free()
     pg.close()
+    del hc
     r.close()
 
 

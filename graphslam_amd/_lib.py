@@ -25,6 +25,7 @@ PGO_E_HIP = -7
 PGO_E_NO_DEVICE = -8
 PGO_E_NOMEM = -9
 PGO_E_BAD_EDGE = -10
+PGO_E_COMM = -11
 PGO_W_MAXITER = 1
 PGO_ALG_LM = 0
 PGO_ALG_GN = 1
@@ -56,10 +57,21 @@ class PgoStats(C.Structure):
                 ("kernel_linearize_ms", C.c_double), ("kernel_linearize_count", C.c_longlong),
                 ("kernel_syrk_ms", C.c_double), ("kernel_syrk_count", C.c_longlong),
                 ("syrk_flops", C.c_double), ("factor_flops", C.c_double),
-                ("kernel_syrk_launches", C.c_longlong)]
+                ("kernel_syrk_launches", C.c_longlong), ("lambda_rounds", C.c_int), ("ranks", C.c_int),
+                ("solves", C.c_longlong), ("ms_comm", C.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
+BROADCAST_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int)
+
+
+class PgoHostComm(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("rank", C.c_int), ("size", C.c_int),
+                ("allgather", ALLGATHER_FN), ("broadcast", BROADCAST_FN)]
+
 
 
 def build():
@@ -112,12 +124,18 @@ def lib():
         "pgo_debug_plan": (C.c_int, [vp, dp, C.c_int]),
         "pgo_marginal_covariances": (C.c_int, [vp, C.c_size_t, C.POINTER(C.c_uint64), dp]),
         "pgo_debug_fronts": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int]),
+        "pgo_comm_unique_id": (C.c_int, [vp, C.c_size_t]),
+        "pgo_comm_init_rccl": (C.c_int, [vp, vp, C.c_size_t, C.c_int, C.c_int]),
+        "pgo_comm_init_host": (C.c_int, [vp, C.POINTER(PgoHostComm)]),
+        "pgo_comm_free": (C.c_int, [vp]),
+        "pgo_comm_rank": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        "pgo_comm_selftest": (C.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.pgo_abi_version() != 2:
+    if L.pgo_abi_version() != 3:
         raise RuntimeError("libpgo.so ABI version mismatch")
     _lib = L
     return L

@@ -19,6 +19,7 @@
 
 #include "pgo.h"
 #include "pgo_chol.h"
+#include "pgo_comm.h"
 #include "pgo_device.h"
 
 using pgo::DevGraph;
@@ -59,6 +60,8 @@ struct pgo_graph {
   long long factorizations = 0;
   hipGraphExec_t chol_exec = nullptr;       // captured factor + solve (static per structure)
   double* h_lam = nullptr;                  // pinned lambda staging
+  // ---- multi-GPU speculative lambda search (pgo_comm_*) ----
+  pgo::Comm comm;
 };
 
 namespace {
@@ -610,6 +613,7 @@ const char* pgo_status_string(int s) {
     case PGO_E_NO_DEVICE: return "no HIP device";
     case PGO_E_NOMEM: return "out of memory";
     case PGO_E_BAD_EDGE: return "between factor connects a key to itself";
+    case PGO_E_COMM: return "inter-rank exchange failed";
     case PGO_W_MAXITER: return "stopped at max_iterations";
     default: return "unknown status";
   }
@@ -647,6 +651,8 @@ pgo_graph* pgo_create(const pgo_opts* opts) {
 
 void pgo_destroy(pgo_graph* g) {
   if (!g) return;
+  if (g->comm.nccl || g->comm.d_gather) (void)hipSetDevice(g->device);
+  pgo::comm_free(&g->comm);
   if (g->hip_ready) {
     (void)hipSetDevice(g->device);
     (void)hipStreamSynchronize(g->d.stream);
@@ -867,91 +873,154 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   // linearisation writes only the blocks the assembly reads
   if (p.linear_solver != PGO_SOLVER_PCG && d.n > 0) RC_TRY(ensure_chol(g));
   d.write_all = p.linear_solver == PGO_SOLVER_PCG ? 1 : 0;
+  // One lambda try (GTSAM tryLambda): solve (H + lam I) delta = -g, retract into
+  // pose_cand, error there and the linear model decrease; one read-back.
+  // out = {solved, new error, delta'H delta, g'delta}.
+  bool first_try = true;
+  auto run_try = [&](double lam_try, double* out) -> int {
+    SolveState ss;
+    HIP_TRY(g, hipEventRecord(ev[2], d.stream));
+    RC_TRY(linear_solve(g, p, lam_try, &st, &ss));
+    st.solves++;
+    HIP_TRY(g, hipEventRecord(ev[3], d.stream));
+    if (!ss.known || ss.solved) {
+      if (p.algorithm != PGO_ALG_GN) HIP_TRY(g, pgo::launch_model_decrease(d, d.x, d.scal + 1));
+      HIP_TRY(g, pgo::launch_retract(d, d.x));
+      HIP_TRY(g, pgo::launch_error(d, d.pose_cand, d.scal));
+    }
+    HIP_TRY(g, hipEventRecord(ev[4], d.stream));
+    RC_TRY(sync_scalars(g, 3));
+    RC_TRY(finish_solve(g, &st, &ss));
+    if (first_try) {
+      const double lin_ms = ms_between(ev[0], ev[1]);
+      st.ms_linearize += lin_ms;
+      if (p.profile_every > 0) {
+        st.kernel_linearize_ms += lin_ms;
+        st.kernel_linearize_count++;
+      }
+      first_try = false;
+    }
+    st.ms_solve += ms_between(ev[2], ev[3]);
+    st.ms_update += ms_between(ev[3], ev[4]);
+    out[0] = ss.solved ? 1.0 : 0.0;
+    out[1] = g->h_scal[0];
+    out[2] = g->h_scal[1];
+    out[3] = g->h_scal[2];
+    return PGO_OK;
+  };
+  pgo::Comm& cm = g->comm;
+  const int P = cm.size, me = cm.rank;
+  st.ranks = P;
+  std::vector<double> lam_k(P), fac_k(P), outs(4 * P);
+  std::vector<char> valid(P);
   if (!(err <= p.error_tol) && iters < p.max_iterations && d.n > 0) {
     double new_err = err;
     for (;;) {
       const double cur_err = new_err;
       HIP_TRY(g, pgo::launch_linearize(d, ev[0], ev[1]));
       st.linearizations++;
-      bool first_try = true;
-      for (;;) {  // tryLambda (GN: one plain step)
-        const double lam_try = p.algorithm == PGO_ALG_GN ? 0.0 : lam;
-        SolveState ss;
-        HIP_TRY(g, hipEventRecord(ev[2], d.stream));
-        RC_TRY(linear_solve(g, p, lam_try, &st, &ss));
-        HIP_TRY(g, hipEventRecord(ev[3], d.stream));
-        const bool run_update = !ss.known || ss.solved;
-        if (run_update) {
-          // linear model decrease = -(g'delta + 0.5 delta'H delta) (LM only), retract,
-          // new error: one read-back for every scalar of this try
-          if (p.algorithm != PGO_ALG_GN) HIP_TRY(g, pgo::launch_model_decrease(d, d.x, d.scal + 1));
-          HIP_TRY(g, pgo::launch_retract(d, d.x));
-          HIP_TRY(g, pgo::launch_error(d, d.pose_cand, d.scal));
-        }
-        HIP_TRY(g, hipEventRecord(ev[4], d.stream));
-        RC_TRY(sync_scalars(g, 3));
-        RC_TRY(finish_solve(g, &st, &ss));
-        if (first_try) {
-          const double lin_ms = ms_between(ev[0], ev[1]);
-          st.ms_linearize += lin_ms;
-          if (p.profile_every > 0) {
-            st.kernel_linearize_ms += lin_ms;
-            st.kernel_linearize_count++;
-          }
-          first_try = false;
-        }
-        st.ms_solve += ms_between(ev[2], ev[3]);
-        st.ms_update += ms_between(ev[3], ev[4]);
-        const bool solved = ss.solved;
-        if (p.algorithm == PGO_ALG_GN) {
-          if (!solved) {
-            status = PGO_E_INDETERMINANT;
-            break;
-          }
-          std::swap(d.pose, d.pose_cand);
-          err = g->h_scal[0];
-          iters++;
-          inner++;
+      first_try = true;
+      if (p.algorithm == PGO_ALG_GN) {  // one plain step; every rank computes the same one
+        double o[4];
+        RC_TRY(run_try(0.0, o));
+        if (o[0] == 0.0) {
+          status = PGO_E_INDETERMINANT;
           break;
         }
-        double fidelity = 0.0, new_e = INFINITY;
-        bool success = false, stop = false;
-        if (solved) {
-          const double xhx = g->h_scal[1], gx = g->h_scal[2];
-          const double lin_change = -(gx + 0.5 * xhx);
-          if (lin_change >= 0) {
-            new_e = g->h_scal[0];
-            const double cost_change = err - new_e;
-            if (lin_change > 2.220446049250313e-16 * err) {
-              fidelity = cost_change / lin_change;
-              success = fidelity > p.min_model_fidelity;
-            }
-            if (std::fabs(cost_change) < p.relative_error_tol * err) stop = true;
+        std::swap(d.pose, d.pose_cand);
+        err = o[1];
+        iters++;
+        inner++;
+      } else {
+        // Lambda rounds.  GTSAM tries lam_0 = lam, lam_{k+1} = lam_k * f_k (f_k
+        // doubling when the factor is not fixed) until one is accepted, the cost
+        // change is negligible, or lam_{k+1} reaches the upper bound.  Rank r
+        // solves try r of the round; the outcomes are walked in sequence order
+        // with GTSAM's rules, so the accepted step is the sequential one.
+        for (;;) {
+          lam_k[0] = lam;
+          fac_k[0] = factor;
+          valid[0] = 1;
+          for (int k = 1; k < P; k++) {
+            lam_k[k] = lam_k[k - 1] * fac_k[k - 1];
+            fac_k[k] = p.use_fixed_lambda_factor ? fac_k[k - 1] : 2.0 * fac_k[k - 1];
+            valid[k] = valid[k - 1] && lam_k[k] < p.lambda_upper_bound;
           }
-        }
-        if (success) {  // decreaseLambda
-          if (p.use_fixed_lambda_factor) {
-            lam /= p.lambda_factor;
+          double mine[4] = {-1.0, 0.0, 0.0, 0.0};  // -1: no try (past the bound)
+          if (valid[me]) RC_TRY(run_try(lam_k[me], mine));
+          st.lambda_rounds++;
+          if (P > 1) {
+            const auto c0 = std::chrono::steady_clock::now();
+            std::string why;
+            const int rc = pgo::comm_allgather(&cm, mine, 4, outs.data(), d.stream, &why);
+            if (rc != PGO_OK) return fail(g, rc, "lambda round all-gather: " + why);
+            st.ms_comm += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
           } else {
-            const double q = 2.0 * fidelity - 1.0;
-            lam *= std::max(1.0 / 3.0, 1.0 - q * q * q);
-            factor *= 2.0;
+            std::copy(mine, mine + 4, outs.begin());
           }
-          lam = std::max(p.lambda_lower_bound, lam);
-          std::swap(d.pose, d.pose_cand);
-          err = new_e;
-          iters++;
-          inner++;
-          break;
+          int winner = -1;
+          bool done = false;
+          double new_e = INFINITY;
+          for (int k = 0; k < P && valid[k]; k++) {
+            const double* o = &outs[4 * k];
+            double fidelity = 0.0;
+            bool success = false, stop = false;
+            if (o[0] == 1.0) {
+              const double xhx = o[2], gx = o[3];
+              const double lin_change = -(gx + 0.5 * xhx);
+              if (lin_change >= 0) {
+                new_e = o[1];
+                const double cost_change = err - new_e;
+                if (lin_change > 2.220446049250313e-16 * err) {
+                  fidelity = cost_change / lin_change;
+                  success = fidelity > p.min_model_fidelity;
+                }
+                if (std::fabs(cost_change) < p.relative_error_tol * err) stop = true;
+              }
+            }
+            lam = lam_k[k];
+            factor = fac_k[k];
+            if (success) {  // decreaseLambda
+              if (p.use_fixed_lambda_factor) {
+                lam /= p.lambda_factor;
+              } else {
+                const double q = 2.0 * fidelity - 1.0;
+                lam *= std::max(1.0 / 3.0, 1.0 - q * q * q);
+                factor *= 2.0;
+              }
+              lam = std::max(p.lambda_lower_bound, lam);
+              winner = k;
+              done = true;
+              break;
+            }
+            if (stop) {
+              done = true;
+              break;
+            }
+            lam *= factor;  // increaseLambda
+            inner++;
+            if (!p.use_fixed_lambda_factor) factor *= 2.0;
+            if (lam >= p.lambda_upper_bound) {
+              done = true;
+              break;
+            }
+          }
+          if (winner >= 0) {
+            if (P > 1) {  // the accepted candidate values live on rank `winner`
+              const auto c0 = std::chrono::steady_clock::now();
+              std::string why;
+              const int rc = pgo::comm_broadcast_device(&cm, d.pose_cand, sizeof(double4) * (size_t)d.n, winner,
+                                                        d.stream, &why);
+              if (rc != PGO_OK) return fail(g, rc, "accepted values broadcast: " + why);
+              st.ms_comm += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
+            }
+            std::swap(d.pose, d.pose_cand);
+            err = new_e;
+            iters++;
+            inner++;
+          }
+          if (done) break;
         }
-        if (!stop) {  // increaseLambda
-          lam *= factor;
-          inner++;
-          if (!p.use_fixed_lambda_factor) factor *= 2.0;
-          if (lam >= p.lambda_upper_bound) break;
-          continue;
-        }
-        break;
       }
       if (status != PGO_OK) break;
       new_err = err;
@@ -969,6 +1038,80 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   if (stats) *stats = st;
   if (status < 0) return fail(g, status, pgo_status_string(status));
   return status;
+}
+
+int pgo_comm_unique_id(void* out, size_t cap) {
+  std::string why;
+  return pgo::comm_unique_id(out, cap, &why);
+}
+
+int pgo_comm_init_rccl(pgo_graph* g, const void* unique_id, size_t id_bytes, int rank, int size) {
+  if (!g) return PGO_E_ARG;
+  RC_TRY(ensure_hip(g));
+  HIP_TRY(g, hipSetDevice(g->device));
+  std::string why;
+  const int rc = pgo::comm_init_rccl(&g->comm, unique_id, id_bytes, rank, size, &why);
+  return rc == PGO_OK ? rc : fail(g, rc, why);
+}
+
+int pgo_comm_init_host(pgo_graph* g, const pgo_host_comm* comm) {
+  if (!g) return PGO_E_ARG;
+  if (g->comm.nccl) (void)hipSetDevice(g->device);
+  std::string why;
+  const int rc = pgo::comm_init_host(&g->comm, comm, &why);
+  return rc == PGO_OK ? rc : fail(g, rc, why);
+}
+
+int pgo_comm_free(pgo_graph* g) {
+  if (!g) return PGO_E_ARG;
+  if (g->comm.nccl) (void)hipSetDevice(g->device);
+  pgo::comm_free(&g->comm);
+  return PGO_OK;
+}
+
+int pgo_comm_rank(const pgo_graph* g, int* rank, int* size) {
+  if (!g || !rank || !size) return PGO_E_ARG;
+  *rank = g->comm.rank;
+  *size = g->comm.size;
+  return PGO_OK;
+}
+
+int pgo_comm_selftest(pgo_graph* g) {
+  if (!g) return PGO_E_ARG;
+  pgo::Comm& c = g->comm;
+  hipStream_t s = nullptr;
+  if (!c.host) {
+    RC_TRY(ensure_hip(g));
+    HIP_TRY(g, hipSetDevice(g->device));
+    s = g->d.stream;
+  }
+  const double mine[4] = {(double)c.rank, (double)c.size, (double)c.rank * c.rank, 1.0};
+  std::vector<double> all(4 * (size_t)c.size);
+  std::string why;
+  int rc = pgo::comm_allgather(&c, mine, 4, all.data(), s, &why);
+  if (rc != PGO_OK) return fail(g, rc, why);
+  for (int r = 0; r < c.size; r++)
+    if (all[4 * r] != r || all[4 * r + 1] != c.size || all[4 * r + 2] != (double)r * r || all[4 * r + 3] != 1.0)
+      return fail(g, PGO_E_COMM, "all-gather returned wrong data for rank " + std::to_string(r));
+  // broadcast from the last rank: 1000 doubles root * 1e6 + i
+  const int root = c.size - 1, nb = 1000;
+  std::vector<double> h(nb);
+  for (int i = 0; i < nb; i++) h[i] = c.rank == root ? root * 1e6 + i : -1.0;
+  if (c.host) {  // host transport: exercise the callback directly on host memory
+    if (c.hc.broadcast(c.hc.ctx, h.data(), sizeof(double) * nb, root) != 0)
+      return fail(g, PGO_E_COMM, "host broadcast callback failed");
+  } else {
+    double* dbuf = nullptr;
+    HIP_TRY(g, hipMalloc((void**)&dbuf, sizeof(double) * nb));
+    HIP_TRY(g, hipMemcpy(dbuf, h.data(), sizeof(double) * nb, hipMemcpyHostToDevice));
+    rc = pgo::comm_broadcast_device(&c, dbuf, sizeof(double) * nb, root, s, &why);
+    if (rc == PGO_OK) (void)hipMemcpy(h.data(), dbuf, sizeof(double) * nb, hipMemcpyDeviceToHost);
+    (void)hipFree(dbuf);
+    if (rc != PGO_OK) return fail(g, rc, why);
+  }
+  for (int i = 0; i < nb; i++)
+    if (h[i] != root * 1e6 + i) return fail(g, PGO_E_COMM, "broadcast returned wrong data");
+  return PGO_OK;
 }
 
 int pgo_debug_fronts(pgo_graph* g, int* w, int* m, int* level, int cap) {

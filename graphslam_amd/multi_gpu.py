@@ -1,0 +1,77 @@
+"""Multi-GPU speculative lambda search: attach a communicator to a PoseGraph.
+
+One process per GPU, every rank holding the same graph (include/pgo.h,
+"multi-GPU").  The library does the exchange itself; this module only sets the
+communicator up:
+
+* ``attach_rccl`` -- rank 0 makes an RCCL unique id (``pgo_comm_unique_id``),
+  the id's 128 bytes travel over the caller's torch.distributed group (gloo,
+  host), every rank calls ``pgo_comm_init_rccl`` on its own device.  The
+  per-round all-gather and the accepted-values broadcast then run as RCCL
+  collectives on the library's HIP stream, over xGMI.
+* ``HostComm`` / ``attach_host`` -- the same exchange through host callbacks on
+  a torch.distributed gloo group (tests: two ranks sharing one GPU, where RCCL
+  refuses duplicate devices, or CPU-only self tests).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+def unique_id() -> bytes:
+    buf = C.create_string_buffer(256)
+    n = L.lib().pgo_comm_unique_id(buf, 256)
+    if n < 0:
+        raise RuntimeError(f"pgo_comm_unique_id failed ({n}): RCCL not loadable")
+    return buf.raw[:n]
+
+
+def attach_rccl(pg, dist, rank: int, world: int):
+    """RCCL communicator over all `world` ranks of the default torch.distributed group."""
+    obj = [unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(obj, src=0)
+    pg.comm_init_rccl(obj[0], rank, world)
+
+
+class HostComm:
+    """pgo_host_comm over a torch.distributed (gloo) group, host buffers."""
+
+    def __init__(self, dist, rank: int, world: int, group=None):
+        import torch
+        self._torch, self._dist, self._group = torch, dist, group
+        self.rank, self.world = rank, world
+        self._ag = L.ALLGATHER_FN(self._allgather)
+        self._bc = L.BROADCAST_FN(self._broadcast)
+        self.struct = L.PgoHostComm(None, rank, world, self._ag, self._bc)
+
+    def _view(self, ptr, n):
+        return self._torch.from_numpy(np.ctypeslib.as_array((C.c_uint8 * n).from_address(ptr)))
+
+    def _allgather(self, ctx, src, dst, n):
+        try:
+            t = self._view(src, n).clone()
+            outs = [self._torch.empty(n, dtype=self._torch.uint8) for _ in range(self.world)]
+            self._dist.all_gather(outs, t, group=self._group)
+            flat = self._torch.cat(outs).numpy()      # keep alive across the copy
+            C.memmove(dst, flat.ctypes.data, n * self.world)
+            return 0
+        except Exception:  # noqa: BLE001 -- no exception may cross the C-ABI
+            return 1
+
+    def _broadcast(self, ctx, buf, n, root):
+        try:
+            self._dist.broadcast(self._view(buf, n), src=root, group=self._group)
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
+
+
+def attach_host(pg, dist, rank: int, world: int, group=None) -> HostComm:
+    hc = HostComm(dist, rank, world, group)
+    pg.comm_init_host(hc.struct)
+    return hc

@@ -191,6 +191,28 @@ class PoseGraph:
         return e.value
 
     # ------------------------------------------------------------ diagnostics
+    # ------------------------------------------------- multi-GPU (pgo_comm_*)
+    def comm_init_rccl(self, unique_id: bytes, rank: int, size: int):
+        """ncclCommInitRank on this handle's device (collective over all ranks)."""
+        buf = C.create_string_buffer(bytes(unique_id), len(unique_id))
+        self._check(self._L.pgo_comm_init_rccl(self._h, buf, len(unique_id), rank, size))
+
+    def comm_init_host(self, comm: L.PgoHostComm):
+        """The caller's own host transport (callbacks must outlive the handle's use)."""
+        self._comm_keepalive = comm
+        self._check(self._L.pgo_comm_init_host(self._h, C.byref(comm)))
+
+    def comm_free(self):
+        self._check(self._L.pgo_comm_free(self._h))
+
+    def comm_rank(self):
+        r, n = C.c_int(), C.c_int()
+        self._check(self._L.pgo_comm_rank(self._h, C.byref(r), C.byref(n)))
+        return r.value, n.value
+
+    def comm_selftest(self):
+        self._check(self._L.pgo_comm_selftest(self._h))
+
     def debug_linearize(self, num_edges):
         n = self.num_vertices
         hd = np.zeros((n, 3, 3))

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PGO_ABI_VERSION 2
+#define PGO_ABI_VERSION 3
 
 /* ---- status codes (GTSAM exception each one replaces) -------------------- */
 #define PGO_OK 0
@@ -48,6 +48,7 @@ extern "C" {
 #define PGO_E_NO_DEVICE (-8)     /* no usable MI355X / HIP device                   */
 #define PGO_E_NOMEM (-9)
 #define PGO_E_BAD_EDGE (-10)     /* between factor with key1 == key2                */
+#define PGO_E_COMM (-11)         /* inter-rank exchange failed (RCCL / host callback) */
 #define PGO_W_MAXITER 1          /* informational: stopped at max_iterations        */
 
 /* ---- algorithms / solvers ------------------------------------------------ */
@@ -114,6 +115,12 @@ typedef struct {
   double factor_flops;          /* flops of one numeric factorisation              */
   long long kernel_syrk_launches; /* timed Schur-update launches (all profiled
                                    factorisations)                                  */
+  /* multi-GPU speculative lambda search (pgo_comm_*; zero / 1 on one rank) */
+  int lambda_rounds;            /* lambda rounds: one parallel try on every rank    */
+  int ranks;                    /* ranks that took part                             */
+  long long solves;             /* linear solves this rank performed (incl. the
+                                   speculative tries GTSAM's sequence never reached) */
+  double ms_comm;               /* wall time in the all-gathers and broadcasts      */
 } pgo_stats;
 
 /* ---- lifetime ------------------------------------------------------------ */
@@ -165,6 +172,42 @@ int pgo_error(pgo_graph *g, double *err);
    damping).  out: n x 9 doubles, row-major.  A singular H (a component without
    prior) returns PGO_E_INDETERMINANT, as GTSAM's Cholesky throws. */
 int pgo_marginal_covariances(pgo_graph *g, size_t n, const uint64_t *keys, double *out);
+
+/* ---- multi-GPU: speculative lambda search ---------------------
+   One process per GPU, every rank holding the same graph and values.  Where
+   GTSAM's LM (graph.cpp:119) tries lambda, lambda*f, lambda*f^2, ... one after
+   another until a try is accepted, the ranks of a communicator solve the next
+   `size` tries of that sequence at once (rank r: the r-th), all-gather the
+   outcomes (error, model decrease), apply GTSAM's accept rule in sequence order
+   and take the first accepted candidate from the rank that computed it
+   (broadcast of N poses).  Accepted steps, lambdas and values are bitwise those
+   of the one-GPU run; the wall time of a linearisation drops from its number of
+   lambda tries to ceil(tries / size) factorisations.
+   Transports: RCCL over xGMI (pgo_comm_init_rccl; rank 0 makes the id with
+   pgo_comm_unique_id and the caller distributes its bytes), or the caller's
+   own host transport (pgo_comm_init_host).  Every rank must call pgo_optimize
+   with the same params. */
+typedef struct {
+  void *ctx;
+  int rank, size;
+  /* out[size * bytes] = every rank's in[bytes], rank order; 0 on success */
+  int (*allgather)(void *ctx, const void *in, void *out, size_t bytes);
+  /* buf[bytes] of rank `root` to every rank, in place; 0 on success */
+  int (*broadcast)(void *ctx, void *buf, size_t bytes, int root);
+} pgo_host_comm;
+
+/* ncclGetUniqueId; returns the id size in bytes (128) or < 0 */
+int pgo_comm_unique_id(void *out, size_t cap);
+/* ncclCommInitRank on the handle's device (collective: all ranks call it) */
+int pgo_comm_init_rccl(pgo_graph *g, const void *unique_id, size_t id_bytes, int rank, int size);
+int pgo_comm_init_host(pgo_graph *g, const pgo_host_comm *comm);
+int pgo_comm_free(pgo_graph *g);
+/* rank / size of the handle's communicator (0 / 1 without one) */
+int pgo_comm_rank(const pgo_graph *g, int *rank, int *size);
+/* exchange check (no solve): all-gather of (rank, size, rank^2, 1) and a
+   broadcast from rank size-1; PGO_OK when every rank saw the right data.  The
+   host transport needs no GPU. */
+int pgo_comm_selftest(pgo_graph *g);
 
 /* ---- diagnostics (parity tests; device results at the current values) ---- */
 /* H diagonal blocks (9 doubles row-major per vertex, insertion order), the

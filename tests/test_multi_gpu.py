@@ -1,0 +1,175 @@
+"""Multi-rank speculative lambda search (include/pgo.h "multi-GPU").
+
+CPU (gloo, world size 2): the host transport's all-gather / broadcast through
+the C-ABI (pgo_comm_selftest needs no GPU with host callbacks).
+
+GPU: two and three ranks sharing cuda:0 (RCCL refuses two ranks on one
+device, so these ranks exchange through the host transport over gloo; the
+library's round logic is the same for both transports) must reproduce the
+one-rank run bitwise -- same accepted steps, same lambda tries, same final
+values -- while solving the tries of a round in parallel.  A one-rank RCCL
+communicator checks the RCCL transport's calls on the box.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.multiprocessing as mp  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _init(rank, world, port):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def _selftest_worker(rank, world, port, q):
+    try:
+        dist = _init(rank, world, port)
+        from graphslam_amd import multi_gpu
+        from graphslam_amd.pose_graph import PoseGraph
+        pg = PoseGraph(device=0)
+        hc = multi_gpu.attach_host(pg, dist, rank, world)
+        pg.comm_selftest()
+        q.put((rank, pg.comm_rank(), None))
+        del hc
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+def _run(world, target, args, timeout=300):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(k, world, port, q) + args) for k in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=timeout) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(out, key=lambda o: o[0])
+
+
+def test_host_comm_selftest_gloo_world2():
+    out = _run(2, _selftest_worker, ())
+    for rank, rs, err in out:
+        assert err is None, err
+        assert rs == (rank, 2)
+
+
+# ---------------------------------------------------------------- GPU
+def perturbed_c2():
+    """C2 with heavy heading noise on the initial values: GTSAM's LM rejects
+    up to 12 lambda tries in a row on it (oracle trace)."""
+    from graphslam_amd import datasets
+    g = datasets.make("C2")
+    init = np.array(g.initial, copy=True)
+    init[:, 2] += np.random.default_rng(7).normal(0, 0.5, len(init))
+    return g, init
+
+
+def _graph(case):
+    from graphslam_amd import datasets
+    if case == "C2p":
+        return perturbed_c2()
+    g = datasets.make(case)
+    return g, np.array(g.initial, copy=True)
+
+
+def _opt_worker(rank, world, port, q, case, kw):
+    try:
+        dist = _init(rank, world, port)
+        from graphslam_amd import multi_gpu
+        from graphslam_amd.pose_graph import PoseGraph
+        g, init = _graph(case)
+        pg = PoseGraph.from_dataset(g, device=0)
+        pg.set_poses(init)
+        hc = multi_gpu.attach_host(pg, dist, rank, world)
+        st = pg.optimize(**kw)
+        q.put((rank, st, pg.poses(), None))
+        del hc
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, None, repr(e)))
+
+
+def _single(case, kw):
+    from graphslam_amd.pose_graph import PoseGraph
+    g, init = _graph(case)
+    pg = PoseGraph.from_dataset(g, device=0)
+    pg.set_poses(init)
+    st = pg.optimize(**kw)
+    return st, pg.poses()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,world,kw", [
+    ("C2p", 2, {}),
+    ("C2p", 3, {}),
+    ("C2p", 2, {"use_fixed_lambda_factor": 0}),
+    ("C3", 2, {}),
+    ("C3", 4, {}),
+])
+def test_speculative_lambda_matches_one_rank(case, world, kw):
+    st1, x1 = _single(case, kw)
+    out = _run(world, _opt_worker, (case, kw), timeout=600)
+    for rank, st, x, err in out:
+        assert err is None, err
+        assert st["ranks"] == world
+        for k in ("iterations", "inner_iterations", "linearizations", "status"):
+            assert st[k] == st1[k], (k, st[k], st1[k])
+        assert st["final_error"] == st1["final_error"]
+        np.testing.assert_array_equal(x, x1)          # bitwise: the same accepted candidates
+        # a round solves `world` tries at once: fewer rounds than sequential tries
+        if st1["inner_iterations"] > st1["linearizations"]:
+            assert st["lambda_rounds"] < st1["lambda_rounds"]
+    assert st1["ranks"] == 1 and st1["solves"] == st1["lambda_rounds"] >= st1["inner_iterations"]
+
+
+@pytest.mark.gpu
+def test_speculative_lambda_oracle_trajectory():
+    """The 2-rank run on the perturbed C2 graph follows the C oracle's LM
+    trajectory (iterations, lambda tries, final error)."""
+    from oracle.oracle import Oracle
+    g, init = perturbed_c2()
+    ref = Oracle(g).optimize(init=init)
+    out = _run(2, _opt_worker, ("C2p", {}), timeout=600)
+    st = out[0][1]
+    assert st["iterations"] == ref.stats["iterations"]
+    assert st["inner_iterations"] == ref.stats["inner_iterations"]
+    assert abs(st["final_error"] - ref.stats["final_error"]) <= 1e-8 * ref.stats["final_error"]
+
+
+@pytest.mark.gpu
+def test_rccl_one_rank_communicator():
+    """RCCL transport on the box: a one-rank communicator (the only RCCL
+    communicator one GPU allows) loads librccl, passes the exchange self test
+    and leaves the optimisation unchanged."""
+    from graphslam_amd import multi_gpu
+    from graphslam_amd.pose_graph import PoseGraph
+    g, init = perturbed_c2()
+    pg = PoseGraph.from_dataset(g, device=0)
+    pg.set_poses(init)
+    pg.comm_init_rccl(multi_gpu.unique_id(), 0, 1)
+    assert pg.comm_rank() == (0, 1)
+    pg.comm_selftest()
+    st = pg.optimize()
+    st1, x1 = _single("C2p", {})
+    assert st["inner_iterations"] == st1["inner_iterations"]
+    np.testing.assert_array_equal(pg.poses(), x1)
+    pg.comm_free()
