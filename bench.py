@@ -87,6 +87,8 @@ def main():
                     help="eager launches instead of the captured factor+solve hipGraph (rocprofv3 runs)")
     ap.add_argument("--marginals", type=int, default=64,
                     help="after the timed steps: time marginal covariances of this many poses (0: skip)")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="lambda tries solved concurrently per GPU (pgo_params.lambda_lanes)")
     ap.add_argument("--multi", choices=["spec", "replicas"], default="spec",
                     help="N>1: speculative lambda search over RCCL (one job) or independent replicas")
     ap.add_argument("--same-device", action="store_true",
@@ -114,7 +116,7 @@ def main():
     pg.save_values()                     # upload graph + values once; snapshot the initial values
     params = default_params(profile_every=args.profile_every, max_outer=args.max_outer,
                             linear_solver=1 if args.solver == "cholesky" else 0,
-                            use_graphs=0 if args.no_graphs else 1)
+                            use_graphs=0 if args.no_graphs else 1, lambda_lanes=args.lanes)
 
     def step():
         pg.restore_values()
@@ -196,6 +198,7 @@ def main():
                             f"(seed {g.meta.get('seed')}), GTSAM-default LM from dead-reckoned values",
                 "poses": n, "edges": ne, "parallelism": (f"spec-lambda{world}" + ("-host" if args.same_device else "-rccl")) if spec
                 else f"replicas{world}",
+                "lambda_lanes": args.lanes,
                 "solver": ("GPU supernodal multifrontal Cholesky (AMD ordering, fp64 MFMA Schur updates)"
                            if args.solver == "cholesky" else
                            "block-Jacobi PCG, rel tol %.0e" % params.pcg_relative_tol),

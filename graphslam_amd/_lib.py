@@ -45,7 +45,7 @@ class PgoParams(C.Structure):
                 ("min_model_fidelity", C.c_double), ("use_fixed_lambda_factor", C.c_int),
                 ("algorithm", C.c_int), ("linear_solver", C.c_int), ("pcg_relative_tol", C.c_double),
                 ("pcg_max_iterations", C.c_int), ("pcg_check_interval", C.c_int), ("max_outer", C.c_int),
-                ("profile_every", C.c_int), ("use_graphs", C.c_int)]
+                ("profile_every", C.c_int), ("use_graphs", C.c_int), ("lambda_lanes", C.c_int)]
 
 
 class PgoStats(C.Structure):

@@ -24,6 +24,22 @@
 
 using pgo::DevGraph;
 
+// An extra concurrent lambda try on the handle's GPU (lanes 1..L-1; lane 0 is
+// the handle's own stream and buffers): its own factor workspace (a clone of
+// the Cholesky plan's numeric buffers), solution, candidate values, scalars,
+// stream and captured factor+solve graph.  The linearisation (D, V, g) and the
+// current values are shared read-only.
+struct Lane {
+  pgo::CholPlan plan;
+  double* x = nullptr;
+  double4* pose_cand = nullptr;
+  double* part = nullptr;
+  double* scal = nullptr;
+  hipStream_t stream = nullptr;
+  hipGraphExec_t exec = nullptr;
+  double* h_buf = nullptr;                  // pinned: [0..2] scalars, [3] flag, [4] lambda
+};
+
 struct pgo_graph {
   int device = 0;
   std::string last_error;
@@ -62,6 +78,9 @@ struct pgo_graph {
   double* h_lam = nullptr;                  // pinned lambda staging
   // ---- multi-GPU speculative lambda search (pgo_comm_*) ----
   pgo::Comm comm;
+  std::vector<Lane> lanes;                  // lanes 1..L-1 (speculative tries on this GPU)
+  hipEvent_t lin_done = nullptr;            // linearisation complete (lanes wait on it)
+  int lane_cap = 8;                         // 1 after a lane allocation failed (reset per plan)
 };
 
 namespace {
@@ -115,7 +134,23 @@ int information(const double* q, double* om6) {
   return PGO_OK;
 }
 
+void free_lanes(pgo_graph* g) {
+  for (Lane& ln : g->lanes) {
+    if (ln.stream) (void)hipStreamSynchronize(ln.stream);
+    if (ln.exec) (void)hipGraphExecDestroy(ln.exec);
+    pgo::chol_free_clone(ln.plan);
+    void* ptrs[] = {ln.x, ln.pose_cand, ln.part, ln.scal};
+    for (void* q : ptrs)
+      if (q) (void)hipFree(q);
+    if (ln.stream) (void)hipStreamDestroy(ln.stream);
+    if (ln.h_buf) (void)hipHostFree(ln.h_buf);
+  }
+  g->lanes.clear();
+}
+
 void free_device(pgo_graph* g) {
+  free_lanes(g);
+  g->lane_cap = 8;
   DevGraph& d = g->d;
   void* ptrs[] = {d.eij, d.ez, d.eom, d.prior_ptr, d.prior_vtx, d.pz, d.pom, d.row_ptr, d.slot_edge, d.slot_col, d.V,
                   d.D, d.g, d.pose, d.pose_cand, d.pose_saved, d.x, d.r, d.z, d.p, d.q, d.Minv, d.part, d.scal, d.ctrl};
@@ -145,6 +180,7 @@ int ensure_hip(pgo_graph* g) {
   HIP_TRY(g, hipHostMalloc((void**)&g->h_lam, sizeof(double), hipHostMallocDefault));
   for (auto& e : g->ev) HIP_TRY(g, hipEventCreate(&e));
   for (auto& e : g->pev) HIP_TRY(g, hipEventCreate(&e));
+  HIP_TRY(g, hipEventCreateWithFlags(&g->lin_done, hipEventDisableTiming));
   g->sev.resize(2 * 512);
   g->sev_flops.resize(512);
   for (auto& e : g->sev) HIP_TRY(g, hipEventCreate(&e));
@@ -580,6 +616,95 @@ int finish_solve(pgo_graph* g, pgo_stats* st, SolveState* ss) {
   return PGO_OK;
 }
 
+// Lanes 1..want-1 over the current Cholesky plan; returns the lane count
+// available (fewer when HBM runs out: each lane holds a full factor workspace).
+int ensure_lanes(pgo_graph* g, int want) {
+  want = std::max(1, std::min({want, 8, g->lane_cap}));
+  if ((int)g->lanes.size() == want - 1) return want;
+  free_lanes(g);
+  const DevGraph& d = g->d;
+  for (int l = 1; l < want; l++) {
+    g->lanes.emplace_back();
+    Lane& ln = g->lanes.back();
+    bool ok = pgo::chol_clone(g->chol, ln.plan, d.stream) == hipSuccess &&
+              hipMalloc((void**)&ln.x, sizeof(double) * 3 * std::max(d.n, 1)) == hipSuccess &&
+              hipMalloc((void**)&ln.pose_cand, sizeof(double4) * std::max(d.n, 1)) == hipSuccess &&
+              hipMalloc((void**)&ln.part, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices) == hipSuccess &&
+              hipMalloc((void**)&ln.scal, sizeof(double) * 16) == hipSuccess &&
+              hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking) == hipSuccess &&
+              hipHostMalloc((void**)&ln.h_buf, 8 * sizeof(double), hipHostMallocDefault) == hipSuccess;
+    if (ok) ok = hipMemsetAsync(ln.part, 0, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices, ln.stream) ==
+                 hipSuccess && hipStreamSynchronize(ln.stream) == hipSuccess;
+    if (!ok) {  // out of memory (or similar): one lane, and do not try again for this plan
+      (void)hipGetLastError();
+      free_lanes(g);
+      g->lane_cap = 1;
+      return 1;
+    }
+  }
+  return (int)g->lanes.size() + 1;
+}
+
+// The device view of lane l (lane 0: the handle's own)
+DevGraph lane_view(const pgo_graph* g, int l) {
+  DevGraph v = g->d;
+  if (l == 0) return v;
+  const Lane& ln = g->lanes[l - 1];
+  v.x = ln.x;
+  v.pose_cand = ln.pose_cand;
+  v.part = ln.part;
+  v.scal = ln.scal;
+  v.stream = ln.stream;
+  return v;
+}
+
+// Enqueue one lambda try on lane l >= 1 (after the linearisation, lin_done):
+// factor + solve (captured graph), model decrease, retract, error; scalars and
+// the pivot flag land in the lane's pinned buffer once its stream drains.
+int enqueue_lane_try(pgo_graph* g, const pgo_params& p, int l, double lam) {
+  Lane& ln = g->lanes[l - 1];
+  const DevGraph v = lane_view(g, l);
+  HIP_TRY(g, hipStreamWaitEvent(ln.stream, g->lin_done, 0));
+  ln.h_buf[4] = lam;
+  HIP_TRY(g, hipMemcpyAsync(ln.plan.d_lambda, ln.h_buf + 4, sizeof(double), hipMemcpyHostToDevice, ln.stream));
+  if (p.use_graphs) {
+    if (!ln.exec) {
+      hipGraph_t graph = nullptr;
+      HIP_TRY(g, hipStreamBeginCapture(ln.stream, hipStreamCaptureModeThreadLocal));
+      const hipError_t e1 = pgo::chol_factor(ln.plan, v.D, v.V, v.g, -1.0, ln.stream, nullptr);
+      const hipError_t e2 = pgo::chol_solve(ln.plan, ln.x, ln.stream);
+      HIP_TRY(g, hipStreamEndCapture(ln.stream, &graph));
+      HIP_TRY(g, e1);
+      HIP_TRY(g, e2);
+      HIP_TRY(g, hipGraphInstantiate(&ln.exec, graph, nullptr, nullptr, 0));
+      HIP_TRY(g, hipGraphDestroy(graph));
+    }
+    HIP_TRY(g, hipGraphLaunch(ln.exec, ln.stream));
+  } else {
+    HIP_TRY(g, pgo::chol_factor(ln.plan, v.D, v.V, v.g, -1.0, ln.stream, nullptr));
+    HIP_TRY(g, pgo::chol_solve(ln.plan, ln.x, ln.stream));
+  }
+  HIP_TRY(g, pgo::launch_model_decrease(v, v.x, v.scal + 1));
+  HIP_TRY(g, pgo::launch_retract(v, v.x));
+  HIP_TRY(g, pgo::launch_error(v, v.pose_cand, v.scal));
+  HIP_TRY(g, hipMemcpyAsync(ln.h_buf, v.scal, 3 * sizeof(double), hipMemcpyDeviceToHost, ln.stream));
+  HIP_TRY(g, hipMemcpyAsync(ln.h_buf + 3, ln.plan.d_flag, sizeof(int), hipMemcpyDeviceToHost, ln.stream));
+  return PGO_OK;
+}
+
+// after enqueue_lane_try: out = {solved, new error, delta'H delta, g'delta}
+int collect_lane_try(pgo_graph* g, int l, double* out) {
+  Lane& ln = g->lanes[l - 1];
+  HIP_TRY(g, hipStreamSynchronize(ln.stream));
+  int flag = 0;
+  std::memcpy(&flag, ln.h_buf + 3, sizeof(int));
+  out[0] = flag == 0 ? 1.0 : 0.0;
+  out[1] = ln.h_buf[0];
+  out[2] = ln.h_buf[1];
+  out[3] = ln.h_buf[2];
+  return PGO_OK;
+}
+
 double ms_between(hipEvent_t a, hipEvent_t b) {
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
@@ -640,6 +765,7 @@ void pgo_default_params(pgo_params* p) {
   p->max_outer = 0;
   p->profile_every = 0;
   p->use_graphs = 1;
+  p->lambda_lanes = 1;
 }
 
 pgo_graph* pgo_create(const pgo_opts* opts) {
@@ -664,6 +790,7 @@ void pgo_destroy(pgo_graph* g) {
     if (g->h_lam) (void)hipHostFree(g->h_lam);
     for (auto& e : g->pev)
       if (e) (void)hipEventDestroy(e);
+    if (g->lin_done) (void)hipEventDestroy(g->lin_done);
     if (g->d.stream) (void)hipStreamDestroy(g->d.stream);
   }
   delete g;
@@ -911,13 +1038,28 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   pgo::Comm& cm = g->comm;
   const int P = cm.size, me = cm.rank;
   st.ranks = P;
-  std::vector<double> lam_k(P), fac_k(P), outs(4 * P);
-  std::vector<char> valid(P);
+  // lanes: concurrent tries on this GPU (Cholesky LM only)
+  int L = 1;
+  if (p.algorithm != PGO_ALG_GN && p.linear_solver != PGO_SOLVER_PCG && p.lambda_lanes > 1 && d.n > 0)
+    L = ensure_lanes(g, p.lambda_lanes);
+  // every rank must agree on the lanes per rank (a lane allocation may fail on one)
+  if (P > 1) {
+    std::vector<double> all(P);
+    const double mineL = L;
+    std::string why;
+    const int rc = pgo::comm_allgather(&cm, &mineL, 1, all.data(), d.stream, &why);
+    if (rc != PGO_OK) return fail(g, rc, "lane count all-gather: " + why);
+    for (double v : all) L = std::min(L, (int)v);
+  }
+  const int T = P * L;                       // tries per round
+  std::vector<double> lam_k(T), fac_k(T), outs(4 * T);
+  std::vector<char> valid(T);
   if (!(err <= p.error_tol) && iters < p.max_iterations && d.n > 0) {
     double new_err = err;
     for (;;) {
       const double cur_err = new_err;
       HIP_TRY(g, pgo::launch_linearize(d, ev[0], ev[1]));
+      HIP_TRY(g, hipEventRecord(g->lin_done, d.stream));
       st.linearizations++;
       first_try = true;
       if (p.algorithm == PGO_ALG_GN) {  // one plain step; every rank computes the same one
@@ -934,34 +1076,53 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
       } else {
         // Lambda rounds.  GTSAM tries lam_0 = lam, lam_{k+1} = lam_k * f_k (f_k
         // doubling when the factor is not fixed) until one is accepted, the cost
-        // change is negligible, or lam_{k+1} reaches the upper bound.  Rank r
-        // solves try r of the round; the outcomes are walked in sequence order
-        // with GTSAM's rules, so the accepted step is the sequential one.
+        // change is negligible, or lam_{k+1} reaches the upper bound.  Try k of a
+        // round runs on rank k / L, lane k % L; the outcomes are walked in
+        // sequence order with GTSAM's rules, so the accepted step is the
+        // sequential one.
         for (;;) {
           lam_k[0] = lam;
           fac_k[0] = factor;
           valid[0] = 1;
-          for (int k = 1; k < P; k++) {
+          for (int k = 1; k < T; k++) {
             lam_k[k] = lam_k[k - 1] * fac_k[k - 1];
             fac_k[k] = p.use_fixed_lambda_factor ? fac_k[k - 1] : 2.0 * fac_k[k - 1];
             valid[k] = valid[k - 1] && lam_k[k] < p.lambda_upper_bound;
           }
-          double mine[4] = {-1.0, 0.0, 0.0, 0.0};  // -1: no try (past the bound)
-          if (valid[me]) RC_TRY(run_try(lam_k[me], mine));
+          // a profiled factorisation (lane 0, eager, timed launches) runs alone
+          const bool prof_next = p.profile_every > 0 && (g->factorizations % p.profile_every) == 0;
+          const int Lr = prof_next ? 1 : L;
+          std::vector<double> mine(4 * L, 0.0);
+          for (int l = 0; l < L; l++) mine[4 * l] = -1.0;  // -1: no try (past the bound / lane idle)
+          for (int l = 1; l < Lr; l++)
+            if (valid[me * L + l]) {
+              RC_TRY(enqueue_lane_try(g, p, l, lam_k[me * L + l]));
+              st.solves++;
+            }
+          if (valid[me * L]) RC_TRY(run_try(lam_k[me * L], &mine[0]));
+          for (int l = 1; l < Lr; l++)
+            if (valid[me * L + l]) RC_TRY(collect_lane_try(g, l, &mine[4 * l]));
           st.lambda_rounds++;
           if (P > 1) {
             const auto c0 = std::chrono::steady_clock::now();
             std::string why;
-            const int rc = pgo::comm_allgather(&cm, mine, 4, outs.data(), d.stream, &why);
+            const int rc = pgo::comm_allgather(&cm, mine.data(), 4 * L, outs.data(), d.stream, &why);
             if (rc != PGO_OK) return fail(g, rc, "lambda round all-gather: " + why);
             st.ms_comm += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
           } else {
-            std::copy(mine, mine + 4, outs.begin());
+            std::copy(mine.begin(), mine.end(), outs.begin());
           }
+          // a lane that sat out a profiled round: its tries count as not made,
+          // the walk stops there and the next round resumes from it
+          for (int k = 0; k < T; k++)
+            if (outs[4 * k] == -1.0) {
+              for (int j = k; j < T; j++) valid[j] = 0;
+              break;
+            }
           int winner = -1;
           bool done = false;
           double new_e = INFINITY;
-          for (int k = 0; k < P && valid[k]; k++) {
+          for (int k = 0; k < T && valid[k]; k++) {
             const double* o = &outs[4 * k];
             double fidelity = 0.0;
             bool success = false, stop = false;
@@ -1006,15 +1167,17 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
             }
           }
           if (winner >= 0) {
-            if (P > 1) {  // the accepted candidate values live on rank `winner`
+            const int wr = winner / L, wl = winner % L;
+            // the accepted candidate values: lane wl's buffer on rank wr
+            double4** cand = wr == me && wl > 0 ? &g->lanes[wl - 1].pose_cand : &d.pose_cand;
+            if (P > 1) {
               const auto c0 = std::chrono::steady_clock::now();
               std::string why;
-              const int rc = pgo::comm_broadcast_device(&cm, d.pose_cand, sizeof(double4) * (size_t)d.n, winner,
-                                                        d.stream, &why);
+              const int rc = pgo::comm_broadcast_device(&cm, *cand, sizeof(double4) * (size_t)d.n, wr, d.stream, &why);
               if (rc != PGO_OK) return fail(g, rc, "accepted values broadcast: " + why);
               st.ms_comm += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
             }
-            std::swap(d.pose, d.pose_cand);
+            std::swap(d.pose, *cand);
             err = new_e;
             iters++;
             inner++;

@@ -133,6 +133,10 @@ void xcd_order(std::vector<int4>& tasks, int tile);
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
 hipError_t chol_upload(CholPlan& P, hipStream_t s);
 void chol_free(CholPlan& P);
+// second numeric workspace over src's symbolic plan (shares src's device index
+// arrays; free with chol_free_clone before src is freed)
+hipError_t chol_clone(const CholPlan& src, CholPlan& dst, hipStream_t s);
+void chol_free_clone(CholPlan& P);
 
 // device: factor H + lambda I (D: 6 doubles/pose upper, V: slot blocks as structure of
 // arrays V[q * nslots + slot], old indexing; only the slots in asm_src are read)

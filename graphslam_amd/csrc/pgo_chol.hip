@@ -1437,6 +1437,43 @@ void chol_free(CholPlan& P) {
   P = CholPlan();
 }
 
+// A second numeric workspace over the same symbolic plan: the host schedules
+// and the device index arrays are shared with src (not owned); the fronts,
+// inverses, frontal vectors, flags, partials, side streams and events are the
+// clone's own, so two factorisations (two lambda tries) can run at once.
+hipError_t chol_clone(const CholPlan& src, CholPlan& P, hipStream_t s) {
+  P = src;
+  P.F = P.Tinv = P.fv = P.xv = P.d_lambda = P.d_partial = nullptr;
+  P.d_flag = nullptr;
+  P.side = P.side2 = P.side3 = nullptr;
+  for (auto& e : P.evs) e = nullptr;
+  CH_TRY(hipMalloc((void**)&P.F, std::max<long long>(P.ftotal, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.Tinv, std::max<long long>(P.ttotal, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.fv, std::max(P.vtotal, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.xv, std::max(3 * P.n, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.d_flag, sizeof(int)));
+  CH_TRY(hipMalloc((void**)&P.d_lambda, sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.d_partial, std::max(P.npart, 1) * 64 * sizeof(double)));
+  CH_TRY(hipMemsetAsync(P.F, 0, std::max<long long>(P.ftotal, 1) * sizeof(double), s));
+  CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
+  CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
+  CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));
+  for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return hipStreamSynchronize(s);
+}
+
+void chol_free_clone(CholPlan& P) {
+  void* ptrs[] = {P.F, P.Tinv, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_partial};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  for (hipEvent_t e : P.evs)
+    if (e) (void)hipEventDestroy(e);
+  if (P.side) (void)hipStreamDestroy(P.side);
+  if (P.side2) (void)hipStreamDestroy(P.side2);
+  if (P.side3) (void)hipStreamDestroy(P.side3);
+  P = CholPlan();
+}
+
 hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
                        hipStream_t s, SyrkProfile* prof) {
   if (P.n == 0) return hipSuccess;

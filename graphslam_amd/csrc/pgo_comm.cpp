@@ -96,7 +96,7 @@ int comm_init_rccl(Comm* c, const void* uid, size_t uid_bytes, int rank, int siz
   const ncclResult_t e = r.init_rank(&comm, size, id, rank);
   if (e != ncclSuccess) return nccl_fail(e, "ncclCommInitRank", err);
   double* buf = nullptr;
-  const hipError_t he = hipMalloc((void**)&buf, sizeof(double) * 4 * (size_t)size);
+  const hipError_t he = hipMalloc((void**)&buf, sizeof(double) * kMaxGather * (size_t)size);
   if (he != hipSuccess) {
     r.destroy(comm);
     return hip_fail(he, "hipMalloc(all-gather buffer)", err);
@@ -141,8 +141,8 @@ int comm_allgather(Comm* c, const double* mine, int count, double* all, hipStrea
     }
     return PGO_OK;
   }
-  if (count > 4) {
-    *err = "all-gather of more than 4 doubles per rank";
+  if (count > kMaxGather) {
+    *err = "all-gather of more than kMaxGather doubles per rank";
     return PGO_E_ARG;
   }
   // in place: rank r's slice of the receive buffer is its send buffer

@@ -18,12 +18,14 @@
 
 namespace pgo {
 
+constexpr int kMaxGather = 64;       // doubles per rank in one all-gather
+
 struct Comm {
   int rank = 0, size = 1;
   bool host = false;                 // host callbacks (else RCCL)
   pgo_host_comm hc{};
   void* nccl = nullptr;              // ncclComm_t
-  double* d_gather = nullptr;        // [4 * size] device all-gather buffer (RCCL)
+  double* d_gather = nullptr;        // [kMaxGather * size] device all-gather buffer (RCCL)
   std::vector<char> stage;           // host staging of device broadcasts (host transport)
 };
 

@@ -108,35 +108,64 @@ def _opt_worker(rank, world, port, q, case, kw):
         q.put((rank, None, None, repr(e)))
 
 
-def _single(case, kw):
+def _single(case, kw, lanes=1):
+    """One rank; lanes=1 is GTSAM's plain sequential lambda search."""
     from graphslam_amd.pose_graph import PoseGraph
     g, init = _graph(case)
     pg = PoseGraph.from_dataset(g, device=0)
     pg.set_poses(init)
-    st = pg.optimize(**kw)
+    st = pg.optimize(**dict(kw, lambda_lanes=lanes))
     return st, pg.poses()
+
+
+def _same(st, x, st1, x1):
+    for k in ("iterations", "inner_iterations", "linearizations", "status"):
+        assert st[k] == st1[k], (k, st[k], st1[k])
+    assert st["final_error"] == st1["final_error"]
+    np.testing.assert_array_equal(x, x1)          # bitwise: the same accepted candidates
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,lanes,kw", [
+    ("C2p", 2, {}),
+    ("C2p", 3, {}),
+    ("C2p", 2, {"use_fixed_lambda_factor": 0}),
+    ("C2p", 3, {"profile_every": 3}),
+    ("C2p", 2, {"use_graphs": 0}),
+    ("C3", 2, {}),
+    ("C3", 4, {}),
+])
+def test_lanes_match_sequential(case, lanes, kw):
+    """Concurrent lambda tries on one GPU (pgo_params.lambda_lanes) reproduce
+    the sequential search bit for bit, in fewer rounds."""
+    st1, x1 = _single(case, kw, lanes=1)
+    st, x = _single(case, kw, lanes=lanes)
+    _same(st, x, st1, x1)
+    if st1["inner_iterations"] > st1["linearizations"]:
+        # profiled factorisations run alone: their rounds need not shrink
+        assert st["lambda_rounds"] <= st1["lambda_rounds"] if kw.get("profile_every") else \
+            st["lambda_rounds"] < st1["lambda_rounds"]
+    assert st["solves"] >= st1["solves"]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case,world,kw", [
-    ("C2p", 2, {}),
-    ("C2p", 3, {}),
+    ("C2p", 2, {"lambda_lanes": 1}),
+    ("C2p", 3, {"lambda_lanes": 1}),
     ("C2p", 2, {"use_fixed_lambda_factor": 0}),
+    ("C2p", 2, {"lambda_lanes": 2, "profile_every": 2}),
     ("C3", 2, {}),
-    ("C3", 4, {}),
+    ("C3", 4, {"lambda_lanes": 1}),
 ])
 def test_speculative_lambda_matches_one_rank(case, world, kw):
-    st1, x1 = _single(case, kw)
+    st1, x1 = _single(case, {k: v for k, v in kw.items() if k != "lambda_lanes"})
     out = _run(world, _opt_worker, (case, kw), timeout=600)
     for rank, st, x, err in out:
         assert err is None, err
         assert st["ranks"] == world
-        for k in ("iterations", "inner_iterations", "linearizations", "status"):
-            assert st[k] == st1[k], (k, st[k], st1[k])
-        assert st["final_error"] == st1["final_error"]
-        np.testing.assert_array_equal(x, x1)          # bitwise: the same accepted candidates
-        # a round solves `world` tries at once: fewer rounds than sequential tries
-        if st1["inner_iterations"] > st1["linearizations"]:
+        _same(st, x, st1, x1)
+        # a round solves `world` x lanes tries at once: fewer rounds than sequential tries
+        if st1["inner_iterations"] > st1["linearizations"] and not kw.get("profile_every"):
             assert st["lambda_rounds"] < st1["lambda_rounds"]
     assert st1["ranks"] == 1 and st1["solves"] == st1["lambda_rounds"] >= st1["inner_iterations"]
 
@@ -168,7 +197,7 @@ def test_rccl_one_rank_communicator():
     pg.comm_init_rccl(multi_gpu.unique_id(), 0, 1)
     assert pg.comm_rank() == (0, 1)
     pg.comm_selftest()
-    st = pg.optimize()
+    st = pg.optimize(lambda_lanes=1)
     st1, x1 = _single("C2p", {})
     assert st["inner_iterations"] == st1["inner_iterations"]
     np.testing.assert_array_equal(pg.poses(), x1)
