@@ -73,6 +73,38 @@ def cpu_baseline(g, max_outer):
     }
 
 
+def closest_keyframe_bench(pg, g, skip=10, reps=20):
+    """closest_keyframe service (graph.cpp:146-178) at the optimum: one query
+    over all keyframes (HBM scan: 16 B of (x, y) per candidate; the values are
+    double4, so the scan touches 32 B) and the batched form with every keyframe
+    as keyframes.back() (N queries, ~N^2/2 distance evaluations, fp64 VALU)."""
+    import numpy as np
+    n = g.num_poses
+    last = pg.poses(np.asarray(g.keys[-1:], dtype=np.uint64))[0]
+    pg.closest_keyframe(last[0], last[1], skip)            # warm
+    scan = []
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        pg.closest_keyframe(last[0], last[1], skip)
+        scan.append(pg.debug_search_ms()[0])
+    wall_ms = 1e3 * (time.perf_counter() - t0) / reps
+    keys = np.asarray(g.keys, dtype=np.uint64)
+    pg.closest_keyframes(keys[:1024], skip)                # warm
+    t0 = time.perf_counter()
+    pg.closest_keyframes(keys, skip)
+    bwall = 1e3 * (time.perf_counter() - t0)
+    bms = pg.debug_search_ms()[1]
+    pairs = sum(max(i + 1 - skip, 0) for i in range(n))
+    scan_ms = float(np.mean(scan))
+    return {
+        "single_query": {"candidates": n - skip, "kernel_ms": scan_ms, "call_ms": wall_ms,
+                         "achieved_gbs": 16.0 * (n - skip) / (scan_ms * 1e-3) / 1e9,
+                         "bytes_per_candidate": 16},
+        "batched": {"queries": n, "pairs": pairs, "kernel_ms": bms, "call_ms": bwall,
+                    "gpairs_per_s": pairs / (bms * 1e-3) / 1e9},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,6 +125,8 @@ def main():
                     help="N>1: speculative lambda search over RCCL (one job) or independent replicas")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a one-GPU box: every rank on device 0, host (gloo) transport")
+    ap.add_argument("--search", type=int, default=1,
+                    help="after the timed steps: time the closest_keyframe search at the optimum (0: skip)")
     ap.add_argument("--max-outer", type=int, default=0,
                     help="profiling runs only: stop each optimize after this many linearisations")
     args = ap.parse_args()
@@ -137,6 +171,9 @@ def main():
         marg = {"keys": int(len(keys)), "ms": 1e3 * dt,
                 "note": "gtsam::Marginals::marginalCovariance per pose at the optimum: one undamped "
                         "factorisation + per-pose path solves (Y'Y, Y = L^-1 E)"}
+    search = None
+    if args.search and rank == 0:
+        search = closest_keyframe_bench(pg, g)
     stats = [s for _, s in results]
     last = stats[-1]
     totals = dict(spmv_ms=sum(s["kernel_spmv_ms"] for s in stats), spmv_n=sum(s["kernel_spmv_count"] for s in stats),
@@ -219,6 +256,7 @@ def main():
             },
             "cpu_baseline": None,
             "marginals": marg,
+            "closest_keyframe": search,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(g, args.cpu_outer)

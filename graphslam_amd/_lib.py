@@ -26,6 +26,8 @@ PGO_E_NO_DEVICE = -8
 PGO_E_NOMEM = -9
 PGO_E_BAD_EDGE = -10
 PGO_E_COMM = -11
+PGO_E_NOT_ENOUGH = -12
+PGO_NO_KEY = (1 << 64) - 1
 PGO_W_MAXITER = 1
 PGO_ALG_LM = 0
 PGO_ALG_GN = 1
@@ -124,6 +126,9 @@ def lib():
         "pgo_debug_plan": (C.c_int, [vp, dp, C.c_int]),
         "pgo_marginal_covariances": (C.c_int, [vp, C.c_size_t, C.POINTER(C.c_uint64), dp]),
         "pgo_debug_fronts": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int]),
+        "pgo_closest_keyframe": (C.c_int, [vp, C.c_double, C.c_double, C.c_int, u64p, dp]),
+        "pgo_closest_keyframes": (C.c_int, [vp, C.c_size_t, u64p, C.c_int, u64p, dp]),
+        "pgo_debug_search_ms": (C.c_int, [vp, dp, dp]),
         "pgo_comm_unique_id": (C.c_int, [vp, C.c_size_t]),
         "pgo_comm_init_rccl": (C.c_int, [vp, vp, C.c_size_t, C.c_int, C.c_int]),
         "pgo_comm_init_host": (C.c_int, [vp, C.POINTER(PgoHostComm)]),

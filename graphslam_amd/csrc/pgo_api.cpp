@@ -20,6 +20,7 @@
 #include "pgo.h"
 #include "pgo_chol.h"
 #include "pgo_comm.h"
+#include "pgo_search.h"
 #include "pgo_device.h"
 
 using pgo::DevGraph;
@@ -81,6 +82,17 @@ struct pgo_graph {
   std::vector<Lane> lanes;                  // lanes 1..L-1 (speculative tries on this GPU)
   hipEvent_t lin_done = nullptr;            // linearisation complete (lanes wait on it)
   int lane_cap = 8;                         // 1 after a lane allocation failed (reset per plan)
+  // ---- closest-keyframe search scratch ----
+  double* s_d = nullptr;                    // [kMaxBlocks + 1] partial / final distances
+  int* s_i = nullptr;                       // [kMaxBlocks + 1] partial / final indices
+  double* sb_d = nullptr;                   // batched: per-query distance, index, query pose index
+  int* sb_i = nullptr;
+  int* sb_q = nullptr;
+  double* sbp_d = nullptr;                  // batched: per (chunk, query) partials
+  int* sbp_i = nullptr;
+  size_t sb_cap = 0, sbp_cap = 0;
+  hipEvent_t sev_scan[2] = {}, sev_batch[2] = {};
+  bool scan_timed = false, batch_timed = false;
 };
 
 namespace {
@@ -705,6 +717,16 @@ int collect_lane_try(pgo_graph* g, int l, double* out) {
   return PGO_OK;
 }
 
+// scratch + timing events of the closest-keyframe search (first use)
+int ensure_search(pgo_graph* g) {
+  if (g->s_d) return PGO_OK;
+  HIP_TRY(g, hipMalloc((void**)&g->s_i, sizeof(int) * (pgo::kMaxBlocks + 1)));
+  for (hipEvent_t* e : {&g->sev_scan[0], &g->sev_scan[1], &g->sev_batch[0], &g->sev_batch[1]})
+    HIP_TRY(g, hipEventCreate(e));
+  HIP_TRY(g, hipMalloc((void**)&g->s_d, sizeof(double) * (pgo::kMaxBlocks + 1)));
+  return PGO_OK;
+}
+
 double ms_between(hipEvent_t a, hipEvent_t b) {
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
@@ -739,6 +761,7 @@ const char* pgo_status_string(int s) {
     case PGO_E_NOMEM: return "out of memory";
     case PGO_E_BAD_EDGE: return "between factor connects a key to itself";
     case PGO_E_COMM: return "inter-rank exchange failed";
+    case PGO_E_NOT_ENOUGH: return "not enough keyframes";
     case PGO_W_MAXITER: return "stopped at max_iterations";
     default: return "unknown status";
   }
@@ -791,6 +814,11 @@ void pgo_destroy(pgo_graph* g) {
     for (auto& e : g->pev)
       if (e) (void)hipEventDestroy(e);
     if (g->lin_done) (void)hipEventDestroy(g->lin_done);
+    void* sp[] = {g->s_d, g->s_i, g->sb_d, g->sb_i, g->sb_q, g->sbp_d, g->sbp_i};
+    for (void* q : sp)
+      if (q) (void)hipFree(q);
+    for (hipEvent_t e : {g->sev_scan[0], g->sev_scan[1], g->sev_batch[0], g->sev_batch[1]})
+      if (e) (void)hipEventDestroy(e);
     if (g->d.stream) (void)hipStreamDestroy(g->d.stream);
   }
   delete g;
@@ -1201,6 +1229,88 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   if (stats) *stats = st;
   if (status < 0) return fail(g, status, pgo_status_string(status));
   return status;
+}
+
+int pgo_closest_keyframe(pgo_graph* g, double x, double y, int skip, uint64_t* key, double* dist) {
+  if (!g || !key || !dist || skip < 0 || !std::isfinite(x) || !std::isfinite(y)) return PGO_E_ARG;
+  const size_t n = g->keys.size();
+  if (n <= (size_t)skip)
+    return fail(g, PGO_E_NOT_ENOUGH, "closest_keyframe: not enough keyframes (" + std::to_string(n) + " <= skip " +
+                                         std::to_string(skip) + ")");
+  RC_TRY(ensure_device(g));
+  HIP_TRY(g, hipSetDevice(g->device));
+  const DevGraph& d = g->d;
+  RC_TRY(ensure_search(g));
+  const int limit = (int)(n - skip);
+  HIP_TRY(g, pgo::launch_closest_scan(d.pose, limit, x, y, g->s_d, g->s_i, g->s_d + pgo::kMaxBlocks,
+                                      g->s_i + pgo::kMaxBlocks, d.stream, g->sev_scan[0], g->sev_scan[1]));
+  g->scan_timed = true;
+  HIP_TRY(g, hipMemcpyAsync(g->h_scal, g->s_d + pgo::kMaxBlocks, sizeof(double), hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(g, hipMemcpyAsync(g->h_ctrl, g->s_i + pgo::kMaxBlocks, sizeof(int), hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(g, hipStreamSynchronize(d.stream));
+  const int idx = g->h_ctrl[0];
+  if (idx < 0 || idx >= limit) return fail(g, PGO_E_NONFINITE, "closest_keyframe: no finite distance");
+  *key = g->keys[idx];
+  *dist = g->h_scal[0];
+  return PGO_OK;
+}
+
+int pgo_closest_keyframes(pgo_graph* g, size_t q, const uint64_t* query_keys, int skip, uint64_t* keys_out,
+                          double* dist_out) {
+  if (!g || skip < 0 || (q && (!query_keys || !keys_out || !dist_out)) || q > (size_t)INT32_MAX) return PGO_E_ARG;
+  if (q == 0) return PGO_OK;
+  // queries sorted by vertex index: a workgroup's candidate ranges are then alike
+  std::vector<std::pair<int, int>> order(q);
+  for (size_t k = 0; k < q; k++) {
+    auto it = g->index.find(query_keys[k]);
+    if (it == g->index.end()) return fail(g, PGO_E_NO_KEY, "closest_keyframes: key " + std::to_string(query_keys[k]) + " has no value");
+    order[k] = {it->second, (int)k};
+  }
+  std::stable_sort(order.begin(), order.end());
+  std::vector<int> qv(q);
+  for (size_t k = 0; k < q; k++) qv[k] = order[k].first;
+  RC_TRY(ensure_device(g));
+  HIP_TRY(g, hipSetDevice(g->device));
+  const DevGraph& d = g->d;
+  RC_TRY(ensure_search(g));
+  const int max_limit = std::max(qv.back() + 1 - skip, 0);
+  const size_t parts = q * (size_t)pgo::closest_batch_chunks(max_limit);
+  if (g->sb_cap < q || g->sbp_cap < parts) {
+    for (void* p : {(void*)g->sb_d, (void*)g->sb_i, (void*)g->sb_q, (void*)g->sbp_d, (void*)g->sbp_i})
+      if (p) (void)hipFree(p);
+    g->sb_d = g->sbp_d = nullptr;
+    g->sb_i = g->sb_q = g->sbp_i = nullptr;
+    g->sb_cap = g->sbp_cap = 0;
+    HIP_TRY(g, hipMalloc((void**)&g->sb_d, sizeof(double) * q));
+    HIP_TRY(g, hipMalloc((void**)&g->sb_i, sizeof(int) * q));
+    HIP_TRY(g, hipMalloc((void**)&g->sb_q, sizeof(int) * q));
+    HIP_TRY(g, hipMalloc((void**)&g->sbp_d, sizeof(double) * parts));
+    HIP_TRY(g, hipMalloc((void**)&g->sbp_i, sizeof(int) * parts));
+    g->sb_cap = q;
+    g->sbp_cap = parts;
+  }
+  HIP_TRY(g, hipMemcpyAsync(g->sb_q, qv.data(), sizeof(int) * q, hipMemcpyHostToDevice, d.stream));
+  HIP_TRY(g, pgo::launch_closest_batch(d.pose, g->sb_q, (int)q, skip, max_limit, g->sbp_d, g->sbp_i, g->sb_d,
+                                       g->sb_i, d.stream, g->sev_batch[0], g->sev_batch[1]));
+  g->batch_timed = true;
+  std::vector<double> hd(q);
+  std::vector<int> hi(q);
+  HIP_TRY(g, hipMemcpyAsync(hd.data(), g->sb_d, sizeof(double) * q, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(g, hipMemcpyAsync(hi.data(), g->sb_i, sizeof(int) * q, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(g, hipStreamSynchronize(d.stream));
+  for (size_t k = 0; k < q; k++) {
+    const int o = order[k].second;
+    keys_out[o] = hi[k] >= 0 ? g->keys[hi[k]] : PGO_NO_KEY;
+    dist_out[o] = hi[k] >= 0 ? hd[k] : INFINITY;
+  }
+  return PGO_OK;
+}
+
+int pgo_debug_search_ms(pgo_graph* g, double* scan_ms, double* batch_ms) {
+  if (!g || !scan_ms || !batch_ms) return PGO_E_ARG;
+  *scan_ms = g->scan_timed ? ms_between(g->sev_scan[0], g->sev_scan[1]) : 0.0;
+  *batch_ms = g->batch_timed ? ms_between(g->sev_batch[0], g->sev_batch[1]) : 0.0;
+  return PGO_OK;
 }
 
 int pgo_comm_unique_id(void* out, size_t cap) {

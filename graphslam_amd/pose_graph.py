@@ -35,12 +35,19 @@ class BadCovariance(PgoError, ValueError):
     """Covariance is not symmetric positive definite (GTSAM's LLT would fail)."""
 
 
+class NotEnoughKeyframes(PgoError):
+    """closest_keyframe service returning false (graph.cpp:170-171)."""
+
+
 _EXC = {
     L.PGO_E_DUP_KEY: ValuesKeyAlreadyExists,
     L.PGO_E_NO_KEY: ValuesKeyDoesNotExist,
     L.PGO_E_INDETERMINANT: IndeterminantLinearSystemException,
     L.PGO_E_BAD_COV: BadCovariance,
+    L.PGO_E_NOT_ENOUGH: NotEnoughKeyframes,
 }
+
+KEYFRAMES_TO_SKIP_IN_LOOP_CLOSING = 10   # graph.cpp:15
 
 
 def default_params(**kw) -> L.PgoParams:
@@ -191,6 +198,31 @@ class PoseGraph:
         return e.value
 
     # ------------------------------------------------------------ diagnostics
+    # ------------------------------------------------- loop-closure search
+    def closest_keyframe(self, x, y, skip=KEYFRAMES_TO_SKIP_IN_LOOP_CLOSING):
+        """closest_keyframe service (graph.cpp:146-178): (key, distance) of the
+        vertex nearest to (x, y) among all but the last `skip` inserted."""
+        key, dist = C.c_uint64(), C.c_double()
+        self._check(self._L.pgo_closest_keyframe(self._h, float(x), float(y), int(skip), C.byref(key),
+                                                 C.byref(dist)))
+        return key.value, dist.value
+
+    def closest_keyframes(self, query_keys, skip=KEYFRAMES_TO_SKIP_IN_LOOP_CLOSING):
+        """Batched service: for each query key, the answer when it was the last
+        keyframe (candidates inserted before it, minus skip - 1).  Keys with no
+        candidate get PGO_NO_KEY and +inf."""
+        q = np.ascontiguousarray(query_keys, dtype=np.uint64)
+        keys = np.zeros(len(q), np.uint64)
+        dist = np.zeros(len(q))
+        self._check(self._L.pgo_closest_keyframes(self._h, len(q), L.u64ptr(q), int(skip), L.u64ptr(keys),
+                                                  L.dptr(dist)))
+        return keys, dist
+
+    def debug_search_ms(self):
+        a, b = C.c_double(), C.c_double()
+        self._check(self._L.pgo_debug_search_ms(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     # ------------------------------------------------- multi-GPU (pgo_comm_*)
     def comm_init_rccl(self, unique_id: bytes, rank: int, size: int):
         """ncclCommInitRank on this handle's device (collective over all ranks)."""

@@ -49,6 +49,9 @@ extern "C" {
 #define PGO_E_NOMEM (-9)
 #define PGO_E_BAD_EDGE (-10)     /* between factor with key1 == key2                */
 #define PGO_E_COMM (-11)         /* inter-rank exchange failed (RCCL / host callback) */
+#define PGO_E_NOT_ENOUGH (-12)   /* closest_keyframe: no more keyframes than `skip`
+                                    (the service returns false, graph.cpp:170-171) */
+#define PGO_NO_KEY UINT64_MAX    /* batched search: the query has no candidate      */
 #define PGO_W_MAXITER 1          /* informational: stopped at max_iterations        */
 
 /* ---- algorithms / solvers ------------------------------------------------ */
@@ -179,6 +182,22 @@ int pgo_error(pgo_graph *g, double *err);
    damping).  out: n x 9 doubles, row-major.  A singular H (a component without
    prior) returns PGO_E_INDETERMINANT, as GTSAM's Cholesky throws. */
 int pgo_marginal_covariances(pgo_graph *g, size_t n, const uint64_t *keys, double *out);
+
+/* ---- loop-closure candidate search -----------------------
+   The closest_keyframe service (graph.cpp:146-178): among the vertices in
+   insertion order except the last `skip` (keyframes_to_skip_in_loop_closing,
+   graph.cpp:15, = 10), the one whose current (x, y) is nearest to (x, y):
+   distance sqrt((x2-x1)^2 + (y2-y1)^2) as the reference forms it, ties to the
+   earliest inserted.  Fewer than skip + 1 vertices -> PGO_E_NOT_ENOUGH. */
+int pgo_closest_keyframe(pgo_graph *g, double x, double y, int skip, uint64_t *key, double *dist);
+/* Batched: for every query key (vertex i in insertion order) the service's
+   answer when that key was keyframes.back(): query = its current (x, y),
+   candidates = the vertices inserted before it except the last skip - 1 of
+   them (indices [0, i + 1 - skip)).  No candidate: key PGO_NO_KEY, dist +inf. */
+int pgo_closest_keyframes(pgo_graph *g, size_t q, const uint64_t *query_keys, int skip, uint64_t *keys_out,
+                          double *dist_out);
+/* device time (ms) of the last scan / batch search kernel launch */
+int pgo_debug_search_ms(pgo_graph *g, double *scan_ms, double *batch_ms);
 
 /* ---- multi-GPU: speculative lambda search ---------------------
    One process per GPU, every rank holding the same graph and values.  Where

@@ -59,6 +59,8 @@ def lib():
         L.orc_error.argtypes = [C.c_void_p, dp]
         L.orc_error.restype = C.c_double
         L.orc_information.argtypes = [dp, dp]
+        L.orc_closest_keyframe.argtypes = [C.c_int, dp, C.c_double, C.c_double, C.c_int, dp]
+        L.orc_closest_keyframe.restype = C.c_int
         _lib = L
     return _lib
 
@@ -69,6 +71,14 @@ def _dp(a):
 
 def _ip(a):
     return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def closest_keyframe(xy, qx, qy, skip=10):
+    """graph.cpp:146-178 restated in C: (index, distance) or (-1, nan)."""
+    xy = np.ascontiguousarray(xy, dtype=np.float64)
+    d = C.c_double(float("nan"))
+    i = lib().orc_closest_keyframe(len(xy), _dp(xy), float(qx), float(qy), int(skip), C.byref(d))
+    return i, d.value
 
 
 def information(cov):

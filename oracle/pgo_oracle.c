@@ -1307,3 +1307,27 @@ double orc_error(void *h, const double *poses) {
   free(P);
   return e;
 }
+
+/* ---- closest_keyframe service ----------------------------
+ * Restates /root/reference/src/graph/src/graph.cpp:146-178: with
+ * keyframes.size() > keyframes_to_skip_in_loop_closing (graph.cpp:15, = 10),
+ * distances to keyframes[0 .. size - skip - 1] are
+ * sqrt(pow(x2 - x1, 2) + pow(y2 - y1, 2)) (:153-158), and the first index with
+ * the smallest distance wins (strict <, :161-166).  Returns the index or -1
+ * when there are not enough keyframes (:170-171, service returns false).
+ * fp-contract off: the reference's x86-64 build has no FMA contraction. */
+__attribute__((optimize("fp-contract=off")))
+int orc_closest_keyframe(int n, const double *xy, double qx, double qy, int skip, double *dist) {
+  if (n <= 0 || n <= skip) return -1;
+  int best = 0;
+  double dbest = 0.0;
+  for (int i = 0; i < n - skip; i++) {
+    const double d = sqrt(pow(xy[2 * i] - qx, 2) + pow(xy[2 * i + 1] - qy, 2));
+    if (i == 0 || d < dbest) {
+      best = i;
+      dbest = d;
+    }
+  }
+  *dist = dbest;
+  return best;
+}

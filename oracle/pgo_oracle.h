@@ -90,6 +90,10 @@ double orc_error(void *h, const double *poses);
 /* Omega for noiseModel::Gaussian::Covariance(cov) (GTSAM smart check).  0 / ORC_E_BAD_COV. */
 int orc_information(const double *cov, double *omega);
 
+/* closest_keyframe service, graph.cpp:146-178 (xy: n x 2 keyframe positions in
+ * insertion order); index of the closest of the first n - skip, -1 if n <= skip */
+int orc_closest_keyframe(int n, const double *xy, double qx, double qy, int skip, double *dist);
+
 #ifdef __cplusplus
 }
 #endif
