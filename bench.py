@@ -125,6 +125,8 @@ def main():
                     help="N>1: speculative lambda search over RCCL (one job) or independent replicas")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a one-GPU box: every rank on device 0, host (gloo) transport")
+    ap.add_argument("--ordering", choices=["nd", "amd"], default="nd",
+                    help="fill-reducing ordering of the Cholesky solver (pgo_opts.ordering)")
     ap.add_argument("--search", type=int, default=1,
                     help="after the timed steps: time the closest_keyframe search at the optimum (0: skip)")
     ap.add_argument("--max-outer", type=int, default=0,
@@ -138,7 +140,9 @@ def main():
     r = init_from_env()
     world, rank = r.world, r.rank
     g = datasets.make(args.config)
-    pg = PoseGraph.from_dataset(g, device=0 if args.same_device else r.local_rank)
+    from graphslam_amd import _lib
+    ordering = _lib.PGO_ORDERING_AMD if args.ordering == "amd" else _lib.PGO_ORDERING_ND
+    pg = PoseGraph.from_dataset(g, device=0 if args.same_device else r.local_rank, ordering=ordering)
     spec = world > 1 and args.multi == "spec"
     hc = None
     if spec:
@@ -236,7 +240,7 @@ def main():
                 "poses": n, "edges": ne, "parallelism": (f"spec-lambda{world}" + ("-host" if args.same_device else "-rccl")) if spec
                 else f"replicas{world}",
                 "lambda_lanes": args.lanes,
-                "solver": ("GPU supernodal multifrontal Cholesky (AMD ordering, fp64 MFMA Schur updates)"
+                "solver": (f"GPU supernodal multifrontal Cholesky ({'nested-dissection' if args.ordering == 'nd' else 'AMD'} ordering, fp64 MFMA Schur updates)"
                            if args.solver == "cholesky" else
                            "block-Jacobi PCG, rel tol %.0e" % params.pcg_relative_tol),
             },

@@ -29,6 +29,8 @@ PGO_E_COMM = -11
 PGO_E_NOT_ENOUGH = -12
 PGO_NO_KEY = (1 << 64) - 1
 PGO_W_MAXITER = 1
+PGO_ORDERING_ND = 0
+PGO_ORDERING_AMD = 1
 PGO_ALG_LM = 0
 PGO_ALG_GN = 1
 PGO_SOLVER_PCG = 0
@@ -36,7 +38,7 @@ PGO_SOLVER_CHOLESKY = 1
 
 
 class PgoOpts(C.Structure):
-    _fields_ = [("device", C.c_int), ("reserved", C.c_int * 7)]
+    _fields_ = [("device", C.c_int), ("ordering", C.c_int), ("reserved", C.c_int * 6)]
 
 
 class PgoParams(C.Structure):

@@ -71,6 +71,7 @@ struct pgo_graph {
   // ---- supernodal Cholesky (built on first use; structure-dependent) ----
   std::vector<int> h_row_ptr, h_slot_col;   // block-CSR pattern (old indices)
   pgo::CholPlan chol;
+  int ordering = pgo::kOrderNd;             // fill-reducing ordering (pgo_opts.ordering)
   bool chol_ready = false;
   std::vector<hipEvent_t> sev;              // syrk profiling event pairs
   std::vector<double> sev_flops;
@@ -489,6 +490,7 @@ double ms_between(hipEvent_t a, hipEvent_t b);
 
 int ensure_chol(pgo_graph* g) {
   if (g->chol_ready) return PGO_OK;
+  g->chol.ordering = g->ordering;
   pgo::chol_analyze(g->chol, g->d.n, g->h_row_ptr, g->h_slot_col);
   const hipError_t e = pgo::chol_upload(g->chol, g->d.stream);
   if (e != hipSuccess) {
@@ -794,7 +796,14 @@ void pgo_default_params(pgo_params* p) {
 pgo_graph* pgo_create(const pgo_opts* opts) {
   pgo_graph* g = new (std::nothrow) pgo_graph();
   if (!g) return nullptr;
-  if (opts) g->device = opts->device;
+  if (opts) {
+    if (opts->ordering != PGO_ORDERING_ND && opts->ordering != PGO_ORDERING_AMD) {
+      delete g;
+      return nullptr;
+    }
+    g->device = opts->device;
+    g->ordering = opts->ordering == PGO_ORDERING_AMD ? pgo::kOrderAmd : pgo::kOrderNd;
+  }
   return g;
 }
 
@@ -1393,6 +1402,7 @@ int pgo_debug_fronts(pgo_graph* g, int* w, int* m, int* level, int cap) {
   HostStructure H;
   RC_TRY(build_structure(g, H));
   pgo::CholPlan P;
+  P.ordering = g->ordering;
   pgo::chol_analyze(P, (int)g->keys.size(), H.row_ptr, H.slot_col);
   for (int s = 0; s < P.ns && s < cap; s++) {
     w[s] = P.w[s];
@@ -1408,6 +1418,7 @@ int pgo_debug_plan(pgo_graph* g, double* out, int cap) {
   HostStructure H;
   RC_TRY(build_structure(g, H));
   pgo::CholPlan P;
+  P.ordering = g->ordering;
   pgo::chol_analyze(P, (int)g->keys.size(), H.row_ptr, H.slot_col);
   // launches: factor = memsets, assembly, rhs permutation, per level extend-add
   // ranks + vector assembly + small classes + per panel diag/trsm/Schur (+look-ahead);

@@ -61,7 +61,10 @@ struct CholLevel {
   SolveStep bwd_part{0, 0};        // partial products feeding the init tasks
 };
 
+enum { kOrderNd = 0, kOrderAmd = 1 };
+
 struct CholPlan {
+  int ordering = kOrderNd;         // fill-reducing ordering of the pose graph (input of chol_analyze)
   // ---- host symbolic result ----
   int n = 0, ns = 0;
   long long nslots = 0;            // block-CSR slots of the analysed pattern (stride of V)
@@ -128,6 +131,11 @@ struct CholPlan {
 // (workgroup i runs on XCD i mod 8), so each XCD's L2 holds the panel rows and
 // columns of the blocks it works on
 void xcd_order(std::vector<int4>& tasks, int tile);
+
+// host: fill-reducing orderings of a pose graph (adjacency without self loops
+// allowed); both return new -> old.  pgo_order.cpp / pgo_symbolic.cpp
+std::vector<int> order_amd(int n, const std::vector<int>& xadj, const std::vector<int>& adj);
+std::vector<int> order_nd(int n, const std::vector<int>& xadj, const std::vector<int>& adj);
 
 // host: symbolic analysis from the block-CSR pattern (old pose indices)
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);

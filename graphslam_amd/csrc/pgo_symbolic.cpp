@@ -11,13 +11,12 @@
 #include "pgo_chol.h"
 
 namespace pgo {
-namespace {
 
 // Approximate minimum degree on the quotient graph (Amestoy, Davis & Duff):
 // eliminated pivots become elements that absorb their adjacent elements;
 // external degrees are bounded by |A_i| + |L_p \ i| + sum_e |L_e \ L_p|,
 // with |L_e \ L_p| from the w(e) counters; aggressive element absorption.
-std::vector<int> amd(int n, const std::vector<int>& xadj, const std::vector<int>& adj) {
+std::vector<int> order_amd(int n, const std::vector<int>& xadj, const std::vector<int>& adj) {
   std::vector<std::vector<int>> var(n), elem(n), members(n);
   std::vector<char> state(n, 0);  // 0 variable, 1 element, 2 absorbed
   std::vector<int> deg(n), w(n, 0), wstamp(n, -1), mark(n, -1);
@@ -111,8 +110,6 @@ std::vector<int> amd(int n, const std::vector<int>& xadj, const std::vector<int>
   return order;
 }
 
-}  // namespace
-
 void xcd_order(std::vector<int4>& tasks, int tile) {
   constexpr int kXcd = 8, kBlk = 8;
   if ((int)tasks.size() < 4 * kXcd * kBlk) return;   // small launches: keep the natural order
@@ -164,7 +161,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       xadj[i + 1] = (int)adj.size();
     }
   }
-  const std::vector<int> order0 = amd(n, xadj, adj);
+  const std::vector<int> order0 = P.ordering == kOrderAmd ? order_amd(n, xadj, adj) : order_nd(n, xadj, adj);
   std::vector<int> ip0(n);
   for (int k = 0; k < n; k++) ip0[order0[k]] = k;
   // ---- elimination tree of the permuted pattern (Liu, path compression)

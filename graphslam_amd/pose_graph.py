@@ -63,10 +63,11 @@ def default_params(**kw) -> L.PgoParams:
 class PoseGraph:
     """One pgo_graph handle (one HIP stream, graph + values resident in HBM)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, ordering: int = L.PGO_ORDERING_ND):
         self._L = L.lib()
         opts = L.PgoOpts()
         opts.device = device
+        opts.ordering = ordering
         self._h = self._L.pgo_create(C.byref(opts))
         if not self._h:
             raise MemoryError("pgo_create failed")
@@ -127,9 +128,9 @@ class PoseGraph:
                                           L.dptr(cov), stride))
 
     @classmethod
-    def from_dataset(cls, g, device=0):
+    def from_dataset(cls, g, device=0, ordering=L.PGO_ORDERING_ND):
         """Load a graphslam_amd.datasets.PoseGraph (vertices, priors, edges)."""
-        pg = cls(device)
+        pg = cls(device, ordering)
         pg.add_vertices(g.keys, g.initial)
         for k, p, c in zip(g.prior_keys, g.prior_pose, g.prior_cov):
             pg.add_prior(int(k), p, c)

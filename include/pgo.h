@@ -63,9 +63,16 @@ extern "C" {
 
 typedef struct pgo_graph pgo_graph;
 
+#define PGO_ORDERING_ND 0        /* multilevel nested dissection of the pose graph
+                                    (default: balanced elimination tree, C3 half
+                                    the flops of minimum degree)                   */
+#define PGO_ORDERING_AMD 1       /* approximate minimum degree                       */
+
 typedef struct {
   int device;        /* HIP device ordinal (default 0) */
-  int reserved[7];
+  int ordering;      /* fill-reducing ordering of the Cholesky solver, computed once
+                        per graph structure (GTSAM: COLAMD every solve) [PGO_ORDERING_ND] */
+  int reserved[6];
 } pgo_opts;
 
 typedef struct {

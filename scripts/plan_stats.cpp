@@ -1,10 +1,12 @@
 // Host-only statistics of the supernodal plan for an edge list (int32 pairs):
 // per level the fronts, panel steps and extend-add volume.
 //   hipcc -O2 -std=c++17 -I include scripts/plan_stats.cpp graphslam_amd/csrc/pgo_symbolic.cpp -o /tmp/plan_stats
-//   /tmp/plan_stats edges.bin n
+//   /tmp/plan_stats edges.bin n [nd|amd]
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <string>
+#include <chrono>
 
 #include "../graphslam_amd/csrc/pgo_chol.h"
 
@@ -33,7 +35,10 @@ int main(int argc, char** argv) {
     col[fill[e[2 * q + 1]]++] = e[2 * q];
   }
   pgo::CholPlan P;
+  if (argc > 3 && std::string(argv[3]) == "amd") P.ordering = pgo::kOrderAmd;
+  const auto t0 = std::chrono::steady_clock::now();
   pgo::chol_analyze(P, n, row_ptr, col);
+  printf("analysis %.3f s\n", std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
   double tri = 0, ftot = 0;
   for (int s = 0; s < P.ns; s++) {
     tri += 0.5 * P.m[s] * (P.m[s] + 1.0);
