@@ -27,7 +27,7 @@ constexpr int kNB = 64;            // panel width of the blocked path
 constexpr int kTile = 64;          // Schur-update output tile
 constexpr int kBigTile = 128;      // Schur-update output tile of the LDS-pipelined kernel
 constexpr int kKB = 256;
-constexpr int kEaPiece = 4096;   // update-matrix elements per extend-add workgroup
+constexpr int kZeroBackgroundGrid = 32;   // workgroups of the background (late) zeroing
 constexpr int kBwdRows = 512;      // rows per partial product of the backward solve           // Schur-update depth: trailing matrix updated once per kKB columns
 
 struct PanelStep {                 // one panel of the blocked path, all big fronts of a level
@@ -53,7 +53,7 @@ struct SmallClass {                // small fronts of one level with m <= mmax
 struct CholLevel {
   std::vector<SmallClass> small;   // fronts in small_list, by size class
   std::vector<PanelStep> panels;   // blocked path
-  std::vector<int> ea_off, ea_cnt; // per child rank: tasks in ea_tasks (children whose parents are in this level)
+  std::vector<int> ea_off, ea_cnt; // [0]: extend-add tile tasks in ea_tasks (parents in this level)
   int front_off, front_cnt;        // all fronts of the level in level_fronts (solves)
   int small_maxm = 0, maxm = 0;    // LDS sizing
   int maxblk = 0;                  // max 64-column blocks of a front's pivot columns
@@ -89,13 +89,24 @@ struct CholPlan {
   std::vector<int> small_list, level_fronts, potrf_list;
   std::vector<int2> trsm_tasks;
   std::vector<int4> syrk_tasks, sdiag_tasks;
-  std::vector<int4> zero_tasks;     // (front, first column, end column): lower triangles zeroed per factorisation
+  // Fronts must be zero (lower triangles) before a factorisation assembles into
+  // them.  zero_tasks (front, first column, end column), pieces of ~32k doubles:
+  // [0, zero_split) leaf-level fronts and [zero_split, zero_late) the rest, zeroed
+  // at the start of every factorisation; [zero_late, end) the update matrices
+  // of the fronts whose parents are at levels <= zero_level, zeroed by the
+  // factorisation itself on a side stream once the extend-add of zero_level has
+  // consumed them (beside the latency-bound top levels, when HBM is idle), so
+  // they are zero again when the next factorisation starts.
+  std::vector<int4> zero_tasks;
+  int zero_late = 0, zero_level = -1;
   std::vector<int4> bwd_tasks;
   std::vector<int2> bwd_pref;      // per bwd task: first partial, partial count (init tasks)
   std::vector<int4> bwd_part_tasks;  // (front, c0, r0, partial slot)
   int npart = 0;
-  std::vector<int4> ea_tasks;      // (child, first, end): pieces of a child's update-matrix lower triangle
-                                   // (column-major element order), grouped per (level, child rank)
+  std::vector<int4> ea_tasks;      // (parent, tile row << 16 | tile col, first pair, pairs): 64x64
+                                   // tiles of parent fronts receiving update-matrix elements, per level
+  std::vector<int4> ea_pairs;      // (child, first row a0, first column b0, rows | columns << 8):
+                                   // a child's rectangle of one tile, children in order
   double flops = 0, nnzl = 0, syrk_flops = 0;
   long long ftotal = 0, ttotal = 0;
   int vtotal = 0;
@@ -122,6 +133,7 @@ struct CholPlan {
   int2* d_bwd_pref = nullptr;
   double* d_partial = nullptr;
   int4* d_ea_tasks = nullptr;
+  int4* d_ea_pairs = nullptr;
   int* d_flag = nullptr;           // non-positive pivot seen
   double* d_lambda = nullptr;      // damping read by the assembly (graph-replay friendly)
 };

@@ -3,8 +3,8 @@
 //
 // Factorisation, per level of the supernodal tree (leaves first):
 //   k_extend_add   children's update matrices -> parent fronts, one launch per
-//                  child rank (each parent receives from one child per launch:
-//                  no atomics, fixed order, bitwise reproducible)
+//                  level, one workgroup per parent tile walking the children in
+//                  order (no atomics, fixed order, bitwise reproducible)
 //   k_front_small  fronts with m <= 128: whole front in LDS, one workgroup each
 //   k_panel_trsm   blocked path, per 64-column panel: the diagonal tile is
 //                  factored in LDS (redundantly by every workgroup of the front)
@@ -102,55 +102,54 @@ __global__ __launch_bounds__(256) void k_asm_diag(CholDev c, const double* __res
 }
 
 // ------------------------------------------------------------ extend-add
-// A piece of a child's update-matrix lower triangle (elements [e0, e1) in
-// column-major order) added into the parent front, 16 elements per thread,
-// loads first.  One launch per child rank: a parent receives from one child
-// per launch (no atomics, fixed order, bitwise reproducible).
-__device__ __forceinline__ int tri_col(long long e, int u) {   // column b of element e: b*u - b(b-1)/2 <= e
-  const double q = 2.0 * u + 1.0;
-  int b = (int)((q - sqrt(fmax(q * q - 8.0 * (double)e, 0.0))) * 0.5);
-  b = max(0, min(b, u - 1));
-  while (b > 0 && (long long)b * u - (long long)b * (b - 1) / 2 > e) b--;
-  while (b + 1 < u && (long long)(b + 1) * u - (long long)(b + 1) * b / 2 <= e) b++;
-  return b;
-}
-__global__ __launch_bounds__(256) void k_extend_add(CholDev c, const int4* __restrict__ tasks) {
+// One 64x64 tile of a parent front's lower triangle per workgroup: the
+// parent's children in order (fixed summation order, bitwise reproducible, no
+// atomics, one launch per level), each adding its rectangle of update-matrix
+// elements (rows [a0, a0+nr), columns [b0, b0+nc), element (a, b) only for
+// b <= a).  Lane r <-> child row a0 + r (column-major: loads of a column are
+// coalesced), the 4 waves take every 4th column; loads first.
+__global__ __launch_bounds__(256) void k_extend_add(CholDev c, const int4* __restrict__ tasks,
+                                                    const int4* __restrict__ pairs) {
+  __shared__ int prow[64];
+  __shared__ long long pcol[64];
   const int4 t = tasks[blockIdx.x];
-  const int ch = t.x;
-  const int mc = c.m[ch], wc = c.w[ch], u = mc - wc;
-  const int p = c.parent[ch];
-  const int mp = c.m[p];
-  const int* __restrict__ rel = c.ea_rel + c.ea_ptr[ch];
-  const double* __restrict__ U = c.F + c.foff[ch] + wc + (size_t)wc * mc;
+  const int p = t.x, mp = c.m[p];
   double* __restrict__ Fp = c.F + c.foff[p];
-  constexpr int R = kEaPiece / 256;
-  const int e0 = t.y + threadIdx.x, e1 = t.z;
-  // element e0 + 256 q: walk the columns from the first one
-  int b = e0 < e1 ? tri_col(e0, u) : 0;
-  long long cs = (long long)b * u - (long long)b * (b - 1) / 2;   // first element of column b
-  int src[R], dst[R];
-#pragma unroll
-  for (int q = 0; q < R; q++) {
-    const int e = e0 + 256 * q;
-    src[q] = -1;
-    if (e < e1) {
-      while (e - cs >= u - b) {   // next column
-        cs += u - b;
-        b++;
-      }
-      const int a = b + (int)(e - cs);
-      src[q] = a + b * mc;
-      dst[q] = (3 * rel[a / 3] + a % 3) + (3 * rel[b / 3] + b % 3) * mp;
+  const int tid = threadIdx.x, r = tid & 63, cg = tid >> 6;
+  for (int k = 0; k < t.w; k++) {
+    const int4 q = pairs[t.z + k];
+    const int ch = q.x, a0 = q.y, b0 = q.z, nr = q.w & 0xff, nc = q.w >> 8;
+    const int mc = c.m[ch], wc = c.w[ch];
+    const int* __restrict__ rel = c.ea_rel + c.ea_ptr[ch];
+    if (k > 0) __syncthreads();   // the previous child's adds are done, prow / pcol reusable
+    if (tid < nr) {
+      const int a = a0 + tid;
+      prow[tid] = 3 * rel[a / 3] + a % 3;
+    } else if (tid >= 64 && tid - 64 < nc) {
+      const int b = b0 + tid - 64;
+      pcol[tid - 64] = (long long)(3 * rel[b / 3] + b % 3) * mp;
     }
+    __syncthreads();
+    if (r >= nr) continue;
+    const int a = a0 + r;
+    const double* __restrict__ U = c.F + c.foff[ch] + wc + (size_t)wc * mc + a;
+    constexpr int R = 16;
+    double v[R], f[R];
+    long long dst[R];
+    bool ok[R];
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      const int bb = cg + 4 * j;
+      ok[j] = bb < nc && b0 + bb <= a;
+      dst[j] = ok[j] ? prow[r] + pcol[bb] : 0;
+      v[j] = ok[j] ? U[(size_t)(b0 + bb) * mc] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < R; j++) f[j] = ok[j] ? Fp[dst[j]] : 0.0;
+#pragma unroll
+    for (int j = 0; j < R; j++)
+      if (ok[j]) Fp[dst[j]] = f[j] + v[j];
   }
-  double v[R], f[R];
-#pragma unroll
-  for (int q = 0; q < R; q++) v[q] = src[q] >= 0 ? U[src[q]] : 0.0;
-#pragma unroll
-  for (int q = 0; q < R; q++) f[q] = src[q] >= 0 ? Fp[dst[q]] : 0.0;
-#pragma unroll
-  for (int q = 0; q < R; q++)
-    if (src[q] >= 0) Fp[dst[q]] = f[q] + v[q];
 }
 
 // ------------------------------------------------------------ triangular inverse
@@ -1050,19 +1049,23 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
 
 // Lower triangles of the fronts (columns [j0, j1) of a front per workgroup)
 // zeroed before assembly; the upper triangles are never written.
-__global__ __launch_bounds__(256) void k_zero_lower(CholDev c, const int4* __restrict__ tasks) {
-  const int4 t = tasks[blockIdx.x];
-  const int m = c.m[t.x];
-  const long long base = c.foff[t.x];
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-  for (int j = t.y + wv; j < t.z; j += 4) {   // a wave per column, 16-B stores
-    const long long g0 = base + (long long)j * m + j, g1 = base + (long long)j * m + m;
-    const long long a0 = (g0 + 1) & ~1LL;       // first 16-B aligned element
-    if (l == 0 && a0 != g0) c.F[g0] = 0.0;
-    double2* p = reinterpret_cast<double2*>(c.F + a0);
-    const long long np = (g1 - a0) >> 1;
-    for (long long q = l; q < np; q += 64) p[q] = make_double2(0.0, 0.0);
-    if (l == 0 && a0 + 2 * np < g1) c.F[g1 - 1] = 0.0;
+// tasks [0, n), grid-stride: a small grid zeroes in the background without
+// taking the CUs the latency-bound panel kernels need
+__global__ __launch_bounds__(256) void k_zero_lower(CholDev c, const int4* __restrict__ tasks, int n) {
+  for (int q0 = blockIdx.x; q0 < n; q0 += gridDim.x) {
+    const int4 t = tasks[q0];
+    const int m = c.m[t.x];
+    const long long base = c.foff[t.x];
+    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+    for (int j = t.y + wv; j < t.z; j += 4) {   // a wave per column, 16-B stores
+      const long long g0 = base + (long long)j * m + j, g1 = base + (long long)j * m + m;
+      const long long a0 = (g0 + 1) & ~1LL;       // first 16-B aligned element
+      if (l == 0 && a0 != g0) c.F[g0] = 0.0;
+      double2* p = reinterpret_cast<double2*>(c.F + a0);
+      const long long np = (g1 - a0) >> 1;
+      for (long long q = l; q < np; q += 64) p[q] = make_double2(0.0, 0.0);
+      if (l == 0 && a0 + 2 * np < g1) c.F[g1 - 1] = 0.0;
+    }
   }
 }
 
@@ -1419,6 +1422,7 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));   // (a non-default priority measured 1.5x slower)
   for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   CH_TRY(up(&P.d_ea_tasks, P.ea_tasks, s));
+  CH_TRY(up(&P.d_ea_pairs, P.ea_pairs, s));
   return hipStreamSynchronize(s);
 }
 
@@ -1426,7 +1430,7 @@ void chol_free(CholPlan& P) {
   void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
                   P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
                   P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
-                  P.d_trsm, P.d_syrk, P.d_ea_tasks, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_zero, P.d_dg_order};
+                  P.d_trsm, P.d_syrk, P.d_ea_tasks, P.d_ea_pairs, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_zero, P.d_dg_order};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : P.evs)
@@ -1482,9 +1486,9 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
   CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int), s));
   // zeroing + assembly: leaf-level fronts on the main stream, the others on
   // side3 beside the leaf level (joined before level 1's extend-add)
-  const int nz = (int)P.zero_tasks.size(), nt = (int)P.asm_front.size();
+  const int nz = P.zero_late, nt = (int)P.asm_front.size();
   auto assemble = [&](int z0, int z1, int a0, int a1, int d0, int d1, hipStream_t st) {
-    if (z1 > z0) k_zero_lower<<<z1 - z0, 256, 0, st>>>(c, P.d_zero + z0);
+    if (z1 > z0) k_zero_lower<<<z1 - z0, 256, 0, st>>>(c, P.d_zero + z0, z1 - z0);
     if (a1 > a0) k_asm_offdiag<<<(a1 - a0 + 255) / 256, 256, 0, st>>>(c, V, P.nslots, a0, a1);
     if (d1 > d0) k_asm_diag<<<(d1 - d0 + 255) / 256, 256, 0, st>>>(c, D, P.d_lambda, d0, d1);
   };
@@ -1499,8 +1503,14 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
   for (size_t li = 0; li < P.levels.size(); li++) {
     const CholLevel& lv = P.levels[li];
     if (li == 1 && fork_rest) CH_TRY(hipStreamWaitEvent(s, P.evs[5], 0));
-    for (size_t r = 0; r < lv.ea_off.size(); r++)
-      if (lv.ea_cnt[r]) k_extend_add<<<lv.ea_cnt[r], 256, 0, s>>>(c, P.d_ea_tasks + lv.ea_off[r]);
+    if (lv.ea_cnt[0]) k_extend_add<<<lv.ea_cnt[0], 256, 0, s>>>(c, P.d_ea_tasks + lv.ea_off[0], P.d_ea_pairs);
+    if ((int)li == P.zero_level) {   // update matrices consumed by now: zero them for the next factorisation
+      CH_TRY(hipEventRecord(P.evs[4], s));
+      CH_TRY(hipStreamWaitEvent(P.side3, P.evs[4], 0));
+      const int nlate = (int)P.zero_tasks.size() - P.zero_late;
+      k_zero_lower<<<std::min(nlate, kZeroBackgroundGrid), 256, 0, P.side3>>>(c, P.d_zero + P.zero_late, nlate);
+      CH_TRY(hipEventRecord(P.evs[5], P.side3));
+    }
     k_vec_assemble<<<lv.front_cnt, 256, (size_t)lv.maxm * sizeof(double), s>>>(c, P.d_level_fronts + lv.front_off);
     // small fronts on the second side stream, beside the blocked path of the
     // same level (disjoint fronts); joined before the next level
@@ -1554,6 +1564,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       CH_TRY(hipStreamWaitEvent(s, P.evs[1], 0));
     }
   }
+  if (P.zero_level >= 0) CH_TRY(hipStreamWaitEvent(s, P.evs[5], 0));
   return hipGetLastError();
 }
 

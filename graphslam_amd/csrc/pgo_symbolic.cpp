@@ -430,30 +430,46 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.trsm_tasks.clear();
   P.syrk_tasks.clear();
   P.sdiag_tasks.clear();
+  // zeroing (see CholPlan::zero_tasks): the level whose extend-add is the last
+  // to read the early update matrices = the first level with few fronts (the
+  // latency-bound top of the tree)
+  P.zero_level = -1;
+  for (int L = 1; L < nl; L++)
+    if ((int)bylevel[L].size() <= 64) {
+      P.zero_level = L;
+      break;
+    }
   P.zero_tasks.clear();
-  P.zero_split = 0;
-  for (int qq = 0; qq < 2 * P.ns; qq++) {   // lower triangles in pieces of ~32k doubles, leaf level first
-    const int q = qq % P.ns;
-    if (qq == P.ns) P.zero_split = (int)P.zero_tasks.size();
-    if ((P.height[q] > 0) != (qq >= P.ns)) continue;
+  auto zero_cols = [&](int q, int c0, int c1) {   // columns [c0, c1) of front q, ~32k doubles per task
     const int m = P.m[q];
-    int j0 = 0;
+    int j0 = c0;
     long long acc = 0;
-    for (int j = 0; j < m; j++) {
+    for (int j = c0; j < c1; j++) {
       acc += m - j;
-      if (acc >= 32768 || j == m - 1) {
+      if (acc >= 32768 || j == c1 - 1) {
         P.zero_tasks.push_back(make_int4(q, j0, j + 1, 0));
         j0 = j + 1;
         acc = 0;
       }
     }
+  };
+  auto late = [&](int q) { return P.zero_level >= 0 && P.parent[q] >= 0 && P.height[P.parent[q]] <= P.zero_level; };
+  for (int pass = 0; pass < 2; pass++) {   // leaf-level fronts, then the others
+    if (pass == 1) P.zero_split = (int)P.zero_tasks.size();
+    for (int q = 0; q < P.ns; q++)
+      if ((P.height[q] > 0) == (pass == 1)) zero_cols(q, 0, late(q) ? P.w[q] : P.m[q]);
   }
+  P.zero_late = (int)P.zero_tasks.size();
+  for (int q = 0; q < P.ns; q++)
+    if (late(q)) zero_cols(q, P.w[q], P.m[q]);
+  if (P.zero_late == (int)P.zero_tasks.size()) P.zero_level = -1;
   P.potrf_list.clear();
   P.bwd_tasks.clear();
   P.bwd_pref.clear();
   P.bwd_part_tasks.clear();
   P.npart = 0;
   P.ea_tasks.clear();
+  P.ea_pairs.clear();
   for (int L = 0; L < nl; L++) {
     CholLevel& lv = P.levels[L];
     lv.front_off = (int)P.level_fronts.size();
@@ -499,19 +515,39 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       st.cnt = (int)P.bwd_tasks.size() - st.off;
       lv.bwd.push_back(st);
     }
-    // extend-add groups: children of this level's fronts, grouped by rank
-    int maxc = 0;
-    for (int s : bylevel[L]) maxc = std::max(maxc, P.cptr[s + 1] - P.cptr[s]);
-    for (int r = 0; r < maxc; r++) {
-      lv.ea_off.push_back((int)P.ea_tasks.size());
-      for (int s : bylevel[L]) {
-        if (P.cptr[s] + r >= P.cptr[s + 1]) continue;
-        const int c = P.children[P.cptr[s] + r];
-        const int u = P.m[c] - P.w[c], tri = u * (u + 1) / 2;
-        for (int e0 = 0; e0 < tri; e0 += kEaPiece) P.ea_tasks.push_back(make_int4(c, e0, std::min(e0 + kEaPiece, tri), 0));
+    // extend-add: one task per 64x64 tile of a parent front's lower triangle
+    // that receives update-matrix elements; a task walks the parent's children
+    // in order (fixed summation order, no atomics), each contributing a
+    // rectangle of its update matrix (child rows [a0, a0+nr) x columns
+    // [b0, b0+nc), the rows / columns whose parent index falls in the tile)
+    lv.ea_off.push_back((int)P.ea_tasks.size());
+    for (int sp : bylevel[L]) {
+      if (P.cptr[sp] == P.cptr[sp + 1]) continue;
+      const int nt = (P.m[sp] + 63) / 64;
+      std::vector<std::vector<int4>> tiles((size_t)nt * (nt + 1) / 2);
+      for (int q = P.cptr[sp]; q < P.cptr[sp + 1]; q++) {
+        const int c = P.children[q];
+        const int u = P.m[c] - P.w[c];
+        std::vector<int3> runs;   // (tile, first child row, rows)
+        for (int a = 0; a < u; a++) {
+          const int t = (3 * P.ea_rel[P.ea_ptr[c] + a / 3] + a % 3) / 64;
+          if (runs.empty() || runs.back().x != t) runs.push_back(make_int3(t, a, 0));
+          runs.back().z++;
+        }
+        for (size_t i = 0; i < runs.size(); i++)
+          for (size_t j = 0; j <= i; j++)
+            tiles[(size_t)runs[i].x * (runs[i].x + 1) / 2 + runs[j].x].push_back(
+                make_int4(c, runs[i].y, runs[j].y, runs[i].z | (runs[j].z << 8)));
       }
-      lv.ea_cnt.push_back((int)P.ea_tasks.size() - lv.ea_off.back());
+      for (int ti = 0; ti < nt; ti++)
+        for (int tj = 0; tj <= ti; tj++) {
+          const auto& v = tiles[(size_t)ti * (ti + 1) / 2 + tj];
+          if (v.empty()) continue;
+          P.ea_tasks.push_back(make_int4(sp, (ti << 16) | tj, (int)P.ea_pairs.size(), (int)v.size()));
+          P.ea_pairs.insert(P.ea_pairs.end(), v.begin(), v.end());
+        }
     }
+    lv.ea_cnt.push_back((int)P.ea_tasks.size() - lv.ea_off.back());
     // small fronts (m <= kSmallFront): with w <= kWaveW one wavefront each (the
     // m x w panel in LDS, the rank-w Schur update streamed), largest first;
     // else one workgroup each with the whole front in LDS, launched per size
@@ -521,7 +557,10 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       const int classes[4] = {32, 64, 96, kSmallFront};
       std::vector<int> bucket[4], wave;
       for (int s : bylevel[L]) {
-        if (P.m[s] > kSmallFront) {
+        // w > kWaveW: the blocked path (64-column panels, every front of the
+        // level in the same launches) -- a whole-front-in-LDS workgroup runs
+        // its w pivots one after the other at ~2 us each
+        if (P.m[s] > kSmallFront || (P.w[s] > kWaveW && !getenv("PGO_SMALL_LDS"))) {
           big.push_back(s);
           continue;
         }

@@ -59,11 +59,13 @@ int main(int argc, char** argv) {
     int nsmall = 0;
     for (const auto& sc : lv.small) nsmall += sc.cnt;
     double ea = 0;   // update matrices extended into this level (lower triangles, doubles)
-    for (size_t r = 0; r < lv.ea_off.size(); r++)
-      for (int q = 0; q < lv.ea_cnt[r]; q++) {
-        const int4 t = P.ea_tasks[lv.ea_off[r] + q];
-        ea += t.z - t.y;
+    for (int q = 0; q < lv.ea_cnt[0]; q++) {
+      const int4 t = P.ea_tasks[lv.ea_off[0] + q];
+      for (int k = 0; k < t.w; k++) {
+        const int4 pr = P.ea_pairs[t.z + k];
+        ea += (pr.w & 0xff) * (pr.w >> 8);
       }
+    }
     int nfused = 0, ntr = 0, nsy = 0, npotrf = 0;
     for (const auto& ps : lv.panels) {
       nfused += ps.fused;
@@ -71,8 +73,8 @@ int main(int argc, char** argv) {
       nsy += ps.syrk_cnt;
       npotrf += ps.potrf_cnt;
     }
-    printf("level %2d: fronts %6d (small %6d) maxm %5d ranks %zu ea %6.1fM dbl, steps %3zu (fused %3d) potrf %5d trsm %6d syrk %7d\n",
-           li++, lv.front_cnt, nsmall, lv.maxm, lv.ea_off.size(), ea / 1e6, lv.panels.size(), nfused, npotrf, ntr, nsy);
+    printf("level %2d: fronts %6d (small %6d) maxm %5d tiles %6d ea %6.1fM dbl, steps %3zu (fused %3d) potrf %5d trsm %6d syrk %7d\n",
+           li++, lv.front_cnt, nsmall, lv.maxm, lv.ea_cnt[0], ea / 1e6, lv.panels.size(), nfused, npotrf, ntr, nsy);
   }
   return 0;
 }

@@ -191,6 +191,27 @@ def test_save_restore_and_determinism(pg_cls):
     assert np.array_equal(pg.poses(), p1)
 
 
+def test_fronts_rezeroed_after_marginals(pg_cls):
+    """The backward solve zeroes the fronts behind itself (the next factorisation
+    skips its zeroing); a factorisation without a solve (the marginals) leaves
+    them dirty, and the next optimize must zero them first: results bitwise
+    equal to a run that never computed marginals, graph replay and eager."""
+    g = datasets.make("C2")
+    ref = pg_cls.from_dataset(g)
+    ref.save_values()
+    st0 = ref.optimize()
+    p0 = ref.poses()
+    for graphs in (1, 0):
+        pg = pg_cls.from_dataset(g)
+        pg.save_values()
+        pg.optimize(use_graphs=graphs, max_outer=2)
+        pg.marginal_covariances(np.asarray(g.keys)[:8])
+        pg.restore_values()
+        st = pg.optimize(use_graphs=graphs)
+        assert st["final_error"] == st0["final_error"], graphs
+        assert np.array_equal(pg.poses(), p0), graphs
+
+
 # ------------------------------------------------------------ headline size
 @pytest.mark.parametrize("solver", [1, 0])
 def test_c3_full_size_against_golden(pg_cls, solver):
