@@ -119,8 +119,8 @@ def main():
                     help="eager launches instead of the captured factor+solve hipGraph (rocprofv3 runs)")
     ap.add_argument("--marginals", type=int, default=64,
                     help="after the timed steps: time marginal covariances of this many poses (0: skip)")
-    ap.add_argument("--lanes", type=int, default=1,
-                    help="lambda tries solved concurrently per GPU (pgo_params.lambda_lanes)")
+    ap.add_argument("--lanes", type=int, default=2,
+                    help="consecutive lambda tries per batched factorisation (pgo_params.lambda_lanes)")
     ap.add_argument("--multi", choices=["spec", "replicas"], default="spec",
                     help="N>1: speculative lambda search over RCCL (one job) or independent replicas")
     ap.add_argument("--same-device", action="store_true",

@@ -25,20 +25,16 @@
 
 using pgo::DevGraph;
 
-// An extra concurrent lambda try on the handle's GPU (lanes 1..L-1; lane 0 is
-// the handle's own stream and buffers): its own factor workspace (a clone of
-// the Cholesky plan's numeric buffers), solution, candidate values, scalars,
-// stream and captured factor+solve graph.  The linearisation (D, V, g) and the
-// current values are shared read-only.
+// Lambda lane l >= 1 of a batched factorisation (lane 0 is the handle's own
+// buffers): the Cholesky plan holds a numeric workspace per lane and every
+// launch of the factor + solve carries the lanes as grid dimension y, so L
+// consecutive lambda tries cost one pass over the (mostly latency-bound)
+// schedule.  Per lane: candidate values, reduction partials and scalars of its
+// try; the linearisation (D, V, g) and the current values are shared.
 struct Lane {
-  pgo::CholPlan plan;
-  double* x = nullptr;
   double4* pose_cand = nullptr;
   double* part = nullptr;
   double* scal = nullptr;
-  hipStream_t stream = nullptr;
-  hipGraphExec_t exec = nullptr;
-  double* h_buf = nullptr;                  // pinned: [0..2] scalars, [3] flag, [4] lambda
 };
 
 struct pgo_graph {
@@ -81,7 +77,10 @@ struct pgo_graph {
   // ---- multi-GPU speculative lambda search (pgo_comm_*) ----
   pgo::Comm comm;
   std::vector<Lane> lanes;                  // lanes 1..L-1 (speculative tries on this GPU)
-  hipEvent_t lin_done = nullptr;            // linearisation complete (lanes wait on it)
+  double* xb = nullptr;                     // [L x 3n] solutions of a batched factor + solve
+  hipGraphExec_t lane_exec[9] = {};         // captured batched factor + solve, per lane count
+  double* h_lanes = nullptr;                // pinned [48]: 4 scalars per lane, lambdas at 32, flags at 40
+  hipEvent_t lin_done = nullptr;            // linearisation complete
   int lane_cap = 8;                         // 1 after a lane allocation failed (reset per plan)
   // ---- closest-keyframe search scratch ----
   double* s_d = nullptr;                    // [kMaxBlocks + 1] partial / final distances
@@ -148,17 +147,19 @@ int information(const double* q, double* om6) {
 }
 
 void free_lanes(pgo_graph* g) {
+  if (g->d.stream) (void)hipStreamSynchronize(g->d.stream);
   for (Lane& ln : g->lanes) {
-    if (ln.stream) (void)hipStreamSynchronize(ln.stream);
-    if (ln.exec) (void)hipGraphExecDestroy(ln.exec);
-    pgo::chol_free_clone(ln.plan);
-    void* ptrs[] = {ln.x, ln.pose_cand, ln.part, ln.scal};
+    void* ptrs[] = {ln.pose_cand, ln.part, ln.scal};
     for (void* q : ptrs)
       if (q) (void)hipFree(q);
-    if (ln.stream) (void)hipStreamDestroy(ln.stream);
-    if (ln.h_buf) (void)hipHostFree(ln.h_buf);
   }
   g->lanes.clear();
+  if (g->xb) (void)hipFree(g->xb);
+  g->xb = nullptr;
+  for (auto& e : g->lane_exec) {
+    if (e) (void)hipGraphExecDestroy(e);
+    e = nullptr;
+  }
 }
 
 void free_device(pgo_graph* g) {
@@ -191,6 +192,7 @@ int ensure_hip(pgo_graph* g) {
   HIP_TRY(g, hipHostMalloc((void**)&g->h_scal, 16 * sizeof(double), hipHostMallocDefault));
   HIP_TRY(g, hipHostMalloc((void**)&g->h_ctrl, 4 * sizeof(int), hipHostMallocDefault));
   HIP_TRY(g, hipHostMalloc((void**)&g->h_lam, sizeof(double), hipHostMallocDefault));
+  HIP_TRY(g, hipHostMalloc((void**)&g->h_lanes, 48 * sizeof(double), hipHostMallocDefault));
   for (auto& e : g->ev) HIP_TRY(g, hipEventCreate(&e));
   for (auto& e : g->pev) HIP_TRY(g, hipEventCreate(&e));
   HIP_TRY(g, hipEventCreateWithFlags(&g->lin_done, hipEventDisableTiming));
@@ -630,92 +632,111 @@ int finish_solve(pgo_graph* g, pgo_stats* st, SolveState* ss) {
   return PGO_OK;
 }
 
-// Lanes 1..want-1 over the current Cholesky plan; returns the lane count
-// available (fewer when HBM runs out: each lane holds a full factor workspace).
+// Lanes 1..want-1 over the current Cholesky plan (numeric workspaces for want
+// lanes); returns the lane count available (fewer when HBM runs out: each lane
+// holds a full set of fronts).
 int ensure_lanes(pgo_graph* g, int want) {
   want = std::max(1, std::min({want, 8, g->lane_cap}));
-  if ((int)g->lanes.size() == want - 1) return want;
+  if ((int)g->lanes.size() == want - 1 && g->chol.batch >= want) return want;
   free_lanes(g);
   const DevGraph& d = g->d;
-  for (int l = 1; l < want; l++) {
-    g->lanes.emplace_back();
-    Lane& ln = g->lanes.back();
-    bool ok = pgo::chol_clone(g->chol, ln.plan, d.stream) == hipSuccess &&
-              hipMalloc((void**)&ln.x, sizeof(double) * 3 * std::max(d.n, 1)) == hipSuccess &&
-              hipMalloc((void**)&ln.pose_cand, sizeof(double4) * std::max(d.n, 1)) == hipSuccess &&
-              hipMalloc((void**)&ln.part, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices) == hipSuccess &&
-              hipMalloc((void**)&ln.scal, sizeof(double) * 16) == hipSuccess &&
-              hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking) == hipSuccess &&
-              hipHostMalloc((void**)&ln.h_buf, 8 * sizeof(double), hipHostMallocDefault) == hipSuccess;
-    if (ok) ok = hipMemsetAsync(ln.part, 0, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices, ln.stream) ==
-                 hipSuccess && hipStreamSynchronize(ln.stream) == hipSuccess;
-    if (!ok) {  // out of memory (or similar): one lane, and do not try again for this plan
+  if (g->chol.batch != want) {
+    // the captured one-lane graph holds the old workspace pointers
+    if (g->chol_exec) (void)hipGraphExecDestroy(g->chol_exec);
+    g->chol_exec = nullptr;
+    if (pgo::chol_set_batch(g->chol, want, d.stream) != hipSuccess) {
       (void)hipGetLastError();
-      free_lanes(g);
       g->lane_cap = 1;
       return 1;
     }
   }
-  return (int)g->lanes.size() + 1;
+  bool ok = hipMalloc((void**)&g->xb, sizeof(double) * 3 * std::max(d.n, 1) * want) == hipSuccess;
+  for (int l = 1; l < want && ok; l++) {
+    g->lanes.emplace_back();
+    Lane& ln = g->lanes.back();
+    ok = hipMalloc((void**)&ln.pose_cand, sizeof(double4) * std::max(d.n, 1)) == hipSuccess &&
+         hipMalloc((void**)&ln.part, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices) == hipSuccess &&
+         hipMalloc((void**)&ln.scal, sizeof(double) * 16) == hipSuccess &&
+         hipMemsetAsync(ln.part, 0, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices, d.stream) == hipSuccess;
+  }
+  if (ok) ok = hipStreamSynchronize(d.stream) == hipSuccess;
+  if (!ok) {  // out of memory (or similar): one lane, and do not try again for this plan
+    (void)hipGetLastError();
+    free_lanes(g);
+    if (g->chol_exec) (void)hipGraphExecDestroy(g->chol_exec);
+    g->chol_exec = nullptr;
+    (void)pgo::chol_set_batch(g->chol, 1, d.stream);
+    g->lane_cap = 1;
+    return 1;
+  }
+  return want;
 }
 
-// The device view of lane l (lane 0: the handle's own)
+// The device view of lane l's try (lane 0: the handle's own buffers), solution in xb
 DevGraph lane_view(const pgo_graph* g, int l) {
   DevGraph v = g->d;
+  v.x = g->xb + (size_t)l * 3 * g->d.n;
   if (l == 0) return v;
   const Lane& ln = g->lanes[l - 1];
-  v.x = ln.x;
   v.pose_cand = ln.pose_cand;
   v.part = ln.part;
   v.scal = ln.scal;
-  v.stream = ln.stream;
   return v;
 }
 
-// Enqueue one lambda try on lane l >= 1 (after the linearisation, lin_done):
-// factor + solve (captured graph), model decrease, retract, error; scalars and
-// the pivot flag land in the lane's pinned buffer once its stream drains.
-int enqueue_lane_try(pgo_graph* g, const pgo_params& p, int l, double lam) {
-  Lane& ln = g->lanes[l - 1];
-  const DevGraph v = lane_view(g, l);
-  HIP_TRY(g, hipStreamWaitEvent(ln.stream, g->lin_done, 0));
-  ln.h_buf[4] = lam;
-  HIP_TRY(g, hipMemcpyAsync(ln.plan.d_lambda, ln.h_buf + 4, sizeof(double), hipMemcpyHostToDevice, ln.stream));
-  if (p.use_graphs) {
-    if (!ln.exec) {
+// nb >= 2 consecutive lambda tries in one batched factor + solve (captured
+// graph per lane count), then per lane: model decrease, retract, error; one
+// read-back.  out[4 l ..] = {solved, new error, delta'H delta, g'delta}.
+int run_lanes(pgo_graph* g, const pgo_params& p, int nb, const double* lams, double* out, pgo_stats* st) {
+  DevGraph& d = g->d;
+  hipEvent_t* ev = g->ev;
+  g->factorizations++;
+  for (int l = 0; l < nb; l++) g->h_lanes[4 * 8 + l] = lams[l];
+  HIP_TRY(g, hipEventRecord(ev[2], d.stream));
+  HIP_TRY(g, hipMemcpyAsync(g->chol.d_lambda, g->h_lanes + 4 * 8, nb * sizeof(double), hipMemcpyHostToDevice,
+                            d.stream));
+  if (!p.use_graphs) {
+    HIP_TRY(g, pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr, nb));
+    HIP_TRY(g, pgo::chol_solve(g->chol, g->xb, d.stream, nb, 3LL * d.n));
+  } else {
+    if (!g->lane_exec[nb]) {
       hipGraph_t graph = nullptr;
-      HIP_TRY(g, hipStreamBeginCapture(ln.stream, hipStreamCaptureModeThreadLocal));
-      const hipError_t e1 = pgo::chol_factor(ln.plan, v.D, v.V, v.g, -1.0, ln.stream, nullptr);
-      const hipError_t e2 = pgo::chol_solve(ln.plan, ln.x, ln.stream);
-      HIP_TRY(g, hipStreamEndCapture(ln.stream, &graph));
+      HIP_TRY(g, hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal));
+      const hipError_t e1 = pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr, nb);
+      const hipError_t e2 = pgo::chol_solve(g->chol, g->xb, d.stream, nb, 3LL * d.n);
+      HIP_TRY(g, hipStreamEndCapture(d.stream, &graph));
       HIP_TRY(g, e1);
       HIP_TRY(g, e2);
-      HIP_TRY(g, hipGraphInstantiate(&ln.exec, graph, nullptr, nullptr, 0));
+      HIP_TRY(g, hipGraphInstantiate(&g->lane_exec[nb], graph, nullptr, nullptr, 0));
       HIP_TRY(g, hipGraphDestroy(graph));
     }
-    HIP_TRY(g, hipGraphLaunch(ln.exec, ln.stream));
-  } else {
-    HIP_TRY(g, pgo::chol_factor(ln.plan, v.D, v.V, v.g, -1.0, ln.stream, nullptr));
-    HIP_TRY(g, pgo::chol_solve(ln.plan, ln.x, ln.stream));
+    HIP_TRY(g, hipGraphLaunch(g->lane_exec[nb], d.stream));
   }
-  HIP_TRY(g, pgo::launch_model_decrease(v, v.x, v.scal + 1));
-  HIP_TRY(g, pgo::launch_retract(v, v.x));
-  HIP_TRY(g, pgo::launch_error(v, v.pose_cand, v.scal));
-  HIP_TRY(g, hipMemcpyAsync(ln.h_buf, v.scal, 3 * sizeof(double), hipMemcpyDeviceToHost, ln.stream));
-  HIP_TRY(g, hipMemcpyAsync(ln.h_buf + 3, ln.plan.d_flag, sizeof(int), hipMemcpyDeviceToHost, ln.stream));
-  return PGO_OK;
-}
-
-// after enqueue_lane_try: out = {solved, new error, delta'H delta, g'delta}
-int collect_lane_try(pgo_graph* g, int l, double* out) {
-  Lane& ln = g->lanes[l - 1];
-  HIP_TRY(g, hipStreamSynchronize(ln.stream));
-  int flag = 0;
-  std::memcpy(&flag, ln.h_buf + 3, sizeof(int));
-  out[0] = flag == 0 ? 1.0 : 0.0;
-  out[1] = ln.h_buf[0];
-  out[2] = ln.h_buf[1];
-  out[3] = ln.h_buf[2];
+  HIP_TRY(g, hipEventRecord(ev[3], d.stream));
+  for (int l = 0; l < nb; l++) {
+    const DevGraph v = lane_view(g, l);
+    HIP_TRY(g, pgo::launch_model_decrease(v, v.x, v.scal + 1));
+    HIP_TRY(g, pgo::launch_retract(v, v.x));
+    HIP_TRY(g, pgo::launch_error(v, v.pose_cand, v.scal));
+    HIP_TRY(g, hipMemcpyAsync(g->h_lanes + 4 * l, v.scal, 3 * sizeof(double), hipMemcpyDeviceToHost, d.stream));
+  }
+  HIP_TRY(g, hipMemcpyAsync(g->h_lanes + 4 * 8 + 8, g->chol.d_flag, nb * sizeof(int), hipMemcpyDeviceToHost,
+                            d.stream));
+  HIP_TRY(g, hipEventRecord(ev[4], d.stream));
+  HIP_TRY(g, hipStreamSynchronize(d.stream));
+  int flags[8];
+  std::memcpy(flags, g->h_lanes + 4 * 8 + 8, nb * sizeof(int));
+  for (int l = 0; l < nb; l++) {
+    out[4 * l] = flags[l] == 0 ? 1.0 : 0.0;
+    out[4 * l + 1] = g->h_lanes[4 * l];
+    out[4 * l + 2] = g->h_lanes[4 * l + 1];
+    out[4 * l + 3] = g->h_lanes[4 * l + 2];
+  }
+  if (st) {
+    st->ms_solve += ms_between(ev[2], ev[3]);
+    st->ms_update += ms_between(ev[3], ev[4]);
+    st->factor_flops = g->chol.flops;
+  }
   return PGO_OK;
 }
 
@@ -820,6 +841,7 @@ void pgo_destroy(pgo_graph* g) {
     if (g->h_scal) (void)hipHostFree(g->h_scal);
     if (g->h_ctrl) (void)hipHostFree(g->h_ctrl);
     if (g->h_lam) (void)hipHostFree(g->h_lam);
+    if (g->h_lanes) (void)hipHostFree(g->h_lanes);
     for (auto& e : g->pev)
       if (e) (void)hipEventDestroy(e);
     if (g->lin_done) (void)hipEventDestroy(g->lin_done);
@@ -1041,6 +1063,16 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   // pose_cand, error there and the linear model decrease; one read-back.
   // out = {solved, new error, delta'H delta, g'delta}.
   bool first_try = true;
+  auto account_linearize = [&]() {   // after the first try of a linearisation has synchronised
+    if (!first_try) return;
+    const double lin_ms = ms_between(ev[0], ev[1]);
+    st.ms_linearize += lin_ms;
+    if (p.profile_every > 0) {
+      st.kernel_linearize_ms += lin_ms;
+      st.kernel_linearize_count++;
+    }
+    first_try = false;
+  };
   auto run_try = [&](double lam_try, double* out) -> int {
     SolveState ss;
     HIP_TRY(g, hipEventRecord(ev[2], d.stream));
@@ -1055,15 +1087,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
     HIP_TRY(g, hipEventRecord(ev[4], d.stream));
     RC_TRY(sync_scalars(g, 3));
     RC_TRY(finish_solve(g, &st, &ss));
-    if (first_try) {
-      const double lin_ms = ms_between(ev[0], ev[1]);
-      st.ms_linearize += lin_ms;
-      if (p.profile_every > 0) {
-        st.kernel_linearize_ms += lin_ms;
-        st.kernel_linearize_count++;
-      }
-      first_try = false;
-    }
+    account_linearize();
     st.ms_solve += ms_between(ev[2], ev[3]);
     st.ms_update += ms_between(ev[3], ev[4]);
     out[0] = ss.solved ? 1.0 : 0.0;
@@ -1131,14 +1155,15 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
           const int Lr = prof_next ? 1 : L;
           std::vector<double> mine(4 * L, 0.0);
           for (int l = 0; l < L; l++) mine[4 * l] = -1.0;  // -1: no try (past the bound / lane idle)
-          for (int l = 1; l < Lr; l++)
-            if (valid[me * L + l]) {
-              RC_TRY(enqueue_lane_try(g, p, l, lam_k[me * L + l]));
-              st.solves++;
-            }
-          if (valid[me * L]) RC_TRY(run_try(lam_k[me * L], &mine[0]));
-          for (int l = 1; l < Lr; l++)
-            if (valid[me * L + l]) RC_TRY(collect_lane_try(g, l, &mine[4 * l]));
+          int nb = 0;   // this rank's valid tries (a prefix of its lanes)
+          while (nb < Lr && valid[me * L + nb]) nb++;
+          if (nb == 1) {
+            RC_TRY(run_try(lam_k[me * L], &mine[0]));
+          } else if (nb > 1) {
+            RC_TRY(run_lanes(g, p, nb, &lam_k[me * L], mine.data(), &st));
+            st.solves += nb;
+            account_linearize();
+          }
           st.lambda_rounds++;
           if (P > 1) {
             const auto c0 = std::chrono::steady_clock::now();

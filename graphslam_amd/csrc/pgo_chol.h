@@ -65,6 +65,7 @@ enum { kOrderNd = 0, kOrderAmd = 1 };
 
 struct CholPlan {
   int ordering = kOrderNd;         // fill-reducing ordering of the pose graph (input of chol_analyze)
+  int batch = 1;                   // lambda lanes with a numeric workspace (input of chol_upload)
   // ---- host symbolic result ----
   int n = 0, ns = 0;
   long long nslots = 0;            // block-CSR slots of the analysed pattern (stride of V)
@@ -153,10 +154,9 @@ std::vector<int> order_nd(int n, const std::vector<int>& xadj, const std::vector
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
 hipError_t chol_upload(CholPlan& P, hipStream_t s);
 void chol_free(CholPlan& P);
-// second numeric workspace over src's symbolic plan (shares src's device index
-// arrays; free with chol_free_clone before src is freed)
-hipError_t chol_clone(const CholPlan& src, CholPlan& dst, hipStream_t s);
-void chol_free_clone(CholPlan& P);
+// numeric workspaces for nb lambda lanes (P.batch); on failure one lane is kept
+// and the allocation error returned
+hipError_t chol_set_batch(CholPlan& P, int nb, hipStream_t s);
 
 // device: factor H + lambda I (D: 6 doubles/pose upper, V: slot blocks as structure of
 // arrays V[q * nslots + slot], old indexing; only the slots in asm_src are read)
@@ -170,12 +170,16 @@ struct SyrkProfile {
 // lambda is read from P.d_lambda (set it with a stream-ordered copy first).  The
 // right-hand side scale_b * b (old pose indexing) is carried through the
 // factorisation as an extra column: on return the frontal vectors hold y = L^-1 b.
+// nb <= P.batch lanes at once: lane y factors H + lambda[y] I (lambda = P.d_lambda[y])
+// in its own workspace, grid dimension y of every launch (bitwise equal to a
+// one-lane factorisation)
 hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
-                       hipStream_t s, SyrkProfile* prof = nullptr);
+                       hipStream_t s, SyrkProfile* prof = nullptr, int nb = 1);
 // after chol_factor: 3x3 blocks of (L L^T)^{-1} at the given poses (old index),
 // row-major 9 doubles each into host memory out (synchronises the stream)
 hipError_t chol_marginals(const CholPlan& P, const int* poses, int n, double* out, hipStream_t s);
 // after chol_factor: x = L^-T y = (L L^T)^{-1} scale_b b, indexed by old pose
-hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s);
+// lane y's solution to x + y * xstride
+hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb = 1, long long xstride = 0);
 
 }  // namespace pgo

@@ -34,7 +34,21 @@ struct CholDev {
   const int *asm_front, *asm_li, *asm_lj, *asm_ptr, *asm_src;
   const int *dg_front, *dg_loc, *perm, *dg_order;
   int* flag;
+  // lambda lanes: lane y = blockIdx.y works on its own numeric workspace
+  long long fst, tst;              // F, Tinv doubles per lane
+  int vst, xst, pst;               // fv, xv, backward partials per lane
 };
+
+// this workgroup's lane (blockIdx.y): every lane factors H + lambda_y I with
+// the same schedule, so lanes are bitwise equal to one-lane runs
+__device__ __forceinline__ void lane_offset(CholDev& c) {
+  const int y = blockIdx.y;
+  c.F += y * c.fst;
+  c.Tinv += y * c.tst;
+  c.fv += y * c.vst;
+  c.xv += y * c.xst;
+  c.flag += y;
+}
 
 static CholDev dev_view(const CholPlan& P) {
   CholDev c;
@@ -46,6 +60,11 @@ static CholDev dev_view(const CholPlan& P) {
   c.asm_src = P.d_asm_src; c.dg_front = P.d_dg_front; c.dg_loc = P.d_dg_loc; c.perm = P.d_perm;
   c.dg_order = P.d_dg_order;
   c.flag = P.d_flag;
+  c.fst = P.ftotal;
+  c.tst = P.ttotal;
+  c.vst = P.vtotal;
+  c.xst = 3 * P.n;
+  c.pst = std::max(P.npart, 1) * 64;
   return c;
 }
 
@@ -63,6 +82,7 @@ __device__ long long g_diag_clk[32];
 // off-diagonal lower blocks H_{i,j} (i > j) of a front: sum of their slots
 __global__ __launch_bounds__(256) void k_asm_offdiag(CholDev c, const double* __restrict__ V, long long S,
                                                      int t0, int t1) {
+  lane_offset(c);
   const int t = t0 + blockIdx.x * 256 + threadIdx.x;
   if (t >= t1) return;
   const int s = c.asm_front[t];
@@ -84,6 +104,8 @@ __global__ __launch_bounds__(256) void k_asm_offdiag(CholDev c, const double* __
 // diagonal blocks H_jj + lambda I (lower part)
 __global__ __launch_bounds__(256) void k_asm_diag(CholDev c, const double* __restrict__ D,
                                                  const double* __restrict__ lam_p, int t0, int t1) {
+  lane_offset(c);
+  lam_p += blockIdx.y;
   const int t = t0 + blockIdx.x * 256 + threadIdx.x;
   if (t >= t1) return;
   const int j = c.dg_order[t];
@@ -110,6 +132,7 @@ __global__ __launch_bounds__(256) void k_asm_diag(CholDev c, const double* __res
 // coalesced), the 4 waves take every 4th column; loads first.
 __global__ __launch_bounds__(256) void k_extend_add(CholDev c, const int4* __restrict__ tasks,
                                                     const int4* __restrict__ pairs) {
+  lane_offset(c);
   __shared__ int prow[64];
   __shared__ long long pcol[64];
   const int4 t = tasks[blockIdx.x];
@@ -221,6 +244,7 @@ __device__ __forceinline__ void copy_in(double* __restrict__ dst, const double* 
 // m <= 128: the whole front in LDS; right-looking, two threads per row (the
 // row's columns split even/odd) so LDS accesses of a wave are consecutive rows.
 __global__ __launch_bounds__(256) void k_front_small(CholDev c, const int* __restrict__ list) {
+  lane_offset(c);
   extern __shared__ __attribute__((aligned(16))) double A[];   // m*m front, 64 scratch, m frontal vector
   const int s = list[blockIdx.x];
   const int m = c.m[s], w = c.w[s];
@@ -276,6 +300,7 @@ __global__ __launch_bounds__(256) void k_front_small(CholDev c, const int* __res
 // the w x w inverse for the backward solve is formed lane = column.
 template <bool kTwoRows>   // m > 64: lane also owns row l + 64
 __global__ __launch_bounds__(64) void k_front_wave(CholDev c, const int* __restrict__ list) {
+  lane_offset(c);
   constexpr int W = kWaveW, LDP = kWaveW + 1;   // odd row stride: conflict-free per-lane rows
   extern __shared__ __attribute__((aligned(16))) double S[];
   const int s = list[blockIdx.x];
@@ -566,6 +591,7 @@ __device__ __forceinline__ void panel_rhs(double* v, const double* X, int nb, do
 // (diag_factor_invert); L back into the front, L^-1 into Tinv for the TRSM GEMM
 // and the solves.
 __global__ __launch_bounds__(256) void k_panel_diag(CholDev c, const int* __restrict__ list, int kb) {
+  lane_offset(c);
   __shared__ double Ts[64 * 65];
   __shared__ double Ws[64 * 65];
   __shared__ double bc[64];
@@ -594,6 +620,7 @@ __global__ __launch_bounds__(256) void k_panel_diag(CholDev c, const int* __rest
 // Rows below the diagonal tile, 64 per workgroup (16 per wave): X = B L^-T as a
 // GEMM with the inverted tile, v_mfma_f64_16x16x4_f64, B fragments from global.
 __global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __restrict__ tasks, int kb) {
+  lane_offset(c);
   constexpr int LDB = 81;
   __shared__ __attribute__((aligned(16))) double Tb[64 * LDB];  // Tb[k*LDB + j] = Tinv[j][k]
   const int2 task = tasks[blockIdx.x];
@@ -726,6 +753,7 @@ __device__ __forceinline__ void syrk_tile64(const CholDev& c, const int4 t, int 
 
 // register-fragment variant (kept for the microbenchmark; k_panel_syrk_lds is launched)
 __global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int4* __restrict__ tasks, int kb) {
+  lane_offset(c);
   syrk_tile64<false>(c, tasks[blockIdx.x], kb, nullptr);
 }
 
@@ -819,6 +847,7 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
 }
 
 __global__ __launch_bounds__(256) void k_panel_syrk_lds(CholDev c, const int4* __restrict__ tasks, int kb) {
+  lane_offset(c);
   __shared__ __attribute__((aligned(16))) double smem[4 * 16 * 68];
   syrk_lds_body(c, tasks[blockIdx.x], kb, smem);
 }
@@ -934,6 +963,7 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
 constexpr int kDiagSmem = 64 * 65 + 64 * 68 + 64;
 
 __global__ __launch_bounds__(256) void k_syrk_diag(CholDev c, const int4* __restrict__ tasks, int kb) {
+  lane_offset(c);
   __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
   syrk_diag_body(c, tasks[blockIdx.x], kb, smem);
 }
@@ -944,6 +974,7 @@ __global__ __launch_bounds__(256) void k_syrk_diag(CholDev c, const int4* __rest
 // rest the 64x64 update tiles (k_panel_syrk_lds).
 __global__ __launch_bounds__(256) void k_step_fused(CholDev c, const int4* __restrict__ sdiag, int nsd,
                                                     const int4* __restrict__ tasks, int kb) {
+  lane_offset(c);
   __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
   const int b = blockIdx.x;
   if (b < nsd) syrk_diag_body(c, sdiag[b], kb, smem);
@@ -956,6 +987,7 @@ __global__ __launch_bounds__(256) void k_step_fused(CholDev c, const int4* __res
 // MFMAs of chunk c run); each wave owns 64x64 of the tile as 4x4
 // v_mfma_f64_16x16x4_f64 blocks.
 __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __restrict__ tasks, int kb) {
+  lane_offset(c);
   constexpr int LD = 144;   // [k][row] rows of 128 + pad
   __shared__ __attribute__((aligned(16))) double Sr[2][16 * LD];
   __shared__ __attribute__((aligned(16))) double Sc[2][16 * LD];
@@ -1052,6 +1084,7 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
 // tasks [0, n), grid-stride: a small grid zeroes in the background without
 // taking the CUs the latency-bound panel kernels need
 __global__ __launch_bounds__(256) void k_zero_lower(CholDev c, const int4* __restrict__ tasks, int n) {
+  lane_offset(c);
   for (int q0 = blockIdx.x; q0 < n; q0 += gridDim.x) {
     const int4 t = tasks[q0];
     const int m = c.m[t.x];
@@ -1071,6 +1104,7 @@ __global__ __launch_bounds__(256) void k_zero_lower(CholDev c, const int4* __res
 
 // ------------------------------------------------------------ solves
 __global__ __launch_bounds__(256) void k_perm_in(CholDev c, const double* __restrict__ b, double scale, int n) {
+  lane_offset(c);
   const int j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
   const int o = c.perm[j];
@@ -1078,7 +1112,9 @@ __global__ __launch_bounds__(256) void k_perm_in(CholDev c, const double* __rest
   for (int a = 0; a < 3; a++) c.xv[3 * j + a] = scale * b[3 * o + a];
 }
 
-__global__ __launch_bounds__(256) void k_perm_out(CholDev c, double* __restrict__ x, int n) {
+__global__ __launch_bounds__(256) void k_perm_out(CholDev c, double* __restrict__ x, int n, long long xstride) {
+  lane_offset(c);
+  x += blockIdx.y * xstride;
   const int j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
   const int o = c.perm[j];
@@ -1112,6 +1148,7 @@ __device__ __forceinline__ double tinv_col_dot(const TinvCol& t, const double* z
 // vectors (fixed order).  The factorisation then carries them as an extra
 // column (forward substitution fused into the panels).
 __global__ __launch_bounds__(256) void k_vec_assemble(CholDev c, const int* __restrict__ list) {
+  lane_offset(c);
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* v = sm;                  // m
   const int s = list[blockIdx.x];
@@ -1150,6 +1187,8 @@ __device__ __forceinline__ void halve(double* acc, int lane) {
 // L[r, c0+j] x_r (rows below the pivot columns; x gathered from xv).
 __global__ __launch_bounds__(256) void k_bwd_part(CholDev c, const int4* __restrict__ tasks,
                                                   double* __restrict__ part) {
+  lane_offset(c);
+  part += blockIdx.y * c.pst;
   __shared__ double red[4][64];
   const int4 t = tasks[blockIdx.x];
   const int s = t.x, c0 = t.y, r0 = t.z, slot = t.w;
@@ -1183,6 +1222,8 @@ __global__ __launch_bounds__(256) void k_bwd_part(CholDev c, const int4* __restr
 // order); the owner of the last block then solves it.
 __global__ __launch_bounds__(256) void k_bwd_init(CholDev c, const int4* __restrict__ tasks,
                                                   const int2* __restrict__ pref, const double* __restrict__ part) {
+  lane_offset(c);
+  part += blockIdx.y * c.pst;
   __shared__ double z[64];
   const int4 t = tasks[blockIdx.x];
   const int s = t.x, c0 = t.y, c1 = t.z, owner = t.w;
@@ -1215,6 +1256,7 @@ __global__ __launch_bounds__(256) void k_bwd_init(CholDev c, const int4* __restr
 // Backward step b: z_j -= L[block b, j]' x_b for the task's columns (< 64 b);
 // the owner of block b-1 then solves it.
 __global__ __launch_bounds__(256) void k_bwd_step(CholDev c, const int4* __restrict__ tasks, int b) {
+  lane_offset(c);
   __shared__ double xbk[64];
   __shared__ double z[64];
   const int4 t = tasks[blockIdx.x];
@@ -1273,6 +1315,7 @@ __global__ __launch_bounds__(256) void k_bwd_step(CholDev c, const int4* __restr
 // v lives in a per-workgroup global scratch (two buffers of 3 x maxm).
 __global__ __launch_bounds__(256) void k_marginals(CholDev c, const int2* __restrict__ start, int maxm,
                                                    double* __restrict__ scratch, double* __restrict__ out) {
+  lane_offset(c);
   __shared__ double ys[3][64];
   __shared__ double red[6][4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1377,14 +1420,45 @@ static hipError_t up(T** d, const std::vector<T>& h, hipStream_t s) {
     if (e_ != hipSuccess) return e_;    \
   } while (0)
 
+// numeric workspaces of nb lanes (fronts zeroed: the upper triangles stay zero)
+static void free_numeric(CholPlan& P) {
+  void* ptrs[] = {P.F, P.Tinv, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_partial};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  P.F = P.Tinv = P.fv = P.xv = P.d_lambda = P.d_partial = nullptr;
+  P.d_flag = nullptr;
+  P.batch = 0;
+}
+
+static hipError_t alloc_numeric(CholPlan& P, int nb, hipStream_t s) {
+  CH_TRY(hipMalloc((void**)&P.F, nb * std::max<long long>(P.ftotal, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.Tinv, nb * std::max<long long>(P.ttotal, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.fv, (size_t)nb * std::max(P.vtotal, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.xv, (size_t)nb * std::max(3 * P.n, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.d_flag, nb * sizeof(int)));
+  CH_TRY(hipMalloc((void**)&P.d_lambda, nb * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.d_partial, (size_t)nb * std::max(P.npart, 1) * 64 * sizeof(double)));
+  CH_TRY(hipMemsetAsync(P.F, 0, nb * std::max<long long>(P.ftotal, 1) * sizeof(double), s));
+  P.batch = nb;
+  return hipStreamSynchronize(s);
+}
+
+hipError_t chol_set_batch(CholPlan& P, int nb, hipStream_t s) {
+  if (nb == P.batch) return hipSuccess;
+  CH_TRY(hipStreamSynchronize(s));
+  free_numeric(P);
+  const hipError_t e = alloc_numeric(P, nb, s);
+  if (e != hipSuccess) {   // keep one lane
+    (void)hipGetLastError();
+    free_numeric(P);
+    CH_TRY(alloc_numeric(P, 1, s));
+    return e;
+  }
+  return hipSuccess;
+}
+
 hipError_t chol_upload(CholPlan& P, hipStream_t s) {
-  CH_TRY(hipMalloc((void**)&P.F, std::max<long long>(P.ftotal, 1) * sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.Tinv, std::max<long long>(P.ttotal, 1) * sizeof(double)));
   CH_TRY(up(&P.d_toff, P.toff, s));
-  CH_TRY(hipMalloc((void**)&P.fv, std::max(P.vtotal, 1) * sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.xv, std::max(3 * P.n, 1) * sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.d_flag, sizeof(int)));
-  CH_TRY(hipMalloc((void**)&P.d_lambda, sizeof(double)));
   CH_TRY(up(&P.d_m, P.m, s));
   CH_TRY(up(&P.d_w, P.w, s));
   CH_TRY(up(&P.d_voff, P.voff, s));
@@ -1411,12 +1485,11 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(up(&P.d_bwd, P.bwd_tasks, s));
   CH_TRY(up(&P.d_bwd_pref, P.bwd_pref, s));
   CH_TRY(up(&P.d_bwd_part, P.bwd_part_tasks, s));
-  CH_TRY(hipMalloc((void**)&P.d_partial, std::max(P.npart, 1) * 64 * sizeof(double)));
   CH_TRY(up(&P.d_syrk, P.syrk_tasks, s));
   CH_TRY(up(&P.d_sdiag, P.sdiag_tasks, s));
   CH_TRY(up(&P.d_zero, P.zero_tasks, s));
   CH_TRY(up(&P.d_dg_order, P.dg_order, s));
-  CH_TRY(hipMemsetAsync(P.F, 0, std::max<long long>(P.ftotal, 1) * sizeof(double), s));   // upper triangles stay zero
+  CH_TRY(alloc_numeric(P, std::max(P.batch, 1), s));
   CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
   CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
   CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));   // (a non-default priority measured 1.5x slower)
@@ -1441,56 +1514,20 @@ void chol_free(CholPlan& P) {
   P = CholPlan();
 }
 
-// A second numeric workspace over the same symbolic plan: the host schedules
-// and the device index arrays are shared with src (not owned); the fronts,
-// inverses, frontal vectors, flags, partials, side streams and events are the
-// clone's own, so two factorisations (two lambda tries) can run at once.
-hipError_t chol_clone(const CholPlan& src, CholPlan& P, hipStream_t s) {
-  P = src;
-  P.F = P.Tinv = P.fv = P.xv = P.d_lambda = P.d_partial = nullptr;
-  P.d_flag = nullptr;
-  P.side = P.side2 = P.side3 = nullptr;
-  for (auto& e : P.evs) e = nullptr;
-  CH_TRY(hipMalloc((void**)&P.F, std::max<long long>(P.ftotal, 1) * sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.Tinv, std::max<long long>(P.ttotal, 1) * sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.fv, std::max(P.vtotal, 1) * sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.xv, std::max(3 * P.n, 1) * sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.d_flag, sizeof(int)));
-  CH_TRY(hipMalloc((void**)&P.d_lambda, sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.d_partial, std::max(P.npart, 1) * 64 * sizeof(double)));
-  CH_TRY(hipMemsetAsync(P.F, 0, std::max<long long>(P.ftotal, 1) * sizeof(double), s));
-  CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
-  CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
-  CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));
-  for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  return hipStreamSynchronize(s);
-}
-
-void chol_free_clone(CholPlan& P) {
-  void* ptrs[] = {P.F, P.Tinv, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_partial};
-  for (void* p : ptrs)
-    if (p) (void)hipFree(p);
-  for (hipEvent_t e : P.evs)
-    if (e) (void)hipEventDestroy(e);
-  if (P.side) (void)hipStreamDestroy(P.side);
-  if (P.side2) (void)hipStreamDestroy(P.side2);
-  if (P.side3) (void)hipStreamDestroy(P.side3);
-  P = CholPlan();
-}
-
 hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
-                       hipStream_t s, SyrkProfile* prof) {
+                       hipStream_t s, SyrkProfile* prof, int nb) {
   if (P.n == 0) return hipSuccess;
+  if (nb < 1 || nb > P.batch) return hipErrorInvalidValue;
   const CholDev c = dev_view(P);
-  k_perm_in<<<(P.n + 255) / 256, 256, 0, s>>>(c, b, scale_b, P.n);
-  CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int), s));
+  k_perm_in<<<dim3((P.n + 255) / 256, nb), 256, 0, s>>>(c, b, scale_b, P.n);
+  CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int) * nb, s));
   // zeroing + assembly: leaf-level fronts on the main stream, the others on
   // side3 beside the leaf level (joined before level 1's extend-add)
   const int nz = P.zero_late, nt = (int)P.asm_front.size();
   auto assemble = [&](int z0, int z1, int a0, int a1, int d0, int d1, hipStream_t st) {
-    if (z1 > z0) k_zero_lower<<<z1 - z0, 256, 0, st>>>(c, P.d_zero + z0, z1 - z0);
-    if (a1 > a0) k_asm_offdiag<<<(a1 - a0 + 255) / 256, 256, 0, st>>>(c, V, P.nslots, a0, a1);
-    if (d1 > d0) k_asm_diag<<<(d1 - d0 + 255) / 256, 256, 0, st>>>(c, D, P.d_lambda, d0, d1);
+    if (z1 > z0) k_zero_lower<<<dim3(z1 - z0, nb), 256, 0, st>>>(c, P.d_zero + z0, z1 - z0);
+    if (a1 > a0) k_asm_offdiag<<<dim3((a1 - a0 + 255) / 256, nb), 256, 0, st>>>(c, V, P.nslots, a0, a1);
+    if (d1 > d0) k_asm_diag<<<dim3((d1 - d0 + 255) / 256, nb), 256, 0, st>>>(c, D, P.d_lambda, d0, d1);
   };
   assemble(0, P.zero_split, 0, P.asm_split, 0, P.dg_split, s);
   const bool fork_rest = P.zero_split < nz || P.asm_split < nt || P.dg_split < P.n;
@@ -1503,15 +1540,15 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
   for (size_t li = 0; li < P.levels.size(); li++) {
     const CholLevel& lv = P.levels[li];
     if (li == 1 && fork_rest) CH_TRY(hipStreamWaitEvent(s, P.evs[5], 0));
-    if (lv.ea_cnt[0]) k_extend_add<<<lv.ea_cnt[0], 256, 0, s>>>(c, P.d_ea_tasks + lv.ea_off[0], P.d_ea_pairs);
+    if (lv.ea_cnt[0]) k_extend_add<<<dim3(lv.ea_cnt[0], nb), 256, 0, s>>>(c, P.d_ea_tasks + lv.ea_off[0], P.d_ea_pairs);
     if ((int)li == P.zero_level) {   // update matrices consumed by now: zero them for the next factorisation
       CH_TRY(hipEventRecord(P.evs[4], s));
       CH_TRY(hipStreamWaitEvent(P.side3, P.evs[4], 0));
       const int nlate = (int)P.zero_tasks.size() - P.zero_late;
-      k_zero_lower<<<std::min(nlate, kZeroBackgroundGrid), 256, 0, P.side3>>>(c, P.d_zero + P.zero_late, nlate);
+      k_zero_lower<<<dim3(std::min(nlate, kZeroBackgroundGrid), nb), 256, 0, P.side3>>>(c, P.d_zero + P.zero_late, nlate);
       CH_TRY(hipEventRecord(P.evs[5], P.side3));
     }
-    k_vec_assemble<<<lv.front_cnt, 256, (size_t)lv.maxm * sizeof(double), s>>>(c, P.d_level_fronts + lv.front_off);
+    k_vec_assemble<<<dim3(lv.front_cnt, nb), 256, (size_t)lv.maxm * sizeof(double), s>>>(c, P.d_level_fronts + lv.front_off);
     // small fronts on the second side stream, beside the blocked path of the
     // same level (disjoint fronts); joined before the next level
     const bool fork_small = !lv.small.empty() && !lv.panels.empty();
@@ -1524,25 +1561,25 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
     for (const SmallClass& sc : lv.small) {
       if (sc.wave) {
         const size_t lds = (size_t)(sc.mmax * (kWaveW + 1) + 130 + kWaveW) * sizeof(double);
-        if (sc.mmax > 64) k_front_wave<true><<<sc.cnt, 64, lds, ss>>>(c, P.d_small + sc.off);
-        else k_front_wave<false><<<sc.cnt, 64, lds, ss>>>(c, P.d_small + sc.off);
+        if (sc.mmax > 64) k_front_wave<true><<<dim3(sc.cnt, nb), 64, lds, ss>>>(c, P.d_small + sc.off);
+        else k_front_wave<false><<<dim3(sc.cnt, nb), 64, lds, ss>>>(c, P.d_small + sc.off);
       }
       else
-        k_front_small<<<sc.cnt, 256, (size_t)(sc.mmax * sc.mmax + 64 + sc.mmax) * sizeof(double), ss>>>(
+        k_front_small<<<dim3(sc.cnt, nb), 256, (size_t)(sc.mmax * sc.mmax + 64 + sc.mmax) * sizeof(double), ss>>>(
             c, P.d_small + sc.off);
     }
     for (const PanelStep& ps : lv.panels) {
-      if (ps.potrf_cnt) k_panel_diag<<<ps.potrf_cnt, 256, 0, s>>>(c, P.d_potrf + ps.potrf_off, ps.kb);
-      if (ps.trsm_cnt) k_panel_trsm<<<ps.trsm_cnt, 256, 0, s>>>(c, P.d_trsm + ps.trsm_off, ps.kb);
+      if (ps.potrf_cnt) k_panel_diag<<<dim3(ps.potrf_cnt, nb), 256, 0, s>>>(c, P.d_potrf + ps.potrf_off, ps.kb);
+      if (ps.trsm_cnt) k_panel_trsm<<<dim3(ps.trsm_cnt, nb), 256, 0, s>>>(c, P.d_trsm + ps.trsm_off, ps.kb);
       if (ps.fused) {
-        k_step_fused<<<ps.sdiag_cnt + ps.syrk_cnt, 256, 0, s>>>(c, P.d_sdiag + ps.sdiag_off, ps.sdiag_cnt,
+        k_step_fused<<<dim3(ps.sdiag_cnt + ps.syrk_cnt, nb), 256, 0, s>>>(c, P.d_sdiag + ps.sdiag_off, ps.sdiag_cnt,
                                                                  (const int4*)(P.d_syrk + ps.syrk_off), ps.kb);
         continue;
       }
       if (ps.sdiag_cnt) {   // look-ahead: next panel's diagonal tiles on the side stream
         CH_TRY(hipEventRecord(P.evs[2], s));
         CH_TRY(hipStreamWaitEvent(P.side, P.evs[2], 0));
-        k_syrk_diag<<<ps.sdiag_cnt, 256, 0, P.side>>>(c, P.d_sdiag + ps.sdiag_off, ps.kb);
+        k_syrk_diag<<<dim3(ps.sdiag_cnt, nb), 256, 0, P.side>>>(c, P.d_sdiag + ps.sdiag_off, ps.kb);
         CH_TRY(hipEventRecord(P.evs[3], P.side));
       }
       if (ps.syrk_cnt) {
@@ -1551,10 +1588,10 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
         if (prof && prof->used < prof->cap) {
           const int u = prof->used++;
           prof->flops[u] = ps.syrk_flops;
-          hipExtLaunchKernelGGL(kern, dim3(ps.syrk_cnt), dim3(256), 0, s, prof->ev[2 * u], prof->ev[2 * u + 1], 0, c,
+          hipExtLaunchKernelGGL(kern, dim3(ps.syrk_cnt, nb), dim3(256), 0, s, prof->ev[2 * u], prof->ev[2 * u + 1], 0, c,
                                 tasks, ps.kb);
         } else {
-          kern<<<ps.syrk_cnt, 256, 0, s>>>(c, tasks, ps.kb);
+          kern<<<dim3(ps.syrk_cnt, nb), 256, 0, s>>>(c, tasks, ps.kb);
         }
       }
       if (ps.sdiag_cnt) CH_TRY(hipStreamWaitEvent(s, P.evs[3], 0));
@@ -1595,21 +1632,22 @@ hipError_t chol_marginals(const CholPlan& P, const int* poses, int n, double* ou
   return e;
 }
 
-hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s) {
+hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb, long long xstride) {
   if (P.n == 0) return hipSuccess;
+  if (nb < 1 || nb > P.batch) return hipErrorInvalidValue;
   const CholDev c = dev_view(P);
   const int g = (P.n + 255) / 256;
   for (auto it = P.levels.rbegin(); it != P.levels.rend(); ++it) {
     const CholLevel& lv = *it;
     if (lv.bwd_part.cnt)
-      k_bwd_part<<<lv.bwd_part.cnt, 256, 0, s>>>(c, P.d_bwd_part + lv.bwd_part.off, P.d_partial);
-    k_bwd_init<<<lv.bwd[0].cnt, 256, 0, s>>>(c, P.d_bwd + lv.bwd[0].off, P.d_bwd_pref + lv.bwd[0].off, P.d_partial);
+      k_bwd_part<<<dim3(lv.bwd_part.cnt, nb), 256, 0, s>>>(c, P.d_bwd_part + lv.bwd_part.off, P.d_partial);
+    k_bwd_init<<<dim3(lv.bwd[0].cnt, nb), 256, 0, s>>>(c, P.d_bwd + lv.bwd[0].off, P.d_bwd_pref + lv.bwd[0].off, P.d_partial);
     for (size_t q = 1; q < lv.bwd.size(); q++) {
       const int bb = lv.maxblk - (int)q;   // step b = maxblk-1 .. 1
-      if (lv.bwd[q].cnt) k_bwd_step<<<lv.bwd[q].cnt, 256, 0, s>>>(c, P.d_bwd + lv.bwd[q].off, bb);
+      if (lv.bwd[q].cnt) k_bwd_step<<<dim3(lv.bwd[q].cnt, nb), 256, 0, s>>>(c, P.d_bwd + lv.bwd[q].off, bb);
     }
   }
-  k_perm_out<<<g, 256, 0, s>>>(c, x, P.n);
+  k_perm_out<<<dim3(g, nb), 256, 0, s>>>(c, x, P.n, xstride);
   return hipGetLastError();
 }
 

@@ -99,13 +99,14 @@ typedef struct {
                                    linearisation with HIP events on the handle's
                                    stream (pgo_stats.kernel_*) [0] */
   int use_graphs;               /* replay the captured factor+solve hipGraph [1] */
-  int lambda_lanes;             /* Cholesky LM: lambda tries solved concurrently on
-                                   this GPU, each with its own factor workspace and
-                                   streams (speculative lambda search, see
-                                   pgo_comm_*); results are those of 1 lane bit for
-                                   bit.  Pays only with GPU_MAX_HW_QUEUES >= 4 x
-                                   lanes (C3: 2 lanes, 8 queues +10%; 4 queues -15%,
-                                   the lanes' streams share hardware queues) [1] */
+  int lambda_lanes;             /* Cholesky LM: consecutive lambda tries solved in
+                                   one batched factor + solve on this GPU (the plan
+                                   holds a numeric workspace per lane; every launch
+                                   carries the lanes as grid dimension y, so the
+                                   latency-bound top of the elimination tree costs
+                                   about one pass for all lanes).  Speculative
+                                   lambda search (see pgo_comm_*): results are
+                                   those of 1 lane bit for bit [1] */
 } pgo_params;
 
 typedef struct {

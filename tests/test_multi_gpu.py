@@ -149,6 +149,21 @@ def test_lanes_match_sequential(case, lanes, kw):
 
 
 @pytest.mark.gpu
+def test_lane_count_changes_on_one_handle():
+    """Lanes are numeric workspaces of the one plan (grid dimension y of every
+    launch): switching 2 -> 1 -> 3 -> 2 on the same handle re-allocates them and
+    re-captures the graphs; every run equals the sequential search bit for bit."""
+    from graphslam_amd.pose_graph import PoseGraph
+    g, init = _graph("C2p")
+    st1, x1 = _single("C2p", {})
+    pg = PoseGraph.from_dataset(g, device=0)
+    for lanes in (2, 1, 3, 2):
+        pg.set_poses(init)
+        st = pg.optimize(lambda_lanes=lanes)
+        _same(st, pg.poses(), st1, x1)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("case,world,kw", [
     ("C2p", 2, {"lambda_lanes": 1}),
     ("C2p", 3, {"lambda_lanes": 1}),
