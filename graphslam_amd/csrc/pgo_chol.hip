@@ -546,9 +546,18 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
     if (J == 3) break;
     __syncthreads();
     DIAG_CLK(2 + 3 * J);
-    // phase C: trailing updates of T and W
+    // phase C: trailing updates of T and W.  A wave's (up to 3) products read
+    // only block column / row J and write blocks outside it: all products'
+    // loads and MFMAs first, then the read-modify-write stores, so their
+    // latencies overlap instead of adding up
     const int nA = (3 - J) * (4 - J) / 2, nW = (3 - J) * (J + 1);
-    for (int t = wv; t < nA + nW; t += 4) {
+    d4 acc[3];
+    double* dst[3];
+#pragma unroll
+    for (int u = 0; u < 3; u++) {
+      const int t = wv + 4 * u;
+      dst[u] = nullptr;
+      if (t >= nA + nW) continue;               // wave-uniform
       if (t < nA) {
         int I = J + 1, q = t;                 // t-th pair J < K <= I
         while (q >= I - J) {
@@ -557,15 +566,18 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
         }
         const int K = J + 1 + q;
         const int oi = 16 * I, ok = 16 * K;
-        const d4 v = mm16(T + oi + o * 65, 1, 65, T + ok + o * 65, 65, 1);
-        st16(T + oi + ok * 65, v, true);
+        acc[u] = mm16(T + oi + o * 65, 1, 65, T + ok + o * 65, 65, 1);
+        dst[u] = T + oi + ok * 65;
       } else {
         const int q = t - nA, I = J + 1 + q / (J + 1), K = q % (J + 1);
         const int oi = 16 * I, ok = 16 * K;
-        const d4 v = mm16(T + oi + o * 65, 1, 65, W + o + ok * 65, 1, 65);
-        st16(W + oi + ok * 65, v, true);
+        acc[u] = mm16(T + oi + o * 65, 1, 65, W + o + ok * 65, 1, 65);
+        dst[u] = W + oi + ok * 65;
       }
     }
+#pragma unroll
+    for (int u = 0; u < 3; u++)
+      if (dst[u]) st16(dst[u], acc[u], true);
     __syncthreads();
     DIAG_CLK(3 + 3 * J);
   }
@@ -576,15 +588,18 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
 
 // Forward substitution of the panel's rows of the frontal vector: y = X v with
 // X = L_bb^-1 (LDS, ld 65); the rows below get v -= L y in k_panel_trsm.
+// (4 waves: wave q sums k in [16q, 16q + 16), then a fixed-order sum of the 4)
 __device__ __forceinline__ void panel_rhs(double* v, const double* X, int nb, double* buf) {
-  const int tid = threadIdx.x;
+  __shared__ double part[4][64];
+  const int tid = threadIdx.x, r = tid & 63, q = tid >> 6;
   if (tid < 64) buf[tid] = tid < nb ? v[tid] : 0.0;
   __syncthreads();
-  if (tid < nb) {
-    double acc = 0.0;
-    for (int k = 0; k <= tid; k++) acc = fma(X[tid + k * 65], buf[k], acc);
-    v[tid] = acc;
-  }
+  double acc = 0.0;
+#pragma unroll
+  for (int k = 16 * q; k < 16 * q + 16; k++) acc = fma(k <= r ? X[r + k * 65] : 0.0, buf[k], acc);
+  part[q][r] = acc;
+  __syncthreads();
+  if (tid < nb) v[tid] = ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
 }
 
 // Diagonal tile of each listed front at panel kb: factored and inverted in LDS
@@ -600,9 +615,16 @@ __global__ __launch_bounds__(256) void k_panel_diag(CholDev c, const int* __rest
   const int nb = min(kNB, w - kb);
   double* Fs = c.F + c.foff[s] + kb + (size_t)kb * m;
   const int tid = threadIdx.x;
-  for (int idx = tid; idx < 4096; idx += 256) {
-    const int i = idx & 63, j = idx >> 6;
-    Ts[i + j * 65] = (i < nb && j < nb) ? (i >= j ? Fs[i + (size_t)j * m] : 0.0) : (i == j ? 1.0 : 0.0);
+  double tv[16];
+#pragma unroll
+  for (int u = 0; u < 16; u++) {   // all 16 loads in flight
+    const int idx = tid + 256 * u, i = idx & 63, j = idx >> 6;
+    tv[u] = (i < nb && j < nb) ? (i >= j ? Fs[i + (size_t)j * m] : 0.0) : (i == j ? 1.0 : 0.0);
+  }
+#pragma unroll
+  for (int u = 0; u < 16; u++) {
+    const int idx = tid + 256 * u, i = idx & 63, j = idx >> 6;
+    Ts[i + j * 65] = tv[u];
     Ws[i + j * 65] = 0.0;
   }
   __syncthreads();
