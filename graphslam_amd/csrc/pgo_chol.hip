@@ -36,6 +36,7 @@ struct CholDev {
   int* flag;
   // lambda lanes: lane y = blockIdx.y works on its own numeric workspace
   long long fst, tst;              // F, Tinv doubles per lane
+  long long tfo;                   // Tinv + tfo: the inverses again, in the trsm's MFMA operand order
   int vst, xst, pst;               // fv, xv, backward partials per lane
 };
 
@@ -61,7 +62,8 @@ static CholDev dev_view(const CholPlan& P) {
   c.dg_order = P.d_dg_order;
   c.flag = P.d_flag;
   c.fst = P.ftotal;
-  c.tst = P.ttotal;
+  c.tst = 2 * P.ttotal;
+  c.tfo = P.ttotal;
   c.vst = P.vtotal;
   c.xst = 3 * P.n;
   c.pst = std::max(P.npart, 1) * 64;
@@ -602,6 +604,23 @@ __device__ __forceinline__ void panel_rhs(double* v, const double* X, int nb, do
   if (tid < nb) v[tid] = ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
 }
 
+// L (LDS Ts, ld 65) back into the front, X = L^-1 (LDS Ws, ld 65) row-major to
+// M and in the trsm's operand order to Mf: Mf[(4 ks + ct) * 64 + l] =
+// X[16 ct + (l & 15)][4 ks + (l >> 4)] (each trsm lane loads 64 consecutive-by-lane values)
+__device__ __forceinline__ void store_inverse(double* Fs, int m, double* __restrict__ M, double* __restrict__ Mf,
+                                              const double* Ts, const double* Ws, int nb) {
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < 4096; idx += 256) {
+    const int i = idx & 63, j = idx >> 6;
+    if (i < nb && j < nb && i >= j) Fs[i + (size_t)j * m] = Ts[i + j * 65];
+    const int a = idx >> 6, b = idx & 63;
+    M[idx] = (a < nb && b < nb && a >= b) ? Ws[a + b * 65] : 0.0;
+    const int l = idx & 63, ct = (idx >> 6) & 3, ks = idx >> 8;
+    const int fa = 16 * ct + (l & 15), fb = 4 * ks + (l >> 4);
+    Mf[idx] = (fa < nb && fb < nb && fa >= fb) ? Ws[fa + fb * 65] : 0.0;
+  }
+}
+
 // Diagonal tile of each listed front at panel kb: factored and inverted in LDS
 // (diag_factor_invert); L back into the front, L^-1 into Tinv for the TRSM GEMM
 // and the solves.
@@ -630,12 +649,7 @@ __global__ __launch_bounds__(256) void k_panel_diag(CholDev c, const int* __rest
   __syncthreads();
   if (diag_factor_invert(Ts, Ws, bc)) *c.flag = 1;
   double* M = c.Tinv + c.toff[s] + (kb / 64) * 4096;   // row-major L^-1 of the tile
-  for (int idx = tid; idx < 4096; idx += 256) {
-    const int i = idx & 63, j = idx >> 6;
-    if (i < nb && j < nb && i >= j) Fs[i + (size_t)j * m] = Ts[i + j * 65];
-    const int a = idx >> 6, b = idx & 63;
-    M[idx] = (a < nb && b < nb && a >= b) ? Ws[a + b * 65] : 0.0;
-  }
+  store_inverse(Fs, m, M, M + c.tfo, Ts, Ws, nb);
   panel_rhs(c.fv + c.voff[s] + kb, Ws, nb, bc);
 }
 
@@ -643,47 +657,48 @@ __global__ __launch_bounds__(256) void k_panel_diag(CholDev c, const int* __rest
 // GEMM with the inverted tile, v_mfma_f64_16x16x4_f64, B fragments from global.
 __global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __restrict__ tasks, int kb) {
   lane_offset(c);
-  constexpr int LDB = 81;
-  __shared__ __attribute__((aligned(16))) double Tb[64 * LDB];  // Tb[k*LDB + j] = Tinv[j][k]
   const int2 task = tasks[blockIdx.x];
   const int s = task.x, chunk = task.y;
   const int m = c.m[s], w = c.w[s];
-  __shared__ double ys[64];
   const int nb = min(kNB, w - kb);
-  const double* M = c.Tinv + c.toff[s] + (kb / 64) * 4096;
+  const double* Mf = c.Tinv + c.tfo + c.toff[s] + (kb / 64) * 4096;   // inverse, operand order
   double* fv = c.fv + c.voff[s];
   const int tid = threadIdx.x;
   const int wv = tid >> 6, l = tid & 63;
   const int r0 = kb + nb + chunk * 64 + wv * 16;
+  if (r0 >= m) return;                               // (no barriers below)
   double* Fc = c.F + c.foff[s] + (size_t)kb * m;   // column kb of the front
   const int arow = r0 + (l & 15), kl = l >> 4;
-  double a[16];   // B fragments, in flight with the staging of the inverse
+  double a[16], tb[16][4], yc[4];   // B fragments, inverse fragments, y: all loads in flight
 #pragma unroll
   for (int ks = 0; ks < 16; ks++) {
     const int k = 4 * ks + kl;
     a[ks] = (arow < m && k < nb) ? Fc[arow + (size_t)k * m] : 0.0;
   }
-  for (int idx = tid; idx < 4096; idx += 256) Tb[(idx & 63) * LDB + (idx >> 6)] = M[idx];   // M row-major
-  if (tid < 64) ys[tid] = tid < nb ? fv[kb + tid] : 0.0;   // y of the panel (diagonal step)
-  __syncthreads();
-  if (r0 >= m) return;
+#pragma unroll
+  for (int ks = 0; ks < 16; ks++)
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++) tb[ks][ct] = Mf[(4 * ks + ct) * 64 + l];
+#pragma unroll
+  for (int ct = 0; ct < 4; ct++) {
+    const int col = 16 * ct + (l & 15);
+    yc[ct] = col < nb ? fv[kb + col] : 0.0;          // y of the panel (diagonal step)
+  }
   d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0}, acc3 = {0, 0, 0, 0};
 #pragma unroll
   for (int ks = 0; ks < 16; ks++) {
-    const double* tb = Tb + (4 * ks + kl) * LDB + (l & 15);
-    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[0], acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[16], acc1, 0, 0, 0);
-    acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[32], acc2, 0, 0, 0);
-    acc3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[48], acc3, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[ks][0], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[ks][1], acc1, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[ks][2], acc2, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[ks][3], acc3, 0, 0, 0);
   }
   double part[4] = {0, 0, 0, 0};   // L[row, panel] y for the lane's 4 rows
 #pragma unroll
   for (int ct = 0; ct < 4; ct++) {
     const d4 v = ct == 0 ? acc0 : (ct == 1 ? acc1 : (ct == 2 ? acc2 : acc3));
     const int col = 16 * ct + (l & 15);
-    const double yc = ys[col];
 #pragma unroll
-    for (int r = 0; r < 4; r++) part[r] = fma(v[r], yc, part[r]);
+    for (int r = 0; r < 4; r++) part[r] = fma(v[r], yc[ct], part[r]);
     if (col >= nb) continue;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -973,12 +988,7 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
   if (diag_factor_invert(Ts, Ws, bc)) *c.flag = 1;
   double* Fs = c.F + c.foff[s] + kn + (size_t)kn * m;
   double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;   // row-major L^-1 of the tile
-  for (int idx = tid; idx < 4096; idx += 256) {
-    const int i = idx & 63, j = idx >> 6;
-    if (i < nb && j < nb && i >= j) Fs[i + (size_t)j * m] = Ts[i + j * 65];
-    const int a = idx >> 6, b = idx & 63;
-    M[idx] = (a < nb && b < nb && a >= b) ? Ws[a + b * 65] : 0.0;
-  }
+  store_inverse(Fs, m, M, M + c.tfo, Ts, Ws, nb);
   panel_rhs(c.fv + c.voff[s] + kn, Ws, nb, bc);
 }
 
@@ -1454,7 +1464,7 @@ static void free_numeric(CholPlan& P) {
 
 static hipError_t alloc_numeric(CholPlan& P, int nb, hipStream_t s) {
   CH_TRY(hipMalloc((void**)&P.F, nb * std::max<long long>(P.ftotal, 1) * sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.Tinv, nb * std::max<long long>(P.ttotal, 1) * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.Tinv, nb * std::max<long long>(2 * P.ttotal, 1) * sizeof(double)));
   CH_TRY(hipMalloc((void**)&P.fv, (size_t)nb * std::max(P.vtotal, 1) * sizeof(double)));
   CH_TRY(hipMalloc((void**)&P.xv, (size_t)nb * std::max(3 * P.n, 1) * sizeof(double)));
   CH_TRY(hipMalloc((void**)&P.d_flag, nb * sizeof(int)));
