@@ -11,7 +11,7 @@ import re
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpgo.so")
+LIB_PATH = os.environ.get("PGO_LIB_PATH") or os.path.join(HERE, "libpgo.so")   # override: A/B builds
 HEADER = os.path.join(os.path.dirname(HERE), "include", "pgo.h")
 
 PGO_OK = 0
