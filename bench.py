@@ -46,9 +46,12 @@ def spmv_bytes(n, slots):
 
 
 def linearize_bytes(n, ne):
-    """Algorithmic bytes of one k_linearize launch: per factor ids 8 + z 32 + Omega 48
-    read, two 72 B blocks written; per pose 32 B read, D 48 + g 24 written."""
-    return ne * (8 + 32 + 48 + 144) + n * (32 + 48 + 24)
+    """Algorithmic bytes of one linearisation: per factor ids 8 +
+    z 24 + Omega 48 read, the owner block H_ij 72 written (152 B); per pose the
+    pose 24 read, H_ii upper 48 + b_i 24 written (96 B).  The Cholesky-mode
+    sweep is two launches (k_linearize_own + k_linearize_side1), timed together
+    from the first one's start to the second one's end."""
+    return ne * 152 + n * 96
 
 
 def cpu_baseline(g, max_outer):
@@ -253,10 +256,15 @@ def main():
             },
             "roofline": roofline,
             "linearize_kernel": {
-                "kernel": "k_linearize",
+                "kernel": "k_linearize_own+k_linearize_side1",
                 "avg_launch_ms": lin_avg_ms,
                 "bytes_per_launch": linearize_bytes(n, ne),
                 "achieved_gbs": linearize_bytes(n, ne) / (lin_avg_ms * 1e-3) / 1e9 if totals["lin_n"] else None,
+                "peak_gbs": 8000.0,
+                "frac": linearize_bytes(n, ne) / (lin_avg_ms * 1e-3) / 8e12 if totals["lin_n"] else None,
+                "traffic": (pmc["k_linearize_own_bytes_per_launch"] + pmc["k_linearize_side1_bytes_per_launch"]
+                            if "k_linearize_own_bytes_per_launch" in pmc and "k_linearize_side1_bytes_per_launch" in pmc
+                            else None),
             },
             "cpu_baseline": None,
             "marginals": marg,

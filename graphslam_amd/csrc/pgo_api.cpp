@@ -167,7 +167,7 @@ void free_device(pgo_graph* g) {
   g->lane_cap = 8;
   DevGraph& d = g->d;
   void* ptrs[] = {d.eij, d.ez, d.eom, d.prior_ptr, d.prior_vtx, d.pz, d.pom, d.row_ptr, d.slot_edge, d.slot_col, d.V,
-                  d.D, d.g, d.pose, d.pose_cand, d.pose_saved, d.x, d.r, d.z, d.p, d.q, d.Minv, d.part, d.scal, d.ctrl};
+                  d.erow, d.s1_ptr, d.s1_edge, d.eside, d.Dc, d.W, d.D, d.g, d.pose, d.pose_cand, d.pose_saved, d.x, d.r, d.z, d.p, d.q, d.Minv, d.part, d.scal, d.ctrl};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   hipStream_t s = d.stream;
@@ -422,6 +422,40 @@ int upload_structure(pgo_graph* g) {
   const double mean_deg = n ? (double)ns / n : 0.0;
   d.G = 4;
   while (d.G < 32 && d.G < mean_deg) d.G *= 2;
+  d.G1 = 4;
+  while (d.G1 < 32 && d.G1 < (n ? (double)ne / n : 0.0)) d.G1 *= 2;
+  // Cholesky-mode sweep structure: factors are sorted by (ei, ej), so the
+  // side-0 factors of row i are the contiguous range [erow[i], erow[i+1]);
+  // side-1 factors of row j are listed in s1_edge in device order.  Dc[j] is
+  // the (iteration-invariant) sum of Omega over row j's side-1 factors.
+  std::vector<int> erow(n + 1, 0), s1_ptr(n + 1, 0), s1_edge(ne);
+  std::vector<double> Dc(6 * (size_t)n, 0.0);
+  for (int e = 0; e < ne; e++) {
+    erow[eij[e].x + 1]++;
+    s1_ptr[eij[e].y + 1]++;
+  }
+  for (int i = 0; i < n; i++) {
+    erow[i + 1] += erow[i];
+    s1_ptr[i + 1] += s1_ptr[i];
+  }
+  {
+    std::vector<int> f(s1_ptr.begin(), s1_ptr.end() - 1);
+    for (int e = 0; e < ne; e++) {
+      const int j = eij[e].y;
+      s1_edge[f[j]++] = e;
+      const double* o = &g->eom[6 * (size_t)H.dorder[e]];
+      for (int q = 0; q < 6; q++) Dc[6 * (size_t)j + q] += o[q];
+    }
+  }
+  RC_TRY(dev_alloc(g, &d.erow, n + 1));
+  RC_TRY(dev_alloc(g, &d.s1_ptr, n + 1));
+  RC_TRY(dev_alloc(g, &d.s1_edge, ne));
+  RC_TRY(dev_alloc(g, &d.Dc, 6 * (size_t)n));
+  RC_TRY(dev_alloc(g, &d.W, ne));
+  RC_TRY(h2d(g, d.erow, erow.data(), n + 1));
+  RC_TRY(h2d(g, d.s1_ptr, s1_ptr.data(), n + 1));
+  RC_TRY(h2d(g, d.s1_edge, s1_edge.data(), ne));
+  RC_TRY(h2d(g, d.Dc, Dc.data(), 6 * (size_t)n));
   RC_TRY(dev_alloc(g, &d.eij, ne));
   RC_TRY(dev_alloc(g, &d.ez, ne));
   RC_TRY(dev_alloc(g, &d.eom, 3 * (size_t)ne));
@@ -494,12 +528,6 @@ int ensure_chol(pgo_graph* g) {
   if (g->chol_ready) return PGO_OK;
   g->chol.ordering = g->ordering;
   pgo::chol_analyze(g->chol, g->d.n, g->h_row_ptr, g->h_slot_col);
-  const hipError_t e = pgo::chol_upload(g->chol, g->d.stream);
-  if (e != hipSuccess) {
-    pgo::chol_free(g->chol);
-    return fail(g, e == hipErrorOutOfMemory ? PGO_E_NOMEM : PGO_E_HIP,
-                std::string("Cholesky plan upload: ") + hipGetErrorString(e));
-  }
   // owner slot of every factor := its block in the lower triangle of the
   // permuted matrix (the one the assembly reads); with write_all = 0 the
   // linearisation writes only these
@@ -512,6 +540,20 @@ int ensure_chol(pgo_graph* g) {
         slot_edge[k] = (slot_edge[k] & ~2) | (own ? 2 : 0);
       }
     g->h_slot_edge = slot_edge;
+    // Cholesky-mode linearisation writes each factor's owner block at its
+    // device factor index (coalesced), so the assembly reads V[q*S + e]
+    std::vector<unsigned char> eside(g->d.ne, 0);
+    for (size_t k = 0; k < slot_edge.size(); k++)
+      if (slot_edge[k] & 2) eside[slot_edge[k] >> 2] = (unsigned char)(slot_edge[k] & 1);
+    for (auto& src : g->chol.asm_src) src = slot_edge[src] >> 2;
+    const hipError_t e = pgo::chol_upload(g->chol, g->d.stream);
+    if (e != hipSuccess) {
+      pgo::chol_free(g->chol);
+      return fail(g, e == hipErrorOutOfMemory ? PGO_E_NOMEM : PGO_E_HIP,
+                  std::string("Cholesky plan upload: ") + hipGetErrorString(e));
+    }
+    if (!g->d.eside) RC_TRY(dev_alloc(g, &g->d.eside, g->d.ne));
+    RC_TRY(h2d(g, g->d.eside, eside.data(), eside.size()));
     if (!slot_edge.empty())
       HIP_TRY(g, hipMemcpyAsync(g->d.slot_edge, slot_edge.data(), slot_edge.size() * sizeof(int),
                                 hipMemcpyHostToDevice, g->d.stream));
@@ -1541,7 +1583,9 @@ int pgo_debug_solve(pgo_graph* g, double lambda, const pgo_params* params, doubl
   else pgo_default_params(&p);
   RC_TRY(ensure_device(g));
   DevGraph& d = g->d;
-  d.write_all = 1;   // diagnostics read every block
+  // the Cholesky assembly reads the owner blocks in factor order (k_linearize_own)
+  if (p.linear_solver != PGO_SOLVER_PCG && d.n > 0) RC_TRY(ensure_chol(g));
+  d.write_all = p.linear_solver == PGO_SOLVER_PCG ? 1 : 0;
   HIP_TRY(g, pgo::launch_linearize(d));
   pgo_stats st;
   std::memset(&st, 0, sizeof(st));

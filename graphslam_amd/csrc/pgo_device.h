@@ -42,6 +42,15 @@ struct DevGraph {
   int write_all = 1;                // 1: both blocks of every edge in V (PCG, diagnostics);
                                     // 0: owner blocks only (the Cholesky assembly reads no others)
   int* slot_col = nullptr;
+  // Cholesky-mode linearisation (write_all = 0 with a plan: owner blocks in
+  // device factor order, V[q * S + e]; see k_linearize_own)
+  int G1 = 8;                       // lanes per row for the side-0 / side-1 sweeps
+  int* erow = nullptr;              // [n+1] side-0 factors of row i: [erow[i], erow[i+1])
+  int* s1_ptr = nullptr;            // [n+1] side-1 factors of row j in s1_edge
+  int* s1_edge = nullptr;           // [E]
+  unsigned char* eside = nullptr;   // [E] side of the factor's owner block (set with the plan)
+  double* Dc = nullptr;             // [6n] sum of Omega over the side-1 factors of each row
+  double4* W = nullptr;             // [E] Omega e of each factor (side-1 gradient hand-off)
   double* V = nullptr;
   double* D = nullptr;
   double* g = nullptr;

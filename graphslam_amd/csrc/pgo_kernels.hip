@@ -157,6 +157,114 @@ __global__ __launch_bounds__(kThreads) void k_linearize(DevGraph d) {
   if (threadIdx.x == 0) d.part[kPartA * kMaxBlocks + blockIdx.x] = chi;
 }
 
+// Cholesky-mode linearisation (write_all = 0 with a plan).  One sub-group of
+// G lanes per row i, one lane per side-0 factor: factors are sorted by
+// (ei, ej), so the factors of consecutive rows are consecutive in memory and a
+// wave streams eij / z / Omega once each, coalesced (the two-slot sweep above
+// reads every factor twice, gathered).  Each factor's owner block goes to
+// V[q * S + e] in factor order (the assembly's source index), its Omega e to
+// W[e] for row ej's gradient (k_linearize_side1); row i's diagonal block is
+// the side-0 sum plus Dc[i] = sum of Omega over its side-1 factors.  No
+// error partials: the error is k_error's (the two-slot sweep's chi partials
+// are not read either).  One sub-group per row (grid not capped): no
+// row loop, so the erow -> eij -> pose load chains of all rows are in flight.
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_linearize_own(DevGraph d) {
+  const int lane = threadIdx.x & (G - 1);
+  const int nsg = gridDim.x * (kThreads / G);
+  const size_t S = d.nslots;
+  for (int row = (blockIdx.x * kThreads + threadIdx.x) / G; row < d.n; row += nsg) {
+    double a00 = 0, a01 = 0, a02 = 0, a11 = 0, a12 = 0, a22 = 0, g0 = 0, g1 = 0, g2 = 0;
+    const int beg = d.erow[row], end = d.erow[row + 1];
+    const double4 p1 = d.pose[row];
+    for (int e = beg + lane; e < end; e += G) {
+      const double4 p2 = d.pose[d.eij[e].y], z = d.ez[e];
+      const double2 oA = d.eom[3 * e], oB = d.eom[3 * e + 1], oC = d.eom[3 * e + 2];
+      const double o00 = oA.x, o01 = oA.y, o02 = oB.x, o11 = oB.y, o12 = oC.x, o22 = oC.y;
+      double hc = p1.z * p2.z + p1.w * p2.w, hs = -p1.w * p2.z + p1.z * p2.w;
+      rot_normalize(hc, hs);
+      const double dx = p2.x - p1.x, dy = p2.y - p1.y;
+      const double hx = p1.z * dx + p1.w * dy, hy = -p1.w * dx + p1.z * dy;
+      double ec = z.z * hc + z.w * hs, es = -z.w * hc + z.z * hs;
+      rot_normalize(ec, es);
+      const double tx = hx - z.x, ty = hy - z.y;
+      const double e0 = z.z * tx + z.w * ty, e1 = -z.w * tx + z.z * ty, e2 = atan2(es, ec);
+      const double dt1 = -p2.w * dx + p2.z * dy, dt2 = -p2.z * dx - p2.w * dy;
+      const double m00 = -hc * o00 + hs * o01, m01 = -hs * o00 - hc * o01, m02 = dt1 * o00 + dt2 * o01 - o02;
+      const double m10 = -hc * o01 + hs * o11, m11 = -hs * o01 - hc * o11, m12 = dt1 * o01 + dt2 * o11 - o12;
+      const double m20 = -hc * o02 + hs * o12, m21 = -hs * o02 - hc * o12, m22 = dt1 * o02 + dt2 * o12 - o22;
+      const double w0 = o00 * e0 + o01 * e1 + o02 * e2;
+      const double w1 = o01 * e0 + o11 * e1 + o12 * e2;
+      const double w2 = o02 * e0 + o12 * e1 + o22 * e2;
+      double* v = d.V + e;
+      if (d.eside[e] == 0) {   // owner block H_ij = M'
+        v[0] = m00; v[S] = m10; v[2 * S] = m20;
+        v[3 * S] = m01; v[4 * S] = m11; v[5 * S] = m21;
+        v[6 * S] = m02; v[7 * S] = m12; v[8 * S] = m22;
+      } else {                 // owner block H_ji = M
+        v[0] = m00; v[S] = m01; v[2 * S] = m02;
+        v[3 * S] = m10; v[4 * S] = m11; v[5 * S] = m12;
+        v[6 * S] = m20; v[7 * S] = m21; v[8 * S] = m22;
+      }
+      d.W[e] = make_double4(w0, w1, w2, 0.0);
+      a00 += -hc * m00 + hs * m10;
+      a01 += -hc * m01 + hs * m11;
+      a02 += -hc * m02 + hs * m12;
+      a11 += -hs * m01 - hc * m11;
+      a12 += -hs * m02 - hc * m12;
+      a22 += dt1 * m02 + dt2 * m12 - m22;
+      g0 += -hc * w0 + hs * w1;
+      g1 += -hs * w0 - hc * w1;
+      g2 += dt1 * w0 + dt2 * w1 - w2;
+    }
+    a00 = sg_sum<G>(a00); a01 = sg_sum<G>(a01); a02 = sg_sum<G>(a02);
+    a11 = sg_sum<G>(a11); a12 = sg_sum<G>(a12); a22 = sg_sum<G>(a22);
+    g0 = sg_sum<G>(g0); g1 = sg_sum<G>(g1); g2 = sg_sum<G>(g2);
+    if (lane == 0) {
+      const double* dc = d.Dc + 6 * (size_t)row;
+      a00 += dc[0]; a01 += dc[1]; a02 += dc[2]; a11 += dc[3]; a12 += dc[4]; a22 += dc[5];
+      for (int q = d.prior_ptr[row]; q < d.prior_ptr[row + 1]; q++) {   // PriorFactor<Pose2>
+        const double4 pz = d.pz[q];
+        double c = p1.z * pz.z + p1.w * pz.w, s = -p1.w * pz.z + p1.z * pz.w;
+        rot_normalize(c, s);
+        const double dx = pz.x - p1.x, dy = pz.y - p1.y;
+        const double e0 = -(p1.z * dx + p1.w * dy), e1 = -(-p1.w * dx + p1.z * dy), e2 = -atan2(s, c);
+        const double2 oA = d.pom[3 * q], oB = d.pom[3 * q + 1], oC = d.pom[3 * q + 2];
+        const double o00 = oA.x, o01 = oA.y, o02 = oB.x, o11 = oB.y, o12 = oC.x, o22 = oC.y;
+        const double w0 = o00 * e0 + o01 * e1 + o02 * e2;
+        const double w1 = o01 * e0 + o11 * e1 + o12 * e2;
+        const double w2 = o02 * e0 + o12 * e1 + o22 * e2;
+        a00 += o00; a01 += o01; a02 += o02; a11 += o11; a12 += o12; a22 += o22;
+        g0 += w0; g1 += w1; g2 += w2;
+      }
+      double* D = d.D + 6 * (size_t)row;
+      D[0] = a00; D[1] = a01; D[2] = a02; D[3] = a11; D[4] = a12; D[5] = a22;
+      double* g = d.g + 3 * (size_t)row;
+      g[0] = g0; g[1] = g1; g[2] = g2;
+    }
+  }
+}
+
+// Row j's side-1 gradient terms: g_j += sum of Omega e over the factors with
+// ej = j (fixed order: device factor order), after k_linearize_own.
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_linearize_side1(DevGraph d) {
+  const int lane = threadIdx.x & (G - 1);
+  const int nsg = gridDim.x * (kThreads / G);
+  for (int row = (blockIdx.x * kThreads + threadIdx.x) / G; row < d.n; row += nsg) {
+    double s0 = 0, s1 = 0, s2 = 0;
+    for (int t = d.s1_ptr[row] + lane; t < d.s1_ptr[row + 1]; t += G) {
+      const double4 w = d.W[d.s1_edge[t]];
+      s0 += w.x; s1 += w.y; s2 += w.z;
+    }
+    s0 = sg_sum<G>(s0); s1 = sg_sum<G>(s1); s2 = sg_sum<G>(s2);
+    if (lane == 0) {
+      double* g = d.g + 3 * (size_t)row;
+      g[0] += s0; g[1] += s1; g[2] += s2;
+    }
+  }
+}
+
 // ------------------------------------------------------------ error / retract
 // 0.5 e'Omega e per factor (NonlinearFactorGraph::error), block partials.
 __global__ __launch_bounds__(kThreads) void k_error(DevGraph d, const double4* __restrict__ pose) {
@@ -358,14 +466,16 @@ __global__ __launch_bounds__(kThreads) void k_model_decrease(DevGraph d, const d
   const int nsg = gridDim.x * (kThreads / G);
   const size_t S = d.nslots;
   double xhx = 0.0, gx = 0.0;
+  const bool own_at_edge = !d.write_all && d.eside;   // k_linearize_own layout
   for (int row = (blockIdx.x * kThreads + threadIdx.x) / G; row < d.n; row += nsg) {
     const double r0 = X[3 * row], r1 = X[3 * row + 1], r2 = X[3 * row + 2];
     double t = 0.0;
     const int beg = d.row_ptr[row], end = d.row_ptr[row + 1];
     for (int k = beg + lane; k < end; k += G) {
-      if (!(d.slot_edge[k] & 2)) continue;
+      const int se = d.slot_edge[k];
+      if (!(se & 2)) continue;
       const int c = d.slot_col[k];
-      const double* v = d.V + k;
+      const double* v = d.V + (own_at_edge ? (se >> 2) : k);
       const double x0 = X[3 * c], x1 = X[3 * c + 1], x2 = X[3 * c + 2];
       const double y0 = v[0] * x0 + v[S] * x1 + v[2 * S] * x2;
       const double y1 = v[3 * S] * x0 + v[4 * S] * x1 + v[5 * S] * x2;
@@ -445,7 +555,23 @@ int grid_rows(const DevGraph& d) {
 
 hipError_t launch_linearize(const DevGraph& d, hipEvent_t start, hipEvent_t stop) {
   if (d.n == 0) return hipSuccess;
-  const dim3 grid(grid_rows(d)), block(kThreads);
+  const dim3 block(kThreads);
+  if (!d.write_all && d.eside) {   // Cholesky mode: owner blocks in factor order
+    const long long b = ((long long)d.n * d.G1 + kThreads - 1) / kThreads;
+    const dim3 grid1((unsigned)b);
+    switch (d.G1) {
+      case 4: hipExtLaunchKernelGGL(k_linearize_own<4>, grid1, block, 0, d.stream, start, nullptr, 0, d);
+              hipExtLaunchKernelGGL(k_linearize_side1<4>, grid1, block, 0, d.stream, nullptr, stop, 0, d); break;
+      case 8: hipExtLaunchKernelGGL(k_linearize_own<8>, grid1, block, 0, d.stream, start, nullptr, 0, d);
+              hipExtLaunchKernelGGL(k_linearize_side1<8>, grid1, block, 0, d.stream, nullptr, stop, 0, d); break;
+      case 16: hipExtLaunchKernelGGL(k_linearize_own<16>, grid1, block, 0, d.stream, start, nullptr, 0, d);
+               hipExtLaunchKernelGGL(k_linearize_side1<16>, grid1, block, 0, d.stream, nullptr, stop, 0, d); break;
+      default: hipExtLaunchKernelGGL(k_linearize_own<32>, grid1, block, 0, d.stream, start, nullptr, 0, d);
+               hipExtLaunchKernelGGL(k_linearize_side1<32>, grid1, block, 0, d.stream, nullptr, stop, 0, d); break;
+    }
+    return hipGetLastError();
+  }
+  const dim3 grid(grid_rows(d));
   switch (d.G) {
     case 4: hipExtLaunchKernelGGL(k_linearize<4>, grid, block, 0, d.stream, start, stop, 0, d); break;
     case 8: hipExtLaunchKernelGGL(k_linearize<8>, grid, block, 0, d.stream, start, stop, 0, d); break;

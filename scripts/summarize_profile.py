@@ -74,7 +74,7 @@ def main():
     traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
     ent = traffic.get("C3", {})
     ent["source"] = f"{tag}_pmc.json"
-    for k in ("k_panel_syrk_lds", "k_panel_syrk", "k_linearize", "k_pcg_spmv"):
+    for k in ("k_panel_syrk_lds", "k_panel_syrk", "k_linearize", "k_linearize_own", "k_linearize_side1", "k_pcg_spmv"):
         v = summary["kernels"].get(k, {}).get("hbm_bytes_per_launch")
         if v is not None:
             ent[f"{k}_bytes_per_launch"] = v
