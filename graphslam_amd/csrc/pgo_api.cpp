@@ -167,7 +167,7 @@ void free_device(pgo_graph* g) {
   g->lane_cap = 8;
   DevGraph& d = g->d;
   void* ptrs[] = {d.eij, d.ez, d.eom, d.prior_ptr, d.prior_vtx, d.pz, d.pom, d.row_ptr, d.slot_edge, d.slot_col, d.V,
-                  d.erow, d.s1_ptr, d.s1_edge, d.eside, d.Dc, d.W, d.D, d.g, d.pose, d.pose_cand, d.pose_saved, d.x, d.r, d.z, d.p, d.q, d.Minv, d.part, d.scal, d.ctrl};
+                  d.erow, d.brow, d.s1_ptr, d.s1_edge, d.eside, d.Dc, d.W, d.D, d.g, d.pose, d.pose_cand, d.pose_saved, d.x, d.r, d.z, d.p, d.q, d.Minv, d.part, d.scal, d.ctrl};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   hipStream_t s = d.stream;
@@ -447,6 +447,18 @@ int upload_structure(pgo_graph* g) {
       for (int q = 0; q < 6; q++) Dc[6 * (size_t)j + q] += o[q];
     }
   }
+  // k_linearize_own blocks: whole rows, greedily packed to <= kThreads side-0
+  // factors and <= kThreads rows (a row with more factors is a block alone)
+  std::vector<int> brow(1, 0);
+  for (int r = 0; r < n;) {
+    int r1 = r + 1;
+    while (r1 < n && r1 - r < pgo::kThreads && erow[r1 + 1] - erow[r] <= pgo::kThreads) r1++;
+    brow.push_back(r1);
+    r = r1;
+  }
+  d.nlb = (int)brow.size() - 1;
+  RC_TRY(dev_alloc(g, &d.brow, brow.size()));
+  RC_TRY(h2d(g, d.brow, brow.data(), brow.size()));
   RC_TRY(dev_alloc(g, &d.erow, n + 1));
   RC_TRY(dev_alloc(g, &d.s1_ptr, n + 1));
   RC_TRY(dev_alloc(g, &d.s1_edge, ne));

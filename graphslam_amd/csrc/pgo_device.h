@@ -46,6 +46,9 @@ struct DevGraph {
   // device factor order, V[q * S + e]; see k_linearize_own)
   int G1 = 8;                       // lanes per row for the side-0 / side-1 sweeps
   int* erow = nullptr;              // [n+1] side-0 factors of row i: [erow[i], erow[i+1])
+  int nlb = 0;                      // k_linearize_own blocks
+  int* brow = nullptr;              // [nlb+1] whole rows of each block (<= kThreads rows,
+                                    // side-0 factors <= kThreads unless a single row)
   int* s1_ptr = nullptr;            // [n+1] side-1 factors of row j in s1_edge
   int* s1_edge = nullptr;           // [E]
   unsigned char* eside = nullptr;   // [E] side of the factor's owner block (set with the plan)

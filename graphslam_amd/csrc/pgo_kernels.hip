@@ -24,7 +24,7 @@ namespace pgo {
 __device__ __forceinline__ void rot_normalize(double& c, double& s) {
   const double scale = c * c + s * s;
   if (fabs(scale - 1.0) > 1e-10) {
-    const double f = pow(scale, -0.5);
+    const double f = 1.0 / sqrt(scale);   // pow(scale, -0.5) up to rounding; taken only off the unit circle
     c *= f;
     s *= f;
   }
@@ -64,20 +64,18 @@ __device__ __forceinline__ double sum_partials(const double* __restrict__ part, 
 // (side-0 slots only) 0.5 e'Omega e are summed across the sub-group.
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_linearize(DevGraph d) {
-  __shared__ double lds[kThreads / 64];
   const int lane = threadIdx.x & (G - 1);
   const int nsg = gridDim.x * (kThreads / G);
-  double chi = 0.0;
   for (int row = (blockIdx.x * kThreads + threadIdx.x) / G; row < d.n; row += nsg) {
     double a00 = 0, a01 = 0, a02 = 0, a11 = 0, a12 = 0, a22 = 0, g0 = 0, g1 = 0, g2 = 0;
     const int beg = d.row_ptr[row], end = d.row_ptr[row + 1];
+#pragma unroll 1
     for (int k = beg + lane; k < end; k += G) {
       const int se = d.slot_edge[k];
-      const int e = se >> 2;
       const bool put = d.write_all || (se & 2);   // owner blocks only for the Cholesky assembly
-      const int2 ij = d.eij[e];
-      const double4 p1 = d.pose[ij.x], p2 = d.pose[ij.y], z = d.ez[e];
-      const double2 oA = d.eom[3 * e], oB = d.eom[3 * e + 1], oC = d.eom[3 * e + 2];
+      const int2 ij = d.eij[se >> 2];
+      const double4 p1 = d.pose[ij.x], p2 = d.pose[ij.y], z = d.ez[se >> 2];
+      const double2 oA = d.eom[3 * (se >> 2)], oB = d.eom[3 * (se >> 2) + 1], oC = d.eom[3 * (se >> 2) + 2];
       const double o00 = oA.x, o01 = oA.y, o02 = oB.x, o11 = oB.y, o12 = oC.x, o22 = oC.y;
       // hx = between(p1, p2)                                 [GTSAM Pose2::between]
       double hc = p1.z * p2.z + p1.w * p2.w, hs = -p1.w * p2.z + p1.z * p2.w;
@@ -115,7 +113,6 @@ __global__ __launch_bounds__(kThreads) void k_linearize(DevGraph d) {
         g0 += -hc * w0 + hs * w1;
         g1 += -hs * w0 - hc * w1;
         g2 += dt1 * w0 + dt2 * w1 - w2;
-        chi += 0.5 * (e0 * w0 + e1 * w1 + e2 * w2);
       } else {              // row ej: H_ji = Omega J1 = M, H_jj += Omega, g_j += w
         if (put) {
           v[0] = m00; v[S] = m01; v[2 * S] = m02;
@@ -140,7 +137,6 @@ __global__ __launch_bounds__(kThreads) void k_linearize(DevGraph d) {
         const double w2 = o02 * e0 + o12 * e1 + o22 * e2;
         a00 += o00; a01 += o01; a02 += o02; a11 += o11; a12 += o12; a22 += o22;
         g0 += w0; g1 += w1; g2 += w2;
-        chi += 0.5 * (e0 * w0 + e1 * w1 + e2 * w2);
       }
     }
     a00 = sg_sum<G>(a00); a01 = sg_sum<G>(a01); a02 = sg_sum<G>(a02);
@@ -153,32 +149,34 @@ __global__ __launch_bounds__(kThreads) void k_linearize(DevGraph d) {
       g[0] = g0; g[1] = g1; g[2] = g2;
     }
   }
-  chi = block_sum(chi, lds);
-  if (threadIdx.x == 0) d.part[kPartA * kMaxBlocks + blockIdx.x] = chi;
 }
 
-// Cholesky-mode linearisation (write_all = 0 with a plan).  One sub-group of
-// G lanes per row i, one lane per side-0 factor: factors are sorted by
-// (ei, ej), so the factors of consecutive rows are consecutive in memory and a
-// wave streams eij / z / Omega once each, coalesced (the two-slot sweep above
-// reads every factor twice, gathered).  Each factor's owner block goes to
-// V[q * S + e] in factor order (the assembly's source index), its Omega e to
-// W[e] for row ej's gradient (k_linearize_side1); row i's diagonal block is
-// the side-0 sum plus Dc[i] = sum of Omega over its side-1 factors.  No
-// error partials: the error is k_error's (the two-slot sweep's chi partials
-// are not read either).  One sub-group per row (grid not capped): no
-// row loop, so the erow -> eij -> pose load chains of all rows are in flight.
-template <int G>
+// Cholesky-mode linearisation (write_all = 0 with a plan), one thread per
+// between factor.  Factors are sorted by (ei, ej); block b owns the whole rows
+// [brow[b], brow[b+1]) (at most kThreads rows, their side-0 factors in chunks
+// of kThreads), so a wave streams eij / z / Omega once each, coalesced, with
+// every lane busy and no erow -> factor load chain.  Each factor's owner block
+// goes to V[q * S + e] in factor order (the assembly's source index), its
+// Omega e to W[e] for row ej's gradient (k_linearize_side1); the factor's
+// side-0 terms (J1' Omega J1, J1' Omega e) go through LDS to one thread per
+// row, which sums them in factor order and adds Dc[i] (sum of Omega over the
+// row's side-1 factors) and the row's priors.  No error partials: the error
+// is k_error's.
 __global__ __launch_bounds__(kThreads) void k_linearize_own(DevGraph d) {
-  const int lane = threadIdx.x & (G - 1);
-  const int nsg = gridDim.x * (kThreads / G);
+  __shared__ double sm[9][kThreads];
+  const int t = threadIdx.x;
+  const int r0 = d.brow[blockIdx.x], r1 = d.brow[blockIdx.x + 1];
+  const int e0 = d.erow[r0], e1 = d.erow[r1];
   const size_t S = d.nslots;
-  for (int row = (blockIdx.x * kThreads + threadIdx.x) / G; row < d.n; row += nsg) {
-    double a00 = 0, a01 = 0, a02 = 0, a11 = 0, a12 = 0, a22 = 0, g0 = 0, g1 = 0, g2 = 0;
-    const int beg = d.erow[row], end = d.erow[row + 1];
-    const double4 p1 = d.pose[row];
-    for (int e = beg + lane; e < end; e += G) {
-      const double4 p2 = d.pose[d.eij[e].y], z = d.ez[e];
+  const int row = r0 + t;
+  const bool rowt = row < r1;
+  const int rb = rowt ? d.erow[row] : 0, re = rowt ? d.erow[row + 1] : 0;
+  double a00 = 0, a01 = 0, a02 = 0, a11 = 0, a12 = 0, a22 = 0, g0 = 0, g1 = 0, g2 = 0;
+  for (int c0 = e0; c0 < e1; c0 += kThreads) {
+    const int e = c0 + t;
+    if (e < e1) {
+      const int2 ij = d.eij[e];
+      const double4 p1 = d.pose[ij.x], p2 = d.pose[ij.y], z = d.ez[e];
       const double2 oA = d.eom[3 * e], oB = d.eom[3 * e + 1], oC = d.eom[3 * e + 2];
       const double o00 = oA.x, o01 = oA.y, o02 = oB.x, o11 = oB.y, o12 = oC.x, o22 = oC.y;
       double hc = p1.z * p2.z + p1.w * p2.w, hs = -p1.w * p2.z + p1.z * p2.w;
@@ -188,14 +186,14 @@ __global__ __launch_bounds__(kThreads) void k_linearize_own(DevGraph d) {
       double ec = z.z * hc + z.w * hs, es = -z.w * hc + z.z * hs;
       rot_normalize(ec, es);
       const double tx = hx - z.x, ty = hy - z.y;
-      const double e0 = z.z * tx + z.w * ty, e1 = -z.w * tx + z.z * ty, e2 = atan2(es, ec);
+      const double r0e = z.z * tx + z.w * ty, r1e = -z.w * tx + z.z * ty, r2e = atan2(es, ec);
       const double dt1 = -p2.w * dx + p2.z * dy, dt2 = -p2.z * dx - p2.w * dy;
       const double m00 = -hc * o00 + hs * o01, m01 = -hs * o00 - hc * o01, m02 = dt1 * o00 + dt2 * o01 - o02;
       const double m10 = -hc * o01 + hs * o11, m11 = -hs * o01 - hc * o11, m12 = dt1 * o01 + dt2 * o11 - o12;
       const double m20 = -hc * o02 + hs * o12, m21 = -hs * o02 - hc * o12, m22 = dt1 * o02 + dt2 * o12 - o22;
-      const double w0 = o00 * e0 + o01 * e1 + o02 * e2;
-      const double w1 = o01 * e0 + o11 * e1 + o12 * e2;
-      const double w2 = o02 * e0 + o12 * e1 + o22 * e2;
+      const double w0 = o00 * r0e + o01 * r1e + o02 * r2e;
+      const double w1 = o01 * r0e + o11 * r1e + o12 * r2e;
+      const double w2 = o02 * r0e + o12 * r1e + o22 * r2e;
       double* v = d.V + e;
       if (d.eside[e] == 0) {   // owner block H_ij = M'
         v[0] = m00; v[S] = m10; v[2 * S] = m20;
@@ -207,41 +205,47 @@ __global__ __launch_bounds__(kThreads) void k_linearize_own(DevGraph d) {
         v[6 * S] = m20; v[7 * S] = m21; v[8 * S] = m22;
       }
       d.W[e] = make_double4(w0, w1, w2, 0.0);
-      a00 += -hc * m00 + hs * m10;
-      a01 += -hc * m01 + hs * m11;
-      a02 += -hc * m02 + hs * m12;
-      a11 += -hs * m01 - hc * m11;
-      a12 += -hs * m02 - hc * m12;
-      a22 += dt1 * m02 + dt2 * m12 - m22;
-      g0 += -hc * w0 + hs * w1;
-      g1 += -hs * w0 - hc * w1;
-      g2 += dt1 * w0 + dt2 * w1 - w2;
+      sm[0][t] = -hc * m00 + hs * m10;
+      sm[1][t] = -hc * m01 + hs * m11;
+      sm[2][t] = -hc * m02 + hs * m12;
+      sm[3][t] = -hs * m01 - hc * m11;
+      sm[4][t] = -hs * m02 - hc * m12;
+      sm[5][t] = dt1 * m02 + dt2 * m12 - m22;
+      sm[6][t] = -hc * w0 + hs * w1;
+      sm[7][t] = -hs * w0 - hc * w1;
+      sm[8][t] = dt1 * w0 + dt2 * w1 - w2;
     }
-    a00 = sg_sum<G>(a00); a01 = sg_sum<G>(a01); a02 = sg_sum<G>(a02);
-    a11 = sg_sum<G>(a11); a12 = sg_sum<G>(a12); a22 = sg_sum<G>(a22);
-    g0 = sg_sum<G>(g0); g1 = sg_sum<G>(g1); g2 = sg_sum<G>(g2);
-    if (lane == 0) {
-      const double* dc = d.Dc + 6 * (size_t)row;
-      a00 += dc[0]; a01 += dc[1]; a02 += dc[2]; a11 += dc[3]; a12 += dc[4]; a22 += dc[5];
-      for (int q = d.prior_ptr[row]; q < d.prior_ptr[row + 1]; q++) {   // PriorFactor<Pose2>
-        const double4 pz = d.pz[q];
-        double c = p1.z * pz.z + p1.w * pz.w, s = -p1.w * pz.z + p1.z * pz.w;
-        rot_normalize(c, s);
-        const double dx = pz.x - p1.x, dy = pz.y - p1.y;
-        const double e0 = -(p1.z * dx + p1.w * dy), e1 = -(-p1.w * dx + p1.z * dy), e2 = -atan2(s, c);
-        const double2 oA = d.pom[3 * q], oB = d.pom[3 * q + 1], oC = d.pom[3 * q + 2];
-        const double o00 = oA.x, o01 = oA.y, o02 = oB.x, o11 = oB.y, o12 = oC.x, o22 = oC.y;
-        const double w0 = o00 * e0 + o01 * e1 + o02 * e2;
-        const double w1 = o01 * e0 + o11 * e1 + o12 * e2;
-        const double w2 = o02 * e0 + o12 * e1 + o22 * e2;
-        a00 += o00; a01 += o01; a02 += o02; a11 += o11; a12 += o12; a22 += o22;
-        g0 += w0; g1 += w1; g2 += w2;
+    __syncthreads();
+    if (rowt) {
+      const int kb = rb > c0 ? rb : c0, ke = re < c0 + kThreads ? re : c0 + kThreads;
+      for (int k = kb - c0; k < ke - c0; k++) {
+        a00 += sm[0][k]; a01 += sm[1][k]; a02 += sm[2][k]; a11 += sm[3][k]; a12 += sm[4][k];
+        a22 += sm[5][k]; g0 += sm[6][k]; g1 += sm[7][k]; g2 += sm[8][k];
       }
-      double* D = d.D + 6 * (size_t)row;
-      D[0] = a00; D[1] = a01; D[2] = a02; D[3] = a11; D[4] = a12; D[5] = a22;
-      double* g = d.g + 3 * (size_t)row;
-      g[0] = g0; g[1] = g1; g[2] = g2;
     }
+    __syncthreads();
+  }
+  if (rowt) {
+    const double* dc = d.Dc + 6 * (size_t)row;
+    a00 += dc[0]; a01 += dc[1]; a02 += dc[2]; a11 += dc[3]; a12 += dc[4]; a22 += dc[5];
+    for (int q = d.prior_ptr[row]; q < d.prior_ptr[row + 1]; q++) {   // PriorFactor<Pose2>
+      const double4 p1 = d.pose[row], pz = d.pz[q];
+      double c = p1.z * pz.z + p1.w * pz.w, s = -p1.w * pz.z + p1.z * pz.w;
+      rot_normalize(c, s);
+      const double dx = pz.x - p1.x, dy = pz.y - p1.y;
+      const double e0 = -(p1.z * dx + p1.w * dy), e1 = -(-p1.w * dx + p1.z * dy), e2 = -atan2(s, c);
+      const double2 oA = d.pom[3 * q], oB = d.pom[3 * q + 1], oC = d.pom[3 * q + 2];
+      const double o00 = oA.x, o01 = oA.y, o02 = oB.x, o11 = oB.y, o12 = oC.x, o22 = oC.y;
+      const double w0 = o00 * e0 + o01 * e1 + o02 * e2;
+      const double w1 = o01 * e0 + o11 * e1 + o12 * e2;
+      const double w2 = o02 * e0 + o12 * e1 + o22 * e2;
+      a00 += o00; a01 += o01; a02 += o02; a11 += o11; a12 += o12; a22 += o22;
+      g0 += w0; g1 += w1; g2 += w2;
+    }
+    double* D = d.D + 6 * (size_t)row;
+    D[0] = a00; D[1] = a01; D[2] = a02; D[3] = a11; D[4] = a12; D[5] = a22;
+    double* g = d.g + 3 * (size_t)row;
+    g[0] = g0; g[1] = g1; g[2] = g2;
   }
 }
 
@@ -557,21 +561,17 @@ hipError_t launch_linearize(const DevGraph& d, hipEvent_t start, hipEvent_t stop
   if (d.n == 0) return hipSuccess;
   const dim3 block(kThreads);
   if (!d.write_all && d.eside) {   // Cholesky mode: owner blocks in factor order
-    const long long b = ((long long)d.n * d.G1 + kThreads - 1) / kThreads;
-    const dim3 grid1((unsigned)b);
+    const dim3 grid1((unsigned)(((long long)d.n * d.G1 + kThreads - 1) / kThreads));
+    hipExtLaunchKernelGGL(k_linearize_own, dim3(d.nlb), block, 0, d.stream, start, nullptr, 0, d);
     switch (d.G1) {
-      case 4: hipExtLaunchKernelGGL(k_linearize_own<4>, grid1, block, 0, d.stream, start, nullptr, 0, d);
-              hipExtLaunchKernelGGL(k_linearize_side1<4>, grid1, block, 0, d.stream, nullptr, stop, 0, d); break;
-      case 8: hipExtLaunchKernelGGL(k_linearize_own<8>, grid1, block, 0, d.stream, start, nullptr, 0, d);
-              hipExtLaunchKernelGGL(k_linearize_side1<8>, grid1, block, 0, d.stream, nullptr, stop, 0, d); break;
-      case 16: hipExtLaunchKernelGGL(k_linearize_own<16>, grid1, block, 0, d.stream, start, nullptr, 0, d);
-               hipExtLaunchKernelGGL(k_linearize_side1<16>, grid1, block, 0, d.stream, nullptr, stop, 0, d); break;
-      default: hipExtLaunchKernelGGL(k_linearize_own<32>, grid1, block, 0, d.stream, start, nullptr, 0, d);
-               hipExtLaunchKernelGGL(k_linearize_side1<32>, grid1, block, 0, d.stream, nullptr, stop, 0, d); break;
+      case 4: hipExtLaunchKernelGGL(k_linearize_side1<4>, grid1, block, 0, d.stream, nullptr, stop, 0, d); break;
+      case 8: hipExtLaunchKernelGGL(k_linearize_side1<8>, grid1, block, 0, d.stream, nullptr, stop, 0, d); break;
+      case 16: hipExtLaunchKernelGGL(k_linearize_side1<16>, grid1, block, 0, d.stream, nullptr, stop, 0, d); break;
+      default: hipExtLaunchKernelGGL(k_linearize_side1<32>, grid1, block, 0, d.stream, nullptr, stop, 0, d); break;
     }
     return hipGetLastError();
   }
-  const dim3 grid(grid_rows(d));
+  const dim3 grid((unsigned)(((long long)d.n * d.G + kThreads - 1) / kThreads));   // one sub-group per row
   switch (d.G) {
     case 4: hipExtLaunchKernelGGL(k_linearize<4>, grid, block, 0, d.stream, start, stop, 0, d); break;
     case 8: hipExtLaunchKernelGGL(k_linearize<8>, grid, block, 0, d.stream, start, stop, 0, d); break;
