@@ -167,7 +167,7 @@ void free_device(pgo_graph* g) {
   g->lane_cap = 8;
   DevGraph& d = g->d;
   void* ptrs[] = {d.eij, d.ez, d.eom, d.prior_ptr, d.prior_vtx, d.pz, d.pom, d.row_ptr, d.slot_edge, d.slot_col, d.V,
-                  d.erow, d.brow, d.s1_ptr, d.s1_edge, d.eside, d.Dc, d.W, d.D, d.g, d.pose, d.pose_cand, d.pose_saved, d.x, d.r, d.z, d.p, d.q, d.Minv, d.part, d.scal, d.ctrl};
+                  d.erow, d.brow, d.s1_ptr, d.s1pos, d.eside, d.Dc, d.W, d.D, d.g, d.pose, d.pose_cand, d.pose_saved, d.x, d.r, d.z, d.p, d.q, d.Minv, d.part, d.scal, d.ctrl};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   hipStream_t s = d.stream;
@@ -426,9 +426,9 @@ int upload_structure(pgo_graph* g) {
   while (d.G1 < 32 && d.G1 < (n ? (double)ne / n : 0.0)) d.G1 *= 2;
   // Cholesky-mode sweep structure: factors are sorted by (ei, ej), so the
   // side-0 factors of row i are the contiguous range [erow[i], erow[i+1]);
-  // side-1 factors of row j are listed in s1_edge in device order.  Dc[j] is
+  // side-1 factors of row j take positions s1_ptr[j].. in device order (s1pos).  Dc[j] is
   // the (iteration-invariant) sum of Omega over row j's side-1 factors.
-  std::vector<int> erow(n + 1, 0), s1_ptr(n + 1, 0), s1_edge(ne);
+  std::vector<int> erow(n + 1, 0), s1_ptr(n + 1, 0), s1pos(ne);
   std::vector<double> Dc(6 * (size_t)n, 0.0);
   for (int e = 0; e < ne; e++) {
     erow[eij[e].x + 1]++;
@@ -442,7 +442,7 @@ int upload_structure(pgo_graph* g) {
     std::vector<int> f(s1_ptr.begin(), s1_ptr.end() - 1);
     for (int e = 0; e < ne; e++) {
       const int j = eij[e].y;
-      s1_edge[f[j]++] = e;
+      s1pos[e] = f[j]++;
       const double* o = &g->eom[6 * (size_t)H.dorder[e]];
       for (int q = 0; q < 6; q++) Dc[6 * (size_t)j + q] += o[q];
     }
@@ -461,12 +461,12 @@ int upload_structure(pgo_graph* g) {
   RC_TRY(h2d(g, d.brow, brow.data(), brow.size()));
   RC_TRY(dev_alloc(g, &d.erow, n + 1));
   RC_TRY(dev_alloc(g, &d.s1_ptr, n + 1));
-  RC_TRY(dev_alloc(g, &d.s1_edge, ne));
+  RC_TRY(dev_alloc(g, &d.s1pos, ne));
   RC_TRY(dev_alloc(g, &d.Dc, 6 * (size_t)n));
   RC_TRY(dev_alloc(g, &d.W, ne));
   RC_TRY(h2d(g, d.erow, erow.data(), n + 1));
   RC_TRY(h2d(g, d.s1_ptr, s1_ptr.data(), n + 1));
-  RC_TRY(h2d(g, d.s1_edge, s1_edge.data(), ne));
+  RC_TRY(h2d(g, d.s1pos, s1pos.data(), ne));
   RC_TRY(h2d(g, d.Dc, Dc.data(), 6 * (size_t)n));
   RC_TRY(dev_alloc(g, &d.eij, ne));
   RC_TRY(dev_alloc(g, &d.ez, ne));

@@ -49,11 +49,11 @@ struct DevGraph {
   int nlb = 0;                      // k_linearize_own blocks
   int* brow = nullptr;              // [nlb+1] whole rows of each block (<= kThreads rows,
                                     // side-0 factors <= kThreads unless a single row)
-  int* s1_ptr = nullptr;            // [n+1] side-1 factors of row j in s1_edge
-  int* s1_edge = nullptr;           // [E]
+  int* s1_ptr = nullptr;            // [n+1] side-1 factors of row j: W[s1_ptr[j] .. s1_ptr[j+1])
+  int* s1pos = nullptr;             // [E] position of factor e in the side-1 lists
   unsigned char* eside = nullptr;   // [E] side of the factor's owner block (set with the plan)
   double* Dc = nullptr;             // [6n] sum of Omega over the side-1 factors of each row
-  double4* W = nullptr;             // [E] Omega e of each factor (side-1 gradient hand-off)
+  double4* W = nullptr;             // [E] Omega e of each factor, side-1 list order (gradient hand-off)
   double* V = nullptr;
   double* D = nullptr;
   double* g = nullptr;

@@ -157,7 +157,7 @@ __global__ __launch_bounds__(kThreads) void k_linearize(DevGraph d) {
 // of kThreads), so a wave streams eij / z / Omega once each, coalesced, with
 // every lane busy and no erow -> factor load chain.  Each factor's owner block
 // goes to V[q * S + e] in factor order (the assembly's source index), its
-// Omega e to W[e] for row ej's gradient (k_linearize_side1); the factor's
+// Omega e to W[s1pos[e]] (row ej's side-1 list) for k_linearize_side1; the factor's
 // side-0 terms (J1' Omega J1, J1' Omega e) go through LDS to one thread per
 // row, which sums them in factor order and adds Dc[i] (sum of Omega over the
 // row's side-1 factors) and the row's priors.  No error partials: the error
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kThreads) void k_linearize_own(DevGraph d) {
         v[3 * S] = m10; v[4 * S] = m11; v[5 * S] = m12;
         v[6 * S] = m20; v[7 * S] = m21; v[8 * S] = m22;
       }
-      d.W[e] = make_double4(w0, w1, w2, 0.0);
+      d.W[d.s1pos[e]] = make_double4(w0, w1, w2, 0.0);   // row ej's side-1 list order
       sm[0][t] = -hc * m00 + hs * m10;
       sm[1][t] = -hc * m01 + hs * m11;
       sm[2][t] = -hc * m02 + hs * m12;
@@ -250,7 +250,8 @@ __global__ __launch_bounds__(kThreads) void k_linearize_own(DevGraph d) {
 }
 
 // Row j's side-1 gradient terms: g_j += sum of Omega e over the factors with
-// ej = j (fixed order: device factor order), after k_linearize_own.
+// ej = j (fixed order: device factor order), after k_linearize_own.  W is in
+// side-1 list order, so a row's terms are contiguous (no index gather).
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_linearize_side1(DevGraph d) {
   const int lane = threadIdx.x & (G - 1);
@@ -258,7 +259,7 @@ __global__ __launch_bounds__(kThreads) void k_linearize_side1(DevGraph d) {
   for (int row = (blockIdx.x * kThreads + threadIdx.x) / G; row < d.n; row += nsg) {
     double s0 = 0, s1 = 0, s2 = 0;
     for (int t = d.s1_ptr[row] + lane; t < d.s1_ptr[row + 1]; t += G) {
-      const double4 w = d.W[d.s1_edge[t]];
+      const double4 w = d.W[t];
       s0 += w.x; s1 += w.y; s2 += w.z;
     }
     s0 = sg_sum<G>(s0); s1 = sg_sum<G>(s1); s2 = sg_sum<G>(s2);
