@@ -123,6 +123,7 @@ def lib():
         "pgo_num_vertices": (C.c_size_t, [vp]),
         "pgo_error": (C.c_int, [vp, dp]),
         "pgo_debug_linearize": (C.c_int, [vp, dp, dp, dp, dp]),
+        "pgo_debug_linearize_cholesky": (C.c_int, [vp, dp, dp, dp, dp]),
         "pgo_debug_spmv": (C.c_int, [vp, C.c_double, dp, dp]),
         "pgo_debug_solve": (C.c_int, [vp, C.c_double, C.POINTER(PgoParams), dp, C.POINTER(C.c_int)]),
         "pgo_debug_plan": (C.c_int, [vp, dp, C.c_int]),

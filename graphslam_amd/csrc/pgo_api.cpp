@@ -1575,6 +1575,45 @@ int pgo_debug_linearize(pgo_graph* g, double* hdiag, double* hoff, double* grad,
   return PGO_OK;
 }
 
+// Same outputs from the Cholesky-mode linearisation (k_linearize_own +
+// k_linearize_side1): owner blocks in factor order, transposed back to
+// H_{k1,k2} where the owner is the factor's side-1 block.
+int pgo_debug_linearize_cholesky(pgo_graph* g, double* hdiag, double* hoff, double* grad, double* err) {
+  if (!g) return PGO_E_ARG;
+  RC_TRY(ensure_device(g));
+  DevGraph& d = g->d;
+  if (d.n == 0) return PGO_OK;
+  RC_TRY(ensure_chol(g));
+  d.write_all = 0;
+  HIP_TRY(g, pgo::launch_linearize(d));
+  HIP_TRY(g, pgo::launch_error(d, d.pose, d.scal));
+  std::vector<double> V(9 * (size_t)d.nslots), D(6 * (size_t)d.n), G(3 * (size_t)d.n);
+  if (d.nslots) HIP_TRY(g, hipMemcpyAsync(V.data(), d.V, V.size() * 8, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(g, hipMemcpyAsync(D.data(), d.D, D.size() * 8, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(g, hipMemcpyAsync(G.data(), d.g, G.size() * 8, hipMemcpyDeviceToHost, d.stream));
+  RC_TRY(sync_scalars(g, 1));
+  if (err) *err = g->h_scal[0];
+  if (hdiag)
+    for (int i = 0; i < d.n; i++) {
+      const double* s = &D[6 * (size_t)i];
+      double* o = hdiag + 9 * (size_t)i;
+      o[0] = s[0]; o[1] = s[1]; o[2] = s[2];
+      o[3] = s[1]; o[4] = s[3]; o[5] = s[4];
+      o[6] = s[2]; o[7] = s[4]; o[8] = s[5];
+    }
+  if (hoff)
+    for (int e = 0; e < d.ne; e++) {
+      const int se = g->h_slot_edge[g->edge_slot0[e]];
+      const size_t de = (size_t)(se >> 2);
+      const bool side0_owner = (se & 2) != 0;
+      for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++)
+          hoff[9 * (size_t)e + 3 * r + c] = V[(side0_owner ? 3 * r + c : 3 * c + r) * (size_t)d.nslots + de];
+    }
+  if (grad) std::memcpy(grad, G.data(), G.size() * 8);
+  return PGO_OK;
+}
+
 int pgo_debug_spmv(pgo_graph* g, double lambda, const double* x, double* y) {
   if (!g || !x || !y) return PGO_E_ARG;
   RC_TRY(ensure_device(g));

@@ -246,13 +246,17 @@ class PoseGraph:
     def comm_selftest(self):
         self._check(self._L.pgo_comm_selftest(self._h))
 
-    def debug_linearize(self, num_edges):
+    def debug_linearize(self, num_edges, cholesky=False):
+        """H diagonal / off-diagonal blocks, gradient and error at the current
+        values; cholesky=True takes the Cholesky-mode sweep (owner blocks in
+        factor order) instead of the two-slot block-CSR sweep."""
         n = self.num_vertices
         hd = np.zeros((n, 3, 3))
         ho = np.zeros((num_edges, 3, 3))
         g = np.zeros((n, 3))
         e = C.c_double(0)
-        self._check(self._L.pgo_debug_linearize(self._h, L.dptr(hd), L.dptr(ho), L.dptr(g), C.byref(e)))
+        fn = self._L.pgo_debug_linearize_cholesky if cholesky else self._L.pgo_debug_linearize
+        self._check(fn(self._h, L.dptr(hd), L.dptr(ho), L.dptr(g), C.byref(e)))
         return hd, ho, g, e.value
 
     def debug_spmv(self, x, lam=0.0):

@@ -248,6 +248,9 @@ int pgo_comm_selftest(pgo_graph *g);
  * off-diagonal block H_{k1,k2} = J1^T Omega of every between factor (9 per
  * factor, insertion order), gradient g = J^T Omega e (3 per vertex), error. */
 int pgo_debug_linearize(pgo_graph *g, double *hdiag, double *hoff, double *grad, double *err);
+/* The same four outputs from the Cholesky-mode linearisation (owner blocks in
+ * factor order, the path pgo_optimize takes with PGO_SOLVER_CHOLESKY). */
+int pgo_debug_linearize_cholesky(pgo_graph *g, double *hdiag, double *hoff, double *grad, double *err);
 /* y = (H + lambda I) x at the current linearisation (x, y: 3 per vertex) */
 int pgo_debug_spmv(pgo_graph *g, double lambda, const double *x, double *y);
 /* delta = PCG solve of (H + lambda I) delta = -g at the current values */

@@ -62,6 +62,26 @@ def test_linearize_parity(pg_cls, oracle_lib, name):
     assert abs(pg.error() - o.error()) <= 1e-10 * max(err0, 1e-30)
 
 
+@pytest.mark.parametrize("name", ["square", "C1", "C1-nn", "C2"])
+def test_linearize_cholesky_mode_parity(pg_cls, oracle_lib, name):
+    """k_linearize_own + k_linearize_side1 (owner blocks in factor order, W
+    hand-off, row sums through LDS) vs the oracle, same tolerance as the
+    two-slot sweep; also vs that sweep on the same handle."""
+    g = load(name)
+    pg = pg_cls.from_dataset(g)
+    hd, ho, grad, err = pg.debug_linearize(g.num_edges, cholesky=True)
+    hd0, ho0, g0, err0 = oracle_lib.Oracle(g).linearize()
+    scale_h = np.abs(hd0).max()
+    assert np.abs(hd - hd0).max() <= 1e-10 * scale_h
+    assert np.abs(ho - ho0).max() <= 1e-10 * scale_h
+    assert np.abs(grad - g0).max() <= 1e-10 * max(np.abs(g0).max(), 1.0)
+    assert abs(err - err0) <= 1e-10 * max(err0, 1e-30)
+    hd1, ho1, g1, _ = pg.debug_linearize(g.num_edges)
+    assert np.abs(hd - hd1).max() <= 1e-12 * scale_h
+    assert np.abs(ho - ho1).max() <= 1e-14 * scale_h   # same per-factor arithmetic, no sums
+    assert np.abs(grad - g1).max() <= 1e-12 * max(np.abs(g1).max(), 1.0)
+
+
 def test_linearize_nondiagonal_covariance(pg_cls, oracle_lib):
     g = datasets.make("C1")
     rng = np.random.default_rng(5)
