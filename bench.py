@@ -54,26 +54,116 @@ def linearize_bytes(n, ne):
     return ne * 152 + n * 96
 
 
-def cpu_baseline(g, max_outer):
-    """The C oracle (same LM, sparse Cholesky) on a bounded sample: the first
-    max_outer linearisations from the same initial values."""
-    from oracle.oracle import Oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    o = Oracle(g)
-    r = o.optimize(max_outer=max_outer)
-    s = r.stats
-    t = s["t_total"]
+def _host_info():
+    import platform
+    model = platform.processor()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model}
+
+
+def cpu_baseline(g, pg, per_step, reps=5, amd_reps=3):
+    """The C restatement (oracle/pgo_oracle.c: same LM, supernodal multifrontal
+    Cholesky) on the host cores of this box, like-for-like with the GPU step
+    (SURVEY 8d / BASELINE.md):
+
+    * same fill: the CPU factorises on the GPU plan's nested-dissection
+      ordering (handed over from pgo_debug_ordering); the oracle's own AMD is
+      timed too (amd_all_cores);
+    * same try mix: one LM unit (initial error + 1 linearisation + 1 lambda
+      try -- factor, solve, model decrease, retract, error; C3's first
+      linearisation accepts lambda_initial) is timed, median of `reps` after
+      one warm-up, and the GPU trajectory's counts (per_step: L linearisations,
+      T tries, both identical to the oracle's, tests/test_gpu_parity.py) are
+      priced with it: t = t_err0 + L t_lin + T t_try;
+    * all host cores (OMP_NUM_THREADS) and 1 core.
+    """
+    import statistics
+    from oracle.oracle import Oracle, set_threads
+    threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+    L, T = per_step["linearizations"], per_step["lm_tries"]
+
+    def unit(o, n):
+        o.optimize(max_outer=1)                           # warm-up
+        runs = [o.optimize(max_outer=1).stats for _ in range(n)]
+        t_lin = statistics.median(r["t_linearize"] for r in runs)
+        t_err0 = statistics.median(r["t_error"] for r in runs) / 2.0   # initial + candidate error
+        t_try = statistics.median(r["t_total"] - r["t_linearize"] for r in runs) - t_err0
+        t_traj = t_err0 + L * t_lin + T * t_try
+        return {"value": L / t_traj, "ms_per_try": 1e3 * t_try, "ms_per_linearization": 1e3 * t_lin,
+                "ms_trajectory": 1e3 * t_traj, "factor_flops": runs[0]["factor_flops"], "nnz_l": runs[0]["nnz_l"],
+                "reps": n}
+
+    o_nd = Oracle(g, order=pg.debug_ordering())
+    set_threads(threads)
+    allc = unit(o_nd, reps)
+    set_threads(1)
+    one = unit(o_nd, reps)
+    o_nd.close()
+    set_threads(threads)
+    o_amd = Oracle(g)
+    amd = unit(o_amd, amd_reps)
+    o_amd.close()
     return {
-        "value": s["linearizations"] / t,
+        "value": allc["value"],
         "unit": "GN iterations/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"first {s['linearizations']} LM linearisations ({s['inner_iterations']} Cholesky solves, "
-                   f"{s['factor_flops'] / 1e9:.1f} GFLOP each, nnz(L) {s['nnz_l'] / 1e6:.0f}M) of {g.name} "
-                   f"from the same initial values, {t:.1f} s, oracle/pgo_oracle.c AMD + supernodal "
-                   f"multifrontal Cholesky, OMP_NUM_THREADS={threads}"),
-        "ms_per_linearization": 1e3 * t / max(s["linearizations"], 1),
+        "sample": (f"{g.name}: median of {reps} LM units (initial error + 1 linearisation + 1 lambda try: "
+                   f"{allc['factor_flops'] / 1e9:.1f} GFLOP supernodal Cholesky on the GPU plan's nested-dissection "
+                   f"ordering, nnz(L) {allc['nnz_l'] / 1e6:.0f}M) after 1 warm-up, oracle/pgo_oracle.c, "
+                   f"{threads} OpenMP threads; priced on the GPU trajectory's {L} linearisations / {T} tries"),
+        "all_cores": allc,
+        "one_core": one,
+        "amd_all_cores": amd,
+        "host": _host_info(),
     }
+
+
+def factor_roofline(kprof, totals, factor_flops):
+    """Roofline of the dominant kernel family of the factor + solve (largest
+    summed device time over the profiled factorisations, every launch timed
+    with dispatch events on its own stream): achieved = algorithmic flops (MFMA
+    families) or HBM bytes (extend-add, zeroing, assembly) per launch / average
+    launch time.  Also the factorisation aggregate: algorithmic flops of one
+    factorisation / device time from its first to its last launch."""
+    fams = {}
+    for k, v in kprof.items():
+        if v["launches"] == 0:
+            continue
+        mfma = v["flops"] > 0
+        per = (v["flops"] if mfma else v["bytes"]) / v["launches"]
+        avg = v["ms"] / v["launches"]
+        ach = per / (avg * 1e-3) / (1e12 if mfma else 1e9) if avg > 0 else None
+        fams[k] = {"launches": v["launches"], "ms": v["ms"], "avg_launch_ms": avg,
+                   "bound": "mfma" if mfma else "hbm", "unit": "TFLOP/s" if mfma else "GB/s",
+                   ("flops_per_launch" if mfma else "bytes_per_launch"): per, "achieved": ach,
+                   "frac": ach / (FP64_MFMA_PEAK_TFS if mfma else HBM_PEAK_GBS) if ach else None}
+    total_ms = sum(f["ms"] for f in fams.values())
+    for f in fams.values():
+        f["share"] = f["ms"] / total_ms if total_ms else None
+    top = max(fams, key=lambda k: fams[k]["ms"]) if fams else None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    pmc = json.load(open(pmc_path)).get("C3", {}) if os.path.exists(pmc_path) else {}
+    agg = None
+    if totals["fac_n"]:
+        fac_ms = totals["fac_ms"] / totals["fac_n"]
+        tfs = factor_flops / (fac_ms * 1e-3) / 1e12
+        agg = {"flops": factor_flops, "ms": fac_ms, "achieved": tfs, "frac": tfs / FP64_MFMA_PEAK_TFS,
+               "solve_ms": totals["sol_ms"] / totals["fac_n"], "profiled_factorizations": totals["fac_n"]}
+    out = {"kernel": top, "profiled_factorizations": totals["fac_n"], "factorization": agg, "families": fams,
+           "measured_loop_peak_tfs": FP64_MFMA_LOOP_TFS}
+    if top:
+        t = fams[top]
+        out.update(bound=t["bound"], achieved=t["achieved"], unit=t["unit"], frac=t["frac"],
+                   peak=FP64_MFMA_PEAK_TFS if t["bound"] == "mfma" else HBM_PEAK_GBS,
+                   avg_launch_ms=t["avg_launch_ms"], traffic=pmc.get(f"{top}_bytes_per_launch"))
+    return out
 
 
 def closest_keyframe_bench(pg, g, skip=10, reps=20):
@@ -115,7 +205,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--profile-every", type=int, default=16)
-    ap.add_argument("--cpu-outer", type=int, default=2)
+    ap.add_argument("--cpu-reps", type=int, default=5, help="timed CPU LM units per thread count (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--solver", choices=["cholesky", "pcg"], default="cholesky")
     ap.add_argument("--no-graphs", action="store_true",
@@ -159,9 +249,15 @@ def main():
                             linear_solver=1 if args.solver == "cholesky" else 0,
                             use_graphs=0 if args.no_graphs else 1, lambda_lanes=args.lanes)
 
+    kprof = {}
+
     def step():
         pg.restore_values()
         st = pg.optimize(params)         # returns after the handle's stream has drained
+        for k, v in pg.kernel_profile().items():   # profiled factorisations of this step (host copy)
+            a = kprof.setdefault(k, dict(launches=0, ms=0.0, flops=0.0, bytes=0.0))
+            for f in a:
+                a[f] += v[f]
         return st["linearizations"], st
 
     elapsed, lin_total, results = timed_steps(r, step, args.steps, args.warmup)
@@ -186,9 +282,9 @@ def main():
     totals = dict(spmv_ms=sum(s["kernel_spmv_ms"] for s in stats), spmv_n=sum(s["kernel_spmv_count"] for s in stats),
                   lin_ms=sum(s["kernel_linearize_ms"] for s in stats),
                   lin_n=sum(s["kernel_linearize_count"] for s in stats),
-                  syrk_ms=sum(s["kernel_syrk_ms"] for s in stats),
-                  syrk_n=sum(s["kernel_syrk_count"] for s in stats),
-                  syrk_launches=sum(s["kernel_syrk_launches"] for s in stats))
+                  fac_n=sum(s["kernel_syrk_count"] for s in stats),
+                  fac_ms=sum(s["ms_factor_profiled"] for s in stats),
+                  sol_ms=sum(s["ms_solve_profiled"] for s in stats))
 
     if rank == 0:
         n, ne = g.num_poses, g.num_edges
@@ -207,22 +303,7 @@ def main():
                 "timed_launches": totals["spmv_n"],
             }
         else:
-            # Schur updates (k_panel_syrk_lds / k_panel_syrk128 launches) of the
-            # profiled factorisations (every --profile-every'th), each launch timed
-            # by dispatch events on the library's stream: achieved = algorithmic
-            # flops per launch / average launch duration
-            nl = last["kernel_syrk_count"] and totals["syrk_launches"] / totals["syrk_n"]
-            avg_ms = totals["syrk_ms"] / totals["syrk_launches"] if totals["syrk_launches"] else None
-            flops_launch = last["syrk_flops"] / nl if nl else None
-            syrk_tfs = flops_launch / (avg_ms * 1e-3) / 1e12 if avg_ms else None
-            roofline = {
-                "kernel": "k_panel_syrk_lds", "bound": "mfma", "achieved": syrk_tfs, "peak": FP64_MFMA_PEAK_TFS,
-                "unit": "TFLOP/s", "frac": syrk_tfs / FP64_MFMA_PEAK_TFS if syrk_tfs else None,
-                "traffic": pmc.get("k_panel_syrk_lds_bytes_per_launch"),
-                "measured_loop_peak_tfs": FP64_MFMA_LOOP_TFS,
-                "flops_per_launch": flops_launch, "avg_launch_ms": avg_ms, "launches_per_factorization": nl,
-                "profiled_factorizations": totals["syrk_n"], "factor_flops": last["factor_flops"],
-            }
+            roofline = factor_roofline(kprof, totals, last["factor_flops"])
         out = {
             "metric": "GN iterations/sec + ms-to-chi2 convergence, 100k-pose Manhattan graph",
             "value": lin_total / elapsed,
@@ -253,6 +334,9 @@ def main():
                 "initial_error": last["initial_error"], "final_error": last["final_error"],
                 "ms_linearize": last["ms_linearize"], "ms_solve": last["ms_solve"], "ms_update": last["ms_update"],
                 "lambda_rounds": last["lambda_rounds"], "solves_rank0": last["solves"], "ms_comm": last["ms_comm"],
+                "stop_reason": _lib.STOP_REASONS.get(last["stop_reason"], str(last["stop_reason"])),
+                # expected 0.5 chi^2 at the optimum: half the residual dimension minus the pose dof
+                "expected_error_at_optimum": 0.5 * (3 * (ne + len(g.prior_keys)) - 3 * n),
             },
             "roofline": roofline,
             "linearize_kernel": {
@@ -271,7 +355,9 @@ def main():
             "closest_keyframe": search,
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(g, args.cpu_outer)
+            out["cpu_baseline"] = cpu_baseline(g, pg, out["per_step"], reps=args.cpu_reps)
+            out["cpu_baseline"]["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+            out["cpu_baseline"]["gpu_over_cpu_one_core"] = out["value"] / out["cpu_baseline"]["one_core"]["value"]
         print(json.dumps(out))
     if spec:
         pg.comm_free()

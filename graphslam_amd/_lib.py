@@ -35,6 +35,8 @@ PGO_ALG_LM = 0
 PGO_ALG_GN = 1
 PGO_SOLVER_PCG = 0
 PGO_SOLVER_CHOLESKY = 1
+STOP_REASONS = {0: "converged", 1: "lambda_upper_bound", 2: "max_iterations", 3: "max_outer", 4: "small_cost_change",
+                5: "error"}
 
 
 class PgoOpts(C.Structure):
@@ -62,7 +64,8 @@ class PgoStats(C.Structure):
                 ("kernel_syrk_ms", C.c_double), ("kernel_syrk_count", C.c_longlong),
                 ("syrk_flops", C.c_double), ("factor_flops", C.c_double),
                 ("kernel_syrk_launches", C.c_longlong), ("lambda_rounds", C.c_int), ("ranks", C.c_int),
-                ("solves", C.c_longlong), ("ms_comm", C.c_double)]
+                ("solves", C.c_longlong), ("ms_comm", C.c_double),
+                ("ms_factor_profiled", C.c_double), ("ms_solve_profiled", C.c_double), ("stop_reason", C.c_int)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
@@ -138,12 +141,16 @@ def lib():
         "pgo_comm_free": (C.c_int, [vp]),
         "pgo_comm_rank": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "pgo_comm_selftest": (C.c_int, [vp]),
+        "pgo_get_trace": (C.c_int, [vp, dp, C.c_int]),
+        "pgo_get_kernel_profile": (C.c_int, [vp, dp, C.c_int]),
+        "pgo_kernel_family_name": (C.c_char_p, [C.c_int]),
+        "pgo_debug_ordering": (C.c_int, [vp, C.POINTER(C.c_int32), C.c_size_t]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.pgo_abi_version() != 3:
+    if L.pgo_abi_version() != 4:
         raise RuntimeError("libpgo.so ABI version mismatch")
     _lib = L
     return L

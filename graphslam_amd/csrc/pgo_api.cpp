@@ -69,8 +69,15 @@ struct pgo_graph {
   pgo::CholPlan chol;
   int ordering = pgo::kOrderNd;             // fill-reducing ordering (pgo_opts.ordering)
   bool chol_ready = false;
-  std::vector<hipEvent_t> sev;              // syrk profiling event pairs
-  std::vector<double> sev_flops;
+  // profiled factorisations (pgo_params.profile_every): every launch timed
+  std::vector<hipEvent_t> sev;              // event pairs, one per launch
+  std::vector<int> sev_fam;
+  std::vector<double> sev_flops, sev_bytes;
+  std::vector<int> sev_grid, sev_tag;
+  hipEvent_t fev[4] = {};                   // factor start / end, solve end (profiled factorisation)
+  double fam_ms[pgo::kFamCount] = {}, fam_flops[pgo::kFamCount] = {}, fam_bytes[pgo::kFamCount] = {};
+  long long fam_launches[pgo::kFamCount] = {};
+  std::vector<double> trace;                // per lambda try / GN step of the last optimize (kTraceCols each)
   long long factorizations = 0;
   hipGraphExec_t chol_exec = nullptr;       // captured factor + solve (static per structure)
   double* h_lam = nullptr;                  // pinned lambda staging
@@ -96,6 +103,9 @@ struct pgo_graph {
 };
 
 namespace {
+
+constexpr int kProfLaunches = 4096;   // timed launches per profiled factorisation + solve
+constexpr int kTraceCols = 8;         // pgo_get_trace row
 
 int fail(pgo_graph* g, int code, const std::string& msg) {
   if (g) g->last_error = msg;
@@ -196,9 +206,14 @@ int ensure_hip(pgo_graph* g) {
   for (auto& e : g->ev) HIP_TRY(g, hipEventCreate(&e));
   for (auto& e : g->pev) HIP_TRY(g, hipEventCreate(&e));
   HIP_TRY(g, hipEventCreateWithFlags(&g->lin_done, hipEventDisableTiming));
-  g->sev.resize(2 * 512);
-  g->sev_flops.resize(512);
+  g->sev.resize(2 * kProfLaunches);
+  g->sev_fam.resize(kProfLaunches);
+  g->sev_flops.resize(kProfLaunches);
+  g->sev_bytes.resize(kProfLaunches);
+  g->sev_grid.resize(kProfLaunches);
+  g->sev_tag.resize(kProfLaunches);
   for (auto& e : g->sev) HIP_TRY(g, hipEventCreate(&e));
+  for (auto& e : g->fev) HIP_TRY(g, hipEventCreate(&e));
   g->hip_ready = true;
   return PGO_OK;
 }
@@ -620,7 +635,7 @@ int pcg_solve(pgo_graph* g, const pgo_params& p, double lam, PcgResult* out, pgo
 struct SolveState {
   bool known = true, solved = true;
   bool profiled = false;
-  pgo::SyrkProfile prof;
+  pgo::LaunchProfile prof;
 };
 
 int linear_solve(pgo_graph* g, const pgo_params& p, double lam, pgo_stats* st, SolveState* ss) {
@@ -636,19 +651,26 @@ int linear_solve(pgo_graph* g, const pgo_params& p, double lam, pgo_stats* st, S
   const DevGraph& d = g->d;
   ss->profiled = st && p.profile_every > 0 && (g->factorizations % p.profile_every) == 0;
   g->factorizations++;
-  pgo::SyrkProfile* prof = nullptr;
+  pgo::LaunchProfile* prof = nullptr;
   if (ss->profiled) {
     ss->prof.ev = g->sev.data();
-    ss->prof.cap = (int)g->sev_flops.size();
+    ss->prof.cap = kProfLaunches;
     ss->prof.used = 0;
+    ss->prof.fam = g->sev_fam.data();
     ss->prof.flops = g->sev_flops.data();
+    ss->prof.bytes = g->sev_bytes.data();
+    ss->prof.grid = g->sev_grid.data();
+    ss->prof.tag = g->sev_tag.data();
     prof = &ss->prof;
   }
   *g->h_lam = lam;
   HIP_TRY(g, hipMemcpyAsync(g->chol.d_lambda, g->h_lam, sizeof(double), hipMemcpyHostToDevice, d.stream));
-  if (prof || !p.use_graphs) {  // eager: profiled factorisations time their Schur-update launches
+  if (prof || !p.use_graphs) {  // eager: a profiled factorisation times every launch
+    if (prof) HIP_TRY(g, hipEventRecord(g->fev[0], d.stream));
     HIP_TRY(g, pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, prof));
-    HIP_TRY(g, pgo::chol_solve(g->chol, d.x, d.stream));
+    if (prof) HIP_TRY(g, hipEventRecord(g->fev[1], d.stream));
+    HIP_TRY(g, pgo::chol_solve(g->chol, d.x, d.stream, 1, 0, prof));
+    if (prof) HIP_TRY(g, hipEventRecord(g->fev[2], d.stream));
   } else {
     if (!g->chol_exec) {  // capture once per structure: ~1e3 launches -> one graph launch
       hipGraph_t graph = nullptr;
@@ -676,12 +698,36 @@ int finish_solve(pgo_graph* g, pgo_stats* st, SolveState* ss) {
   ss->known = true;
   if (st) st->factor_flops = g->chol.flops;
   if (ss->profiled && st) {
-    double ms = 0.0;
-    for (int u = 0; u < ss->prof.used; u++) ms += ms_between(ss->prof.ev[2 * u], ss->prof.ev[2 * u + 1]);
-    st->kernel_syrk_ms += ms;
+    for (int u = 0; u < ss->prof.used; u++) {
+      const int f = ss->prof.fam[u];
+      const double ms = ms_between(ss->prof.ev[2 * u], ss->prof.ev[2 * u + 1]);
+      g->fam_ms[f] += ms;
+      g->fam_flops[f] += ss->prof.flops[u];
+      g->fam_bytes[f] += ss->prof.bytes[u];
+      g->fam_launches[f]++;
+      if (f == pgo::kFamPanelSyrk || f == pgo::kFamPanelSyrk128) {
+        st->kernel_syrk_ms += ms;
+        st->kernel_syrk_launches++;
+      }
+    }
     st->kernel_syrk_count++;
-    st->kernel_syrk_launches += ss->prof.used;
     st->syrk_flops = g->chol.syrk_flops;
+    // PGO_PROFILE_DUMP=path: append the launch timeline of this factorisation
+    // (family, level, panel step, workgroups, start and duration in ms from the
+    // factorisation's first event, algorithmic flops, bytes)
+    if (const char* path = getenv("PGO_PROFILE_DUMP")) {
+      if (FILE* f = fopen(path, "a")) {
+        fprintf(f, "# factorisation %lld\n", g->factorizations - 1);
+        for (int u = 0; u < ss->prof.used; u++)
+          fprintf(f, "%s %d %d %d %.4f %.4f %.4g %.4g\n", pgo::kernel_family_name(ss->prof.fam[u]),
+                  ss->prof.tag[u] >> 16, ss->prof.tag[u] & 0xffff, ss->prof.grid[u],
+                  ms_between(g->fev[0], ss->prof.ev[2 * u]), ms_between(ss->prof.ev[2 * u], ss->prof.ev[2 * u + 1]),
+                  ss->prof.flops[u], ss->prof.bytes[u]);
+        fclose(f);
+      }
+    }
+    st->ms_factor_profiled += ms_between(g->fev[0], g->fev[1]);
+    st->ms_solve_profiled += ms_between(g->fev[1], g->fev[2]);
   }
   return PGO_OK;
 }
@@ -898,6 +944,10 @@ void pgo_destroy(pgo_graph* g) {
     if (g->h_lanes) (void)hipHostFree(g->h_lanes);
     for (auto& e : g->pev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : g->sev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : g->fev)
+      if (e) (void)hipEventDestroy(e);
     if (g->lin_done) (void)hipEventDestroy(g->lin_done);
     void* sp[] = {g->s_d, g->s_i, g->sb_d, g->sb_i, g->sb_q, g->sbp_d, g->sbp_i};
     for (void* q : sp)
@@ -1086,6 +1136,20 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   std::memset(&st, 0, sizeof(st));
   const auto T0 = std::chrono::steady_clock::now();
   auto upload0 = std::chrono::steady_clock::now();
+  g->trace.clear();
+  for (int f = 0; f < pgo::kFamCount; f++) {
+    g->fam_ms[f] = g->fam_flops[f] = g->fam_bytes[f] = 0.0;
+    g->fam_launches[f] = 0;
+  }
+  auto since_T0 = [&]() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count();
+  };
+  // per-iteration record (pgo_get_trace): the oracle's trace columns + wall ms
+  auto trace_row = [&](double it, double lam_t, double solved, double lin_change, double new_e, double fid,
+                       double acc) {
+    const double row[kTraceCols] = {it, lam_t, solved, lin_change, new_e, fid, acc, since_T0()};
+    g->trace.insert(g->trace.end(), row, row + kTraceCols);
+  };
   int rc = ensure_device(g);
   if (rc != PGO_OK) return rc;
   st.ms_upload = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - upload0).count();
@@ -1152,13 +1216,14 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   };
   pgo::Comm& cm = g->comm;
   const int P = cm.size, me = cm.rank;
+  const bool exchange = P > 1 || pgo::force_collectives(&cm);   // forced: 1-rank RCCL runs the collectives
   st.ranks = P;
   // lanes: concurrent tries on this GPU (Cholesky LM only)
   int L = 1;
   if (p.algorithm != PGO_ALG_GN && p.linear_solver != PGO_SOLVER_PCG && p.lambda_lanes > 1 && d.n > 0)
     L = ensure_lanes(g, p.lambda_lanes);
   // every rank must agree on the lanes per rank (a lane allocation may fail on one)
-  if (P > 1) {
+  if (exchange) {
     std::vector<double> all(P);
     const double mineL = L;
     std::string why;
@@ -1168,6 +1233,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   }
   const int T = P * L;                       // tries per round
   std::vector<double> lam_k(T), fac_k(T), outs(4 * T);
+  int last_outcome = PGO_STOP_CONVERGED;     // how the last linearisation's tries ended
   std::vector<char> valid(T);
   if (!(err <= p.error_tol) && iters < p.max_iterations && d.n > 0) {
     double new_err = err;
@@ -1188,6 +1254,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
         err = o[1];
         iters++;
         inner++;
+        trace_row(iters, 0.0, 1.0, NAN, err, 0.0, 1.0);
       } else {
         // Lambda rounds.  GTSAM tries lam_0 = lam, lam_{k+1} = lam_k * f_k (f_k
         // doubling when the factor is not fixed) until one is accepted, the cost
@@ -1219,7 +1286,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
             account_linearize();
           }
           st.lambda_rounds++;
-          if (P > 1) {
+          if (exchange) {
             const auto c0 = std::chrono::steady_clock::now();
             std::string why;
             const int rc = pgo::comm_allgather(&cm, mine.data(), 4 * L, outs.data(), d.stream, &why);
@@ -1240,13 +1307,13 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
           double new_e = INFINITY;
           for (int k = 0; k < T && valid[k]; k++) {
             const double* o = &outs[4 * k];
-            double fidelity = 0.0;
+            double fidelity = 0.0, lin_change = NAN, try_e = INFINITY;
             bool success = false, stop = false;
             if (o[0] == 1.0) {
               const double xhx = o[2], gx = o[3];
-              const double lin_change = -(gx + 0.5 * xhx);
+              lin_change = -(gx + 0.5 * xhx);
               if (lin_change >= 0) {
-                new_e = o[1];
+                new_e = try_e = o[1];
                 const double cost_change = err - new_e;
                 if (lin_change > 2.220446049250313e-16 * err) {
                   fidelity = cost_change / lin_change;
@@ -1255,8 +1322,11 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
                 if (std::fabs(cost_change) < p.relative_error_tol * err) stop = true;
               }
             }
+            trace_row(iters, lam_k[k], o[0], lin_change, try_e, fidelity, success ? 1.0 : 0.0);
             lam = lam_k[k];
             factor = fac_k[k];
+            if (success) last_outcome = PGO_STOP_CONVERGED;
+            else if (stop) last_outcome = PGO_STOP_SMALL_CHANGE;
             if (success) {  // decreaseLambda
               if (p.use_fixed_lambda_factor) {
                 lam /= p.lambda_factor;
@@ -1278,6 +1348,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
             inner++;
             if (!p.use_fixed_lambda_factor) factor *= 2.0;
             if (lam >= p.lambda_upper_bound) {
+              last_outcome = PGO_STOP_LAMBDA_BOUND;
               done = true;
               break;
             }
@@ -1286,7 +1357,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
             const int wr = winner / L, wl = winner % L;
             // the accepted candidate values: lane wl's buffer on rank wr
             double4** cand = wr == me && wl > 0 ? &g->lanes[wl - 1].pose_cand : &d.pose_cand;
-            if (P > 1) {
+            if (exchange) {
               const auto c0 = std::chrono::steady_clock::now();
               std::string why;
               const int rc = pgo::comm_broadcast_device(&cm, *cand, sizeof(double4) * (size_t)d.n, wr, d.stream, &why);
@@ -1303,11 +1374,16 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
       }
       if (status != PGO_OK) break;
       new_err = err;
-      if (p.max_outer > 0 && st.linearizations >= p.max_outer) break;
+      if (p.max_outer > 0 && st.linearizations >= p.max_outer) {
+        last_outcome = PGO_STOP_MAX_OUTER;
+        break;
+      }
       if (!(iters < p.max_iterations && !check_convergence(p, cur_err, new_err) && std::isfinite(cur_err))) break;
     }
   }
   if (status == PGO_OK && iters >= p.max_iterations && p.max_iterations > 0) status = PGO_W_MAXITER;
+  st.stop_reason = status < 0 ? PGO_STOP_ERROR
+                   : (status == PGO_W_MAXITER && last_outcome != PGO_STOP_MAX_OUTER ? PGO_STOP_MAX_ITER : last_outcome);
   g->host_values = false;
   st.status = status;
   st.iterations = iters;
@@ -1472,6 +1548,44 @@ int pgo_comm_selftest(pgo_graph* g) {
   }
   for (int i = 0; i < nb; i++)
     if (h[i] != root * 1e6 + i) return fail(g, PGO_E_COMM, "broadcast returned wrong data");
+  return PGO_OK;
+}
+
+int pgo_get_trace(const pgo_graph* g, double* out, int cap) {
+  if (!g || cap < 0 || (cap > 0 && !out)) return PGO_E_ARG;
+  const int rows = (int)(g->trace.size() / kTraceCols);
+  std::memcpy(out, g->trace.data(), sizeof(double) * kTraceCols * std::min(rows, cap));
+  return rows;
+}
+
+const char* pgo_kernel_family_name(int f) { return pgo::kernel_family_name(f); }
+
+int pgo_get_kernel_profile(const pgo_graph* g, double* out, int cap) {
+  if (!g || cap < 0 || (cap > 0 && !out)) return PGO_E_ARG;
+  for (int f = 0; f < pgo::kFamCount && f < cap; f++) {
+    double* o = out + 5 * (size_t)f;
+    o[0] = (double)g->fam_launches[f];
+    o[1] = g->fam_ms[f];
+    o[2] = g->fam_flops[f];
+    o[3] = g->fam_bytes[f];
+    o[4] = 0.0;
+  }
+  return pgo::kFamCount;
+}
+
+int pgo_debug_ordering(pgo_graph* g, int32_t* perm, size_t n) {
+  if (!g || (n && !perm) || n != g->keys.size()) return PGO_E_ARG;
+  RC_TRY(download_values(g));
+  if (g->chol_ready) {
+    std::memcpy(perm, g->chol.perm.data(), n * sizeof(int32_t));
+    return PGO_OK;
+  }
+  HostStructure H;
+  RC_TRY(build_structure(g, H));
+  pgo::CholPlan P;
+  P.ordering = g->ordering;
+  pgo::chol_analyze(P, (int)n, H.row_ptr, H.slot_col);
+  std::memcpy(perm, P.perm.data(), n * sizeof(int32_t));
   return PGO_OK;
 }
 

@@ -160,12 +160,25 @@ hipError_t chol_set_batch(CholPlan& P, int nb, hipStream_t s);
 
 // device: factor H + lambda I (D: 6 doubles/pose upper, V: slot blocks as structure of
 // arrays V[q * nslots + slot], old indexing; only the slots in asm_src are read)
-// prof (optional): timing of the Schur-update launches with dispatch events;
-// pairs of events, capacity cap; *used pairs recorded, flops[i] per pair.
-struct SyrkProfile {
+// prof (optional): every launch of the factorisation / solve timed with
+// dispatch events (hipExtLaunchKernelGGL start/stop on the launch's stream),
+// with its kernel family and algorithmic flops / HBM bytes: pairs of events,
+// capacity cap, *used pairs recorded.
+enum KernelFamily {
+  kFamAssemble = 0, kFamZero, kFamPerm, kFamExtendAdd, kFamVecAssemble, kFamFrontWave, kFamFrontSmall,
+  kFamPanelDiag, kFamPanelTrsm, kFamPanelSyrk, kFamPanelSyrk128, kFamSyrkDiag, kFamStepFused,
+  kFamBwdPart, kFamBwdInit, kFamBwdStep, kFamCount
+};
+const char* kernel_family_name(int f);
+struct LaunchProfile {
   hipEvent_t* ev = nullptr;
   int cap = 0, used = 0;
+  int* fam = nullptr;
   double* flops = nullptr;
+  double* bytes = nullptr;
+  int* grid = nullptr;             // workgroups (x) of each launch
+  int* tag = nullptr;              // level << 16 | panel step of each launch (timeline dumps)
+  int cur_tag = 0;
 };
 // lambda is read from P.d_lambda (set it with a stream-ordered copy first).  The
 // right-hand side scale_b * b (old pose indexing) is carried through the
@@ -174,12 +187,13 @@ struct SyrkProfile {
 // in its own workspace, grid dimension y of every launch (bitwise equal to a
 // one-lane factorisation)
 hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
-                       hipStream_t s, SyrkProfile* prof = nullptr, int nb = 1);
+                       hipStream_t s, LaunchProfile* prof = nullptr, int nb = 1);
 // after chol_factor: 3x3 blocks of (L L^T)^{-1} at the given poses (old index),
 // row-major 9 doubles each into host memory out (synchronises the stream)
 hipError_t chol_marginals(const CholPlan& P, const int* poses, int n, double* out, hipStream_t s);
 // after chol_factor: x = L^-T y = (L L^T)^{-1} scale_b b, indexed by old pose
 // lane y's solution to x + y * xstride
-hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb = 1, long long xstride = 0);
+hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb = 1, long long xstride = 0,
+                      LaunchProfile* prof = nullptr);
 
 }  // namespace pgo

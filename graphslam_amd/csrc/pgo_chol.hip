@@ -1546,20 +1546,82 @@ void chol_free(CholPlan& P) {
   P = CholPlan();
 }
 
+const char* kernel_family_name(int f) {
+  static const char* const names[kFamCount] = {
+      "k_asm_offdiag+k_asm_diag", "k_zero_lower", "k_perm_in+k_perm_out", "k_extend_add", "k_vec_assemble",
+      "k_front_wave", "k_front_small", "k_panel_diag", "k_panel_trsm", "k_panel_syrk_lds", "k_panel_syrk128",
+      "k_syrk_diag", "k_step_fused", "k_bwd_part", "k_bwd_init", "k_bwd_step"};
+  return f >= 0 && f < kFamCount ? names[f] : "?";
+}
+
+// Launch through the profile: with prof, the launch is bracketed by dispatch
+// events on its stream and recorded with its family and algorithmic work
+// (cost(): {flops, bytes}, evaluated only for profiled launches).
+template <typename Cost, typename K, typename... Args>
+static void launch(LaunchProfile* prof, int fam, Cost cost, K kern, dim3 grid, dim3 block, size_t smem,
+                   hipStream_t s, Args... args) {
+  if (prof && prof->used < prof->cap) {
+    const int u = prof->used++;
+    const double2 fb = cost();
+    prof->fam[u] = fam;
+    prof->flops[u] = fb.x;
+    prof->bytes[u] = fb.y;
+    if (prof->grid) prof->grid[u] = (int)grid.x;
+    if (prof->tag) prof->tag[u] = prof->cur_tag;
+    hipExtLaunchKernelGGL(kern, grid, block, smem, s, prof->ev[2 * u], prof->ev[2 * u + 1], 0, args...);
+  } else {
+    hipLaunchKernelGGL(kern, grid, block, smem, s, args...);
+  }
+}
+
+// algorithmic work of the factorisation's launches (host, profiled launches only)
+static double chol_flops(int m, int w) {   // dense Cholesky of the w pivot columns of an m-row front
+  double f = 0;
+  for (int k = 0; k < w; k++) {
+    const double r = m - k - 1;
+    f += 1 + r + r * (r + 1);
+  }
+  return f;
+}
+static double potrf_inv_flops(int nb) { return 2.0 * nb * nb * (double)nb / 3.0; }   // factor + inverse
+static double sdiag_flops(const CholPlan& P, const int4& t, int kb) {
+  const int s = t.x, kn = t.y, w = P.w[s];
+  const int nb = std::min(kNB, w - kn), K = std::min(kb + kNB, w) - (t.w & 0x7fffffff);
+  return (double)K * nb * (nb + 1) + potrf_inv_flops(nb);
+}
+
 hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
-                       hipStream_t s, SyrkProfile* prof, int nb) {
+                       hipStream_t s, LaunchProfile* prof, int nb) {
   if (P.n == 0) return hipSuccess;
   if (nb < 1 || nb > P.batch) return hipErrorInvalidValue;
   const CholDev c = dev_view(P);
-  k_perm_in<<<dim3((P.n + 255) / 256, nb), 256, 0, s>>>(c, b, scale_b, P.n);
+  const dim3 B256(256);
+  launch(prof, kFamPerm, [&] { return make_double2(0, 48.0 * P.n * nb); }, k_perm_in, dim3((P.n + 255) / 256, nb),
+         B256, 0, s, c, b, scale_b, P.n);
   CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int) * nb, s));
   // zeroing + assembly: leaf-level fronts on the main stream, the others on
   // side3 beside the leaf level (joined before level 1's extend-add)
   const int nz = P.zero_late, nt = (int)P.asm_front.size();
+  auto zero_bytes = [&](int z0, int z1) {
+    double e = 0;
+    for (int q = z0; q < z1; q++) {
+      const int4 t = P.zero_tasks[q];
+      for (int j = t.y; j < t.z; j++) e += P.m[t.x] - j;
+    }
+    return make_double2(0, 8.0 * e * nb);
+  };
   auto assemble = [&](int z0, int z1, int a0, int a1, int d0, int d1, hipStream_t st) {
-    if (z1 > z0) k_zero_lower<<<dim3(z1 - z0, nb), 256, 0, st>>>(c, P.d_zero + z0, z1 - z0);
-    if (a1 > a0) k_asm_offdiag<<<dim3((a1 - a0 + 255) / 256, nb), 256, 0, st>>>(c, V, P.nslots, a0, a1);
-    if (d1 > d0) k_asm_diag<<<dim3((d1 - d0 + 255) / 256, nb), 256, 0, st>>>(c, D, P.d_lambda, d0, d1);
+    if (z1 > z0)
+      launch(prof, kFamZero, [&] { return zero_bytes(z0, z1); }, k_zero_lower, dim3(z1 - z0, nb), B256, 0, st, c,
+             (const int4*)(P.d_zero + z0), z1 - z0);
+    if (a1 > a0)
+      launch(prof, kFamAssemble, [&] {
+               return make_double2(0, (double)nb * (72.0 * (a1 - a0) + 72.0 * (P.asm_ptr[a1] - P.asm_ptr[a0])));
+             },
+             k_asm_offdiag, dim3((a1 - a0 + 255) / 256, nb), B256, 0, st, c, V, (long long)P.nslots, a0, a1);
+    if (d1 > d0)
+      launch(prof, kFamAssemble, [&] { return make_double2(0, 96.0 * (d1 - d0) * nb); }, k_asm_diag,
+             dim3((d1 - d0 + 255) / 256, nb), B256, 0, st, c, D, (const double*)P.d_lambda, d0, d1);
   };
   assemble(0, P.zero_split, 0, P.asm_split, 0, P.dg_split, s);
   const bool fork_rest = P.zero_split < nz || P.asm_split < nt || P.dg_split < P.n;
@@ -1571,16 +1633,34 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
   }
   for (size_t li = 0; li < P.levels.size(); li++) {
     const CholLevel& lv = P.levels[li];
+    if (prof) prof->cur_tag = (int)li << 16;
     if (li == 1 && fork_rest) CH_TRY(hipStreamWaitEvent(s, P.evs[5], 0));
-    if (lv.ea_cnt[0]) k_extend_add<<<dim3(lv.ea_cnt[0], nb), 256, 0, s>>>(c, P.d_ea_tasks + lv.ea_off[0], P.d_ea_pairs);
+    if (lv.ea_cnt[0])
+      launch(prof, kFamExtendAdd, [&] {
+               double e = 0;   // update-matrix elements moved (read child, read-modify-write parent)
+               for (int q = 0; q < lv.ea_cnt[0]; q++) {
+                 const int4 t = P.ea_tasks[lv.ea_off[0] + q];
+                 for (int k = 0; k < t.w; k++) {
+                   const int4 pr = P.ea_pairs[t.z + k];
+                   const int nr = pr.w & 0xff, ncl = pr.w >> 8;
+                   for (int r = 0; r < nr; r++) e += std::min(std::max(pr.y + r - pr.z + 1, 0), ncl);
+                 }
+               }
+               return make_double2(0, 24.0 * e * nb);
+             },
+             k_extend_add, dim3(lv.ea_cnt[0], nb), B256, 0, s, c, (const int4*)(P.d_ea_tasks + lv.ea_off[0]),
+             (const int4*)P.d_ea_pairs);
     if ((int)li == P.zero_level) {   // update matrices consumed by now: zero them for the next factorisation
       CH_TRY(hipEventRecord(P.evs[4], s));
       CH_TRY(hipStreamWaitEvent(P.side3, P.evs[4], 0));
       const int nlate = (int)P.zero_tasks.size() - P.zero_late;
-      k_zero_lower<<<dim3(std::min(nlate, kZeroBackgroundGrid), nb), 256, 0, P.side3>>>(c, P.d_zero + P.zero_late, nlate);
+      launch(prof, kFamZero, [&] { return zero_bytes(P.zero_late, (int)P.zero_tasks.size()); }, k_zero_lower,
+             dim3(std::min(nlate, kZeroBackgroundGrid), nb), B256, 0, P.side3, c,
+             (const int4*)(P.d_zero + P.zero_late), nlate);
       CH_TRY(hipEventRecord(P.evs[5], P.side3));
     }
-    k_vec_assemble<<<dim3(lv.front_cnt, nb), 256, (size_t)lv.maxm * sizeof(double), s>>>(c, P.d_level_fronts + lv.front_off);
+    launch(prof, kFamVecAssemble, [&] { return make_double2(0, 0); }, k_vec_assemble, dim3(lv.front_cnt, nb), B256,
+           (size_t)lv.maxm * sizeof(double), s, c, (const int*)(P.d_level_fronts + lv.front_off));
     // small fronts on the second side stream, beside the blocked path of the
     // same level (disjoint fronts); joined before the next level
     const bool fork_small = !lv.small.empty() && !lv.panels.empty();
@@ -1591,40 +1671,71 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       ss = P.side2;
     }
     for (const SmallClass& sc : lv.small) {
+      auto small_cost = [&] {
+        double f = 0;
+        for (int q = 0; q < sc.cnt; q++) {
+          const int fr = P.small_list[sc.off + q];
+          f += chol_flops(P.m[fr], P.w[fr]) + (double)P.w[fr] * P.w[fr] * P.w[fr] / 3.0;
+        }
+        return make_double2(f * nb, 0);
+      };
+      const int* list = P.d_small + sc.off;
       if (sc.wave) {
         const size_t lds = (size_t)(sc.mmax * (kWaveW + 1) + 130 + kWaveW) * sizeof(double);
-        if (sc.mmax > 64) k_front_wave<true><<<dim3(sc.cnt, nb), 64, lds, ss>>>(c, P.d_small + sc.off);
-        else k_front_wave<false><<<dim3(sc.cnt, nb), 64, lds, ss>>>(c, P.d_small + sc.off);
+        if (sc.mmax > 64)
+          launch(prof, kFamFrontWave, small_cost, k_front_wave<true>, dim3(sc.cnt, nb), dim3(64), lds, ss, c, list);
+        else
+          launch(prof, kFamFrontWave, small_cost, k_front_wave<false>, dim3(sc.cnt, nb), dim3(64), lds, ss, c, list);
+      } else {
+        launch(prof, kFamFrontSmall, small_cost, k_front_small, dim3(sc.cnt, nb), B256,
+               (size_t)(sc.mmax * sc.mmax + 64 + sc.mmax) * sizeof(double), ss, c, list);
       }
-      else
-        k_front_small<<<dim3(sc.cnt, nb), 256, (size_t)(sc.mmax * sc.mmax + 64 + sc.mmax) * sizeof(double), ss>>>(
-            c, P.d_small + sc.off);
     }
     for (const PanelStep& ps : lv.panels) {
-      if (ps.potrf_cnt) k_panel_diag<<<dim3(ps.potrf_cnt, nb), 256, 0, s>>>(c, P.d_potrf + ps.potrf_off, ps.kb);
-      if (ps.trsm_cnt) k_panel_trsm<<<dim3(ps.trsm_cnt, nb), 256, 0, s>>>(c, P.d_trsm + ps.trsm_off, ps.kb);
+      if (prof) prof->cur_tag = ((int)li << 16) | (ps.kb / kNB + 1);
+      if (ps.potrf_cnt)
+        launch(prof, kFamPanelDiag, [&] {
+                 double f = 0;
+                 for (int q = 0; q < ps.potrf_cnt; q++)
+                   f += potrf_inv_flops(std::min(kNB, P.w[P.potrf_list[ps.potrf_off + q]] - ps.kb));
+                 return make_double2(f * nb, 0);
+               },
+               k_panel_diag, dim3(ps.potrf_cnt, nb), B256, 0, s, c, (const int*)(P.d_potrf + ps.potrf_off), ps.kb);
+      if (ps.trsm_cnt)
+        launch(prof, kFamPanelTrsm, [&] {
+                 double f = 0;
+                 for (int q = 0; q < ps.trsm_cnt; q++) {
+                   const int2 t = P.trsm_tasks[ps.trsm_off + q];
+                   const int w = P.w[t.x], m = P.m[t.x], nbk = std::min(kNB, w - ps.kb);
+                   const int rows = std::min(64, m - ps.kb - nbk - 64 * t.y);
+                   f += (double)rows * nbk * nbk + 2.0 * rows * nbk;
+                 }
+                 return make_double2(f * nb, 0);
+               },
+               k_panel_trsm, dim3(ps.trsm_cnt, nb), B256, 0, s, c, (const int2*)(P.d_trsm + ps.trsm_off), ps.kb);
+      auto sdiag_cost = [&] {
+        double f = 0;
+        for (int q = 0; q < ps.sdiag_cnt; q++) f += sdiag_flops(P, P.sdiag_tasks[ps.sdiag_off + q], ps.kb);
+        return f;
+      };
+      const int4* tasks = (const int4*)(P.d_syrk + ps.syrk_off);
       if (ps.fused) {
-        k_step_fused<<<dim3(ps.sdiag_cnt + ps.syrk_cnt, nb), 256, 0, s>>>(c, P.d_sdiag + ps.sdiag_off, ps.sdiag_cnt,
-                                                                 (const int4*)(P.d_syrk + ps.syrk_off), ps.kb);
+        launch(prof, kFamStepFused, [&] { return make_double2((ps.syrk_flops + sdiag_cost()) * nb, 0); },
+               k_step_fused, dim3(ps.sdiag_cnt + ps.syrk_cnt, nb), B256, 0, s, c,
+               (const int4*)(P.d_sdiag + ps.sdiag_off), ps.sdiag_cnt, tasks, ps.kb);
         continue;
       }
       if (ps.sdiag_cnt) {   // look-ahead: next panel's diagonal tiles on the side stream
         CH_TRY(hipEventRecord(P.evs[2], s));
         CH_TRY(hipStreamWaitEvent(P.side, P.evs[2], 0));
-        k_syrk_diag<<<dim3(ps.sdiag_cnt, nb), 256, 0, P.side>>>(c, P.d_sdiag + ps.sdiag_off, ps.kb);
+        launch(prof, kFamSyrkDiag, [&] { return make_double2(sdiag_cost() * nb, 0); }, k_syrk_diag,
+               dim3(ps.sdiag_cnt, nb), B256, 0, P.side, c, (const int4*)(P.d_sdiag + ps.sdiag_off), ps.kb);
         CH_TRY(hipEventRecord(P.evs[3], P.side));
       }
       if (ps.syrk_cnt) {
-        const int4* tasks = (const int4*)(P.d_syrk + ps.syrk_off);
-        auto kern = ps.syrk_tile == kBigTile ? k_panel_syrk128 : k_panel_syrk_lds;
-        if (prof && prof->used < prof->cap) {
-          const int u = prof->used++;
-          prof->flops[u] = ps.syrk_flops;
-          hipExtLaunchKernelGGL(kern, dim3(ps.syrk_cnt, nb), dim3(256), 0, s, prof->ev[2 * u], prof->ev[2 * u + 1], 0, c,
-                                tasks, ps.kb);
-        } else {
-          kern<<<dim3(ps.syrk_cnt, nb), 256, 0, s>>>(c, tasks, ps.kb);
-        }
+        const bool big = ps.syrk_tile == kBigTile;
+        launch(prof, big ? kFamPanelSyrk128 : kFamPanelSyrk, [&] { return make_double2(ps.syrk_flops * nb, 0); },
+               big ? k_panel_syrk128 : k_panel_syrk_lds, dim3(ps.syrk_cnt, nb), B256, 0, s, c, tasks, ps.kb);
       }
       if (ps.sdiag_cnt) CH_TRY(hipStreamWaitEvent(s, P.evs[3], 0));
     }
@@ -1664,22 +1775,38 @@ hipError_t chol_marginals(const CholPlan& P, const int* poses, int n, double* ou
   return e;
 }
 
-hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb, long long xstride) {
+hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb, long long xstride, LaunchProfile* prof) {
   if (P.n == 0) return hipSuccess;
   if (nb < 1 || nb > P.batch) return hipErrorInvalidValue;
   const CholDev c = dev_view(P);
   const int g = (P.n + 255) / 256;
+  const dim3 B256(256);
   for (auto it = P.levels.rbegin(); it != P.levels.rend(); ++it) {
     const CholLevel& lv = *it;
+    if (prof) prof->cur_tag = (int)(&lv - P.levels.data()) << 16;
     if (lv.bwd_part.cnt)
-      k_bwd_part<<<dim3(lv.bwd_part.cnt, nb), 256, 0, s>>>(c, P.d_bwd_part + lv.bwd_part.off, P.d_partial);
-    k_bwd_init<<<dim3(lv.bwd[0].cnt, nb), 256, 0, s>>>(c, P.d_bwd + lv.bwd[0].off, P.d_bwd_pref + lv.bwd[0].off, P.d_partial);
+      launch(prof, kFamBwdPart, [&] {
+               double f = 0;
+               for (int q = 0; q < lv.bwd_part.cnt; q++) {
+                 const int4 t = P.bwd_part_tasks[lv.bwd_part.off + q];
+                 f += 2.0 * std::min(64, P.w[t.x] - t.y) * std::min(kBwdRows, P.m[t.x] - t.z);
+               }
+               return make_double2(f * nb, 0);
+             },
+             k_bwd_part, dim3(lv.bwd_part.cnt, nb), B256, 0, s, c, (const int4*)(P.d_bwd_part + lv.bwd_part.off),
+             P.d_partial);
+    launch(prof, kFamBwdInit, [&] { return make_double2(0, 0); }, k_bwd_init, dim3(lv.bwd[0].cnt, nb), B256, 0, s, c,
+           (const int4*)(P.d_bwd + lv.bwd[0].off), (const int2*)(P.d_bwd_pref + lv.bwd[0].off),
+           (const double*)P.d_partial);
     for (size_t q = 1; q < lv.bwd.size(); q++) {
       const int bb = lv.maxblk - (int)q;   // step b = maxblk-1 .. 1
-      if (lv.bwd[q].cnt) k_bwd_step<<<dim3(lv.bwd[q].cnt, nb), 256, 0, s>>>(c, P.d_bwd + lv.bwd[q].off, bb);
+      if (lv.bwd[q].cnt)
+        launch(prof, kFamBwdStep, [&] { return make_double2(0, 0); }, k_bwd_step, dim3(lv.bwd[q].cnt, nb), B256, 0,
+               s, c, (const int4*)(P.d_bwd + lv.bwd[q].off), bb);
     }
   }
-  k_perm_out<<<dim3(g, nb), 256, 0, s>>>(c, x, P.n, xstride);
+  launch(prof, kFamPerm, [&] { return make_double2(0, 48.0 * P.n * nb); }, k_perm_out, dim3(g, nb), B256, 0, s, c, x,
+         P.n, xstride);
   return hipGetLastError();
 }
 

@@ -4,6 +4,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 
 namespace pgo {
@@ -129,8 +130,17 @@ void comm_free(Comm* c) {
   *c = Comm();
 }
 
+// PGO_COMM_FORCE_COLLECTIVES=1: a one-rank RCCL communicator still goes
+// through ncclAllGather / ncclBroadcast (instead of the local shortcuts), so
+// the collective path and its slot arithmetic run on a one-GPU box
+bool force_collectives(const Comm* c) {
+  if (!c->nccl) return false;
+  const char* v = getenv("PGO_COMM_FORCE_COLLECTIVES");
+  return v && v[0] == '1';
+}
+
 int comm_allgather(Comm* c, const double* mine, int count, double* all, hipStream_t s, std::string* err) {
-  if (c->size == 1) {
+  if (c->size == 1 && !force_collectives(c)) {
     std::memcpy(all, mine, sizeof(double) * count);
     return PGO_OK;
   }
@@ -160,7 +170,7 @@ int comm_allgather(Comm* c, const double* mine, int count, double* all, hipStrea
 }
 
 int comm_broadcast_device(Comm* c, void* dptr, size_t bytes, int root, hipStream_t s, std::string* err) {
-  if (c->size == 1 || bytes == 0) return PGO_OK;
+  if ((c->size == 1 && !force_collectives(c)) || bytes == 0) return PGO_OK;
   hipError_t he;
   if (c->host) {
     c->stage.resize(bytes);

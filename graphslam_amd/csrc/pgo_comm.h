@@ -43,4 +43,6 @@ int comm_allgather(Comm* c, const double* mine, int count, double* all, hipStrea
 // after the data has arrived (stream synchronised)
 int comm_broadcast_device(Comm* c, void* dptr, size_t bytes, int root, hipStream_t s, std::string* err);
 
+// PGO_COMM_FORCE_COLLECTIVES=1 on an RCCL communicator: exchanges run even at size 1
+bool force_collectives(const Comm* c);
 }  // namespace pgo

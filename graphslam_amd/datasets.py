@@ -207,9 +207,12 @@ def _assemble(name, seed, gt, init, i, j, z, meta):
     )
 
 
-def manhattan(n, side, num_edges, seed, name="manhattan", window=1):
-    """Odometry chain (+ window edges i->i-k, k<=window) + same-cell loop closures
-    subsampled so the graph has exactly ``num_edges`` between factors."""
+def manhattan(n, side, num_edges, seed, name="manhattan", window=1, loop_closures=None):
+    """Odometry chain (+ window edges i->i-k, 2 <= k <= window) + same-cell loop
+    closures, exactly ``num_edges`` between factors: with ``loop_closures``
+    None every window edge is kept and the loop closures fill up to
+    ``num_edges``; otherwise that many loop closures are drawn and the window
+    edges are seeded-subsampled to fill up."""
     rng = np.random.Generator(np.random.PCG64(seed))
     gt, cell = manhattan_walk(n, side, rng)
     oi = np.arange(n - 1, dtype=np.int64)
@@ -217,9 +220,15 @@ def manhattan(n, side, num_edges, seed, name="manhattan", window=1):
     z_odo = _noisy_between(gt, oi, oj, rng)
     init = _dead_reckon(z_odo, n)
     ei, ej, ez = [oi], [oj], [z_odo]
-    for k in range(2, window + 1):
-        wi = np.arange(n - k, dtype=np.int64)
-        wj = wi + k
+    if window > 1:
+        wi = np.concatenate([np.arange(n - k, dtype=np.int64) for k in range(2, window + 1)])
+        wj = wi + np.concatenate([np.full(n - k, k, dtype=np.int64) for k in range(2, window + 1)])
+        if loop_closures is not None:
+            keep = num_edges - (n - 1) - loop_closures
+            if not 0 <= keep <= len(wi):
+                raise ValueError(f"{name}: cannot fill {num_edges} edges with window {window}")
+            pick = np.sort(rng.choice(len(wi), size=keep, replace=False))
+            wi, wj = wi[pick], wj[pick]
         ei.append(wi)
         ej.append(wj)
         ez.append(_noisy_between(gt, wi, wj, rng))
@@ -269,7 +278,10 @@ CONFIGS = {
     "C1": dict(n=1000, side=16, num_edges=1019, seed=1001),
     "C2": dict(n=10_000, side=32, num_edges=40_000, seed=1002),
     "C3": dict(n=100_000, side=100, num_edges=500_000, seed=1003),
-    "C5": dict(n=1_000_000, side=316, num_edges=5_000_000, seed=1005, window=4),
+    # 1M poses / 5M edges, 5 % loop-closure density: 50k same-cell loop closures
+    # (5 % of the poses), odometry, and window edges i->i-k (k = 2..5) subsampled
+    # to 5M in total (BASELINE.json configs[4]; DESIGN.md "Configs")
+    "C5": dict(n=1_000_000, side=316, num_edges=5_000_000, seed=1005, window=5, loop_closures=50_000),
 }
 
 

@@ -251,11 +251,16 @@ class LevenbergMarquardtOptimizer:
         self.params = params if params is not None else self._params_cls()
         self.device = device
         self.stats = None
+        self._handle = None
 
     def optimize(self) -> Values:
-        with _build(self.graph, self.initial, self.device) as pg:
-            self.stats = pg.optimize(self.params.raw)
-            xyt = pg.poses()
+        """GTSAM keeps the optimizer's state: the graph is loaded on the first
+        call, a later call continues from the values the previous one reached."""
+        if self._handle is None:
+            self._handle = _build(self.graph, self.initial, self.device)
+        pg = self._handle.pg
+        self.stats = pg.optimize(self.params.raw)
+        xyt = pg.poses()
         out = Values()
         for k, p in zip(self.initial.keys(), xyt):
             out.insert(k, Pose2(*p))

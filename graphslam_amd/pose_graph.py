@@ -146,6 +146,36 @@ class PoseGraph:
         self._check(rc)
         return self.last_stats
 
+    def trace(self):
+        """Per-iteration record of the last optimize (pgo_get_trace): rows of
+        (accepted steps, lambda, solved, model decrease, candidate error,
+        fidelity, accepted, wall ms)."""
+        n = self._check(self._L.pgo_get_trace(self._h, None, 0))
+        out = np.zeros((n, 8))
+        if n:
+            self._check(self._L.pgo_get_trace(self._h, L.dptr(out), n))
+        return out
+
+    def kernel_profile(self):
+        """Profiled factorisations of the last optimize (profile_every > 0):
+        {family: {launches, ms, flops, bytes}} for the families that ran."""
+        nf = self._check(self._L.pgo_get_kernel_profile(self._h, None, 0))
+        out = np.zeros((nf, 5))
+        self._check(self._L.pgo_get_kernel_profile(self._h, L.dptr(out), nf))
+        res = {}
+        for f in range(nf):
+            if out[f, 0] > 0:
+                res[self._L.pgo_kernel_family_name(f).decode()] = dict(
+                    launches=int(out[f, 0]), ms=float(out[f, 1]), flops=float(out[f, 2]), bytes=float(out[f, 3]))
+        return res
+
+    def debug_ordering(self):
+        """Host-only: the Cholesky solver's pose ordering (new -> insertion index)."""
+        n = self.num_vertices
+        perm = np.zeros(n, np.int32)
+        self._check(self._L.pgo_debug_ordering(self._h, perm.ctypes.data_as(C.POINTER(C.c_int32)), n))
+        return perm
+
     # ---------------------------------------------------------------- values
     @property
     def num_vertices(self):

@@ -1,10 +1,10 @@
-"""One process per GPU running independent pose-graph replicas.
+"""One process per GPU: rank setup and the timed region of bench.py.
 
-The optimiser does not shard yet ("Multi-GPU"): N ranks each
-optimise their own copy of the graph on their own device, with no data-path
-collective.  torch.distributed (gloo, CPU tensors only) is used for the
-barrier around the timed region and for the max-over-ranks time / summed
-work -- plumbing, not the product.
+Used by every multi-GPU mode ("Multi-GPU"): independent replicas
+(`--multi replicas`, no data-path collective), the speculative lambda search
+and the partitioned solve.  torch.distributed (gloo, CPU tensors only) is used
+for the barrier around the timed region and for the max-over-ranks time /
+summed work -- plumbing, not the product.
 """
 from __future__ import annotations
 

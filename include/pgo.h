@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PGO_ABI_VERSION 3
+#define PGO_ABI_VERSION 4
 
 /* ---- status codes (GTSAM exception each one replaces) -------------------- */
 #define PGO_OK 0
@@ -139,7 +139,23 @@ typedef struct {
   long long solves;             /* linear solves this rank performed (incl. the
                                    speculative tries GTSAM's sequence never reached) */
   double ms_comm;               /* wall time in the all-gathers and broadcasts      */
+  /* profiled factorisations (profile_every > 0, eager launches): device time from
+     the first to the last launch of chol_factor / of the triangular solves,
+     summed; per-kernel detail in pgo_get_kernel_profile */
+  double ms_factor_profiled;
+  double ms_solve_profiled;
+  int stop_reason;              /* PGO_STOP_* : why the outer loop ended          */
 } pgo_stats;
+
+/* pgo_stats.stop_reason.  GTSAM reports every one of these as convergence
+   (an LM that gives up leaves the values unchanged, so checkConvergence sees a
+   zero decrease); the library tells them apart. */
+#define PGO_STOP_CONVERGED 0     /* checkConvergence: relative / absolute decrease, error tol */
+#define PGO_STOP_LAMBDA_BOUND 1  /* LM gave up: lambda reached lambda_upper_bound, no step accepted */
+#define PGO_STOP_MAX_ITER 2      /* max_iterations accepted steps                   */
+#define PGO_STOP_MAX_OUTER 3     /* pgo_params.max_outer linearisations              */
+#define PGO_STOP_SMALL_CHANGE 4  /* tryLambda: |cost change| < relative_error_tol * error */
+#define PGO_STOP_ERROR 5         /* error status (singular GN system, HIP, comm)    */
 
 /* ---- lifetime ------------------------------------------------------------ */
 pgo_graph *pgo_create(const pgo_opts *opts);        /* NULL opts: device 0 */
@@ -165,6 +181,23 @@ int pgo_add_edges(pgo_graph *g, size_t n, const uint64_t *k1, const uint64_t *k2
 /* Runs the optimiser from the handle's current values and replaces them with
  * the result (the reference's `initial = poses_opti`).  NULL params: defaults. */
 int pgo_optimize(pgo_graph *g, const pgo_params *params, pgo_stats *stats);
+
+/* Per-iteration record of the last pgo_optimize: one row of 8
+ * doubles per lambda try GTSAM's sequence reached (LM) or per step (GN):
+ *   accepted steps so far (LM: before this try; GN: after the step), lambda,
+ *   solved (1/0), linear model decrease -(g'd + d'H d / 2) (NaN: not solved /
+ *   GN), error at the candidate (+inf: not evaluated), model fidelity,
+ *   accepted (1/0), wall ms since pgo_optimize entry when the outcome was known.
+ * The columns match the oracle's trace (oracle/pgo_oracle.h) plus the ms.
+ * Returns the row count (rows beyond cap are not written). */
+int pgo_get_trace(const pgo_graph *g, double *out, int cap);
+
+/* Profiled factorisations of the last pgo_optimize (pgo_params.profile_every
+ * > 0): per kernel family f (0 <= f < returned count, name from
+ * pgo_kernel_family_name) out[5 f ..] = launches, summed device ms (dispatch
+ * events), algorithmic flops, algorithmic HBM bytes, 0. */
+int pgo_get_kernel_profile(const pgo_graph *g, double *out, int cap);
+const char *pgo_kernel_family_name(int f);
 
 /* ---- values access ------------------------------------------------------- */
 int pgo_get_pose(pgo_graph *g, uint64_t key, double out[3]);           /* Values::at */
@@ -262,6 +295,10 @@ int pgo_debug_solve(pgo_graph *g, double lambda, const pgo_params *params, doubl
  * trsm tasks, syrk tiles, small fronts; from out[16], 6 per level (leaves first):
  * fronts, max m, max 64-blocks, panel steps, small fronts, syrk tiles. */
 int pgo_debug_plan(pgo_graph *g, double *out, int cap);
+/* Host-only: the Cholesky solver's fill-reducing ordering of the poses
+ * (perm[k] = insertion index of the k-th eliminated pose), n = vertex count.
+ * bench.py hands it to the CPU restatement so both factor the same fill. */
+int pgo_debug_ordering(pgo_graph *g, int32_t *perm, size_t n);
 /* per supernode of the same host-only plan: pivot columns w, rows m, level
    (height in the elimination tree); returns the supernode count (arrays are
    filled up to cap entries) or a negative status */

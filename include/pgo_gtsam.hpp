@@ -144,19 +144,11 @@ class LevenbergMarquardtOptimizer {
   LevenbergMarquardtOptimizer(const LevenbergMarquardtOptimizer&) = delete;
   LevenbergMarquardtOptimizer& operator=(const LevenbergMarquardtOptimizer&) = delete;
 
+  // GTSAM keeps the optimizer's state: a second optimize() continues from the
+  // values the first one reached (defaultOptimize on state_), so the handle is
+  // loaded once and later calls only re-run the solver on it.
   Values optimize() {
-    for (size_t i = 0; i < initial_.size(); i++) {
-      const Pose2& p = initial_.poses()[i];
-      throw_status(pgo_add_vertex(g_, initial_.keys()[i], p.x(), p.y(), p.raw_theta()), g_);
-    }
-    for (const auto& f : graph_.priors()) {
-      const double z[3] = {f.prior.x(), f.prior.y(), f.prior.raw_theta()};
-      throw_status(pgo_add_prior(g_, f.key, z, f.noise.cov.m), g_);
-    }
-    for (const auto& f : graph_.betweens()) {
-      const double z[3] = {f.measured.x(), f.measured.y(), f.measured.raw_theta()};
-      throw_status(pgo_add_edge(g_, f.key1, f.key2, z, f.noise.cov.m), g_);
-    }
+    if (!loaded_) load();
     throw_status(pgo_optimize(g_, &params_.p, &stats_), g_);
     Values out;
     std::vector<double> xyt(3 * initial_.size());
@@ -170,11 +162,28 @@ class LevenbergMarquardtOptimizer {
   double error() const { return stats_.final_error; }
 
  private:
+  void load() {
+    for (size_t i = 0; i < initial_.size(); i++) {
+      const Pose2& p = initial_.poses()[i];
+      throw_status(pgo_add_vertex(g_, initial_.keys()[i], p.x(), p.y(), p.raw_theta()), g_);
+    }
+    for (const auto& f : graph_.priors()) {
+      const double z[3] = {f.prior.x(), f.prior.y(), f.prior.raw_theta()};
+      throw_status(pgo_add_prior(g_, f.key, z, f.noise.cov.m), g_);
+    }
+    for (const auto& f : graph_.betweens()) {
+      const double z[3] = {f.measured.x(), f.measured.y(), f.measured.raw_theta()};
+      throw_status(pgo_add_edge(g_, f.key1, f.key2, z, f.noise.cov.m), g_);
+    }
+    loaded_ = true;
+  }
+
   const NonlinearFactorGraph& graph_;
   const Values& initial_;
   LevenbergMarquardtParams params_;
   pgo_graph* g_ = nullptr;
   pgo_stats stats_{};
+  bool loaded_ = false;
 };
 
 // gtsam::Marginals(graph, values) (graph.cpp:120, commented in the reference):

@@ -50,6 +50,10 @@ def lib():
         dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
         L.orc_create.restype = C.c_void_p
         L.orc_create.argtypes = [C.c_int, C.c_int, ip, ip, dp, dp, C.c_int, ip, dp, dp, C.POINTER(C.c_int)]
+        L.orc_create_ordered.restype = C.c_void_p
+        L.orc_create_ordered.argtypes = [C.c_int, C.c_int, ip, ip, dp, dp, C.c_int, ip, dp, dp, ip,
+                                         C.POINTER(C.c_int)]
+        L.orc_set_threads.argtypes = [C.c_int]
         L.orc_destroy.argtypes = [C.c_void_p]
         L.orc_default_params.argtypes = [C.POINTER(OrcParams)]
         L.orc_optimize.argtypes = [C.c_void_p, dp, C.POINTER(OrcParams), dp, C.POINTER(OrcStats), dp,
@@ -63,6 +67,11 @@ def lib():
         L.orc_closest_keyframe.restype = C.c_int
         _lib = L
     return _lib
+
+
+def set_threads(t):
+    """OpenMP threads of later oracle calls."""
+    lib().orc_set_threads(int(t))
 
 
 def _dp(a):
@@ -98,7 +107,10 @@ class OracleResult:
 class Oracle:
     """CPU restatement of LevenbergMarquardtOptimizer(graph, initial).optimize()."""
 
-    def __init__(self, g):
+    def __init__(self, g, order=None):
+        """order (optional): new -> old pose permutation for the sparse Cholesky
+        (e.g. the GPU plan's nested dissection, PoseGraph.debug_ordering());
+        default: the oracle's own AMD."""
         L = lib()
         ei, ej = g.edge_index()
         self._keep = dict(
@@ -112,8 +124,14 @@ class Oracle:
         st = C.c_int(0)
         self.n = g.num_poses
         self.ne = g.num_edges
-        self.h = L.orc_create(self.n, self.ne, _ip(k["ei"]), _ip(k["ej"]), _dp(k["ez"]), _dp(k["ec"]),
-                              len(k["pi"]), _ip(k["pi"]), _dp(k["pz"]), _dp(k["pc"]), C.byref(st))
+        if order is not None:
+            k["order"] = np.ascontiguousarray(order, dtype=np.int32)
+            self.h = L.orc_create_ordered(self.n, self.ne, _ip(k["ei"]), _ip(k["ej"]), _dp(k["ez"]), _dp(k["ec"]),
+                                          len(k["pi"]), _ip(k["pi"]), _dp(k["pz"]), _dp(k["pc"]),
+                                          _ip(k["order"]), C.byref(st))
+        else:
+            self.h = L.orc_create(self.n, self.ne, _ip(k["ei"]), _ip(k["ej"]), _dp(k["ez"]), _dp(k["ec"]),
+                                  len(k["pi"]), _ip(k["pi"]), _dp(k["pz"]), _dp(k["pc"]), C.byref(st))
         self.status = st.value
         if not self.h:
             raise ValueError(f"oracle rejected graph: status {st.value}")

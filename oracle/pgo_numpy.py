@@ -275,6 +275,7 @@ class LMParams:
     lambda_lower_bound: float = 0.0
     min_model_fidelity: float = 1e-3
     use_fixed_lambda_factor: bool = True
+    max_outer: int = 0          # >0: stop after this many linearisations (truncated fixtures)
 
 
 @dataclass
@@ -310,9 +311,11 @@ def levenberg_marquardt(prob: Problem, poses0, params: LMParams | None = None) -
     if err <= p.error_tol or iters >= p.max_iterations:
         return res
     new_err = err
+    outer = 0
     while True:
         cur_err = new_err
         lin = linearize(prob, poses)
+        outer += 1
         while True:                                        # tryLambda loop
             model_fidelity = 0.0
             success = stop = False
@@ -359,6 +362,8 @@ def levenberg_marquardt(prob: Problem, poses0, params: LMParams | None = None) -
                 continue
             break
         new_err = err
+        if p.max_outer > 0 and outer >= p.max_outer:
+            break
         if not (iters < p.max_iterations and not check_convergence(p, cur_err, new_err)
                 and math.isfinite(cur_err)):
             break

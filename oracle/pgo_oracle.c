@@ -320,7 +320,11 @@ static int cmp_int(const void *a, const void *b) {
   return (x > y) - (x < y);
 }
 
-static chol_sym *sym_analyze(int n, int ne, const int32_t *ei, const int32_t *ej) {
+/* order_in (optional, new -> old pose index): a fill-reducing ordering given
+ * by the caller instead of AMD -- bench.py times the CPU path on the same
+ * nested-dissection permutation the GPU plan uses, so the two factorisations
+ * have identical fill and flops */
+static chol_sym *sym_analyze(int n, int ne, const int32_t *ei, const int32_t *ej, const int32_t *order_in) {
   chol_sym *S = (chol_sym *)calloc(1, sizeof(chol_sym));
   S->n = n;
   /* pose adjacency (old index), deduplicated */
@@ -361,7 +365,8 @@ static chol_sym *sym_analyze(int n, int ne, const int32_t *ei, const int32_t *ej
   xadj = xa2;
 
   int *perm0 = (int *)malloc(n * sizeof(int));
-  amd_order(n, xadj, adj, perm0);
+  if (order_in) memcpy(perm0, order_in, n * sizeof(int));
+  else amd_order(n, xadj, adj, perm0);
   int *ip0 = (int *)malloc(n * sizeof(int));
   for (int k = 0; k < n; k++) ip0[perm0[k]] = k;
 
@@ -708,85 +713,114 @@ static int front_factor(double *F, int m, int w) {
 /* ------------------------------------------------------------ numeric */
 typedef struct {
   chol_sym *S;
-  double *L;     /* panels */
-  double *stack; /* update matrices */
-  size_t stack_cap;
-  int *relmap;
-  int *ustack_s; /* supernode id per stacked update */
-  size_t *ustack_off;
+  double *L;      /* panels */
+  double **U;     /* [ns] update matrix of each front until its parent consumed it */
+  int *cptr, *child; /* children of each supernode, increasing */
+  int nlev;
+  int *lptr, *lfront; /* fronts by height (leaves first), largest first within a level */
 } chol_num;
+
+static double front_work(const chol_sym *S, int s) {
+  double wd = 3.0 * (S->sfirst[s + 1] - S->sfirst[s]), m = wd + 3.0 * (S->rptr[s + 1] - S->rptr[s]);
+  return wd * m * m;
+}
 
 static chol_num *num_create(chol_sym *S) {
   chol_num *N = (chol_num *)calloc(1, sizeof(chol_num));
   N->S = S;
-  N->L = (double *)malloc((S->loff[S->ns] > 0 ? S->loff[S->ns] : 1) * sizeof(double));
-  N->relmap = (int *)malloc((S->n > 0 ? S->n : 1) * sizeof(int));
-  N->ustack_s = (int *)malloc((S->ns + 1) * sizeof(int));
-  N->ustack_off = (size_t *)malloc((S->ns + 2) * sizeof(size_t));
+  int ns = S->ns;
+  N->L = (double *)malloc((S->loff[ns] > 0 ? S->loff[ns] : 1) * sizeof(double));
+  N->U = (double **)calloc(ns > 0 ? ns : 1, sizeof(double *));
+  N->cptr = (int *)calloc(ns + 1, sizeof(int));
+  N->child = (int *)malloc((ns > 0 ? ns : 1) * sizeof(int));
+  for (int s = 0; s < ns; s++)
+    if (S->sparent[s] >= 0) N->cptr[S->sparent[s] + 1]++;
+  for (int s = 0; s < ns; s++) N->cptr[s + 1] += N->cptr[s];
+  int *fill = (int *)malloc((ns + 1) * sizeof(int));
+  memcpy(fill, N->cptr, (ns + 1) * sizeof(int));
+  for (int s = 0; s < ns; s++)
+    if (S->sparent[s] >= 0) N->child[fill[S->sparent[s]]++] = s;
+  /* heights (children precede parents in the postorder) */
+  int *h = (int *)calloc(ns > 0 ? ns : 1, sizeof(int));
+  int nlev = 0;
+  for (int s = 0; s < ns; s++) {
+    if (S->sparent[s] >= 0 && h[S->sparent[s]] < h[s] + 1) h[S->sparent[s]] = h[s] + 1;
+    if (h[s] + 1 > nlev) nlev = h[s] + 1;
+  }
+  N->nlev = nlev;
+  N->lptr = (int *)calloc(nlev + 1, sizeof(int));
+  N->lfront = (int *)malloc((ns > 0 ? ns : 1) * sizeof(int));
+  for (int s = 0; s < ns; s++) N->lptr[h[s] + 1]++;
+  for (int l = 0; l < nlev; l++) N->lptr[l + 1] += N->lptr[l];
+  memcpy(fill, N->lptr, (nlev + 1) * sizeof(int));
+  for (int s = 0; s < ns; s++) N->lfront[fill[h[s]]++] = s;
+  for (int l = 0; l < nlev; l++) { /* largest first (insertion sort is fine: levels are small or cheap) */
+    int a = N->lptr[l], b = N->lptr[l + 1];
+    for (int i = a + 1; i < b; i++) {
+      int x = N->lfront[i], j = i - 1;
+      double wx = front_work(S, x);
+      while (j >= a && front_work(S, N->lfront[j]) < wx) {
+        N->lfront[j + 1] = N->lfront[j];
+        j--;
+      }
+      N->lfront[j + 1] = x;
+    }
+  }
+  free(fill);
+  free(h);
   return N;
 }
 static void num_free(chol_num *N) {
   if (!N) return;
   free(N->L);
-  free(N->stack);
-  free(N->relmap);
-  free(N->ustack_s);
-  free(N->ustack_off);
+  if (N->U)
+    for (int s = 0; s < N->S->ns; s++) free(N->U[s]);
+  free(N->U);
+  free(N->cptr);
+  free(N->child);
+  free(N->lptr);
+  free(N->lfront);
   free(N);
 }
 
-/* Factor H + lam I given per-pose diagonal blocks (old index, 9 row-major) and
- * per-edge off-diagonal blocks B_e = H_{ei,ej} (9 row-major). */
-static int num_factor(chol_num *N, const double *hdiag, const double *hoff, double lam) {
+/* One front: assemble A's entries (+lam), extend-add the children's update
+ * matrices in increasing child order, partial Cholesky, keep the panel, keep
+ * the update matrix for the parent.  rel: per-thread scratch of n ints. */
+static int factor_one(chol_num *N, int s, const double *hdiag, const double *hoff, double lam, int *rel) {
   chol_sym *S = N->S;
-  int top = 0;
-  N->ustack_off[0] = 0;
-  int *rel = N->relmap;
-  double *F = NULL;
-  size_t Fcap = 0;
-  int rc = 0;
-  for (int s = 0; s < S->ns; s++) {
-    int f = S->sfirst[s], l = S->sfirst[s + 1];
-    int wp = l - f, nb = S->rptr[s + 1] - S->rptr[s];
-    const int *R = S->rows + S->rptr[s];
-    int m = 3 * (wp + nb), wd = 3 * wp;
-    size_t need = (size_t)m * m;
-    if (need > Fcap) {
-      free(F);
-      Fcap = need;
-      F = (double *)malloc(Fcap * sizeof(double));
+  int f = S->sfirst[s], l = S->sfirst[s + 1];
+  int wp = l - f, nb = S->rptr[s + 1] - S->rptr[s];
+  const int *R = S->rows + S->rptr[s];
+  int m = 3 * (wp + nb), wd = 3 * wp;
+  double *F = (double *)calloc((size_t)m * m > 0 ? (size_t)m * m : 1, sizeof(double));
+  for (int j = f; j < l; j++) rel[j] = j - f;
+  for (int t = 0; t < nb; t++) rel[R[t]] = wp + t;
+  for (int j = f; j < l; j++) {
+    int lj = 3 * (j - f);
+    const double *D = hdiag + 9 * (size_t)S->perm[j];
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b <= a; b++) F[(lj + a) + (size_t)(lj + b) * m] += D[3 * a + b];
+    for (int a = 0; a < 3; a++) F[(lj + a) + (size_t)(lj + a) * m] += lam;
+    for (int q = S->acol[j]; q < S->acol[j + 1]; q++) {
+      int code = S->aent[q];
+      int e = code >= 0 ? code : ~code;
+      const double *B = hoff + 9 * (size_t)e;
+      int li = 3 * rel[S->arow[q]];
+      if (code >= 0) /* rows = ei, cols = ej: block B */
+        for (int a = 0; a < 3; a++)
+          for (int b = 0; b < 3; b++) F[(li + a) + (size_t)(lj + b) * m] += B[3 * a + b];
+      else /* rows = ej, cols = ei: block B^T */
+        for (int a = 0; a < 3; a++)
+          for (int b = 0; b < 3; b++) F[(li + a) + (size_t)(lj + b) * m] += B[3 * b + a];
     }
-    memset(F, 0, need * sizeof(double));
-    for (int j = f; j < l; j++) rel[j] = j - f;
-    for (int t = 0; t < nb; t++) rel[R[t]] = wp + t;
-    /* assemble A: diagonal blocks (+lam) and off-diagonal blocks */
-    for (int j = f; j < l; j++) {
-      int lj = 3 * (j - f);
-      const double *D = hdiag + 9 * (size_t)S->perm[j];
-      for (int a = 0; a < 3; a++)
-        for (int b = 0; b <= a; b++) F[(lj + a) + (size_t)(lj + b) * m] += D[3 * a + b];
-      for (int a = 0; a < 3; a++) F[(lj + a) + (size_t)(lj + a) * m] += lam;
-      for (int q = S->acol[j]; q < S->acol[j + 1]; q++) {
-        int code = S->aent[q];
-        int e = code >= 0 ? code : ~code;
-        const double *B = hoff + 9 * (size_t)e;
-        int li = 3 * rel[S->arow[q]];
-        if (code >= 0) /* rows = ei, cols = ej: block B */
-          for (int a = 0; a < 3; a++)
-            for (int b = 0; b < 3; b++) F[(li + a) + (size_t)(lj + b) * m] += B[3 * a + b];
-        else /* rows = ej, cols = ei: block B^T */
-          for (int a = 0; a < 3; a++)
-            for (int b = 0; b < 3; b++) F[(li + a) + (size_t)(lj + b) * m] += B[3 * b + a];
-      }
-    }
-    /* extend-add children's update matrices (on top of the stack, in order) */
-    int nc = S->nchild[s];
-    for (int c = top - nc; c < top; c++) {
-      int cs = N->ustack_s[c];
-      const int *Rc = S->rows + S->rptr[cs];
-      int nbc = S->rptr[cs + 1] - S->rptr[cs];
-      int mc = 3 * nbc;
-      const double *U = N->stack + N->ustack_off[c];
+  }
+  for (int q = N->cptr[s]; q < N->cptr[s + 1]; q++) {
+    int cs = N->child[q];
+    const int *Rc = S->rows + S->rptr[cs];
+    int nbc = S->rptr[cs + 1] - S->rptr[cs];
+    int mc = 3 * nbc;
+    const double *U = N->U[cs];
+    if (U)
       for (int b = 0; b < nbc; b++) {
         int gb = 3 * rel[Rc[b]];
         for (int y = 0; y < 3; y++) {
@@ -799,35 +833,59 @@ static int num_factor(chol_num *N, const double *hdiag, const double *hoff, doub
           }
         }
       }
-    }
-    top -= nc;
-    if (front_factor(F, m, wd) != 0) {
-      rc = ORC_E_INDETERMINANT;
-      break;
-    }
-    /* save panel */
+    free(N->U[cs]);
+    N->U[cs] = NULL;
+  }
+  int rc = front_factor(F, m, wd) != 0 ? ORC_E_INDETERMINANT : ORC_OK;
+  if (rc == ORC_OK) {
     memcpy(N->L + S->loff[s], F, (size_t)m * wd * sizeof(double));
-    /* push update matrix */
     int mu = m - wd;
     if (S->sparent[s] >= 0 && mu > 0) {
-      size_t off = N->ustack_off[top];
-      size_t needs = off + (size_t)mu * mu;
-      if (needs > N->stack_cap) {
-        N->stack_cap = needs + needs / 2 + 1024;
-        N->stack = (double *)realloc(N->stack, N->stack_cap * sizeof(double));
-      }
-      double *U = N->stack + off;
+      double *U = (double *)malloc((size_t)mu * mu * sizeof(double));
       for (int j = 0; j < mu; j++) memcpy(U + (size_t)j * mu, F + wd + (size_t)(wd + j) * m, mu * sizeof(double));
-      N->ustack_s[top] = s;
-      N->ustack_off[top + 1] = needs;
-      top++;
-    } else if (S->sparent[s] >= 0) {
-      N->ustack_s[top] = s;
-      N->ustack_off[top + 1] = N->ustack_off[top];
-      top++;
+      N->U[s] = U;
     }
   }
   free(F);
+  return rc;
+}
+
+/* Factor H + lam I given per-pose diagonal blocks (old index, 9 row-major) and
+ * per-edge off-diagonal blocks B_e = H_{ei,ej} (9 row-major).  Level by level
+ * (leaves first): the fronts of a level in parallel, one thread each, except
+ * the large fronts, which run one at a time with the Schur updates spread over
+ * the threads.  Every front sums its children in increasing order and every
+ * Schur-update element is one thread's fixed-order dot product, so the result
+ * does not depend on the thread count. */
+static int num_factor(chol_num *N, const double *hdiag, const double *hoff, double lam) {
+  chol_sym *S = N->S;
+  int rc = ORC_OK;
+  const double big = 2e7;   /* flops: above this a front gets all the threads */
+  int *rel0 = (int *)malloc((S->n > 0 ? S->n : 1) * sizeof(int));
+  for (int lv = 0; lv < N->nlev && rc == ORC_OK; lv++) {
+    int a = N->lptr[lv], b = N->lptr[lv + 1];
+    int nbig = 0;   /* fronts are sorted largest first */
+    while (a + nbig < b && front_work(S, N->lfront[a + nbig]) > big) nbig++;
+    for (int q = a; q < a + nbig && rc == ORC_OK; q++) rc = factor_one(N, N->lfront[q], hdiag, hoff, lam, rel0);
+    int bad = 0;
+#pragma omp parallel if (b - a - nbig > 1)
+    {
+      int *rel = (int *)malloc((S->n > 0 ? S->n : 1) * sizeof(int));
+#pragma omp for schedule(dynamic, 1)
+      for (int q = a + nbig; q < b; q++)
+        if (factor_one(N, N->lfront[q], hdiag, hoff, lam, rel) != ORC_OK) {
+#pragma omp atomic write
+          bad = 1;
+        }
+      free(rel);
+    }
+    if (bad) rc = ORC_E_INDETERMINANT;
+  }
+  free(rel0);
+  for (int s = 0; s < S->ns; s++) { /* a failed factorisation leaves updates behind */
+    free(N->U[s]);
+    N->U[s] = NULL;
+  }
   return rc;
 }
 
@@ -940,9 +998,24 @@ void orc_destroy(void *h) {
   free(o);
 }
 
+void *orc_create_ordered(int n, int ne, const int32_t *ei, const int32_t *ej, const double *ez,
+                         const double *ecov, int np, const int32_t *pi, const double *pz,
+                         const double *pcov, const int32_t *order, int *status);
+
 void *orc_create(int n, int ne, const int32_t *ei, const int32_t *ej, const double *ez,
                  const double *ecov, int np, const int32_t *pi, const double *pz,
                  const double *pcov, int *status) {
+  return orc_create_ordered(n, ne, ei, ej, ez, ecov, np, pi, pz, pcov, NULL, status);
+}
+
+/* OpenMP threads of the factorisation / linearisation (bench.py times 1 and all) */
+void orc_set_threads(int t) {
+  if (t > 0) omp_set_num_threads(t);
+}
+
+void *orc_create_ordered(int n, int ne, const int32_t *ei, const int32_t *ej, const double *ez,
+                         const double *ecov, int np, const int32_t *pi, const double *pz,
+                         const double *pcov, const int32_t *order, int *status) {
   *status = ORC_OK;
   if (n < 0 || ne < 0 || np < 0) {
     *status = ORC_E_ARG;
@@ -990,7 +1063,21 @@ void *orc_create(int n, int ne, const int32_t *ei, const int32_t *ej, const doub
     }
   }
   double t0 = now_s();
-  o->S = sym_analyze(n, ne, o->ei, o->ej);
+  if (order) { /* must be a permutation of 0..n-1 */
+    char *seen = (char *)calloc(Nn, 1);
+    int ok = 1;
+    for (int k = 0; k < n && ok; k++) {
+      if (order[k] < 0 || order[k] >= n || seen[order[k]]) ok = 0;
+      else seen[order[k]] = 1;
+    }
+    free(seen);
+    if (!ok) {
+      *status = ORC_E_ARG;
+      orc_destroy(o);
+      return NULL;
+    }
+  }
+  o->S = sym_analyze(n, ne, o->ei, o->ej, order);
   o->N = num_create(o->S);
   o->t_symbolic = now_s() - t0;
   o->hdiag = (double *)malloc(Nn * 9 * 8);

@@ -63,8 +63,15 @@ typedef struct {
 void *orc_create(int n, int ne, const int32_t *ei, const int32_t *ej, const double *ez,
                  const double *ecov, int np, const int32_t *pi, const double *pz,
                  const double *pcov, int *status);
+/* the same with a caller-supplied fill-reducing ordering (order[k] = old
+ * index of the k-th eliminated pose) instead of AMD; NULL: AMD */
+void *orc_create_ordered(int n, int ne, const int32_t *ei, const int32_t *ej, const double *ez,
+                         const double *ecov, int np, const int32_t *pi, const double *pz,
+                         const double *pcov, const int32_t *order, int *status);
 void orc_destroy(void *h);
 void orc_default_params(orc_params *p);
+/* OpenMP threads used by later calls (bench.py: 1 and all host cores) */
+void orc_set_threads(int t);
 
 /* Full optimisation from init (x,y,theta)[n]; writes out (x,y,theta)[n].
  * trace (optional): 7 doubles per lambda try / GN step:

@@ -6,8 +6,12 @@ output of the CPU restatements:
 
 * C1, C1-nn, C2, KAT square/chain -- oracle/pgo_numpy.py (numpy + scipy SuperLU/COLAMD),
   independent of the C oracle, which tests/test_oracle.py checks against them;
-* C3 (100k poses) -- oracle/pgo_oracle.c (the numpy twin is too slow at this size):
-  final error, iteration counts, the error trace and every 100th final pose.
+* C3 (100k poses) -- oracle/pgo_oracle.c for the whole trajectory (the numpy
+  twin is too slow for all 24 tries at this size): final error, iteration
+  counts, the error trace and every 100th final pose;
+* C3-numpy2 -- the numpy twin's first 2 linearisations of C3 (max_outer = 2),
+  so the headline size is also pinned by a source independent of the C code
+  that provides the CPU baseline: trace, error and every 100th pose.
 
 Each fixture also records a SHA-256 of the generated inputs so a change of the
 generator is detected instead of silently comparing different graphs.
@@ -56,6 +60,53 @@ def numpy_fixture(name):
     print(name, "err", r.error, "it", r.iterations)
 
 
+def numpy_truncated_fixture(name, max_outer=2, stride=100):
+    from oracle import pgo_numpy as tw
+    import time
+    g = graph_for(name)
+    t0 = time.time()
+    r = tw.optimize_graph(g, tw.LMParams(max_outer=max_outer))
+    tr = np.array([[t["iteration"], t["lam"], t["new_error"], float(t["accepted"])] for t in r.trace])
+    idx = np.arange(0, g.num_poses, stride)
+    np.savez_compressed(os.path.join(HERE, f"golden_{name}-numpy{max_outer}.npz"), source="pgo_numpy",
+                        digest=input_digest(g), max_outer=max_outer, sample_index=idx, final_sample=r.xyt()[idx],
+                        trace=tr, final_error=r.error, initial_error=r.initial_error, iterations=r.iterations,
+                        inner_iterations=r.inner_iterations)
+    print(name, "numpy max_outer", max_outer, "err", r.error, "it", r.iterations, "t", time.time() - t0)
+
+
+def c5_fixture(stride=1000):
+    """C5 (1M poses / 5M edges) is too big for a full trajectory fixture: the
+    C oracle's first linearisation (error, gradient and H diagonal blocks at
+    every 1000th pose), the first lambda try's Cholesky step (sampled, plus its
+    2-norm) and the state after max_outer = 1 (trace, error, sampled poses).
+    The oracle factorises on the GPU plan's nested-dissection ordering
+    (pgo_debug_ordering, host-only; AMD's fill would not fit this container's
+    memory) -- the ordering changes rounding only."""
+    import time
+    from graphslam_amd.pose_graph import PoseGraph
+    from oracle.oracle import Oracle
+    g = graph_for("C5")
+    pg = PoseGraph.from_dataset(g)
+    order = pg.debug_ordering()
+    pg.close()
+    t0 = time.time()
+    o = Oracle(g, order=order)
+    hd, _, grad, err0 = o.linearize()
+    idx = np.arange(0, g.num_poses, stride)
+    rc, delta = o.solve(1e-5)
+    assert rc == 0
+    r = o.optimize(max_outer=1)
+    s = r.stats
+    np.savez_compressed(os.path.join(HERE, "golden_C5.npz"), source="pgo_oracle.c", digest=input_digest(g),
+                        sample_index=idx, initial_error=err0, grad_sample=grad[idx], hdiag_sample=hd[idx],
+                        delta_lambda=1e-5, delta_sample=delta[idx], delta_norm=np.linalg.norm(delta),
+                        trace=r.trace[:, [0, 1, 4, 6]], error_after=s["final_error"],
+                        poses_after_sample=r.poses[idx], factor_flops=s["factor_flops"], nnz_l=s["nnz_l"])
+    print("C5 err0", err0, "after 1 linearisation", s["final_error"], "tries", s["inner_iterations"],
+          "GFLOP", s["factor_flops"] / 1e9, "t", time.time() - t0)
+
+
 def oracle_fixture(name, stride=100):
     from oracle.oracle import Oracle
     g = graph_for(name)
@@ -75,7 +126,11 @@ def oracle_fixture(name, stride=100):
 if __name__ == "__main__":
     names = sys.argv[1:] or ["square", "chain", "C1", "C1-nn", "C2", "C3"]
     for n in names:
-        if n == "C3":
+        if n == "C5":
+            c5_fixture()
+        elif n.endswith("-numpy2"):
+            numpy_truncated_fixture(n[: -len("-numpy2")], 2)
+        elif n == "C3":
             oracle_fixture(n)
         else:
             numpy_fixture(n)

@@ -55,7 +55,7 @@ int main(void) {
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", f"-I{ROOT}/include", str(src), "-o", str(exe),
                     _lib.LIB_PATH, f"-Wl,-rpath,{os.path.dirname(_lib.LIB_PATH)}"], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
-    assert r.returncode == 0 and r.stdout.startswith("ok 3"), (r.returncode, r.stdout, r.stderr)
+    assert r.returncode == 0 and r.stdout.startswith("ok 4"), (r.returncode, r.stdout, r.stderr)
 
 
 def test_default_params_are_gtsam_defaults(pgo_lib):
@@ -153,7 +153,11 @@ int main() {
   graph.add(BetweenFactor<Pose2>(8, 1, Pose2(L, 0, 1.5707963267948966), noiseModel::Gaussian::Covariance(R)));  // loop_factor
   std::printf("factors %zu\n", graph.nrFactors());
   try {
-    Values poses_opti = LevenbergMarquardtOptimizer(graph, initial).optimize();   // graph.cpp:119
+    LevenbergMarquardtOptimizer optimizer(graph, initial);
+    Values poses_opti = optimizer.optimize();                                     // graph.cpp:119
+    const double e1 = optimizer.error();
+    optimizer.optimize();     // GTSAM keeps the state: a second call starts at the optimum
+    std::printf("second %d %d\n", optimizer.stats().initial_error == e1, optimizer.error() <= e1);
     for (Key k = 1; k <= 8; k++)
       std::printf("%llu %.9f %.9f %.9f\n", (unsigned long long)k, poses_opti.at<Pose2>(k).x(),
                   poses_opti.at<Pose2>(k).y(), poses_opti.at<Pose2>(k).theta());
@@ -183,4 +187,4 @@ def test_cpp_adapter_compiles_and_runs_host_side(tmp_path, pgo_lib):
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("factors 9")
     # no GPU here: the optimiser reports it instead of falling back to the CPU
-    assert ("runtime_error" in r.stdout and "device" in r.stdout) or r.stdout.count("\n") == 10
+    assert ("runtime_error" in r.stdout and "device" in r.stdout) or r.stdout.count("\n") == 11

@@ -178,6 +178,59 @@ def test_lm_trace_matches_oracle_c1nn(pg_cls, oracle_lib):
     assert abs(st["final_error"] - o.stats["final_error"]) <= 1e-11 * o.stats["final_error"]
 
 
+def test_trace_matches_oracle_c1nn(pg_cls, oracle_lib):
+    """pgo_get_trace (per lambda try: accepted steps, lambda, solved, model
+    decrease, candidate error, fidelity, accepted, ms) vs the oracle's trace
+    on C1-nn: decisions and lambdas identical, values to 1e-8 relative; the
+    speculative lambda lanes record the same rows as one lane."""
+    g = datasets.make("C1-nn")
+    o = oracle_lib.Oracle(g).optimize()
+    for lanes in (1, 2):
+        pg = pg_cls.from_dataset(g)
+        st = pg.optimize(lambda_lanes=lanes)
+        tr = pg.trace()
+        ot = o.trace
+        assert tr.shape == (ot.shape[0], 8)
+        for c in (0, 1, 2, 6):   # iteration, lambda, solved, accepted
+            assert np.array_equal(tr[:, c], ot[:, c]), c
+        fin = np.isfinite(ot[:, 4])
+        assert np.array_equal(np.isfinite(tr[:, 4]), fin)
+        assert np.allclose(tr[fin, 4], ot[fin, 4], rtol=1e-8)
+        ok = np.isfinite(ot[:, 3])
+        assert np.allclose(tr[ok, 3], ot[ok, 3], rtol=1e-6, atol=1e-9 * np.abs(ot[ok, 3]).max())
+        assert np.all(np.diff(tr[:, 7]) >= 0) and tr[-1, 7] <= st["ms_total"]
+        assert tr[tr[:, 6] == 1].shape[0] == st["iterations"]
+
+
+def test_stop_reason(pg_cls):
+    """pgo_stats.stop_reason tells apart what GTSAM reports as convergence."""
+    g = datasets.make("C1")
+    pg = pg_cls.from_dataset(g)
+    assert pg.optimize(max_outer=1)["stop_reason"] == 3             # PGO_STOP_MAX_OUTER
+    pg = pg_cls.from_dataset(g)
+    assert pg.optimize(max_iterations=1)["stop_reason"] == 2        # PGO_STOP_MAX_ITER
+    pg = pg_cls.from_dataset(datasets.square_loop())
+    st = pg.optimize()
+    assert st["stop_reason"] in (0, 4) and st["final_error"] < 1e-18
+
+
+def test_kernel_profile_accounts_every_launch(pg_cls):
+    """profile_every: every launch of the profiled factorisations is timed and
+    attributed to its kernel family; the Cholesky flops are all accounted."""
+    g = datasets.make("C2")
+    pg = pg_cls.from_dataset(g)
+    st = pg.optimize(profile_every=1, max_outer=1, lambda_lanes=1)
+    kp = pg.kernel_profile()
+    assert kp and all(v["launches"] > 0 and v["ms"] > 0 for v in kp.values())
+    nfac = st["kernel_syrk_count"]          # profiled factorisations = every solve here
+    assert nfac == st["solves"] >= 1
+    assert st["ms_factor_profiled"] > 0 and st["ms_solve_profiled"] > 0
+    fl = sum(v["flops"] for k, v in kp.items() if not k.startswith("k_bwd"))
+    # the launches' algorithmic flops cover the factorisation's (same formula
+    # for the fronts, plus the inverses the GPU forms for its TRSM / solves)
+    assert fl >= 0.99 * nfac * st["factor_flops"]
+
+
 def test_gauss_newton_parity(pg_cls, oracle_lib):
     g = datasets.make("C1")
     o = oracle_lib.Oracle(g).optimize(algorithm=1)
@@ -250,6 +303,24 @@ def test_c3_full_size_against_golden(pg_cls, solver):
     assert abs(st["final_error"] - float(gold["final_error"])) <= 1e-6 * float(gold["final_error"])
     idx = gold["sample_index"]
     assert_poses(pg.poses()[idx], gold["final_sample"], 1e-4, 1e-5)
+
+
+def test_c3_first_two_linearisations_vs_numpy_twin(pg_cls):
+    """The headline size pinned by a second, independent restatement: the
+    numpy/SuperLU twin's first 2 linearisations of C3 (golden_C3-numpy2.npz)."""
+    gold = np.load(os.path.join(GOLDEN, "golden_C3-numpy2.npz"), allow_pickle=False)
+    g = datasets.make("C3")
+    pg = pg_cls.from_dataset(g)
+    st = pg.optimize(max_outer=2)
+    tr = pg.trace()
+    gt = gold["trace"]
+    assert tr.shape[0] == gt.shape[0]
+    assert np.array_equal(tr[:, 1], gt[:, 1]) and np.array_equal(tr[:, 6], gt[:, 3])
+    ok = np.isfinite(gt[:, 2])
+    assert np.allclose(tr[ok, 4], gt[ok, 2], rtol=1e-6)
+    fe = float(gold["final_error"])
+    assert abs(st["final_error"] - fe) <= 1e-6 * fe
+    assert_poses(pg.poses()[gold["sample_index"]], gold["final_sample"], 1e-5, 1e-6)
 
 
 # ------------------------------------------------------------ edge cases
@@ -339,11 +410,15 @@ def test_gtsam_mirror_end_to_end(pgo_lib):
     for k1, k2, z, c in zip(g.edge_k1, g.edge_k2, g.edge_z, g.edge_cov):
         graph.add(gt.BetweenFactorPose2(int(k1), int(k2), gt.Pose2(*z),
                                         gt.noiseModel.Gaussian.Covariance(c.reshape(3, 3))))
-    poses_opti = gt.LevenbergMarquardtOptimizer(graph, initial).optimize()
+    opt = gt.LevenbergMarquardtOptimizer(graph, initial)
+    poses_opti = opt.optimize()
     for k, p in zip(g.keys, g.ground_truth):
         q = poses_opti.atPose2(int(k))
         assert abs(q.x() - p[0]) < 1e-9 and abs(q.y() - p[1]) < 1e-9
     assert graph.error(poses_opti) < 1e-18
+    e1 = opt.error()
+    opt.optimize()                       # GTSAM state: continues from the optimum
+    assert opt.stats["initial_error"] == e1 and opt.error() <= e1
 
 
 # ------------------------------------------------------------ marginals
@@ -412,8 +487,9 @@ def test_cpp_adapter_on_gpu(tmp_path, pgo_lib):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     lines = r.stdout.strip().splitlines()
-    assert lines[0] == "factors 9" and len(lines) == 10, r.stdout
-    xyt = np.array([[float(v) for v in ln.split()[1:]] for ln in lines[1:9]])
+    assert lines[0] == "factors 9" and len(lines) == 11, r.stdout
+    assert lines[1] == "second 1 1", r.stdout      # optimize() twice: continues from the optimum
+    xyt = np.array([[float(v) for v in ln.split()[1:]] for ln in lines[2:10]])
     assert np.all(np.isfinite(xyt))
-    cov = [float(v) for v in lines[9].split()[1:]]
-    assert lines[9].startswith("cov8") and all(v > 0 for v in cov)
+    cov = [float(v) for v in lines[10].split()[1:]]
+    assert lines[10].startswith("cov8") and all(v > 0 for v in cov)

@@ -200,10 +200,14 @@ def test_speculative_lambda_oracle_trajectory():
 
 
 @pytest.mark.gpu
-def test_rccl_one_rank_communicator():
+@pytest.mark.parametrize("force", ["0", "1"])
+def test_rccl_one_rank_communicator(monkeypatch, force):
     """RCCL transport on the box: a one-rank communicator (the only RCCL
     communicator one GPU allows) loads librccl, passes the exchange self test
     and leaves the optimisation unchanged."""
+    # force = 1 (PGO_COMM_FORCE_COLLECTIVES): the one-rank communicator still
+    # calls ncclAllGather / ncclBroadcast (in-place slot arithmetic included)
+    monkeypatch.setenv("PGO_COMM_FORCE_COLLECTIVES", force)
     from graphslam_amd import multi_gpu
     from graphslam_amd.pose_graph import PoseGraph
     g, init = perturbed_c2()
@@ -213,6 +217,8 @@ def test_rccl_one_rank_communicator():
     assert pg.comm_rank() == (0, 1)
     pg.comm_selftest()
     st = pg.optimize(lambda_lanes=1)
+    if force == "1":
+        assert st["ms_comm"] > 0.0           # the all-gathers / broadcasts ran through RCCL
     st1, x1 = _single("C2p", {})
     assert st["inner_iterations"] == st1["inner_iterations"]
     np.testing.assert_array_equal(pg.poses(), x1)

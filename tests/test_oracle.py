@@ -207,3 +207,43 @@ def test_marginals_twin_dense():
         assert np.all(np.linalg.eigvalsh(cov[q]) > 0)
     # the prior pins pose 0 (Sigma = diag(0.01)): its marginal is at most the prior
     assert np.all(np.diag(cov[0]) <= 0.01 + 1e-12)
+
+
+def test_c3_numpy_truncated_fixture_matches_c_oracle(oracle_lib):
+    """Two-source pin of the headline size: the numpy twin's first 2 LM
+    linearisations of C3 (tests/golden/golden_C3-numpy2.npz, SuperLU/COLAMD)
+    against the C oracle's (AMD supernodal Cholesky): same lambda / accept
+    decisions, errors to 1e-6 relative, sampled poses."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    from make_golden import graph_for, input_digest
+    gold = load_golden("C3-numpy2")
+    assert str(gold["source"]) == "pgo_numpy" and int(gold["max_outer"]) == 2
+    g = graph_for("C3")
+    assert input_digest(g) == str(gold["digest"]), "generator changed: regenerate fixtures"
+    o = oracle_lib.Oracle(g).optimize(max_outer=2)
+    tr, gt = o.trace, gold["trace"]
+    assert tr.shape[0] == gt.shape[0]
+    assert np.array_equal(tr[:, 1], gt[:, 1]) and np.array_equal(tr[:, 6], gt[:, 3])
+    ok = np.isfinite(gt[:, 2])
+    assert np.allclose(tr[ok, 4], gt[ok, 2], rtol=1e-6)
+    fe = float(gold["final_error"])
+    assert abs(o.stats["final_error"] - fe) <= 1e-6 * fe
+    assert pose_close(o.poses[gold["sample_index"]], gold["final_sample"], 1e-5, 1e-6)
+
+
+def test_oracle_given_ordering_same_solution(oracle_lib):
+    """orc_create_ordered (the CPU baseline factorises on the GPU plan's
+    nested-dissection order): any fill-reducing ordering gives the same LM
+    trajectory and solution up to rounding."""
+    g = datasets.make("C1-nn")
+    rng = np.random.default_rng(3)
+    order = rng.permutation(g.num_poses).astype(np.int32)
+    a = oracle_lib.Oracle(g).optimize()
+    b = oracle_lib.Oracle(g, order=order).optimize()
+    assert a.stats["iterations"] == b.stats["iterations"]
+    assert a.stats["inner_iterations"] == b.stats["inner_iterations"]
+    assert abs(a.stats["final_error"] - b.stats["final_error"]) <= 1e-9 * a.stats["final_error"]
+    assert pose_close(a.poses, b.poses, 1e-7, 1e-8)
+    with pytest.raises(ValueError):
+        oracle_lib.Oracle(g, order=np.zeros(g.num_poses, np.int32))   # not a permutation
