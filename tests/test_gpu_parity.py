@@ -493,3 +493,39 @@ def test_cpp_adapter_on_gpu(tmp_path, pgo_lib):
     assert np.all(np.isfinite(xyt))
     cov = [float(v) for v in lines[10].split()[1:]]
     assert lines[10].startswith("cov8") and all(v > 0 for v in cov)
+
+
+# ------------------------------------------------------------ C5 (1M poses / 5M edges)
+def test_c5_full_size_against_fixture(pg_cls):
+    """BASELINE configs[4] at full size on one MI355X (2.4 TFLOP per
+    factorisation, ~34 GB of fronts): the first linearisation (gradient and H
+    diagonal blocks at every 1000th pose, error), the Cholesky step at
+    lambda = 1e-5 (sampled, and its 2-norm) and the first LM linearisation's
+    lambda tries, against the C oracle's (tests/golden/golden_C5.npz)."""
+    gold = np.load(os.path.join(GOLDEN, "golden_C5.npz"), allow_pickle=False)
+    g = datasets.make("C5")
+    import sys
+    sys.path.insert(0, GOLDEN)
+    from make_golden import input_digest
+    assert input_digest(g) == str(gold["digest"])
+    idx = gold["sample_index"]
+    pg = pg_cls.from_dataset(g)
+    hd, _, grad, err = pg.debug_linearize(g.num_edges, cholesky=True)
+    e0 = float(gold["initial_error"])
+    assert abs(err - e0) <= 1e-10 * e0
+    assert np.abs(grad[idx] - gold["grad_sample"]).max() <= 1e-10 * np.abs(gold["grad_sample"]).max()
+    assert np.abs(hd[idx] - gold["hdiag_sample"]).max() <= 1e-10 * np.abs(gold["hdiag_sample"]).max()
+    del hd, grad
+    d, _ = pg.debug_solve(float(gold["delta_lambda"]))
+    dn = float(gold["delta_norm"])
+    assert abs(np.linalg.norm(d) - dn) <= 1e-8 * dn
+    assert np.abs(d[idx] - gold["delta_sample"]).max() <= 1e-8 * np.abs(d).max()
+    st = pg.optimize(max_outer=1)
+    tr, gt = pg.trace(), gold["trace"]
+    assert tr.shape[0] == gt.shape[0]
+    assert np.array_equal(tr[:, 1], gt[:, 1]) and np.array_equal(tr[:, 6], gt[:, 3])
+    ok = np.isfinite(gt[:, 2])
+    assert np.allclose(tr[ok, 4], gt[ok, 2], rtol=1e-8)
+    ea = float(gold["error_after"])
+    assert abs(st["final_error"] - ea) <= 1e-8 * ea
+    assert_poses(pg.poses()[idx], gold["poses_after_sample"], 1e-6, 1e-7)
