@@ -694,6 +694,7 @@ int finish_solve(pgo_graph* g, pgo_stats* st, SolveState* ss) {
   if (ss->known) return PGO_OK;
   int flag = 0;
   HIP_TRY(g, hipMemcpy(&flag, g->chol.d_flag, sizeof(int), hipMemcpyDeviceToHost));
+  if (flag & 2) return fail(g, PGO_E_HIP, "factorisation: an in-launch hand-off timed out");
   ss->solved = flag == 0;
   ss->known = true;
   if (st) st->factor_flops = g->chol.flops;
@@ -826,6 +827,8 @@ int run_lanes(pgo_graph* g, const pgo_params& p, int nb, const double* lams, dou
   HIP_TRY(g, hipStreamSynchronize(d.stream));
   int flags[8];
   std::memcpy(flags, g->h_lanes + 4 * 8 + 8, nb * sizeof(int));
+  for (int l = 0; l < nb; l++)
+    if (flags[l] & 2) return fail(g, PGO_E_HIP, "factorisation: an in-launch hand-off timed out");
   for (int l = 0; l < nb; l++) {
     out[4 * l] = flags[l] == 0 ? 1.0 : 0.0;
     out[4 * l + 1] = g->h_lanes[4 * l];
@@ -1622,10 +1625,11 @@ int pgo_debug_plan(pgo_graph* g, double* out, int cap) {
   for (const auto& lv : P.levels) {
     lf += (long long)lv.ea_off.size() + 1 + lv.small.size();
     for (const auto& ps : lv.panels)
-      lf += (ps.potrf_cnt > 0) + (ps.trsm_cnt > 0) + (ps.fused ? 1 : (ps.syrk_cnt > 0) + (ps.sdiag_cnt > 0));
+      lf += (ps.potrf_cnt > 0) + (ps.sdiag_cnt + ps.col_cnt + (ps.syrk_inline ? ps.syrk_cnt : 0) > 0) +
+            (ps.syrk_cnt > 0 && !ps.syrk_inline);
     ls += (lv.bwd_part.cnt > 0) + (long long)lv.bwd.size();
     for (const auto& ps : lv.panels) {
-      trsm += ps.trsm_cnt;
+      trsm += ps.fcol_cnt + ps.col_cnt;
       syrk += ps.syrk_cnt;
     }
   }

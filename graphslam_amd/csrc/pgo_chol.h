@@ -26,19 +26,25 @@ constexpr int kWaveW = 32;         // ... and w <= this: by one wavefront (panel
 constexpr int kNB = 64;            // panel width of the blocked path
 constexpr int kTile = 64;          // Schur-update output tile
 constexpr int kBigTile = 128;      // Schur-update output tile of the LDS-pipelined kernel
-constexpr int kKB = 256;
+constexpr int kKB = 64;          // Schur-update depth (one panel; kept for the tile kernels' clipping)
+constexpr int kInlineTiles = 512; // syrk tiles per step that ride inside k_step
 constexpr int kZeroBackgroundGrid = 32;   // workgroups of the background (late) zeroing
 constexpr int kBwdRows = 512;      // rows per partial product of the backward solve           // Schur-update depth: trailing matrix updated once per kKB columns
 
-struct PanelStep {                 // one panel of the blocked path, all big fronts of a level
+struct PanelStep {                 // one 64-column panel kb of every big front of a level
   int kb;
-  int potrf_off, potrf_cnt;        // fronts whose diagonal tile is factored (potrf_list)
-  int trsm_off, trsm_cnt;          // tasks (front, row chunk) in trsm_tasks
-  int syrk_off, syrk_cnt;          // tasks in syrk_tasks: (front, row0, col0, k0 | inner<<31)
-  double syrk_flops;               // algorithmic flops of this step's Schur updates (lower triangles)
+  int potrf_off, potrf_cnt;        // first panel: fronts whose diagonal tile k_panel_first factors (potrf_list)
+  int col_off, fcol_cnt, col_cnt;  // col_tasks [col_off, +fcol_cnt): first panel's trsm row tiles (front, r0, 0, -1);
+                                   // then col_cnt (front, r0, kn, kb): next panel's column block below its
+                                   // diagonal tile, updated with panel kb then solved (k_step)
+  int sdiag_off, sdiag_cnt;        // next panel's diagonal tiles (front, kn, kn, kb) updated + factored (k_step)
+  int syrk_off, syrk_cnt;          // the other Schur-update tiles (front, row0, col0, kb)
   int syrk_tile;                   // kTile or kBigTile
-  int sdiag_off, sdiag_cnt;        // look-ahead tasks in sdiag_tasks (next panel's diagonal tile)
-  int fused;                       // 1: look-ahead and update in one launch (k_step_fused) on the main stream
+  int syrk_inline;                 // 1: the (64-)tiles are k_step workgroups, 0: a concurrent launch
+  double syrk_flops;               // algorithmic flops of the whole Schur update of the step
+  double plain_flops;              // ... of the syrk tiles alone
+  double first_flops;              // algorithmic flops of k_panel_first (factor, inverse, trsm)
+  double step_flops;               // ... of k_step (updates, factor, inverse, trsm, inline tiles)
 };
 
 struct SolveStep {                 // one launch of the blocked triangular solves
@@ -88,8 +94,7 @@ struct CholPlan {
   // schedules
   std::vector<CholLevel> levels;
   std::vector<int> small_list, level_fronts, potrf_list;
-  std::vector<int2> trsm_tasks;
-  std::vector<int4> syrk_tasks, sdiag_tasks;
+  std::vector<int4> syrk_tasks, sdiag_tasks, col_tasks;
   // Fronts must be zero (lower triangles) before a factorisation assembles into
   // them.  zero_tasks (front, first column, end column), pieces of ~32k doubles:
   // [0, zero_split) leaf-level fronts and [zero_split, zero_late) the rest, zeroed
@@ -124,8 +129,8 @@ struct CholPlan {
   int *d_asm_front = nullptr, *d_asm_li = nullptr, *d_asm_lj = nullptr, *d_asm_ptr = nullptr, *d_asm_src = nullptr;
   int *d_dg_front = nullptr, *d_dg_loc = nullptr, *d_perm = nullptr, *d_dg_order = nullptr;
   int *d_small = nullptr, *d_level_fronts = nullptr, *d_potrf = nullptr;
-  int2* d_trsm = nullptr;
-  int4 *d_syrk = nullptr, *d_sdiag = nullptr, *d_zero = nullptr;
+  int4 *d_syrk = nullptr, *d_sdiag = nullptr, *d_zero = nullptr, *d_col = nullptr;
+  int* d_stepflag = nullptr;       // [batch][ns]: last panel (kb / 64 + 1) whose diagonal inverse is published
   hipStream_t side = nullptr;      // look-ahead diagonal tiles
   hipStream_t side2 = nullptr;     // small fronts beside the blocked path
   hipStream_t side3 = nullptr;     // zeroing + assembly of the non-leaf fronts beside the leaf level
@@ -166,7 +171,7 @@ hipError_t chol_set_batch(CholPlan& P, int nb, hipStream_t s);
 // capacity cap, *used pairs recorded.
 enum KernelFamily {
   kFamAssemble = 0, kFamZero, kFamPerm, kFamExtendAdd, kFamVecAssemble, kFamFrontWave, kFamFrontSmall,
-  kFamPanelDiag, kFamPanelTrsm, kFamPanelSyrk, kFamPanelSyrk128, kFamSyrkDiag, kFamStepFused,
+  kFamPanelFirst, kFamStep, kFamPanelSyrk, kFamPanelSyrk128,
   kFamBwdPart, kFamBwdInit, kFamBwdStep, kFamCount
 };
 const char* kernel_family_name(int f);

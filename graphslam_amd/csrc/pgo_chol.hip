@@ -5,15 +5,17 @@
 //   k_extend_add   children's update matrices -> parent fronts, one launch per
 //                  level, one workgroup per parent tile walking the children in
 //                  order (no atomics, fixed order, bitwise reproducible)
-//   k_front_small  fronts with m <= 128: whole front in LDS, one workgroup each
-//   k_panel_trsm   blocked path, per 64-column panel: the diagonal tile is
-//                  factored in LDS (redundantly by every workgroup of the front)
-//                  and the rows below are solved against it
-//   k_panel_syrk   Schur update of the trailing matrix, 64x64 output tiles on
-//                  v_mfma_f64_16x16x4_f64 (4 waves x 2x2 MFMA tiles), panels
-//                  staged in LDS
-// Solves: multifrontal forward (frontal vectors pulled from children in fixed
-// order) bottom-up, then backward top-down, one workgroup per front.
+//   k_front_wave   fronts with m <= 128, w <= 32: one wavefront each
+//   k_panel_first  blocked path, first 64-column panel: diagonal tile factored
+//                  and inverted in LDS, the rows below solved as MFMA GEMMs with
+//                  the inverse by workgroups that wait for it in the same launch
+//   k_step         each further panel: the next diagonal tile updated, factored
+//                  and inverted (look-ahead), the tiles below it updated then
+//                  solved (in-launch hand-off), the other trailing tiles updated
+//                  (v_mfma_f64_16x16x4_f64); big updates in k_panel_syrk_lds /
+//                  k_panel_syrk128 beside it
+// Solves: the forward substitution rides in the factorisation (the right-hand
+// side is an extra column), backward top-down per level.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -34,6 +36,8 @@ struct CholDev {
   const int *asm_front, *asm_li, *asm_lj, *asm_ptr, *asm_src;
   const int *dg_front, *dg_loc, *perm, *dg_order;
   int* flag;
+  int* stepflag;                   // [lane][ns] in-launch hand-off of the diagonal inverses
+  int ns;
   // lambda lanes: lane y = blockIdx.y works on its own numeric workspace
   long long fst, tst;              // F, Tinv doubles per lane
   long long tfo;                   // Tinv + tfo: the inverses again, in the trsm's MFMA operand order
@@ -49,6 +53,7 @@ __device__ __forceinline__ void lane_offset(CholDev& c) {
   c.fv += y * c.vst;
   c.xv += y * c.xst;
   c.flag += y;
+  c.stepflag += (long long)y * c.ns;
 }
 
 static CholDev dev_view(const CholPlan& P) {
@@ -61,6 +66,8 @@ static CholDev dev_view(const CholPlan& P) {
   c.asm_src = P.d_asm_src; c.dg_front = P.d_dg_front; c.dg_loc = P.d_dg_loc; c.perm = P.d_perm;
   c.dg_order = P.d_dg_order;
   c.flag = P.d_flag;
+  c.stepflag = P.d_stepflag;
+  c.ns = P.ns;
   c.fst = P.ftotal;
   c.tst = 2 * P.ttotal;
   c.tfo = P.ttotal;
@@ -588,10 +595,49 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
   return bad;
 }
 
+// ---- in-launch hand-off of a diagonal tile's inverse (MI355X_MICROARCH.md,
+// inter-workgroup visibility, the "sc1 stores / sc1 flag / sc1 loads" row): the
+// diagonal workgroup stores the inverse (trsm operand order) and the panel's y
+// with sc1 (write-through) stores, every wave waits for its stores, a barrier,
+// then one lane stores the step flag sc1; a waiting workgroup polls the flag
+// with sc1 loads (one lane, s_sleep, bounded), joins a barrier, and reads the
+// handed-off bytes with sc1 loads only.  The flags are zeroed at the start of
+// every factorisation; a step publishes kn / 64 + 1 for its panel kn.
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void publish_step(int* flag, int val) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Waits (one lane polls, the workgroup joins a barrier) until *flag >= val;
+// gives up after ~0.2 s with bit 2 of the pivot flag set (reported as a HIP
+// failure by the host), so a lost hand-off can never hang the GPU.
+__device__ __forceinline__ void wait_step(const CholDev& c, const int* flag, int val) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = wall_clock64();   // 100 MHz
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < val) {
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > 20000000ull) {
+        __hip_atomic_fetch_or(c.flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // Forward substitution of the panel's rows of the frontal vector: y = X v with
-// X = L_bb^-1 (LDS, ld 65); the rows below get v -= L y in k_panel_trsm.
+// X = L_bb^-1 (LDS, ld 65), published sc1 (the rows below get v -= L y in the
+// trsm); y is also left in ys (LDS).
 // (4 waves: wave q sums k in [16q, 16q + 16), then a fixed-order sum of the 4)
-__device__ __forceinline__ void panel_rhs(double* v, const double* X, int nb, double* buf) {
+__device__ __forceinline__ void panel_rhs(double* v, const double* X, int nb, double* buf, double* ys) {
   __shared__ double part[4][64];
   const int tid = threadIdx.x, r = tid & 63, q = tid >> 6;
   if (tid < 64) buf[tid] = tid < nb ? v[tid] : 0.0;
@@ -601,11 +647,15 @@ __device__ __forceinline__ void panel_rhs(double* v, const double* X, int nb, do
   for (int k = 16 * q; k < 16 * q + 16; k++) acc = fma(k <= r ? X[r + k * 65] : 0.0, buf[k], acc);
   part[q][r] = acc;
   __syncthreads();
-  if (tid < nb) v[tid] = ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid];
+  if (tid < 64) {
+    const double y = tid < nb ? ((part[0][tid] + part[1][tid]) + part[2][tid]) + part[3][tid] : 0.0;
+    ys[tid] = y;
+    if (tid < nb) st_sc1(v + tid, y);
+  }
 }
 
 // L (LDS Ts, ld 65) back into the front, X = L^-1 (LDS Ws, ld 65) row-major to
-// M and in the trsm's operand order to Mf: Mf[(4 ks + ct) * 64 + l] =
+// M and, stored sc1, in the trsm's operand order to Mf: Mf[(4 ks + ct) * 64 + l] =
 // X[16 ct + (l & 15)][4 ks + (l >> 4)] (each trsm lane loads 64 consecutive-by-lane values)
 __device__ __forceinline__ void store_inverse(double* Fs, int m, double* __restrict__ M, double* __restrict__ Mf,
                                               const double* Ts, const double* Ws, int nb) {
@@ -617,72 +667,86 @@ __device__ __forceinline__ void store_inverse(double* Fs, int m, double* __restr
     M[idx] = (a < nb && b < nb && a >= b) ? Ws[a + b * 65] : 0.0;
     const int l = idx & 63, ct = (idx >> 6) & 3, ks = idx >> 8;
     const int fa = 16 * ct + (l & 15), fb = 4 * ks + (l >> 4);
-    Mf[idx] = (fa < nb && fb < nb && fa >= fb) ? Ws[fa + fb * 65] : 0.0;
+    st_sc1(Mf + idx, (fa < nb && fb < nb && fa >= fb) ? Ws[fa + fb * 65] : 0.0);
   }
 }
 
-// Diagonal tile of each listed front at panel kb: factored and inverted in LDS
-// (diag_factor_invert); L back into the front, L^-1 into Tinv for the TRSM GEMM
-// and the solves.
-__global__ __launch_bounds__(256) void k_panel_diag(CholDev c, const int* __restrict__ list, int kb) {
-  lane_offset(c);
-  __shared__ double Ts[64 * 65];
-  __shared__ double Ws[64 * 65];
-  __shared__ double bc[64];
-  const int s = list[blockIdx.x];
-  const int m = c.m[s], w = c.w[s];
-  const int nb = min(kNB, w - kb);
-  double* Fs = c.F + c.foff[s] + kb + (size_t)kb * m;
-  const int tid = threadIdx.x;
-  double tv[16];
-#pragma unroll
-  for (int u = 0; u < 16; u++) {   // all 16 loads in flight
-    const int idx = tid + 256 * u, i = idx & 63, j = idx >> 6;
-    tv[u] = (i < nb && j < nb) ? (i >= j ? Fs[i + (size_t)j * m] : 0.0) : (i == j ? 1.0 : 0.0);
-  }
+// The rows of a diagonal tile below its live nb x nb block (nb < 64: a front's
+// last panel) were kept in `keep` (the thread's 16 elements, idx = tid + 256 u,
+// columns < nb) while the block was factored; solved here: L = A X^T (X = Ws),
+// written to the front (columns < nb) and v -= L y for those rows (rows with
+// r0 + i >= m, i >= rrem, skipped).  Ts is scratch (the live block is stored).
+__device__ __forceinline__ void diag_own_rows(double* Fs, int m, int rrem, double* v, const double* keep, double* Ts,
+                                              const double* Ws, const double* ys, int nb) {
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
 #pragma unroll
   for (int u = 0; u < 16; u++) {
     const int idx = tid + 256 * u, i = idx & 63, j = idx >> 6;
-    Ts[i + j * 65] = tv[u];
-    Ws[i + j * 65] = 0.0;
+    Ts[i + j * 65] = (i >= nb && j < nb) ? keep[u] : 0.0;
   }
   __syncthreads();
-  if (diag_factor_invert(Ts, Ws, bc)) *c.flag = 1;
-  double* M = c.Tinv + c.toff[s] + (kb / 64) * 4096;   // row-major L^-1 of the tile
-  store_inverse(Fs, m, M, M + c.tfo, Ts, Ws, nb);
-  panel_rhs(c.fv + c.voff[s] + kb, Ws, nb, bc);
+  const int J = wv;   // wave wv: column block J = wv, all row blocks
+  d4 acc[4];
+#pragma unroll
+  for (int I = 0; I < 4; I++) {
+    acc[I] = d4{0, 0, 0, 0};
+    if (16 * I + 15 < nb || 16 * J >= nb) continue;   // wave-uniform: no row >= nb / no column < nb
+#pragma unroll
+    for (int K = 0; K < 4; K++) {
+      const d4 p = mm16(Ts + 16 * I + 16 * K * 65, 1, 65, Ws + 16 * J + 16 * K * 65, 65, 1);
+#pragma unroll
+      for (int r = 0; r < 4; r++) acc[I][r] += p[r];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int I = 0; I < 4; I++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int i = 16 * I + (l >> 4) + 4 * r, j = 16 * J + (l & 15);
+      Ts[i + j * 65] = (i >= nb && j < nb) ? acc[I][r] : 0.0;
+    }
+  __syncthreads();
+  if (tid >= nb && tid < 64 && tid < rrem) {
+    double t = 0.0;
+    for (int j = 0; j < nb; j++) {
+      const double lij = Ts[tid + j * 65];
+      Fs[tid + (size_t)j * m] = lij;
+      t = fma(lij, ys[j], t);
+    }
+    v[tid] -= t;
+  }
 }
 
-// Rows below the diagonal tile, 64 per workgroup (16 per wave): X = B L^-T as a
-// GEMM with the inverted tile, v_mfma_f64_16x16x4_f64, B fragments from global.
-__global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __restrict__ tasks, int kb) {
-  lane_offset(c);
-  const int2 task = tasks[blockIdx.x];
-  const int s = task.x, chunk = task.y;
-  const int m = c.m[s], w = c.w[s];
-  const int nb = min(kNB, w - kb);
-  const double* Mf = c.Tinv + c.tfo + c.toff[s] + (kb / 64) * 4096;   // inverse, operand order
+// Rows r0 .. r0+63 of front s below panel kn (nb columns): L = A X^T with the
+// published inverse (operand-order copy Mf, sc1 loads) as a GEMM on
+// v_mfma_f64_16x16x4_f64 (16 rows per wave), L written to the front and the
+// frontal vector's rows updated with v -= L y.  A(i, k) = A[i * ars + k * acs]
+// (an LDS tile or the front itself).
+__device__ __forceinline__ void trsm_rows(const CholDev& c, int s, int r0, int kn, int nb, const double* A, int ars,
+                                          int acs) {
+  const int m = c.m[s];
+  const double* Mf = c.Tinv + c.tfo + c.toff[s] + (kn / 64) * 4096;
   double* fv = c.fv + c.voff[s];
-  const int tid = threadIdx.x;
-  const int wv = tid >> 6, l = tid & 63;
-  const int r0 = kb + nb + chunk * 64 + wv * 16;
-  if (r0 >= m) return;                               // (no barriers below)
-  double* Fc = c.F + c.foff[s] + (size_t)kb * m;   // column kb of the front
-  const int arow = r0 + (l & 15), kl = l >> 4;
-  double a[16], tb[16][4], yc[4];   // B fragments, inverse fragments, y: all loads in flight
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int rw = r0 + wv * 16;
+  if (rw >= m) return;                                // (no barriers below)
+  double* Fc = c.F + c.foff[s] + (size_t)kn * m;
+  const int il = wv * 16 + (l & 15), arow = r0 + il, kl = l >> 4;
+  double a[16], tb[16][4], yc[4];   // A fragments, inverse fragments, y: all loads in flight
 #pragma unroll
   for (int ks = 0; ks < 16; ks++) {
     const int k = 4 * ks + kl;
-    a[ks] = (arow < m && k < nb) ? Fc[arow + (size_t)k * m] : 0.0;
+    a[ks] = (arow < m && k < nb) ? A[il * ars + k * acs] : 0.0;
   }
 #pragma unroll
   for (int ks = 0; ks < 16; ks++)
 #pragma unroll
-    for (int ct = 0; ct < 4; ct++) tb[ks][ct] = Mf[(4 * ks + ct) * 64 + l];
+    for (int ct = 0; ct < 4; ct++) tb[ks][ct] = ld_sc1(Mf + (4 * ks + ct) * 64 + l);
 #pragma unroll
   for (int ct = 0; ct < 4; ct++) {
     const int col = 16 * ct + (l & 15);
-    yc[ct] = col < nb ? fv[kb + col] : 0.0;          // y of the panel (diagonal step)
+    yc[ct] = col < nb ? ld_sc1(fv + kn + col) : 0.0;
   }
   d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0}, acc3 = {0, 0, 0, 0};
 #pragma unroll
@@ -702,7 +766,7 @@ __global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __res
     if (col >= nb) continue;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      const int row = r0 + kl + 4 * r;
+      const int row = rw + kl + 4 * r;
       if (row < m) Fc[row + (size_t)col * m] = v[r];
     }
   }
@@ -711,7 +775,7 @@ __global__ __launch_bounds__(256) void k_panel_trsm(CholDev c, const int2* __res
     double t = part[r];
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o);
-    const int row = r0 + kl + 4 * r;
+    const int row = rw + kl + 4 * r;
     if ((l & 15) == 0 && row < m) fv[row] -= t;
   }
 }
@@ -964,53 +1028,131 @@ __device__ __forceinline__ void diag_tile_update(const CholDev& c, const int4 t,
   }
 }
 
-// The Schur-update tile that is the next panel's diagonal tile (row0 = col0 =
-// kb + nb < w), then that tile factored and inverted in place (look-ahead: runs
-// on a second stream beside the rest of the panel's Schur update, or as the
-// first workgroups of k_step_fused, so the next panel starts without a
-// separate diagonal step).  smem: 64*65 + 64*68 + 64 doubles.
+// The next panel's diagonal tile (row0 = col0 = kn < w): updated with panel kb
+// (diag_tile_update), factored and inverted in LDS, L and the inverses stored,
+// y of the panel formed; at a front's last panel (nb < 64) the tile's rows
+// below the live block are solved here too; then the inverse is published for
+// the workgroups solving the rows below the tile.
+// smem: kDiagSmem = 64*65 + 64*68 + 2*64 doubles.
+constexpr int kDiagSmem = 64 * 65 + 64 * 68 + 2 * 64;
+
 __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, int kb, double* smem) {
   double* Ts = smem;
   double* Ws = smem + 64 * 65;
   double* bc = Ws + 64 * 68;
+  double* ys = bc + 64;
   const int s = t.x, kn = t.y;
   const int m = c.m[s], w = c.w[s];
   const int nb = min(kNB, w - kn);
   const int tid = threadIdx.x;
   diag_tile_update(c, t, kb, Ts, Ws);
   __syncthreads();
-  for (int idx = tid; idx < 4096; idx += 256) {
-    const int i = idx & 63, j = idx >> 6;
+  double keep[16];
+#pragma unroll
+  for (int u = 0; u < 16; u++) {   // same element set as the loop below: no hazard
+    const int idx = tid + 256 * u, i = idx & 63, j = idx >> 6;
+    keep[u] = (i >= nb && j < nb) ? Ts[i + j * 65] : 0.0;
     if (!(i < nb && j < nb)) Ts[i + j * 65] = i == j ? 1.0 : 0.0;
     Ws[i + j * 65] = 0.0;
   }
   __syncthreads();
-  if (diag_factor_invert(Ts, Ws, bc)) *c.flag = 1;
+  if (diag_factor_invert(Ts, Ws, bc)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   double* Fs = c.F + c.foff[s] + kn + (size_t)kn * m;
   double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;   // row-major L^-1 of the tile
+  double* v = c.fv + c.voff[s] + kn;
   store_inverse(Fs, m, M, M + c.tfo, Ts, Ws, nb);
-  panel_rhs(c.fv + c.voff[s] + kn, Ws, nb, bc);
+  panel_rhs(v, Ws, nb, bc, ys);
+  if (nb < kNB) {
+    __syncthreads();
+    diag_own_rows(Fs, m, m - kn, v, keep, Ts, Ws, ys, nb);
+  }
+  publish_step(c.stepflag + s, kn / 64 + 1);
 }
 
-constexpr int kDiagSmem = 64 * 65 + 64 * 68 + 64;
-
-__global__ __launch_bounds__(256) void k_syrk_diag(CholDev c, const int4* __restrict__ tasks, int kb) {
-  lane_offset(c);
-  __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
-  syrk_diag_body(c, tasks[blockIdx.x], kb, smem);
+// First panel of a front: its assembled diagonal tile factored and inverted,
+// the rest as syrk_diag_body.
+__device__ __forceinline__ void first_diag_body(const CholDev& c, int s, double* smem) {
+  double* Ts = smem;
+  double* Ws = smem + 64 * 65;
+  double* bc = Ws + 64 * 68;
+  double* ys = bc + 64;
+  const int m = c.m[s], w = c.w[s];
+  const int nb = min(kNB, w);
+  double* Fs = c.F + c.foff[s];
+  const int tid = threadIdx.x;
+  double tv[16], keep[16];
+#pragma unroll
+  for (int u = 0; u < 16; u++) {   // all loads in flight
+    const int idx = tid + 256 * u, i = idx & 63, j = idx >> 6;
+    tv[u] = (i < nb && j < nb) ? (i >= j ? Fs[i + (size_t)j * m] : 0.0) : (i == j ? 1.0 : 0.0);
+    keep[u] = (i >= nb && i < m && j < nb) ? Fs[i + (size_t)j * m] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < 16; u++) {
+    const int idx = tid + 256 * u, i = idx & 63, j = idx >> 6;
+    Ts[i + j * 65] = tv[u];
+    Ws[i + j * 65] = 0.0;
+  }
+  __syncthreads();
+  if (diag_factor_invert(Ts, Ws, bc)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double* M = c.Tinv + c.toff[s];
+  double* v = c.fv + c.voff[s];
+  store_inverse(Fs, m, M, M + c.tfo, Ts, Ws, nb);
+  panel_rhs(v, Ws, nb, bc, ys);
+  if (nb < kNB) {
+    __syncthreads();
+    diag_own_rows(Fs, m, m, v, keep, Ts, Ws, ys, nb);
+  }
+  publish_step(c.stepflag + s, 1);
 }
 
-// One panel step's Schur update in a single launch on the main stream (steps
-// whose update is small beside the look-ahead diagonal factorisation): the
-// first nsd workgroups are the look-ahead diagonal tiles (k_syrk_diag), the
-// rest the 64x64 update tiles (k_panel_syrk_lds).
-__global__ __launch_bounds__(256) void k_step_fused(CholDev c, const int4* __restrict__ sdiag, int nsd,
-                                                    const int4* __restrict__ tasks, int kb) {
+// First panel of every big front of a level: workgroups [0, np) factor the
+// fronts' first diagonal tiles (list), the others solve 64-row tiles below
+// them (col: (front, r0, 0, -1)) once the tile's inverse is published.
+__global__ __launch_bounds__(256) void k_panel_first(CholDev c, const int* __restrict__ list, int np,
+                                                     const int4* __restrict__ col) {
   lane_offset(c);
   __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
   const int b = blockIdx.x;
-  if (b < nsd) syrk_diag_body(c, sdiag[b], kb, smem);
-  else syrk_lds_body(c, tasks[b - nsd], kb, smem);
+  if (b < np) {
+    first_diag_body(c, list[b], smem);
+    return;
+  }
+  const int4 t = col[b - np];
+  const int s = t.x, m = c.m[s], nb = min(kNB, c.w[s]);
+  wait_step(c, c.stepflag + s, 1);
+  trsm_rows(c, s, t.y, 0, nb, c.F + c.foff[s] + t.y, 1, m);
+}
+
+// One panel step kb of every big front of a level in one launch:
+//   [0, nsd)            the next panel's diagonal tiles (syrk_diag_body)
+//   [nsd, nsd + ncol)   64-row tiles of the next panel's column block below
+//                       its diagonal tile: Schur update with panel kb (kept in
+//                       LDS), then, once the diagonal inverse is published,
+//                       solved against it (trsm_rows)
+//   the rest            the other Schur-update tiles (syrk_lds_body)
+// The diagonal workgroups come first in dispatch order, so every waiting
+// workgroup waits on a workgroup dispatched before it.
+__global__ __launch_bounds__(256) void k_step(CholDev c, const int4* __restrict__ sdiag, int nsd,
+                                              const int4* __restrict__ col, int ncol, const int4* __restrict__ tiles,
+                                              int kb) {
+  lane_offset(c);
+  __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
+  const int b = blockIdx.x;
+  if (b < nsd) {
+    syrk_diag_body(c, sdiag[b], kb, smem);
+    return;
+  }
+  if (b < nsd + ncol) {
+    const int4 t = col[b - nsd];   // (front, r0, kn, kb)
+    syrk_tile64<true>(c, t, kb, smem);
+    __syncthreads();
+    const int s = t.x, kn = t.z, nb = min(kNB, c.w[s] - kn);
+    wait_step(c, c.stepflag + s, kn / 64 + 1);
+    trsm_rows(c, s, t.y, kn, nb, smem, 1, 65);
+    return;
+  }
+  syrk_lds_body(c, tiles[b - nsd - ncol], kb, smem);
 }
 
 // Schur update of one 128x128 lower tile (same task format and semantics as
@@ -1454,11 +1596,11 @@ static hipError_t up(T** d, const std::vector<T>& h, hipStream_t s) {
 
 // numeric workspaces of nb lanes (fronts zeroed: the upper triangles stay zero)
 static void free_numeric(CholPlan& P) {
-  void* ptrs[] = {P.F, P.Tinv, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_partial};
+  void* ptrs[] = {P.F, P.Tinv, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_partial, P.d_stepflag};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   P.F = P.Tinv = P.fv = P.xv = P.d_lambda = P.d_partial = nullptr;
-  P.d_flag = nullptr;
+  P.d_flag = P.d_stepflag = nullptr;
   P.batch = 0;
 }
 
@@ -1468,6 +1610,7 @@ static hipError_t alloc_numeric(CholPlan& P, int nb, hipStream_t s) {
   CH_TRY(hipMalloc((void**)&P.fv, (size_t)nb * std::max(P.vtotal, 1) * sizeof(double)));
   CH_TRY(hipMalloc((void**)&P.xv, (size_t)nb * std::max(3 * P.n, 1) * sizeof(double)));
   CH_TRY(hipMalloc((void**)&P.d_flag, nb * sizeof(int)));
+  CH_TRY(hipMalloc((void**)&P.d_stepflag, (size_t)nb * std::max(P.ns, 1) * sizeof(int)));
   CH_TRY(hipMalloc((void**)&P.d_lambda, nb * sizeof(double)));
   CH_TRY(hipMalloc((void**)&P.d_partial, (size_t)nb * std::max(P.npart, 1) * 64 * sizeof(double)));
   CH_TRY(hipMemsetAsync(P.F, 0, nb * std::max<long long>(P.ftotal, 1) * sizeof(double), s));
@@ -1512,13 +1655,13 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(up(&P.d_perm, P.perm, s));
   CH_TRY(up(&P.d_small, P.small_list, s));
   CH_TRY(up(&P.d_level_fronts, P.level_fronts, s));
-  CH_TRY(up(&P.d_trsm, P.trsm_tasks, s));
   CH_TRY(up(&P.d_potrf, P.potrf_list, s));
   CH_TRY(up(&P.d_bwd, P.bwd_tasks, s));
   CH_TRY(up(&P.d_bwd_pref, P.bwd_pref, s));
   CH_TRY(up(&P.d_bwd_part, P.bwd_part_tasks, s));
   CH_TRY(up(&P.d_syrk, P.syrk_tasks, s));
   CH_TRY(up(&P.d_sdiag, P.sdiag_tasks, s));
+  CH_TRY(up(&P.d_col, P.col_tasks, s));
   CH_TRY(up(&P.d_zero, P.zero_tasks, s));
   CH_TRY(up(&P.d_dg_order, P.dg_order, s));
   CH_TRY(alloc_numeric(P, std::max(P.batch, 1), s));
@@ -1535,7 +1678,7 @@ void chol_free(CholPlan& P) {
   void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
                   P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
                   P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
-                  P.d_trsm, P.d_syrk, P.d_ea_tasks, P.d_ea_pairs, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_zero, P.d_dg_order};
+                  P.d_syrk, P.d_ea_tasks, P.d_ea_pairs, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_zero, P.d_dg_order, P.d_col, P.d_stepflag};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : P.evs)
@@ -1549,8 +1692,8 @@ void chol_free(CholPlan& P) {
 const char* kernel_family_name(int f) {
   static const char* const names[kFamCount] = {
       "k_asm_offdiag+k_asm_diag", "k_zero_lower", "k_perm_in+k_perm_out", "k_extend_add", "k_vec_assemble",
-      "k_front_wave", "k_front_small", "k_panel_diag", "k_panel_trsm", "k_panel_syrk_lds", "k_panel_syrk128",
-      "k_syrk_diag", "k_step_fused", "k_bwd_part", "k_bwd_init", "k_bwd_step"};
+      "k_front_wave", "k_front_small", "k_panel_first", "k_step", "k_panel_syrk_lds", "k_panel_syrk128",
+      "k_bwd_part", "k_bwd_init", "k_bwd_step"};
   return f >= 0 && f < kFamCount ? names[f] : "?";
 }
 
@@ -1583,13 +1726,6 @@ static double chol_flops(int m, int w) {   // dense Cholesky of the w pivot colu
   }
   return f;
 }
-static double potrf_inv_flops(int nb) { return 2.0 * nb * nb * (double)nb / 3.0; }   // factor + inverse
-static double sdiag_flops(const CholPlan& P, const int4& t, int kb) {
-  const int s = t.x, kn = t.y, w = P.w[s];
-  const int nb = std::min(kNB, w - kn), K = std::min(kb + kNB, w) - (t.w & 0x7fffffff);
-  return (double)K * nb * (nb + 1) + potrf_inv_flops(nb);
-}
-
 hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
                        hipStream_t s, LaunchProfile* prof, int nb) {
   if (P.n == 0) return hipSuccess;
@@ -1599,6 +1735,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
   launch(prof, kFamPerm, [&] { return make_double2(0, 48.0 * P.n * nb); }, k_perm_in, dim3((P.n + 255) / 256, nb),
          B256, 0, s, c, b, scale_b, P.n);
   CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int) * nb, s));
+  CH_TRY(hipMemsetAsync(P.d_stepflag, 0, sizeof(int) * std::max(P.ns, 1) * nb, s));
   // zeroing + assembly: leaf-level fronts on the main stream, the others on
   // side3 beside the leaf level (joined before level 1's extend-add)
   const int nz = P.zero_late, nt = (int)P.asm_front.size();
@@ -1693,51 +1830,37 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
     }
     for (const PanelStep& ps : lv.panels) {
       if (prof) prof->cur_tag = ((int)li << 16) | (ps.kb / kNB + 1);
+      const int4* cols = (const int4*)(P.d_col + ps.col_off);
       if (ps.potrf_cnt)
-        launch(prof, kFamPanelDiag, [&] {
-                 double f = 0;
-                 for (int q = 0; q < ps.potrf_cnt; q++)
-                   f += potrf_inv_flops(std::min(kNB, P.w[P.potrf_list[ps.potrf_off + q]] - ps.kb));
-                 return make_double2(f * nb, 0);
-               },
-               k_panel_diag, dim3(ps.potrf_cnt, nb), B256, 0, s, c, (const int*)(P.d_potrf + ps.potrf_off), ps.kb);
-      if (ps.trsm_cnt)
-        launch(prof, kFamPanelTrsm, [&] {
-                 double f = 0;
-                 for (int q = 0; q < ps.trsm_cnt; q++) {
-                   const int2 t = P.trsm_tasks[ps.trsm_off + q];
-                   const int w = P.w[t.x], m = P.m[t.x], nbk = std::min(kNB, w - ps.kb);
-                   const int rows = std::min(64, m - ps.kb - nbk - 64 * t.y);
-                   f += (double)rows * nbk * nbk + 2.0 * rows * nbk;
-                 }
-                 return make_double2(f * nb, 0);
-               },
-               k_panel_trsm, dim3(ps.trsm_cnt, nb), B256, 0, s, c, (const int2*)(P.d_trsm + ps.trsm_off), ps.kb);
-      auto sdiag_cost = [&] {
-        double f = 0;
-        for (int q = 0; q < ps.sdiag_cnt; q++) f += sdiag_flops(P, P.sdiag_tasks[ps.sdiag_off + q], ps.kb);
-        return f;
+        launch(prof, kFamPanelFirst, [&] { return make_double2(ps.first_flops * nb, 0); }, k_panel_first,
+               dim3(ps.potrf_cnt + ps.fcol_cnt, nb), B256, 0, s, c, (const int*)(P.d_potrf + ps.potrf_off),
+               ps.potrf_cnt, cols);
+      const int4* tiles = (const int4*)(P.d_syrk + ps.syrk_off);
+      const int nin = ps.syrk_inline ? ps.syrk_cnt : 0;
+      const bool apart = ps.syrk_cnt > 0 && !ps.syrk_inline;   // plain tiles in their own launch
+      const bool step = ps.sdiag_cnt + ps.col_cnt + nin > 0;
+      auto plain = [&](hipStream_t st) {
+        const bool big = ps.syrk_tile == kBigTile;
+        launch(prof, big ? kFamPanelSyrk128 : kFamPanelSyrk, [&] { return make_double2(ps.plain_flops * nb, 0); },
+               big ? k_panel_syrk128 : k_panel_syrk_lds, dim3(ps.syrk_cnt, nb), B256, 0, st, c, tiles, ps.kb);
       };
-      const int4* tasks = (const int4*)(P.d_syrk + ps.syrk_off);
-      if (ps.fused) {
-        launch(prof, kFamStepFused, [&] { return make_double2((ps.syrk_flops + sdiag_cost()) * nb, 0); },
-               k_step_fused, dim3(ps.sdiag_cnt + ps.syrk_cnt, nb), B256, 0, s, c,
-               (const int4*)(P.d_sdiag + ps.sdiag_off), ps.sdiag_cnt, tasks, ps.kb);
-        continue;
-      }
-      if (ps.sdiag_cnt) {   // look-ahead: next panel's diagonal tiles on the side stream
+      if (apart && step) {   // beside k_step on the side stream, joined before the next step
         CH_TRY(hipEventRecord(P.evs[2], s));
         CH_TRY(hipStreamWaitEvent(P.side, P.evs[2], 0));
-        launch(prof, kFamSyrkDiag, [&] { return make_double2(sdiag_cost() * nb, 0); }, k_syrk_diag,
-               dim3(ps.sdiag_cnt, nb), B256, 0, P.side, c, (const int4*)(P.d_sdiag + ps.sdiag_off), ps.kb);
-        CH_TRY(hipEventRecord(P.evs[3], P.side));
       }
-      if (ps.syrk_cnt) {
-        const bool big = ps.syrk_tile == kBigTile;
-        launch(prof, big ? kFamPanelSyrk128 : kFamPanelSyrk, [&] { return make_double2(ps.syrk_flops * nb, 0); },
-               big ? k_panel_syrk128 : k_panel_syrk_lds, dim3(ps.syrk_cnt, nb), B256, 0, s, c, tasks, ps.kb);
+      if (step)
+        launch(prof, kFamStep, [&] { return make_double2(ps.step_flops * nb, 0); }, k_step,
+               dim3(ps.sdiag_cnt + ps.col_cnt + nin, nb), B256, 0, s, c, (const int4*)(P.d_sdiag + ps.sdiag_off),
+               ps.sdiag_cnt, cols + ps.fcol_cnt, ps.col_cnt, tiles, ps.kb);
+      if (apart) {
+        if (step) {
+          plain(P.side);
+          CH_TRY(hipEventRecord(P.evs[3], P.side));
+          CH_TRY(hipStreamWaitEvent(s, P.evs[3], 0));
+        } else {
+          plain(s);
+        }
       }
-      if (ps.sdiag_cnt) CH_TRY(hipStreamWaitEvent(s, P.evs[3], 0));
     }
     if (fork_small) {
       CH_TRY(hipEventRecord(P.evs[1], P.side2));

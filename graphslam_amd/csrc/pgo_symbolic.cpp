@@ -427,7 +427,6 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.levels.assign(nl, CholLevel());
   P.small_list.clear();
   P.level_fronts.clear();
-  P.trsm_tasks.clear();
   P.syrk_tasks.clear();
   P.sdiag_tasks.clear();
   // zeroing (see CholPlan::zero_tasks): the level whose extend-add is the last
@@ -464,6 +463,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     if (late(q)) zero_cols(q, P.w[q], P.m[q]);
   if (P.zero_late == (int)P.zero_tasks.size()) P.zero_level = -1;
   P.potrf_list.clear();
+  P.col_tasks.clear();
   P.bwd_tasks.clear();
   P.bwd_pref.clear();
   P.bwd_part_tasks.clear();
@@ -600,82 +600,84 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     }
     int maxw = 0;
     for (int s : big) maxw = std::max(maxw, P.w[s]);
-    std::vector<char> diag_ready(ns, 0);
-    static const double fuse_flops = getenv("PGO_FUSE_FLOPS") ? atof(getenv("PGO_FUSE_FLOPS")) : 2e9;
+    // Blocked path, one step per 64-column panel kb of every big front of the
+    // level (right-looking, look-ahead 1, Schur updates of depth 64):
+    //   first step  k_panel_first: the front's first diagonal tile factored +
+    //               inverted, the rows below it solved (trsm) by workgroups that
+    //               wait for that inverse (in-launch hand-off)
+    //   each step   k_step: the next panel's diagonal tile updated with panel kb,
+    //               factored and inverted (sdiag); the tiles below it in the
+    //               next panel's column block updated, then solved against that
+    //               inverse (col); the other trailing tiles updated (syrk:
+    //               inline, or a concurrent k_panel_syrk_lds / 128 launch)
     for (int kb = 0; kb < maxw; kb += kNB) {
       PanelStep ps;
       ps.kb = kb;
-      ps.syrk_flops = 0;
-      ps.trsm_off = (int)P.trsm_tasks.size();
+      ps.syrk_flops = ps.plain_flops = ps.step_flops = ps.first_flops = 0;
+      ps.col_off = (int)P.col_tasks.size();
       ps.syrk_off = (int)P.syrk_tasks.size();
       ps.potrf_off = (int)P.potrf_list.size();
       ps.sdiag_off = (int)P.sdiag_tasks.size();
-      struct Upd {
-        int s, c0, c1, k0;   // columns [c0, c1) of front s, rows c0..m, depth from k0 (bit 31: inner)
-        int next;            // next panel's first column (its diagonal tile is in this update), or -1
-      };
-      std::vector<Upd> upd;
+      // first panel of a front: k_panel_first (diagonal + trsm waiters)
+      for (int s : big) {
+        if (kb != 0 || P.w[s] <= 0) continue;
+        P.potrf_list.push_back(s);
+        const int nb = std::min(kNB, P.w[s]), m = P.m[s];
+        ps.first_flops += 2.0 * nb * nb * (double)nb / 3.0 + (double)std::max(0, m - nb) * nb * nb;
+      }
+      ps.potrf_cnt = (int)P.potrf_list.size() - ps.potrf_off;
+      for (int s : big)
+        if (kb == 0 && P.w[s] > 0)
+          for (int r0 = kNB; r0 < P.m[s]; r0 += kNB) P.col_tasks.push_back(make_int4(s, r0, 0, -1));
+      ps.fcol_cnt = (int)P.col_tasks.size() - ps.col_off;
+      // this panel's Schur update (depth nb) of columns [kn, m), kn = kb + nb
+      std::vector<int4> plain;
       for (int s : big) {
         if (P.w[s] <= kb) continue;
-        if (!diag_ready[s]) P.potrf_list.push_back(s);
-        diag_ready[s] = 0;
-        const int nb = std::min(kNB, P.w[s] - kb);
-        const int below_rows = P.m[s] - kb - nb;
-        const int chunks = (below_rows + 63) / 64;
-        for (int c = 0; c < chunks; c++) P.trsm_tasks.push_back(make_int2(s, c));
-        // Schur updates, blocked by kKB columns: within a block only the block's
-        // remaining columns are updated per 64-column panel ("inner"); after the
-        // block's last panel the trailing matrix gets one update of depth <= kKB
-        const int bs = kb & ~(kKB - 1), be = std::min(bs + kKB, P.w[s]);
-        const int m = P.m[s];
-        if (kb + nb < be) {
-          for (int cc = kb + nb; cc < be; cc++) ps.syrk_flops += 2.0 * nb * (m - cc);
-          upd.push_back({s, kb + nb, be, kb | (int)0x80000000, kb + nb < P.w[s] ? kb + nb : -1});
-        } else if (be < m) {
-          const double K = kb + nb - bs, t = m - be;
-          ps.syrk_flops += K * t * (t + 1.0);
-          upd.push_back({s, be, m, bs, kb + nb < P.w[s] ? kb + nb : -1});
+        const int nb = std::min(kNB, P.w[s] - kb), kn = kb + nb, m = P.m[s];
+        for (int cc = kn; cc < m; cc++) ps.syrk_flops += 2.0 * nb * (m - cc);
+        int cstart = kn;
+        if (kn < P.w[s]) {   // next panel: its diagonal tile and the tiles below it
+          const int nb2 = std::min(kNB, P.w[s] - kn);
+          P.sdiag_tasks.push_back(make_int4(s, kn, kn, kb));
+          ps.step_flops += (double)nb * kNB * (kNB + 1) + 2.0 * nb2 * nb2 * (double)nb2 / 3.0 +
+                           (double)std::min(kNB - nb2, m - kn - nb2) * nb2 * nb2;
+          for (int r0 = kn + kNB; r0 < m; r0 += kNB) {
+            P.col_tasks.push_back(make_int4(s, r0, kn, kb));
+            const int rows = std::min(kNB, m - r0);
+            ps.step_flops += 2.0 * nb * rows * kNB + (double)rows * nb2 * nb2;
+          }
+          cstart = kn + kNB;
         }
+        for (int cc = cstart; cc < m; cc++) ps.plain_flops += 2.0 * nb * (m - cc);
+        plain.push_back(make_int4(s, cstart, m, kb));
       }
-      // output tiles: 128x128 (LDS-pipelined kernel) only when there are many
-      // rounds of them (measured: at <= ~500 tiles the 64x64 kernel's finer
-      // granularity wins, scripts/ubench_syrk.hip), else 64x64
+      ps.sdiag_cnt = (int)P.sdiag_tasks.size() - ps.sdiag_off;
+      ps.col_cnt = (int)P.col_tasks.size() - ps.col_off - ps.fcol_cnt;
+      // plain tiles: 128x128 (LDS-pipelined kernel) when there are many rounds of
+      // them (measured: at <= ~500 tiles the 64x64 kernel's finer granularity
+      // wins, scripts/ubench_syrk.hip), else 64x64
       auto ntiles = [&](int T) {
         long long cnt = 0;
-        for (const Upd& u : upd)
-          for (int c0 = u.c0; c0 < u.c1; c0 += T) cnt += (P.m[u.s] - c0 + T - 1) / T;
+        for (const int4& u : plain)
+          for (int c0 = u.y; c0 < u.z; c0 += T) cnt += (u.z - c0 + T - 1) / T;
         return cnt;
       };
       ps.syrk_tile = ntiles(kBigTile) >= 4096 ? kBigTile : kTile;
-      // with 64-tiles, the tile holding the next panel's diagonal block goes to
-      // k_syrk_diag (look-ahead factorisation on the side stream)
-      for (const Upd& u : upd)
-        for (int c0 = u.c0; c0 < u.c1; c0 += ps.syrk_tile)
-          for (int r0 = c0; r0 < P.m[u.s]; r0 += ps.syrk_tile) {
-            if (ps.syrk_tile == kTile && r0 == c0 && c0 == u.next) {
-              P.sdiag_tasks.push_back(make_int4(u.s, r0, c0, u.k0));
-              diag_ready[u.s] = 1;
-              // its flops leave the k_panel_syrk launch (profiled roofline)
-              const int m = P.m[u.s], depth = std::min(kb + kNB, P.w[u.s]) - (u.k0 & 0x7fffffff);
-              for (int cc = c0; cc < std::min({c0 + kTile, u.c1, m}); cc++)
-                ps.syrk_flops -= 2.0 * depth * (std::min(r0 + kTile, m) - cc);
-            } else {
-              P.syrk_tasks.push_back(make_int4(u.s, r0, c0, u.k0));
-            }
-          }
+      for (const int4& u : plain)
+        for (int c0 = u.y; c0 < u.z; c0 += ps.syrk_tile)
+          for (int r0 = c0; r0 < u.z; r0 += ps.syrk_tile) P.syrk_tasks.push_back(make_int4(u.x, r0, c0, u.w));
       {   // XCD-aware order of this step's Schur-update tiles
         std::vector<int4> mine(P.syrk_tasks.begin() + ps.syrk_off, P.syrk_tasks.end());
         xcd_order(mine, ps.syrk_tile);
         std::copy(mine.begin(), mine.end(), P.syrk_tasks.begin() + ps.syrk_off);
       }
-      ps.sdiag_cnt = (int)P.sdiag_tasks.size() - ps.sdiag_off;
-      ps.potrf_cnt = (int)P.potrf_list.size() - ps.potrf_off;
-      ps.trsm_cnt = (int)P.trsm_tasks.size() - ps.trsm_off;
       ps.syrk_cnt = (int)P.syrk_tasks.size() - ps.syrk_off;
-      // a small update runs in the look-ahead's launch (no second-stream
-      // hand-off); the profiled Schur-update flops count the separate launches only
-      ps.fused = ps.sdiag_cnt > 0 && ps.syrk_flops <= fuse_flops;
-      if (!ps.fused) P.syrk_flops += ps.syrk_flops;
+      // few 64-tiles ride in k_step; many go to a concurrent launch (k_step's
+      // LDS request, sized for the diagonal workgroups, halves their occupancy)
+      ps.syrk_inline = ps.syrk_tile == kTile && ps.syrk_cnt <= kInlineTiles;
+      if (ps.syrk_inline) ps.step_flops += ps.plain_flops;
+      P.syrk_flops += ps.plain_flops;
       lv.panels.push_back(ps);
     }
   }

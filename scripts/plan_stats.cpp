@@ -68,12 +68,12 @@ int main(int argc, char** argv) {
     }
     int nfused = 0, ntr = 0, nsy = 0, npotrf = 0;
     for (const auto& ps : lv.panels) {
-      nfused += ps.fused;
-      ntr += ps.trsm_cnt;
+      nfused += ps.syrk_inline;
+      ntr += ps.fcol_cnt + ps.col_cnt;
       nsy += ps.syrk_cnt;
       npotrf += ps.potrf_cnt;
     }
-    printf("level %2d: fronts %6d (small %6d) maxm %5d tiles %6d ea %6.1fM dbl, steps %3zu (fused %3d) potrf %5d trsm %6d syrk %7d\n",
+    printf("level %2d: fronts %6d (small %6d) maxm %5d tiles %6d ea %6.1fM dbl, steps %3zu (inline %3d) potrf %5d trsm %6d syrk %7d\n",
            li++, lv.front_cnt, nsmall, lv.maxm, lv.ea_cnt[0], ea / 1e6, lv.panels.size(), nfused, npotrf, ntr, nsy);
   }
   return 0;
