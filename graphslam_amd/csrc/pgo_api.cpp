@@ -79,13 +79,13 @@ struct pgo_graph {
   long long fam_launches[pgo::kFamCount] = {};
   std::vector<double> trace;                // per lambda try / GN step of the last optimize (kTraceCols each)
   long long factorizations = 0;
-  hipGraphExec_t chol_exec = nullptr;       // captured factor + solve (static per structure)
+  hipGraphExec_t fac_exec[9] = {};          // captured factorisation, per lane count (1: d.x path)
+  hipGraphExec_t sol_exec[9] = {};          // captured triangular solves, per lane count
   double* h_lam = nullptr;                  // pinned lambda staging
   // ---- multi-GPU speculative lambda search (pgo_comm_*) ----
   pgo::Comm comm;
   std::vector<Lane> lanes;                  // lanes 1..L-1 (speculative tries on this GPU)
   double* xb = nullptr;                     // [L x 3n] solutions of a batched factor + solve
-  hipGraphExec_t lane_exec[9] = {};         // captured batched factor + solve, per lane count
   double* h_lanes = nullptr;                // pinned [48]: 4 scalars per lane, lambdas at 32, flags at 40
   hipEvent_t lin_done = nullptr;            // linearisation complete
   int lane_cap = 8;                         // 1 after a lane allocation failed (reset per plan)
@@ -156,6 +156,15 @@ int information(const double* q, double* om6) {
   return PGO_OK;
 }
 
+// every captured factor / solve graph (they hold the plan's workspace pointers)
+void drop_graphs(pgo_graph* g) {
+  for (int l = 0; l < 9; l++)
+    for (hipGraphExec_t* e : {&g->fac_exec[l], &g->sol_exec[l]}) {
+      if (*e) (void)hipGraphExecDestroy(*e);
+      *e = nullptr;
+    }
+}
+
 void free_lanes(pgo_graph* g) {
   if (g->d.stream) (void)hipStreamSynchronize(g->d.stream);
   for (Lane& ln : g->lanes) {
@@ -166,10 +175,11 @@ void free_lanes(pgo_graph* g) {
   g->lanes.clear();
   if (g->xb) (void)hipFree(g->xb);
   g->xb = nullptr;
-  for (auto& e : g->lane_exec) {
-    if (e) (void)hipGraphExecDestroy(e);
-    e = nullptr;
-  }
+  for (int l = 2; l < 9; l++)   // the batched graphs hold xb
+    for (hipGraphExec_t* e : {&g->fac_exec[l], &g->sol_exec[l]}) {
+      if (*e) (void)hipGraphExecDestroy(*e);
+      *e = nullptr;
+    }
 }
 
 void free_device(pgo_graph* g) {
@@ -185,8 +195,7 @@ void free_device(pgo_graph* g) {
   d.stream = s;
   g->dev_structure = false;
   g->dev_values = false;
-  if (g->chol_exec) (void)hipGraphExecDestroy(g->chol_exec);
-  g->chol_exec = nullptr;
+  drop_graphs(g);
   if (g->chol_ready) pgo::chol_free(g->chol);
   g->chol_ready = false;
 }
@@ -635,8 +644,34 @@ int pcg_solve(pgo_graph* g, const pgo_params& p, double lam, PcgResult* out, pgo
 struct SolveState {
   bool known = true, solved = true;
   bool profiled = false;
+  bool graph = false;                       // factor / solve replayed from graphs (ev[5] between them)
   pgo::LaunchProfile prof;
 };
+
+// Replay of the captured factorisation and solve graphs for nb lanes (captured
+// on first use; one graph launch each instead of ~1e3 kernel launches), with
+// ev[5] recorded between them: the factorisation's device time is ev[2]..ev[5].
+int graph_factor_solve(pgo_graph* g, int nb, double* x, long long xstride) {
+  DevGraph& d = g->d;
+  auto capture = [&](hipGraphExec_t* exec, bool factor) -> int {
+    if (*exec) return PGO_OK;
+    hipGraph_t graph = nullptr;
+    HIP_TRY(g, hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal));
+    const hipError_t e1 = factor ? pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr, nb)
+                                 : pgo::chol_solve(g->chol, x, d.stream, nb, xstride);
+    HIP_TRY(g, hipStreamEndCapture(d.stream, &graph));
+    HIP_TRY(g, e1);
+    HIP_TRY(g, hipGraphInstantiate(exec, graph, nullptr, nullptr, 0));
+    HIP_TRY(g, hipGraphDestroy(graph));
+    return PGO_OK;
+  };
+  RC_TRY(capture(&g->fac_exec[nb], true));
+  RC_TRY(capture(&g->sol_exec[nb], false));
+  HIP_TRY(g, hipGraphLaunch(g->fac_exec[nb], d.stream));
+  HIP_TRY(g, hipEventRecord(g->ev[5], d.stream));
+  HIP_TRY(g, hipGraphLaunch(g->sol_exec[nb], d.stream));
+  return PGO_OK;
+}
 
 int linear_solve(pgo_graph* g, const pgo_params& p, double lam, pgo_stats* st, SolveState* ss) {
   if (p.linear_solver == PGO_SOLVER_PCG) {
@@ -672,18 +707,8 @@ int linear_solve(pgo_graph* g, const pgo_params& p, double lam, pgo_stats* st, S
     HIP_TRY(g, pgo::chol_solve(g->chol, d.x, d.stream, 1, 0, prof));
     if (prof) HIP_TRY(g, hipEventRecord(g->fev[2], d.stream));
   } else {
-    if (!g->chol_exec) {  // capture once per structure: ~1e3 launches -> one graph launch
-      hipGraph_t graph = nullptr;
-      HIP_TRY(g, hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal));
-      const hipError_t e1 = pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr);
-      const hipError_t e2 = pgo::chol_solve(g->chol, d.x, d.stream);
-      HIP_TRY(g, hipStreamEndCapture(d.stream, &graph));
-      HIP_TRY(g, e1);
-      HIP_TRY(g, e2);
-      HIP_TRY(g, hipGraphInstantiate(&g->chol_exec, graph, nullptr, nullptr, 0));
-      HIP_TRY(g, hipGraphDestroy(graph));
-    }
-    HIP_TRY(g, hipGraphLaunch(g->chol_exec, d.stream));
+    RC_TRY(graph_factor_solve(g, 1, d.x, 0));
+    ss->graph = true;
   }
   ss->known = false;
   return PGO_OK;
@@ -692,6 +717,10 @@ int linear_solve(pgo_graph* g, const pgo_params& p, double lam, pgo_stats* st, S
 // after the stream has drained: pivot flag and profile of an enqueued Cholesky solve
 int finish_solve(pgo_graph* g, pgo_stats* st, SolveState* ss) {
   if (ss->known) return PGO_OK;
+  if (ss->graph && st) {
+    st->ms_factor_graph += ms_between(g->ev[2], g->ev[5]);
+    st->factor_graph_flops += g->chol.flops;
+  }
   int flag = 0;
   HIP_TRY(g, hipMemcpy(&flag, g->chol.d_flag, sizeof(int), hipMemcpyDeviceToHost));
   if (flag & 2) return fail(g, PGO_E_HIP, "factorisation: an in-launch hand-off timed out");
@@ -713,6 +742,20 @@ int finish_solve(pgo_graph* g, pgo_stats* st, SolveState* ss) {
     }
     st->kernel_syrk_count++;
     st->syrk_flops = g->chol.syrk_flops;
+    if (getenv("PGO_STEP_STAMPS") && getenv("PGO_PROFILE_DUMP")) {   // top level's k_step stamps
+      std::vector<unsigned long long> stp(10 * pgo::kMaxStampSlots);
+      if (pgo::chol_step_stamps(stp.data(), pgo::kMaxStampSlots) == hipSuccess)
+        if (FILE* f = fopen(getenv("PGO_PROFILE_DUMP"), "a")) {
+          for (int q = 0; q < pgo::kMaxStampSlots; q++) {
+            const unsigned long long* t = &stp[10 * q];
+            if (!t[0] || !t[5]) continue;
+            fprintf(f, "# stamp step %d:", q);
+            for (int k = 1; k < 9; k++) fprintf(f, " %.2f", (double)((long long)(t[k] - t[0])) * 0.01);
+            fprintf(f, "\n");
+          }
+          fclose(f);
+        }
+    }
     // PGO_PROFILE_DUMP=path: append the launch timeline of this factorisation
     // (family, level, panel step, workgroups, start and duration in ms from the
     // factorisation's first event, algorithmic flops, bytes)
@@ -742,9 +785,8 @@ int ensure_lanes(pgo_graph* g, int want) {
   free_lanes(g);
   const DevGraph& d = g->d;
   if (g->chol.batch != want) {
-    // the captured one-lane graph holds the old workspace pointers
-    if (g->chol_exec) (void)hipGraphExecDestroy(g->chol_exec);
-    g->chol_exec = nullptr;
+    // the captured graphs hold the old workspace pointers
+    drop_graphs(g);
     if (pgo::chol_set_batch(g->chol, want, d.stream) != hipSuccess) {
       (void)hipGetLastError();
       g->lane_cap = 1;
@@ -764,8 +806,7 @@ int ensure_lanes(pgo_graph* g, int want) {
   if (!ok) {  // out of memory (or similar): one lane, and do not try again for this plan
     (void)hipGetLastError();
     free_lanes(g);
-    if (g->chol_exec) (void)hipGraphExecDestroy(g->chol_exec);
-    g->chol_exec = nullptr;
+    drop_graphs(g);
     (void)pgo::chol_set_batch(g->chol, 1, d.stream);
     g->lane_cap = 1;
     return 1;
@@ -800,18 +841,7 @@ int run_lanes(pgo_graph* g, const pgo_params& p, int nb, const double* lams, dou
     HIP_TRY(g, pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr, nb));
     HIP_TRY(g, pgo::chol_solve(g->chol, g->xb, d.stream, nb, 3LL * d.n));
   } else {
-    if (!g->lane_exec[nb]) {
-      hipGraph_t graph = nullptr;
-      HIP_TRY(g, hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal));
-      const hipError_t e1 = pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr, nb);
-      const hipError_t e2 = pgo::chol_solve(g->chol, g->xb, d.stream, nb, 3LL * d.n);
-      HIP_TRY(g, hipStreamEndCapture(d.stream, &graph));
-      HIP_TRY(g, e1);
-      HIP_TRY(g, e2);
-      HIP_TRY(g, hipGraphInstantiate(&g->lane_exec[nb], graph, nullptr, nullptr, 0));
-      HIP_TRY(g, hipGraphDestroy(graph));
-    }
-    HIP_TRY(g, hipGraphLaunch(g->lane_exec[nb], d.stream));
+    RC_TRY(graph_factor_solve(g, nb, g->xb, 3LL * d.n));
   }
   HIP_TRY(g, hipEventRecord(ev[3], d.stream));
   for (int l = 0; l < nb; l++) {
@@ -839,6 +869,10 @@ int run_lanes(pgo_graph* g, const pgo_params& p, int nb, const double* lams, dou
     st->ms_solve += ms_between(ev[2], ev[3]);
     st->ms_update += ms_between(ev[3], ev[4]);
     st->factor_flops = g->chol.flops;
+    if (p.use_graphs) {
+      st->ms_factor_graph += ms_between(ev[2], ev[5]);
+      st->factor_graph_flops += nb * g->chol.flops;
+    }
   }
   return PGO_OK;
 }

@@ -26,9 +26,9 @@ constexpr int kWaveW = 32;         // ... and w <= this: by one wavefront (panel
 constexpr int kNB = 64;            // panel width of the blocked path
 constexpr int kTile = 64;          // Schur-update output tile
 constexpr int kBigTile = 128;      // Schur-update output tile of the LDS-pipelined kernel
-constexpr int kKB = 64;          // Schur-update depth (one panel; kept for the tile kernels' clipping)
-constexpr int kInlineTiles = 512; // syrk tiles per step that ride inside k_step
-constexpr int kZeroBackgroundGrid = 32;   // workgroups of the background (late) zeroing
+constexpr int kKB = 256;         // Schur updates deferred per kKB-column block (inner steps update the block only)
+constexpr int kInlineTiles = 512;
+constexpr int kMaxStampSlots = 256;  // PGO_STEP_STAMPS diagnostics // syrk tiles per step that ride inside k_step
 constexpr int kBwdRows = 512;      // rows per partial product of the backward solve           // Schur-update depth: trailing matrix updated once per kKB columns
 
 struct PanelStep {                 // one 64-column panel kb of every big front of a level
@@ -54,6 +54,7 @@ struct SolveStep {                 // one launch of the blocked triangular solve
 struct SmallClass {                // small fronts of one level with m <= mmax
   int off, cnt, mmax;
   int wave;                        // 1: w <= kWaveW, one wavefront per front (k_front_wave)
+  double flops = 0;                // algorithmic flops (factor + diagonal-block inverses)
 };
 
 struct CholLevel {
@@ -65,6 +66,8 @@ struct CholLevel {
   int maxblk = 0;                  // max 64-column blocks of a front's pivot columns
   std::vector<SolveStep> bwd;      // backward: [0] = init (all columns), then steps b = maxblk-1 .. 1
   SolveStep bwd_part{0, 0};        // partial products feeding the init tasks
+  double at_bytes = 0;             // algorithmic HBM bytes of the level's k_assemble_tile
+  double bwd_part_flops = 0;       // ... flops of its k_bwd_part
 };
 
 enum { kOrderNd = 0, kOrderAmd = 1 };
@@ -89,28 +92,18 @@ struct CholPlan {
   // assembly of H: target blocks (front, local row pose, local col pose) and their slots
   std::vector<int> asm_front, asm_li, asm_lj, asm_ptr, asm_src;
   std::vector<int> dg_front, dg_loc;   // per new pose: front and local index (diagonal block)
-  std::vector<int> dg_order;       // new poses, those of leaf-level fronts first
-  int asm_split = 0, dg_split = 0, zero_split = 0;   // leaf-level prefixes of asm targets, dg_order, zero_tasks
   // schedules
   std::vector<CholLevel> levels;
   std::vector<int> small_list, level_fronts, potrf_list;
   std::vector<int4> syrk_tasks, sdiag_tasks, col_tasks;
-  // Fronts must be zero (lower triangles) before a factorisation assembles into
-  // them.  zero_tasks (front, first column, end column), pieces of ~32k doubles:
-  // [0, zero_split) leaf-level fronts and [zero_split, zero_late) the rest, zeroed
-  // at the start of every factorisation; [zero_late, end) the update matrices
-  // of the fronts whose parents are at levels <= zero_level, zeroed by the
-  // factorisation itself on a side stream once the extend-add of zero_level has
-  // consumed them (beside the latency-bound top levels, when HBM is idle), so
-  // they are zero again when the next factorisation starts.
-  std::vector<int4> zero_tasks;
-  int zero_late = 0, zero_level = -1;
   std::vector<int4> bwd_tasks;
   std::vector<int2> bwd_pref;      // per bwd task: first partial, partial count (init tasks)
   std::vector<int4> bwd_part_tasks;  // (front, c0, r0, partial slot)
   int npart = 0;
-  std::vector<int4> ea_tasks;      // (parent, tile row << 16 | tile col, first pair, pairs): 64x64
-                                   // tiles of parent fronts receiving update-matrix elements, per level
+  std::vector<int4> ea_tasks;      // (front, tile row << 16 | tile col, first pair, pairs): every 64x64
+                                   // lower tile of every front, per level (k_assemble_tile)
+  std::vector<int2> at_iptr;       // per tile task: (first, count) of its H entries in at_items
+  std::vector<int> at_items;       // H entries: asm target t >= 0, or ~pose (diagonal block + lambda)
   std::vector<int4> ea_pairs;      // (child, first row a0, first column b0, rows | columns << 8):
                                    // a child's rectangle of one tile, children in order
   double flops = 0, nnzl = 0, syrk_flops = 0;
@@ -127,13 +120,14 @@ struct CholPlan {
   long long* d_toff = nullptr;
   int *d_cptr = nullptr, *d_children = nullptr, *d_ea_rel = nullptr, *d_ea_ptr = nullptr, *d_parent = nullptr;
   int *d_asm_front = nullptr, *d_asm_li = nullptr, *d_asm_lj = nullptr, *d_asm_ptr = nullptr, *d_asm_src = nullptr;
-  int *d_dg_front = nullptr, *d_dg_loc = nullptr, *d_perm = nullptr, *d_dg_order = nullptr;
+  int *d_dg_front = nullptr, *d_dg_loc = nullptr, *d_perm = nullptr;
   int *d_small = nullptr, *d_level_fronts = nullptr, *d_potrf = nullptr;
-  int4 *d_syrk = nullptr, *d_sdiag = nullptr, *d_zero = nullptr, *d_col = nullptr;
+  int4 *d_syrk = nullptr, *d_sdiag = nullptr, *d_col = nullptr;
+  int2* d_at_iptr = nullptr;
+  int* d_at_items = nullptr;
   int* d_stepflag = nullptr;       // [batch][ns]: last panel (kb / 64 + 1) whose diagonal inverse is published
   hipStream_t side = nullptr;      // look-ahead diagonal tiles
   hipStream_t side2 = nullptr;     // small fronts beside the blocked path
-  hipStream_t side3 = nullptr;     // zeroing + assembly of the non-leaf fronts beside the leaf level
   hipEvent_t evs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int4 *d_bwd = nullptr, *d_bwd_part = nullptr;
   int2* d_bwd_pref = nullptr;
@@ -170,7 +164,7 @@ hipError_t chol_set_batch(CholPlan& P, int nb, hipStream_t s);
 // with its kernel family and algorithmic flops / HBM bytes: pairs of events,
 // capacity cap, *used pairs recorded.
 enum KernelFamily {
-  kFamAssemble = 0, kFamZero, kFamPerm, kFamExtendAdd, kFamVecAssemble, kFamFrontWave, kFamFrontSmall,
+  kFamAssemble = 0, kFamUnused1, kFamPerm, kFamUnused3, kFamVecAssemble, kFamFrontWave, kFamFrontSmall,
   kFamPanelFirst, kFamStep, kFamPanelSyrk, kFamPanelSyrk128,
   kFamBwdPart, kFamBwdInit, kFamBwdStep, kFamCount
 };
@@ -195,6 +189,9 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
                        hipStream_t s, LaunchProfile* prof = nullptr, int nb = 1);
 // after chol_factor: 3x3 blocks of (L L^T)^{-1} at the given poses (old index),
 // row-major 9 doubles each into host memory out (synchronises the stream)
+// diagnostics: the step stamps of the last factorisation run with PGO_STEP_STAMPS
+// set (top level's steps, 10 wall-clock ticks of 10 ns each per step)
+hipError_t chol_step_stamps(unsigned long long* out, int slots);
 hipError_t chol_marginals(const CholPlan& P, const int* poses, int n, double* out, hipStream_t s);
 // after chol_factor: x = L^-T y = (L L^T)^{-1} scale_b b, indexed by old pose
 // lane y's solution to x + y * xstride

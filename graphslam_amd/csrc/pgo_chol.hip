@@ -2,9 +2,10 @@
 // solves (gfx950).  Host plan: pgo_symbolic.cpp; layout: pgo_chol.h.
 //
 // Factorisation, per level of the supernodal tree (leaves first):
-//   k_extend_add   children's update matrices -> parent fronts, one launch per
-//                  level, one workgroup per parent tile walking the children in
-//                  order (no atomics, fixed order, bitwise reproducible)
+//   k_assemble_tile every front of the level, one workgroup per 64x64 lower
+//                  tile, written whole: H entries (+ lambda), then the
+//                  children's update matrices in order (no atomics, fixed
+//                  order, bitwise reproducible; no front is ever zeroed)
 //   k_front_wave   fronts with m <= 128, w <= 32: one wavefront each
 //   k_panel_first  blocked path, first 64-column panel: diagonal tile factored
 //                  and inverted in LDS, the rows below solved as MFMA GEMMs with
@@ -34,7 +35,7 @@ struct CholDev {
   const long long* foff;
   const int *cptr, *children, *ea_rel, *ea_ptr, *parent;
   const int *asm_front, *asm_li, *asm_lj, *asm_ptr, *asm_src;
-  const int *dg_front, *dg_loc, *perm, *dg_order;
+  const int *dg_front, *dg_loc, *perm;
   int* flag;
   int* stepflag;                   // [lane][ns] in-launch hand-off of the diagonal inverses
   int ns;
@@ -64,7 +65,6 @@ static CholDev dev_view(const CholPlan& P) {
   c.parent = P.d_parent;
   c.asm_front = P.d_asm_front; c.asm_li = P.d_asm_li; c.asm_lj = P.d_asm_lj; c.asm_ptr = P.d_asm_ptr;
   c.asm_src = P.d_asm_src; c.dg_front = P.d_dg_front; c.dg_loc = P.d_dg_loc; c.perm = P.d_perm;
-  c.dg_order = P.d_dg_order;
   c.flag = P.d_flag;
   c.stepflag = P.d_stepflag;
   c.ns = P.ns;
@@ -79,6 +79,16 @@ static CholDev dev_view(const CholPlan& P) {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+// Step timing stamps (diagnostics, PGO_STEP_STAMPS): k_step launches given a
+// slot >= 0 record wall-clock stamps of their first diagonal workgroup and first
+// waiting workgroup; read back with chol_step_stamps.  Written only here and
+// read only by the host.
+__device__ unsigned long long g_stamps[kMaxStampSlots][10];
+#define STAMP(slot, q)                                                        \
+  do {                                                                        \
+    if ((slot) >= 0 && threadIdx.x == 0) g_stamps[(slot)][(q)] = wall_clock64(); \
+  } while (0)
+
 #ifdef PGO_DIAG_CLOCKS
 __device__ long long g_diag_clk[32];
 #define DIAG_CLK(q) if (threadIdx.x == 0 && blockIdx.x == 0) g_diag_clk[q] = clock64()
@@ -88,99 +98,96 @@ __device__ long long g_diag_clk[32];
 
 
 // ------------------------------------------------------------ assembly
-// off-diagonal lower blocks H_{i,j} (i > j) of a front: sum of their slots
-__global__ __launch_bounds__(256) void k_asm_offdiag(CholDev c, const double* __restrict__ V, long long S,
-                                                     int t0, int t1) {
+// One 64x64 lower tile (ti, tj) of a front per workgroup, written whole (so no
+// front is ever zeroed): in LDS, the tile's H entries -- off-diagonal blocks
+// H_{i,j} (i > j) summed over their slots (V, structure of arrays), diagonal
+// blocks H_jj + lambda I (lower part) -- then the front's children's
+// update-matrix elements in child order (fixed summation order, bitwise
+// reproducible, no atomics), then the lower part of the tile to the front.
+// Lane r <-> child row a0 + r (column-major: a column's loads are coalesced),
+// the 4 waves take every 4th column; loads first.
+__global__ __launch_bounds__(256) void k_assemble_tile(CholDev c, const int4* __restrict__ tasks,
+                                                       const int2* __restrict__ iptr, const int* __restrict__ items,
+                                                       const int4* __restrict__ pairs, const double* __restrict__ V,
+                                                       long long S, const double* __restrict__ D,
+                                                       const double* __restrict__ lam_p) {
   lane_offset(c);
-  const int t = t0 + blockIdx.x * 256 + threadIdx.x;
-  if (t >= t1) return;
-  const int s = c.asm_front[t];
-  const int m = c.m[s];
-  double* Fs = c.F + c.foff[s];
-  double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (int q = c.asm_ptr[t]; q < c.asm_ptr[t + 1]; q++) {
-    const double* v = V + c.asm_src[q];   // structure of arrays: element e at v[e * S]
-#pragma unroll
-    for (int e = 0; e < 9; e++) acc[e] += v[e * S];
-  }
-  const int r0 = 3 * c.asm_li[t], c0 = 3 * c.asm_lj[t];
-#pragma unroll
-  for (int a = 0; a < 3; a++)
-#pragma unroll
-    for (int b = 0; b < 3; b++) Fs[(r0 + a) + (size_t)(c0 + b) * m] = acc[3 * a + b];
-}
-
-// diagonal blocks H_jj + lambda I (lower part)
-__global__ __launch_bounds__(256) void k_asm_diag(CholDev c, const double* __restrict__ D,
-                                                 const double* __restrict__ lam_p, int t0, int t1) {
-  lane_offset(c);
-  lam_p += blockIdx.y;
-  const int t = t0 + blockIdx.x * 256 + threadIdx.x;
-  if (t >= t1) return;
-  const int j = c.dg_order[t];
-  const double lam = *lam_p;
-  const int s = c.dg_front[j];
-  const int m = c.m[s];
-  double* Fs = c.F + c.foff[s];
-  const double* d = D + 6 * (size_t)c.perm[j];
-  const int o = 3 * c.dg_loc[j];
-  Fs[(o + 0) + (size_t)(o + 0) * m] = d[0] + lam;
-  Fs[(o + 1) + (size_t)(o + 0) * m] = d[1];
-  Fs[(o + 2) + (size_t)(o + 0) * m] = d[2];
-  Fs[(o + 1) + (size_t)(o + 1) * m] = d[3] + lam;
-  Fs[(o + 2) + (size_t)(o + 1) * m] = d[4];
-  Fs[(o + 2) + (size_t)(o + 2) * m] = d[5] + lam;
-}
-
-// ------------------------------------------------------------ extend-add
-// One 64x64 tile of a parent front's lower triangle per workgroup: the
-// parent's children in order (fixed summation order, bitwise reproducible, no
-// atomics, one launch per level), each adding its rectangle of update-matrix
-// elements (rows [a0, a0+nr), columns [b0, b0+nc), element (a, b) only for
-// b <= a).  Lane r <-> child row a0 + r (column-major: loads of a column are
-// coalesced), the 4 waves take every 4th column; loads first.
-__global__ __launch_bounds__(256) void k_extend_add(CholDev c, const int4* __restrict__ tasks,
-                                                    const int4* __restrict__ pairs) {
-  lane_offset(c);
-  __shared__ int prow[64];
-  __shared__ long long pcol[64];
+  __shared__ double T[64 * 65];
+  __shared__ int prow[64], pcol[64];
   const int4 t = tasks[blockIdx.x];
   const int p = t.x, mp = c.m[p];
-  double* __restrict__ Fp = c.F + c.foff[p];
+  const int R0 = 64 * (t.y >> 16), C0 = 64 * (t.y & 0xffff);
   const int tid = threadIdx.x, r = tid & 63, cg = tid >> 6;
+  const double lam = lam_p[blockIdx.y];
+#pragma unroll
+  for (int u = 0; u < 16; u++) T[(tid & 63) + ((tid >> 6) + 4 * u) * 65] = 0.0;
+  __syncthreads();
+  const int2 it = iptr[blockIdx.x];
+  for (int q = tid; q < it.y; q += 256) {
+    const int code = items[it.x + q];
+    if (code >= 0) {
+      double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      for (int k = c.asm_ptr[code]; k < c.asm_ptr[code + 1]; k++) {
+        const double* v = V + c.asm_src[k];   // element e at v[e * S]
+#pragma unroll
+        for (int e = 0; e < 9; e++) acc[e] += v[e * S];
+      }
+      const int i0 = 3 * c.asm_li[code] - R0, j0 = 3 * c.asm_lj[code] - C0;
+#pragma unroll
+      for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b = 0; b < 3; b++)
+          if (i0 + a >= 0 && i0 + a < 64 && j0 + b >= 0 && j0 + b < 64) T[(i0 + a) + (j0 + b) * 65] = acc[3 * a + b];
+    } else {
+      const int j = ~code;
+      const double* d = D + 6 * (size_t)c.perm[j];
+      const int o = 3 * c.dg_loc[j];
+      const double dv[6] = {d[0] + lam, d[1], d[2], d[3] + lam, d[4], d[5] + lam};   // (0,0) (1,0) (2,0) (1,1) (2,1) (2,2)
+      const int ia[6] = {0, 1, 2, 1, 2, 2}, ib[6] = {0, 0, 0, 1, 1, 2};
+#pragma unroll
+      for (int e = 0; e < 6; e++) {
+        const int i = o + ia[e] - R0, jj = o + ib[e] - C0;
+        if (i >= 0 && i < 64 && jj >= 0 && jj < 64) T[i + jj * 65] = dv[e];
+      }
+    }
+  }
   for (int k = 0; k < t.w; k++) {
     const int4 q = pairs[t.z + k];
     const int ch = q.x, a0 = q.y, b0 = q.z, nr = q.w & 0xff, nc = q.w >> 8;
     const int mc = c.m[ch], wc = c.w[ch];
     const int* __restrict__ rel = c.ea_rel + c.ea_ptr[ch];
-    if (k > 0) __syncthreads();   // the previous child's adds are done, prow / pcol reusable
+    __syncthreads();   // the H entries / the previous child's adds are done, prow / pcol reusable
     if (tid < nr) {
       const int a = a0 + tid;
-      prow[tid] = 3 * rel[a / 3] + a % 3;
+      prow[tid] = 3 * rel[a / 3] + a % 3 - R0;
     } else if (tid >= 64 && tid - 64 < nc) {
       const int b = b0 + tid - 64;
-      pcol[tid - 64] = (long long)(3 * rel[b / 3] + b % 3) * mp;
+      pcol[tid - 64] = (3 * rel[b / 3] + b % 3 - C0) * 65;
     }
     __syncthreads();
     if (r >= nr) continue;
     const int a = a0 + r;
     const double* __restrict__ U = c.F + c.foff[ch] + wc + (size_t)wc * mc + a;
     constexpr int R = 16;
-    double v[R], f[R];
-    long long dst[R];
-    bool ok[R];
+    double v[R];
 #pragma unroll
     for (int j = 0; j < R; j++) {
       const int bb = cg + 4 * j;
-      ok[j] = bb < nc && b0 + bb <= a;
-      dst[j] = ok[j] ? prow[r] + pcol[bb] : 0;
-      v[j] = ok[j] ? U[(size_t)(b0 + bb) * mc] : 0.0;
+      v[j] = (bb < nc && b0 + bb <= a) ? U[(size_t)(b0 + bb) * mc] : 0.0;
     }
+    const int pr = prow[r];
 #pragma unroll
-    for (int j = 0; j < R; j++) f[j] = ok[j] ? Fp[dst[j]] : 0.0;
+    for (int j = 0; j < R; j++) {
+      const int bb = cg + 4 * j;
+      if (bb < nc && b0 + bb <= a) T[pr + pcol[bb]] += v[j];
+    }
+  }
+  __syncthreads();
+  double* __restrict__ Fp = c.F + c.foff[p];
 #pragma unroll
-    for (int j = 0; j < R; j++)
-      if (ok[j]) Fp[dst[j]] = f[j] + v[j];
+  for (int u = 0; u < 16; u++) {
+    const int i = tid & 63, j = (tid >> 6) + 4 * u, row = R0 + i, col = C0 + j;
+    if (row < mp && col < mp && row >= col) Fp[row + (size_t)col * mp] = T[i + j * 65];
   }
 }
 
@@ -654,20 +661,28 @@ __device__ __forceinline__ void panel_rhs(double* v, const double* X, int nb, do
   }
 }
 
-// L (LDS Ts, ld 65) back into the front, X = L^-1 (LDS Ws, ld 65) row-major to
-// M and, stored sc1, in the trsm's operand order to Mf: Mf[(4 ks + ct) * 64 + l] =
-// X[16 ct + (l & 15)][4 ks + (l >> 4)] (each trsm lane loads 64 consecutive-by-lane values)
-__device__ __forceinline__ void store_inverse(double* Fs, int m, double* __restrict__ M, double* __restrict__ Mf,
-                                              const double* Ts, const double* Ws, int nb) {
+// X = L^-1 (LDS Ws, ld 65), stored sc1 in the trsm's operand order to Mf:
+// Mf[(4 ks + ct) * 64 + l] = X[16 ct + (l & 15)][4 ks + (l >> 4)] (what the
+// trsm's lane l needs for k-step ks, column tile ct) -- the hand-off payload
+__device__ __forceinline__ void publish_inverse(double* __restrict__ Mf, const double* Ws, int nb) {
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < 4096; idx += 256) {
+    const int l = idx & 63, ct = (idx >> 6) & 3, ks = idx >> 8;
+    const int fa = 16 * ct + (l & 15), fb = 4 * ks + (l >> 4);
+    st_sc1(Mf + idx, (fa < nb && fb < nb && fa >= fb) ? Ws[fa + fb * 65] : 0.0);
+  }
+}
+
+// After the hand-off: L (LDS Ts, ld 65) back into the front, X row-major to M
+// (the backward solve's copy)
+__device__ __forceinline__ void store_factor(double* Fs, int m, double* __restrict__ M, const double* Ts,
+                                             const double* Ws, int nb) {
   const int tid = threadIdx.x;
   for (int idx = tid; idx < 4096; idx += 256) {
     const int i = idx & 63, j = idx >> 6;
     if (i < nb && j < nb && i >= j) Fs[i + (size_t)j * m] = Ts[i + j * 65];
     const int a = idx >> 6, b = idx & 63;
     M[idx] = (a < nb && b < nb && a >= b) ? Ws[a + b * 65] : 0.0;
-    const int l = idx & 63, ct = (idx >> 6) & 3, ks = idx >> 8;
-    const int fa = 16 * ct + (l & 15), fb = 4 * ks + (l >> 4);
-    st_sc1(Mf + idx, (fa < nb && fb < nb && fa >= fb) ? Ws[fa + fb * 65] : 0.0);
   }
 }
 
@@ -724,30 +739,38 @@ __device__ __forceinline__ void diag_own_rows(double* Fs, int m, int rrem, doubl
 // frontal vector's rows updated with v -= L y.  A(i, k) = A[i * ars + k * acs]
 // (an LDS tile or the front itself).
 __device__ __forceinline__ void trsm_rows(const CholDev& c, int s, int r0, int kn, int nb, const double* A, int ars,
-                                          int acs) {
+                                          int acs, double* xs) {
   const int m = c.m[s];
   const double* Mf = c.Tinv + c.tfo + c.toff[s] + (kn / 64) * 4096;
   double* fv = c.fv + c.voff[s];
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  {   // the inverse once per workgroup into LDS (xs: 4096 doubles), 16 coalesced sc1 loads per thread in flight
+    double t[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) t[u] = ld_sc1(Mf + tid + 256 * u);
+#pragma unroll
+    for (int u = 0; u < 16; u++) xs[tid + 256 * u] = t[u];
+  }
+  __syncthreads();
   const int rw = r0 + wv * 16;
   if (rw >= m) return;                                // (no barriers below)
   double* Fc = c.F + c.foff[s] + (size_t)kn * m;
   const int il = wv * 16 + (l & 15), arow = r0 + il, kl = l >> 4;
-  double a[16], tb[16][4], yc[4];   // A fragments, inverse fragments, y: all loads in flight
+  double a[16], tb[16][4], yc[4];   // A fragments, inverse fragments, y
 #pragma unroll
   for (int ks = 0; ks < 16; ks++) {
     const int k = 4 * ks + kl;
     a[ks] = (arow < m && k < nb) ? A[il * ars + k * acs] : 0.0;
   }
 #pragma unroll
-  for (int ks = 0; ks < 16; ks++)
-#pragma unroll
-    for (int ct = 0; ct < 4; ct++) tb[ks][ct] = ld_sc1(Mf + (4 * ks + ct) * 64 + l);
-#pragma unroll
   for (int ct = 0; ct < 4; ct++) {
     const int col = 16 * ct + (l & 15);
     yc[ct] = col < nb ? ld_sc1(fv + kn + col) : 0.0;
   }
+#pragma unroll
+  for (int ks = 0; ks < 16; ks++)
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++) tb[ks][ct] = xs[(4 * ks + ct) * 64 + l];
   d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0}, acc3 = {0, 0, 0, 0};
 #pragma unroll
   for (int ks = 0; ks < 16; ks++) {
@@ -1036,7 +1059,7 @@ __device__ __forceinline__ void diag_tile_update(const CholDev& c, const int4 t,
 // smem: kDiagSmem = 64*65 + 64*68 + 2*64 doubles.
 constexpr int kDiagSmem = 64 * 65 + 64 * 68 + 2 * 64;
 
-__device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, int kb, double* smem) {
+__device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, int kb, double* smem, int slot = -1) {
   double* Ts = smem;
   double* Ws = smem + 64 * 65;
   double* bc = Ws + 64 * 68;
@@ -1045,8 +1068,10 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
   const int m = c.m[s], w = c.w[s];
   const int nb = min(kNB, w - kn);
   const int tid = threadIdx.x;
+  STAMP(slot, 0);
   diag_tile_update(c, t, kb, Ts, Ws);
   __syncthreads();
+  STAMP(slot, 1);
   double keep[16];
 #pragma unroll
   for (int u = 0; u < 16; u++) {   // same element set as the loop below: no hazard
@@ -1057,16 +1082,20 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
   }
   __syncthreads();
   if (diag_factor_invert(Ts, Ws, bc)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  STAMP(slot, 2);
   double* Fs = c.F + c.foff[s] + kn + (size_t)kn * m;
   double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;   // row-major L^-1 of the tile
   double* v = c.fv + c.voff[s] + kn;
-  store_inverse(Fs, m, M, M + c.tfo, Ts, Ws, nb);
+  publish_inverse(M + c.tfo, Ws, nb);
   panel_rhs(v, Ws, nb, bc, ys);
+  STAMP(slot, 3);
+  publish_step(c.stepflag + s, kn / 64 + 1);
+  STAMP(slot, 4);
+  store_factor(Fs, m, M, Ts, Ws, nb);
   if (nb < kNB) {
     __syncthreads();
     diag_own_rows(Fs, m, m - kn, v, keep, Ts, Ws, ys, nb);
   }
-  publish_step(c.stepflag + s, kn / 64 + 1);
 }
 
 // First panel of a front: its assembled diagonal tile factored and inverted,
@@ -1097,13 +1126,14 @@ __device__ __forceinline__ void first_diag_body(const CholDev& c, int s, double*
   if (diag_factor_invert(Ts, Ws, bc)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   double* M = c.Tinv + c.toff[s];
   double* v = c.fv + c.voff[s];
-  store_inverse(Fs, m, M, M + c.tfo, Ts, Ws, nb);
+  publish_inverse(M + c.tfo, Ws, nb);
   panel_rhs(v, Ws, nb, bc, ys);
+  publish_step(c.stepflag + s, 1);
+  store_factor(Fs, m, M, Ts, Ws, nb);
   if (nb < kNB) {
     __syncthreads();
     diag_own_rows(Fs, m, m, v, keep, Ts, Ws, ys, nb);
   }
-  publish_step(c.stepflag + s, 1);
 }
 
 // First panel of every big front of a level: workgroups [0, np) factor the
@@ -1121,7 +1151,7 @@ __global__ __launch_bounds__(256) void k_panel_first(CholDev c, const int* __res
   const int4 t = col[b - np];
   const int s = t.x, m = c.m[s], nb = min(kNB, c.w[s]);
   wait_step(c, c.stepflag + s, 1);
-  trsm_rows(c, s, t.y, 0, nb, c.F + c.foff[s] + t.y, 1, m);
+  trsm_rows(c, s, t.y, 0, nb, c.F + c.foff[s] + t.y, 1, m, smem);
 }
 
 // One panel step kb of every big front of a level in one launch:
@@ -1135,21 +1165,26 @@ __global__ __launch_bounds__(256) void k_panel_first(CholDev c, const int* __res
 // workgroup waits on a workgroup dispatched before it.
 __global__ __launch_bounds__(256) void k_step(CholDev c, const int4* __restrict__ sdiag, int nsd,
                                               const int4* __restrict__ col, int ncol, const int4* __restrict__ tiles,
-                                              int kb) {
+                                              int kb, int slot) {
   lane_offset(c);
   __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
   const int b = blockIdx.x;
   if (b < nsd) {
-    syrk_diag_body(c, sdiag[b], kb, smem);
+    syrk_diag_body(c, sdiag[b], kb, smem, b == 0 && blockIdx.y == 0 ? slot : -1);
     return;
   }
   if (b < nsd + ncol) {
+    const int sl = b == nsd && blockIdx.y == 0 ? slot : -1;
+    STAMP(sl, 5);
     const int4 t = col[b - nsd];   // (front, r0, kn, kb)
     syrk_tile64<true>(c, t, kb, smem);
     __syncthreads();
+    STAMP(sl, 6);
     const int s = t.x, kn = t.z, nb = min(kNB, c.w[s] - kn);
     wait_step(c, c.stepflag + s, kn / 64 + 1);
-    trsm_rows(c, s, t.y, kn, nb, smem, 1, 65);
+    STAMP(sl, 7);
+    trsm_rows(c, s, t.y, kn, nb, smem, 1, 65, smem + 64 * 65);
+    STAMP(sl, 8);
     return;
   }
   syrk_lds_body(c, tiles[b - nsd - ncol], kb, smem);
@@ -1250,29 +1285,6 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
         const int row = row0 + 64 * wi + 16 * bi + (l & 15), col = col0 + 64 * wj + 16 * bj + (l >> 4) + 4 * r;
         if (row < m && col < colend && row >= col) Fs[row + (size_t)col * m] = cold[bi][r] - acc[bj][bi][r];
       }
-  }
-}
-
-// Lower triangles of the fronts (columns [j0, j1) of a front per workgroup)
-// zeroed before assembly; the upper triangles are never written.
-// tasks [0, n), grid-stride: a small grid zeroes in the background without
-// taking the CUs the latency-bound panel kernels need
-__global__ __launch_bounds__(256) void k_zero_lower(CholDev c, const int4* __restrict__ tasks, int n) {
-  lane_offset(c);
-  for (int q0 = blockIdx.x; q0 < n; q0 += gridDim.x) {
-    const int4 t = tasks[q0];
-    const int m = c.m[t.x];
-    const long long base = c.foff[t.x];
-    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-    for (int j = t.y + wv; j < t.z; j += 4) {   // a wave per column, 16-B stores
-      const long long g0 = base + (long long)j * m + j, g1 = base + (long long)j * m + m;
-      const long long a0 = (g0 + 1) & ~1LL;       // first 16-B aligned element
-      if (l == 0 && a0 != g0) c.F[g0] = 0.0;
-      double2* p = reinterpret_cast<double2*>(c.F + a0);
-      const long long np = (g1 - a0) >> 1;
-      for (long long q = l; q < np; q += 64) p[q] = make_double2(0.0, 0.0);
-      if (l == 0 && a0 + 2 * np < g1) c.F[g1 - 1] = 0.0;
-    }
   }
 }
 
@@ -1662,12 +1674,11 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(up(&P.d_syrk, P.syrk_tasks, s));
   CH_TRY(up(&P.d_sdiag, P.sdiag_tasks, s));
   CH_TRY(up(&P.d_col, P.col_tasks, s));
-  CH_TRY(up(&P.d_zero, P.zero_tasks, s));
-  CH_TRY(up(&P.d_dg_order, P.dg_order, s));
+  CH_TRY(up(&P.d_at_iptr, P.at_iptr, s));
+  CH_TRY(up(&P.d_at_items, P.at_items, s));
   CH_TRY(alloc_numeric(P, std::max(P.batch, 1), s));
   CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
   CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
-  CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));   // (a non-default priority measured 1.5x slower)
   for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   CH_TRY(up(&P.d_ea_tasks, P.ea_tasks, s));
   CH_TRY(up(&P.d_ea_pairs, P.ea_pairs, s));
@@ -1678,20 +1689,19 @@ void chol_free(CholPlan& P) {
   void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
                   P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
                   P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
-                  P.d_syrk, P.d_ea_tasks, P.d_ea_pairs, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_zero, P.d_dg_order, P.d_col, P.d_stepflag};
+                  P.d_syrk, P.d_ea_tasks, P.d_ea_pairs, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_at_iptr, P.d_at_items, P.d_col, P.d_stepflag};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : P.evs)
     if (e) (void)hipEventDestroy(e);
   if (P.side) (void)hipStreamDestroy(P.side);
   if (P.side2) (void)hipStreamDestroy(P.side2);
-  if (P.side3) (void)hipStreamDestroy(P.side3);
   P = CholPlan();
 }
 
 const char* kernel_family_name(int f) {
   static const char* const names[kFamCount] = {
-      "k_asm_offdiag+k_asm_diag", "k_zero_lower", "k_perm_in+k_perm_out", "k_extend_add", "k_vec_assemble",
+      "k_assemble_tile", "(unused)", "k_perm_in+k_perm_out", "(unused)", "k_vec_assemble",
       "k_front_wave", "k_front_small", "k_panel_first", "k_step", "k_panel_syrk_lds", "k_panel_syrk128",
       "k_bwd_part", "k_bwd_init", "k_bwd_step"};
   return f >= 0 && f < kFamCount ? names[f] : "?";
@@ -1717,85 +1727,25 @@ static void launch(LaunchProfile* prof, int fam, Cost cost, K kern, dim3 grid, d
   }
 }
 
-// algorithmic work of the factorisation's launches (host, profiled launches only)
-static double chol_flops(int m, int w) {   // dense Cholesky of the w pivot columns of an m-row front
-  double f = 0;
-  for (int k = 0; k < w; k++) {
-    const double r = m - k - 1;
-    f += 1 + r + r * (r + 1);
-  }
-  return f;
-}
 hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
                        hipStream_t s, LaunchProfile* prof, int nb) {
   if (P.n == 0) return hipSuccess;
   if (nb < 1 || nb > P.batch) return hipErrorInvalidValue;
   const CholDev c = dev_view(P);
   const dim3 B256(256);
+  static const bool stamps = getenv("PGO_STEP_STAMPS") != nullptr;
   launch(prof, kFamPerm, [&] { return make_double2(0, 48.0 * P.n * nb); }, k_perm_in, dim3((P.n + 255) / 256, nb),
          B256, 0, s, c, b, scale_b, P.n);
   CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int) * nb, s));
   CH_TRY(hipMemsetAsync(P.d_stepflag, 0, sizeof(int) * std::max(P.ns, 1) * nb, s));
-  // zeroing + assembly: leaf-level fronts on the main stream, the others on
-  // side3 beside the leaf level (joined before level 1's extend-add)
-  const int nz = P.zero_late, nt = (int)P.asm_front.size();
-  auto zero_bytes = [&](int z0, int z1) {
-    double e = 0;
-    for (int q = z0; q < z1; q++) {
-      const int4 t = P.zero_tasks[q];
-      for (int j = t.y; j < t.z; j++) e += P.m[t.x] - j;
-    }
-    return make_double2(0, 8.0 * e * nb);
-  };
-  auto assemble = [&](int z0, int z1, int a0, int a1, int d0, int d1, hipStream_t st) {
-    if (z1 > z0)
-      launch(prof, kFamZero, [&] { return zero_bytes(z0, z1); }, k_zero_lower, dim3(z1 - z0, nb), B256, 0, st, c,
-             (const int4*)(P.d_zero + z0), z1 - z0);
-    if (a1 > a0)
-      launch(prof, kFamAssemble, [&] {
-               return make_double2(0, (double)nb * (72.0 * (a1 - a0) + 72.0 * (P.asm_ptr[a1] - P.asm_ptr[a0])));
-             },
-             k_asm_offdiag, dim3((a1 - a0 + 255) / 256, nb), B256, 0, st, c, V, (long long)P.nslots, a0, a1);
-    if (d1 > d0)
-      launch(prof, kFamAssemble, [&] { return make_double2(0, 96.0 * (d1 - d0) * nb); }, k_asm_diag,
-             dim3((d1 - d0 + 255) / 256, nb), B256, 0, st, c, D, (const double*)P.d_lambda, d0, d1);
-  };
-  assemble(0, P.zero_split, 0, P.asm_split, 0, P.dg_split, s);
-  const bool fork_rest = P.zero_split < nz || P.asm_split < nt || P.dg_split < P.n;
-  if (fork_rest) {
-    CH_TRY(hipEventRecord(P.evs[4], s));
-    CH_TRY(hipStreamWaitEvent(P.side3, P.evs[4], 0));
-    assemble(P.zero_split, nz, P.asm_split, nt, P.dg_split, P.n, P.side3);
-    CH_TRY(hipEventRecord(P.evs[5], P.side3));
-  }
   for (size_t li = 0; li < P.levels.size(); li++) {
     const CholLevel& lv = P.levels[li];
     if (prof) prof->cur_tag = (int)li << 16;
-    if (li == 1 && fork_rest) CH_TRY(hipStreamWaitEvent(s, P.evs[5], 0));
     if (lv.ea_cnt[0])
-      launch(prof, kFamExtendAdd, [&] {
-               double e = 0;   // update-matrix elements moved (read child, read-modify-write parent)
-               for (int q = 0; q < lv.ea_cnt[0]; q++) {
-                 const int4 t = P.ea_tasks[lv.ea_off[0] + q];
-                 for (int k = 0; k < t.w; k++) {
-                   const int4 pr = P.ea_pairs[t.z + k];
-                   const int nr = pr.w & 0xff, ncl = pr.w >> 8;
-                   for (int r = 0; r < nr; r++) e += std::min(std::max(pr.y + r - pr.z + 1, 0), ncl);
-                 }
-               }
-               return make_double2(0, 24.0 * e * nb);
-             },
-             k_extend_add, dim3(lv.ea_cnt[0], nb), B256, 0, s, c, (const int4*)(P.d_ea_tasks + lv.ea_off[0]),
-             (const int4*)P.d_ea_pairs);
-    if ((int)li == P.zero_level) {   // update matrices consumed by now: zero them for the next factorisation
-      CH_TRY(hipEventRecord(P.evs[4], s));
-      CH_TRY(hipStreamWaitEvent(P.side3, P.evs[4], 0));
-      const int nlate = (int)P.zero_tasks.size() - P.zero_late;
-      launch(prof, kFamZero, [&] { return zero_bytes(P.zero_late, (int)P.zero_tasks.size()); }, k_zero_lower,
-             dim3(std::min(nlate, kZeroBackgroundGrid), nb), B256, 0, P.side3, c,
-             (const int4*)(P.d_zero + P.zero_late), nlate);
-      CH_TRY(hipEventRecord(P.evs[5], P.side3));
-    }
+      launch(prof, kFamAssemble, [&] { return make_double2(0, lv.at_bytes * nb); },
+             k_assemble_tile, dim3(lv.ea_cnt[0], nb), B256, 0, s, c, (const int4*)(P.d_ea_tasks + lv.ea_off[0]),
+             (const int2*)(P.d_at_iptr + lv.ea_off[0]), (const int*)P.d_at_items, (const int4*)P.d_ea_pairs, V,
+             (long long)P.nslots, D, (const double*)P.d_lambda);
     launch(prof, kFamVecAssemble, [&] { return make_double2(0, 0); }, k_vec_assemble, dim3(lv.front_cnt, nb), B256,
            (size_t)lv.maxm * sizeof(double), s, c, (const int*)(P.d_level_fronts + lv.front_off));
     // small fronts on the second side stream, beside the blocked path of the
@@ -1808,14 +1758,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       ss = P.side2;
     }
     for (const SmallClass& sc : lv.small) {
-      auto small_cost = [&] {
-        double f = 0;
-        for (int q = 0; q < sc.cnt; q++) {
-          const int fr = P.small_list[sc.off + q];
-          f += chol_flops(P.m[fr], P.w[fr]) + (double)P.w[fr] * P.w[fr] * P.w[fr] / 3.0;
-        }
-        return make_double2(f * nb, 0);
-      };
+      auto small_cost = [&] { return make_double2(sc.flops * nb, 0); };
       const int* list = P.d_small + sc.off;
       if (sc.wave) {
         const size_t lds = (size_t)(sc.mmax * (kWaveW + 1) + 130 + kWaveW) * sizeof(double);
@@ -1851,7 +1794,8 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       if (step)
         launch(prof, kFamStep, [&] { return make_double2(ps.step_flops * nb, 0); }, k_step,
                dim3(ps.sdiag_cnt + ps.col_cnt + nin, nb), B256, 0, s, c, (const int4*)(P.d_sdiag + ps.sdiag_off),
-               ps.sdiag_cnt, cols + ps.fcol_cnt, ps.col_cnt, tiles, ps.kb);
+               ps.sdiag_cnt, cols + ps.fcol_cnt, ps.col_cnt, tiles, ps.kb,
+               stamps && li + 1 == P.levels.size() && ps.kb / kNB < kMaxStampSlots ? ps.kb / kNB : -1);
       if (apart) {
         if (step) {
           plain(P.side);
@@ -1867,8 +1811,11 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       CH_TRY(hipStreamWaitEvent(s, P.evs[1], 0));
     }
   }
-  if (P.zero_level >= 0) CH_TRY(hipStreamWaitEvent(s, P.evs[5], 0));
   return hipGetLastError();
+}
+
+hipError_t chol_step_stamps(unsigned long long* out, int slots) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 10 * std::min(slots, kMaxStampSlots));
 }
 
 hipError_t chol_marginals(const CholPlan& P, const int* poses, int n, double* out, hipStream_t s) {
@@ -1908,14 +1855,7 @@ hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb, long 
     const CholLevel& lv = *it;
     if (prof) prof->cur_tag = (int)(&lv - P.levels.data()) << 16;
     if (lv.bwd_part.cnt)
-      launch(prof, kFamBwdPart, [&] {
-               double f = 0;
-               for (int q = 0; q < lv.bwd_part.cnt; q++) {
-                 const int4 t = P.bwd_part_tasks[lv.bwd_part.off + q];
-                 f += 2.0 * std::min(64, P.w[t.x] - t.y) * std::min(kBwdRows, P.m[t.x] - t.z);
-               }
-               return make_double2(f * nb, 0);
-             },
+      launch(prof, kFamBwdPart, [&] { return make_double2(lv.bwd_part_flops * nb, 0); },
              k_bwd_part, dim3(lv.bwd_part.cnt, nb), B256, 0, s, c, (const int4*)(P.d_bwd_part + lv.bwd_part.off),
              P.d_partial);
     launch(prof, kFamBwdInit, [&] { return make_double2(0, 0); }, k_bwd_init, dim3(lv.bwd[0].cnt, nb), B256, 0, s, c,

@@ -141,6 +141,17 @@ void xcd_order(std::vector<int4>& tasks, int tile) {
   tasks.swap(out);
 }
 
+// dense Cholesky flops of the w pivot columns of an m-row front, plus the
+// inverses of its diagonal blocks (what the small-front kernels form)
+static double front_flops(int m, int w) {
+  double f = (double)w * w * w / 3.0;
+  for (int k = 0; k < w; k++) {
+    const double r = m - k - 1;
+    f += 1 + r + r * (r + 1);
+  }
+  return f;
+}
+
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
   P.nslots = (long long)slot_col.size();
   P.n = n;
@@ -382,11 +393,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       if (i > j) ents.push_back({j, i, k});
     }
   }
-  // targets of leaf-level fronts first (assembled on the main stream, the rest
-  // beside the leaf level)
   std::sort(ents.begin(), ents.end(), [&](const Ent& a, const Ent& b) {
-    const bool la = P.height[snode[a.j]] > 0, lb = P.height[snode[b.j]] > 0;
-    if (la != lb) return lb;
     return a.j != b.j ? a.j < b.j : (a.i != b.i ? a.i < b.i : a.k < b.k);
   });
   P.asm_front.clear();
@@ -406,20 +413,26 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   }
   P.asm_ptr.push_back((int)P.asm_src.size());
   if (ents.empty()) P.asm_ptr.assign(1, 0);
-  P.asm_split = 0;
-  while (P.asm_split < (int)P.asm_front.size() && P.height[P.asm_front[P.asm_split]] == 0) P.asm_split++;
   P.dg_front.resize(n);
   P.dg_loc.resize(n);
   for (int j = 0; j < n; j++) {
     P.dg_front[j] = snode[j];
     P.dg_loc[j] = j - P.sfirst[snode[j]];
   }
-  P.dg_order.clear();
-  for (int pass = 0; pass < 2; pass++)
-    for (int j = 0; j < n; j++)
-      if ((P.height[snode[j]] > 0) == (pass == 1)) P.dg_order.push_back(j);
-  P.dg_split = 0;
-  for (int j = 0; j < n; j++) P.dg_split += P.height[snode[j]] == 0;
+  // H entries by front tile: every 64x64 lower tile of a front lists the 3x3
+  // blocks of H (off-diagonal targets t >= 0, diagonal blocks ~pose) with an
+  // element in it (a block can straddle tile boundaries)
+  std::vector<std::vector<std::pair<int, int>>> hitems(ns);   // per front: (tile, item)
+  auto add_item = [&](int sf, int r0, int c0, int item) {
+    for (int ti = r0 / 64; ti <= (r0 + 2) / 64; ti++)
+      for (int tj = c0 / 64; tj <= (c0 + 2) / 64; tj++)
+        if (ti >= tj) hitems[sf].emplace_back(ti * (ti + 1) / 2 + tj, item);
+  };
+  for (size_t t = 0; t < P.asm_front.size(); t++) add_item(P.asm_front[t], 3 * P.asm_li[t], 3 * P.asm_lj[t], (int)t);
+  for (int j = 0; j < n; j++) add_item(P.dg_front[j], 3 * P.dg_loc[j], 3 * P.dg_loc[j], ~j);
+  for (auto& v : hitems) std::stable_sort(v.begin(), v.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
+    return a.first < b.first;
+  });
   // ---- level schedules
   const int nl = ns ? *std::max_element(P.height.begin(), P.height.end()) + 1 : 0;
   std::vector<std::vector<int>> bylevel(nl);
@@ -429,39 +442,6 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.level_fronts.clear();
   P.syrk_tasks.clear();
   P.sdiag_tasks.clear();
-  // zeroing (see CholPlan::zero_tasks): the level whose extend-add is the last
-  // to read the early update matrices = the first level with few fronts (the
-  // latency-bound top of the tree)
-  P.zero_level = -1;
-  for (int L = 1; L < nl; L++)
-    if ((int)bylevel[L].size() <= 64) {
-      P.zero_level = L;
-      break;
-    }
-  P.zero_tasks.clear();
-  auto zero_cols = [&](int q, int c0, int c1) {   // columns [c0, c1) of front q, ~32k doubles per task
-    const int m = P.m[q];
-    int j0 = c0;
-    long long acc = 0;
-    for (int j = c0; j < c1; j++) {
-      acc += m - j;
-      if (acc >= 32768 || j == c1 - 1) {
-        P.zero_tasks.push_back(make_int4(q, j0, j + 1, 0));
-        j0 = j + 1;
-        acc = 0;
-      }
-    }
-  };
-  auto late = [&](int q) { return P.zero_level >= 0 && P.parent[q] >= 0 && P.height[P.parent[q]] <= P.zero_level; };
-  for (int pass = 0; pass < 2; pass++) {   // leaf-level fronts, then the others
-    if (pass == 1) P.zero_split = (int)P.zero_tasks.size();
-    for (int q = 0; q < P.ns; q++)
-      if ((P.height[q] > 0) == (pass == 1)) zero_cols(q, 0, late(q) ? P.w[q] : P.m[q]);
-  }
-  P.zero_late = (int)P.zero_tasks.size();
-  for (int q = 0; q < P.ns; q++)
-    if (late(q)) zero_cols(q, P.w[q], P.m[q]);
-  if (P.zero_late == (int)P.zero_tasks.size()) P.zero_level = -1;
   P.potrf_list.clear();
   P.col_tasks.clear();
   P.bwd_tasks.clear();
@@ -470,6 +450,8 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.npart = 0;
   P.ea_tasks.clear();
   P.ea_pairs.clear();
+  P.at_items.clear();
+  P.at_iptr.clear();
   for (int L = 0; L < nl; L++) {
     CholLevel& lv = P.levels[L];
     lv.front_off = (int)P.level_fronts.size();
@@ -497,6 +479,10 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
         }
       }
       sp.cnt = (int)P.bwd_part_tasks.size() - sp.off;
+      for (int q = sp.off; q < sp.off + sp.cnt; q++) {
+        const int4 t = P.bwd_part_tasks[q];
+        lv.bwd_part_flops += 2.0 * std::min(64, P.w[t.x] - t.y) * std::min(kBwdRows, P.m[t.x] - t.z);
+      }
       st.cnt = (int)P.bwd_tasks.size() - st.off;
       lv.bwd_part = sp;
       lv.bwd.push_back(st);
@@ -515,14 +501,14 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       st.cnt = (int)P.bwd_tasks.size() - st.off;
       lv.bwd.push_back(st);
     }
-    // extend-add: one task per 64x64 tile of a parent front's lower triangle
-    // that receives update-matrix elements; a task walks the parent's children
-    // in order (fixed summation order, no atomics), each contributing a
-    // rectangle of its update matrix (child rows [a0, a0+nr) x columns
-    // [b0, b0+nc), the rows / columns whose parent index falls in the tile)
+    // assembly: one task per 64x64 tile of every front's lower triangle, which
+    // it writes whole: its H entries (+ lambda on the diagonal), then the
+    // update-matrix elements of the front's children in order (fixed
+    // summation order, no atomics), each child contributing a rectangle of its
+    // update matrix (child rows [a0, a0+nr) x columns [b0, b0+nc), the rows /
+    // columns whose parent index falls in the tile).  No front is zeroed.
     lv.ea_off.push_back((int)P.ea_tasks.size());
     for (int sp : bylevel[L]) {
-      if (P.cptr[sp] == P.cptr[sp + 1]) continue;
       const int nt = (P.m[sp] + 63) / 64;
       std::vector<std::vector<int4>> tiles((size_t)nt * (nt + 1) / 2);
       for (int q = P.cptr[sp]; q < P.cptr[sp + 1]; q++) {
@@ -539,15 +525,38 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
             tiles[(size_t)runs[i].x * (runs[i].x + 1) / 2 + runs[j].x].push_back(
                 make_int4(c, runs[i].y, runs[j].y, runs[i].z | (runs[j].z << 8)));
       }
+      const auto& hv = hitems[sp];
+      size_t hq = 0;
       for (int ti = 0; ti < nt; ti++)
         for (int tj = 0; tj <= ti; tj++) {
-          const auto& v = tiles[(size_t)ti * (ti + 1) / 2 + tj];
-          if (v.empty()) continue;
+          const int key = ti * (ti + 1) / 2 + tj;
+          const auto& v = tiles[key];
+          const int i0 = (int)P.at_items.size();
+          while (hq < hv.size() && hv[hq].first < key) hq++;
+          while (hq < hv.size() && hv[hq].first == key) P.at_items.push_back(hv[hq++].second);
+          P.at_iptr.push_back(make_int2(i0, (int)P.at_items.size() - i0));
           P.ea_tasks.push_back(make_int4(sp, (ti << 16) | tj, (int)P.ea_pairs.size(), (int)v.size()));
           P.ea_pairs.insert(P.ea_pairs.end(), v.begin(), v.end());
         }
     }
     lv.ea_cnt.push_back((int)P.ea_tasks.size() - lv.ea_off.back());
+    for (int q = lv.ea_off[0]; q < lv.ea_off[0] + lv.ea_cnt[0]; q++) {   // algorithmic bytes (profiles)
+      const int4 t = P.ea_tasks[q];
+      double e = 0, h = 0;   // children's elements read + tile elements written; H slots read
+      for (int k = 0; k < t.w; k++) {
+        const int4 pr = P.ea_pairs[t.z + k];
+        const int nr = pr.w & 0xff, ncl = pr.w >> 8;
+        for (int r = 0; r < nr; r++) e += std::min(std::max(pr.y + r - pr.z + 1, 0), ncl);
+      }
+      const int2 it = P.at_iptr[q];
+      for (int k = 0; k < it.y; k++) {
+        const int code = P.at_items[it.x + k];
+        h += code >= 0 ? 72.0 * (P.asm_ptr[code + 1] - P.asm_ptr[code]) : 48.0;
+      }
+      const int mp = P.m[t.x], R0 = 64 * (t.y >> 16), C0 = 64 * (t.y & 0xffff);
+      for (int j = C0; j < std::min(C0 + 64, mp); j++) e += std::max(0, std::min(R0 + 64, mp) - std::max(R0, j));
+      lv.at_bytes += 8.0 * e + h;
+    }
     // small fronts (m <= kSmallFront): with w <= kWaveW one wavefront each (the
     // m x w panel in LDS, the rank-w Schur update streamed), largest first;
     // else one workgroup each with the whole front in LDS, launched per size
@@ -585,6 +594,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
         for (int s : part) {
           P.small_list.push_back(s);
           sc.mmax = std::max(sc.mmax, P.m[s]);
+          sc.flops += front_flops(P.m[s], P.w[s]);
         }
         lv.small.push_back(sc);
       }
@@ -594,6 +604,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
         for (int s : bucket[q]) {
           P.small_list.push_back(s);
           sc.mmax = std::max(sc.mmax, P.m[s]);
+          sc.flops += front_flops(P.m[s], P.w[s]);
         }
         lv.small.push_back(sc);
       }
@@ -630,27 +641,41 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
         if (kb == 0 && P.w[s] > 0)
           for (int r0 = kNB; r0 < P.m[s]; r0 += kNB) P.col_tasks.push_back(make_int4(s, r0, 0, -1));
       ps.fcol_cnt = (int)P.col_tasks.size() - ps.col_off;
-      // this panel's Schur update (depth nb) of columns [kn, m), kn = kb + nb
-      std::vector<int4> plain;
+      // this panel's Schur update, deferred by kKB-column blocks: inside a block
+      // only the block's remaining columns [kn, be) are updated (depth nb,
+      // "inner", bit 31 of k0); after the block's last panel the trailing
+      // columns [be, m) get one update of depth kn - bs <= kKB
+      std::vector<int4> plain;   // (front, first column, end column, k0): rows from the column down
       for (int s : big) {
         if (P.w[s] <= kb) continue;
         const int nb = std::min(kNB, P.w[s] - kb), kn = kb + nb, m = P.m[s];
-        for (int cc = kn; cc < m; cc++) ps.syrk_flops += 2.0 * nb * (m - cc);
+        const int bs = kb & ~(kKB - 1), be = std::min(bs + kKB, P.w[s]);
+        const bool inner = kn < be;
+        const int cend = inner ? be : m, depth = inner ? nb : kn - bs;
+        const int k0 = inner ? (kb | (int)0x80000000) : bs;
+        if (inner) {
+          for (int cc = kn; cc < be; cc++) ps.syrk_flops += 2.0 * nb * (m - cc);
+        } else if (be < m) {
+          const double t = m - be;
+          ps.syrk_flops += depth * t * (t + 1.0);
+        }
         int cstart = kn;
         if (kn < P.w[s]) {   // next panel: its diagonal tile and the tiles below it
           const int nb2 = std::min(kNB, P.w[s] - kn);
-          P.sdiag_tasks.push_back(make_int4(s, kn, kn, kb));
-          ps.step_flops += (double)nb * kNB * (kNB + 1) + 2.0 * nb2 * nb2 * (double)nb2 / 3.0 +
+          P.sdiag_tasks.push_back(make_int4(s, kn, kn, k0));
+          ps.step_flops += (double)depth * kNB * (kNB + 1) + 2.0 * nb2 * nb2 * (double)nb2 / 3.0 +
                            (double)std::min(kNB - nb2, m - kn - nb2) * nb2 * nb2;
           for (int r0 = kn + kNB; r0 < m; r0 += kNB) {
-            P.col_tasks.push_back(make_int4(s, r0, kn, kb));
+            P.col_tasks.push_back(make_int4(s, r0, kn, k0));
             const int rows = std::min(kNB, m - r0);
-            ps.step_flops += 2.0 * nb * rows * kNB + (double)rows * nb2 * nb2;
+            ps.step_flops += 2.0 * depth * rows * std::min(kNB, cend - kn) + (double)rows * nb2 * nb2;
           }
           cstart = kn + kNB;
         }
-        for (int cc = cstart; cc < m; cc++) ps.plain_flops += 2.0 * nb * (m - cc);
-        plain.push_back(make_int4(s, cstart, m, kb));
+        if (cstart < cend) {
+          for (int cc = cstart; cc < cend; cc++) ps.plain_flops += 2.0 * depth * (m - cc);
+          plain.push_back(make_int4(s, cstart, cend, k0));
+        }
       }
       ps.sdiag_cnt = (int)P.sdiag_tasks.size() - ps.sdiag_off;
       ps.col_cnt = (int)P.col_tasks.size() - ps.col_off - ps.fcol_cnt;
@@ -660,13 +685,13 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       auto ntiles = [&](int T) {
         long long cnt = 0;
         for (const int4& u : plain)
-          for (int c0 = u.y; c0 < u.z; c0 += T) cnt += (u.z - c0 + T - 1) / T;
+          for (int c0 = u.y; c0 < u.z; c0 += T) cnt += (P.m[u.x] - c0 + T - 1) / T;
         return cnt;
       };
       ps.syrk_tile = ntiles(kBigTile) >= 4096 ? kBigTile : kTile;
       for (const int4& u : plain)
         for (int c0 = u.y; c0 < u.z; c0 += ps.syrk_tile)
-          for (int r0 = c0; r0 < u.z; r0 += ps.syrk_tile) P.syrk_tasks.push_back(make_int4(u.x, r0, c0, u.w));
+          for (int r0 = c0; r0 < P.m[u.x]; r0 += ps.syrk_tile) P.syrk_tasks.push_back(make_int4(u.x, r0, c0, u.w));
       {   // XCD-aware order of this step's Schur-update tiles
         std::vector<int4> mine(P.syrk_tasks.begin() + ps.syrk_off, P.syrk_tasks.end());
         xcd_order(mine, ps.syrk_tile);

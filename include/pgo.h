@@ -145,6 +145,11 @@ typedef struct {
   double ms_factor_profiled;
   double ms_solve_profiled;
   int stop_reason;              /* PGO_STOP_* : why the outer loop ended          */
+  /* graph-replayed factorisations (use_graphs, every unprofiled one): summed
+     device time of the factorisation graphs and the algorithmic flops they
+     performed (lanes x one factorisation's flops) */
+  double ms_factor_graph;
+  double factor_graph_flops;
 } pgo_stats;
 
 /* pgo_stats.stop_reason.  GTSAM reports every one of these as convergence
