@@ -35,6 +35,8 @@ PGO_ALG_LM = 0
 PGO_ALG_GN = 1
 PGO_SOLVER_PCG = 0
 PGO_SOLVER_CHOLESKY = 1
+PGO_MULTI_SPECULATIVE = 0
+PGO_MULTI_PARTITION = 1
 STOP_REASONS = {0: "converged", 1: "lambda_upper_bound", 2: "max_iterations", 3: "max_outer", 4: "small_cost_change",
                 5: "error"}
 
@@ -51,7 +53,8 @@ class PgoParams(C.Structure):
                 ("min_model_fidelity", C.c_double), ("use_fixed_lambda_factor", C.c_int),
                 ("algorithm", C.c_int), ("linear_solver", C.c_int), ("pcg_relative_tol", C.c_double),
                 ("pcg_max_iterations", C.c_int), ("pcg_check_interval", C.c_int), ("max_outer", C.c_int),
-                ("profile_every", C.c_int), ("use_graphs", C.c_int), ("lambda_lanes", C.c_int)]
+                ("profile_every", C.c_int), ("use_graphs", C.c_int), ("lambda_lanes", C.c_int),
+                ("multi_gpu", C.c_int)]
 
 
 class PgoStats(C.Structure):
@@ -146,6 +149,8 @@ def lib():
         "pgo_get_kernel_profile": (C.c_int, [vp, dp, C.c_int]),
         "pgo_kernel_family_name": (C.c_char_p, [C.c_int]),
         "pgo_debug_ordering": (C.c_int, [vp, C.POINTER(C.c_int32), C.c_size_t]),
+        "pgo_debug_partition": (C.c_int, [vp, C.c_int, C.POINTER(C.c_int), dp, C.c_int]),
+        "pgo_debug_parents": (C.c_int, [vp, C.POINTER(C.c_int), C.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

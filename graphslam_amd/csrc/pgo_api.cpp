@@ -68,6 +68,8 @@ struct pgo_graph {
   std::vector<int> h_row_ptr, h_slot_col;   // block-CSR pattern (old indices)
   pgo::CholPlan chol;
   int ordering = pgo::kOrderNd;             // fill-reducing ordering (pgo_opts.ordering)
+  int part_size = 1;                        // subtree partition the plan must have (PGO_MULTI_PARTITION)
+  pgo::ExchangeHook hook;                   // the partitioned factorisation's all-gathers (comm)
   bool chol_ready = false;
   // profiled factorisations (pgo_params.profile_every): every launch timed
   std::vector<hipEvent_t> sev;              // event pairs, one per launch
@@ -560,9 +562,30 @@ struct PcgResult {
 
 double ms_between(hipEvent_t a, hipEvent_t b);
 
+int exchange_allgather(void* ctx, const void* send, void* recv, size_t bytes, hipStream_t s) {
+  pgo_graph* g = static_cast<pgo_graph*>(ctx);
+  std::string why;
+  const int rc = pgo::comm_allgather_device(&g->comm, send, recv, bytes, s, &why);
+  if (rc != PGO_OK) g->last_error = "partition exchange: " + why;
+  return rc == PGO_OK ? 0 : -1;
+}
+
 int ensure_chol(pgo_graph* g) {
+  const int psz = g->part_size > 1 ? g->comm.size : 1, prk = psz > 1 ? g->comm.rank : 0;
+  if (g->chol_ready && (g->chol.part_size != psz || g->chol.part_rank != prk)) {   // other partition: re-plan
+    (void)hipStreamSynchronize(g->d.stream);
+    free_lanes(g);
+    drop_graphs(g);
+    pgo::chol_free(g->chol);
+    g->chol_ready = false;
+    g->lane_cap = 8;
+  }
   if (g->chol_ready) return PGO_OK;
   g->chol.ordering = g->ordering;
+  g->chol.part_size = psz;
+  g->chol.part_rank = prk;
+  g->hook.ctx = g;
+  g->hook.allgather = exchange_allgather;
   pgo::chol_analyze(g->chol, g->d.n, g->h_row_ptr, g->h_slot_col);
   // owner slot of every factor := its block in the lower triangle of the
   // permuted matrix (the one the assembly reads); with write_all = 0 the
@@ -700,11 +723,19 @@ int linear_solve(pgo_graph* g, const pgo_params& p, double lam, pgo_stats* st, S
   }
   *g->h_lam = lam;
   HIP_TRY(g, hipMemcpyAsync(g->chol.d_lambda, g->h_lam, sizeof(double), hipMemcpyHostToDevice, d.stream));
-  if (prof || !p.use_graphs) {  // eager: a profiled factorisation times every launch
+  const bool part = g->chol.part_size > 1;
+  if (prof || !p.use_graphs || part) {  // eager: a profiled factorisation times every launch; the
+                                        // partitioned one runs its exchanges between the phases
+    pgo::ExchangeHook* hook = part ? &g->hook : nullptr;
+    g->hook.failed = false;
     if (prof) HIP_TRY(g, hipEventRecord(g->fev[0], d.stream));
-    HIP_TRY(g, pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, prof));
+    const hipError_t ef = pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, prof, 1, hook);
+    if (g->hook.failed) return fail(g, PGO_E_COMM, g->last_error);
+    HIP_TRY(g, ef);
     if (prof) HIP_TRY(g, hipEventRecord(g->fev[1], d.stream));
-    HIP_TRY(g, pgo::chol_solve(g->chol, d.x, d.stream, 1, 0, prof));
+    const hipError_t es = pgo::chol_solve(g->chol, d.x, d.stream, 1, 0, prof, hook);
+    if (g->hook.failed) return fail(g, PGO_E_COMM, g->last_error);
+    HIP_TRY(g, es);
     if (prof) HIP_TRY(g, hipEventRecord(g->fev[2], d.stream));
   } else {
     RC_TRY(graph_factor_solve(g, 1, d.x, 0));
@@ -949,6 +980,7 @@ void pgo_default_params(pgo_params* p) {
   p->profile_every = 0;
   p->use_graphs = 1;
   p->lambda_lanes = 1;
+  p->multi_gpu = PGO_MULTI_SPECULATIVE;
 }
 
 pgo_graph* pgo_create(const pgo_opts* opts) {
@@ -1138,6 +1170,7 @@ int pgo_marginal_covariances(pgo_graph* g, size_t n, const uint64_t* keys, doubl
   }
   RC_TRY(ensure_device(g));
   HIP_TRY(g, hipSetDevice(g->device));
+  g->part_size = 1;   // the path solves walk every front: a one-rank plan
   RC_TRY(ensure_chol(g));
   DevGraph& d = g->d;
   d.write_all = 0;
@@ -1210,6 +1243,11 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
                 "Gauss-Newton: a connected component has no prior, the linear system is singular");
   }
   hipEvent_t* ev = g->ev;
+  // PGO_MULTI_PARTITION with ranks: every try's factorisation is split over
+  // the ranks (each rank then walks the same, replicated LM control)
+  const bool partition = p.multi_gpu == PGO_MULTI_PARTITION && g->comm.size > 1 &&
+                         p.linear_solver != PGO_SOLVER_PCG && p.algorithm != PGO_ALG_GN;
+  g->part_size = partition ? g->comm.size : 1;
   // Cholesky: the plan (and the owner bits it assigns) first, then the
   // linearisation writes only the blocks the assembly reads
   if (p.linear_solver != PGO_SOLVER_PCG && d.n > 0) RC_TRY(ensure_chol(g));
@@ -1252,12 +1290,13 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
     return PGO_OK;
   };
   pgo::Comm& cm = g->comm;
-  const int P = cm.size, me = cm.rank;
-  const bool exchange = P > 1 || pgo::force_collectives(&cm);   // forced: 1-rank RCCL runs the collectives
-  st.ranks = P;
+  // the speculative search's ranks (a partitioned run is one search: P = 1 here)
+  const int P = partition ? 1 : cm.size, me = partition ? 0 : cm.rank;
+  const bool exchange = !partition && (P > 1 || pgo::force_collectives(&cm));   // forced: 1-rank RCCL too
+  st.ranks = cm.size;
   // lanes: concurrent tries on this GPU (Cholesky LM only)
   int L = 1;
-  if (p.algorithm != PGO_ALG_GN && p.linear_solver != PGO_SOLVER_PCG && p.lambda_lanes > 1 && d.n > 0)
+  if (!partition && p.algorithm != PGO_ALG_GN && p.linear_solver != PGO_SOLVER_PCG && p.lambda_lanes > 1 && d.n > 0)
     L = ensure_lanes(g, p.lambda_lanes);
   // every rank must agree on the lanes per rank (a lane allocation may fail on one)
   if (exchange) {
@@ -1610,6 +1649,35 @@ int pgo_get_kernel_profile(const pgo_graph* g, double* out, int cap) {
   return pgo::kFamCount;
 }
 
+int pgo_debug_parents(pgo_graph* g, int* parent, int cap) {
+  if (!g || cap < 0 || (cap > 0 && !parent)) return PGO_E_ARG;
+  RC_TRY(download_values(g));
+  HostStructure H;
+  RC_TRY(build_structure(g, H));
+  pgo::CholPlan P;
+  P.ordering = g->ordering;
+  pgo::chol_analyze(P, (int)g->keys.size(), H.row_ptr, H.slot_col);
+  for (int s = 0; s < P.ns && s < cap; s++) parent[s] = P.parent[s];
+  return P.ns;
+}
+
+int pgo_debug_partition(pgo_graph* g, int size, int* owner, double* out, int cap) {
+  if (!g || size < 1 || cap < 0 || (cap > 0 && (!owner || !out))) return PGO_E_ARG;
+  RC_TRY(download_values(g));
+  HostStructure H;
+  RC_TRY(build_structure(g, H));
+  pgo::CholPlan P;
+  P.ordering = g->ordering;
+  pgo::chol_analyze(P, (int)g->keys.size(), H.row_ptr, H.slot_col);
+  std::vector<double> rf;
+  double top = 0;
+  const std::vector<int> own = pgo::partition_subtrees(P, size, &rf, &top);
+  for (int s = 0; s < P.ns && s < cap; s++) owner[s] = own[s];
+  for (int r = 0; r < size && r < cap; r++) out[r] = rf[r];
+  if (size < cap) out[size] = top;
+  return P.ns;
+}
+
 int pgo_debug_ordering(pgo_graph* g, int32_t* perm, size_t n) {
   if (!g || (n && !perm) || n != g->keys.size()) return PGO_E_ARG;
   RC_TRY(download_values(g));
@@ -1787,6 +1855,7 @@ int pgo_debug_solve(pgo_graph* g, double lambda, const pgo_params* params, doubl
   RC_TRY(ensure_device(g));
   DevGraph& d = g->d;
   // the Cholesky assembly reads the owner blocks in factor order (k_linearize_own)
+  g->part_size = 1;
   if (p.linear_solver != PGO_SOLVER_PCG && d.n > 0) RC_TRY(ensure_chol(g));
   d.write_all = p.linear_solver == PGO_SOLVER_PCG ? 1 : 0;
   HIP_TRY(g, pgo::launch_linearize(d));

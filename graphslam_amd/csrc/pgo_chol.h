@@ -74,6 +74,7 @@ enum { kOrderNd = 0, kOrderAmd = 1 };
 
 struct CholPlan {
   int ordering = kOrderNd;         // fill-reducing ordering of the pose graph (input of chol_analyze)
+  int part_size = 1, part_rank = 0; // subtree partition over ranks (input of chol_analyze)
   int batch = 1;                   // lambda lanes with a numeric workspace (input of chol_upload)
   // ---- host symbolic result ----
   int n = 0, ns = 0;
@@ -106,6 +107,18 @@ struct CholPlan {
   std::vector<int> at_items;       // H entries: asm target t >= 0, or ~pose (diagonal block + lambda)
   std::vector<int4> ea_pairs;      // (child, first row a0, first column b0, rows | columns << 8):
                                    // a child's rectangle of one tile, children in order
+  // ---- subtree partition (part_size > 1): levels [0, split) are this rank's
+  // subtree fronts, [split, end) the replicated top; between them every rank's
+  // subtree roots' update matrices + vectors are all-gathered (xroot*), after
+  // the backward solve every rank's subtree solution range (xsol_ranges)
+  std::vector<int> owner;          // per front: rank of its subtree, -1 top
+  std::vector<int> subtree_cnt;    // fronts in the subtree of each front (postorder range)
+  int split = 0;
+  std::vector<int> xroot, xroot_rank;   // subtree roots (all ranks) and their ranks
+  std::vector<long long> xroot_off;     // payload offset (doubles) in its rank's buffer
+  std::vector<long long> xsize, xsol_size;
+  long long xmax = 0, xsol_max = 0;     // largest per-rank payload (all-gather slot)
+  std::vector<int4> xsol_ranges;        // (rank, first, end, offset): solution entries (xv) of each subtree
   double flops = 0, nnzl = 0, syrk_flops = 0;
   long long ftotal = 0, ttotal = 0;
   int vtotal = 0;
@@ -125,6 +138,9 @@ struct CholPlan {
   int4 *d_syrk = nullptr, *d_sdiag = nullptr, *d_col = nullptr;
   int2* d_at_iptr = nullptr;
   int* d_at_items = nullptr;
+  int4 *d_xown = nullptr, *d_xforeign = nullptr, *d_xsol_own = nullptr, *d_xsol_foreign = nullptr;
+  int n_xown = 0, n_xforeign = 0, n_xsol_own = 0, n_xsol_foreign = 0;
+  double *d_xsend = nullptr, *d_xrecv = nullptr;   // exchange buffers (xmax / size x xmax doubles)
   int* d_stepflag = nullptr;       // [batch][ns]: last panel (kb / 64 + 1) whose diagonal inverse is published
   hipStream_t side = nullptr;      // look-ahead diagonal tiles
   hipStream_t side2 = nullptr;     // small fronts beside the blocked path
@@ -149,6 +165,11 @@ void xcd_order(std::vector<int4>& tasks, int tile);
 std::vector<int> order_amd(int n, const std::vector<int>& xadj, const std::vector<int>& adj);
 std::vector<int> order_nd(int n, const std::vector<int>& xadj, const std::vector<int>& adj);
 
+// host: subtree partition of the supernodal tree over `size` ranks (owner per
+// front, -1 = replicated top); per-rank subtree flops and the top's flops
+std::vector<int> partition_subtrees(const CholPlan& P, int size, std::vector<double>* rank_flops = nullptr,
+                                    double* top_flops = nullptr);
+
 // host: symbolic analysis from the block-CSR pattern (old pose indices)
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
 hipError_t chol_upload(CholPlan& P, hipStream_t s);
@@ -156,6 +177,16 @@ void chol_free(CholPlan& P);
 // numeric workspaces for nb lambda lanes (P.batch); on failure one lane is kept
 // and the allocation error returned
 hipError_t chol_set_batch(CholPlan& P, int nb, hipStream_t s);
+
+// Exchange of the partitioned factorisation (part_size > 1): all-gather of
+// `bytes` per rank from send into recv (size x bytes, rank order), device
+// buffers, enqueued on / completed with respect to stream s.  Returns 0 on
+// success; a failure is remembered in `failed`.
+struct ExchangeHook {
+  void* ctx = nullptr;
+  int (*allgather)(void* ctx, const void* send, void* recv, size_t bytes, hipStream_t s) = nullptr;
+  bool failed = false;
+};
 
 // device: factor H + lambda I (D: 6 doubles/pose upper, V: slot blocks as structure of
 // arrays V[q * nslots + slot], old indexing; only the slots in asm_src are read)
@@ -185,8 +216,10 @@ struct LaunchProfile {
 // nb <= P.batch lanes at once: lane y factors H + lambda[y] I (lambda = P.d_lambda[y])
 // in its own workspace, grid dimension y of every launch (bitwise equal to a
 // one-lane factorisation)
+// With a partitioned plan, hook performs the subtree roots' exchange between
+// the phases (nb must be 1).
 hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
-                       hipStream_t s, LaunchProfile* prof = nullptr, int nb = 1);
+                       hipStream_t s, LaunchProfile* prof = nullptr, int nb = 1, ExchangeHook* hook = nullptr);
 // after chol_factor: 3x3 blocks of (L L^T)^{-1} at the given poses (old index),
 // row-major 9 doubles each into host memory out (synchronises the stream)
 // diagnostics: the step stamps of the last factorisation run with PGO_STEP_STAMPS
@@ -196,6 +229,6 @@ hipError_t chol_marginals(const CholPlan& P, const int* poses, int n, double* ou
 // after chol_factor: x = L^-T y = (L L^T)^{-1} scale_b b, indexed by old pose
 // lane y's solution to x + y * xstride
 hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb = 1, long long xstride = 0,
-                      LaunchProfile* prof = nullptr);
+                      LaunchProfile* prof = nullptr, ExchangeHook* hook = nullptr);
 
 }  // namespace pgo

@@ -1288,6 +1288,47 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
   }
 }
 
+// ------------------------------------------------------------ partition exchange
+// Subtree roots' payloads (partitioned factorisation): the lower triangle of
+// the update matrix U (u x u, column-major inside the front at (w, w)), packed
+// column by column (column j: rows j..u-1 at j u - j (j - 1) / 2), then the
+// update vector fv[w..m).  One workgroup per root, a wave per column.
+// tasks: (front, payload offset in buf, u, 0); unpack reverses it.
+template <bool kPack>
+__global__ __launch_bounds__(256) void k_xroots(CholDev c, const int4* __restrict__ tasks, double* __restrict__ buf) {
+  const int4 t = tasks[blockIdx.x];
+  const int s = t.x, u = t.z, m = c.m[s], w = c.w[s];
+  double* U = c.F + c.foff[s] + w + (size_t)w * m;
+  double* v = c.fv + c.voff[s] + w;
+  double* b = buf + t.y;
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (int j = wv; j < u; j += 4) {
+    double* col = b + (size_t)j * u - (size_t)j * (j - 1) / 2;
+    for (int i = j + l; i < u; i += 64) {
+      if (kPack) col[i - j] = U[i + (size_t)j * m];
+      else U[i + (size_t)j * m] = col[i - j];
+    }
+  }
+  double* bv = b + (size_t)u * (u + 1) / 2;
+  for (int i = threadIdx.x; i < u; i += 256) {
+    if (kPack) bv[i] = v[i];
+    else v[i] = bv[i];
+  }
+}
+
+// Solution ranges of the subtrees: (rank, first, end, offset) -- pack: buf[off +
+// k] = xv[first + k]; unpack: xv[first + k] = buf[rank * slot + off + k]
+template <bool kPack>
+__global__ __launch_bounds__(256) void k_xsol(CholDev c, const int4* __restrict__ ranges, double* __restrict__ buf,
+                                              long long slot) {
+  const int4 r = ranges[blockIdx.y];
+  const int n = r.z - r.y;
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
+    if (kPack) buf[r.w + k] = c.xv[r.y + k];
+    else c.xv[r.y + k] = buf[r.x * slot + r.w + k];
+  }
+}
+
 // ------------------------------------------------------------ solves
 __global__ __launch_bounds__(256) void k_perm_in(CholDev c, const double* __restrict__ b, double scale, int n) {
   lane_offset(c);
@@ -1674,6 +1715,30 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(up(&P.d_syrk, P.syrk_tasks, s));
   CH_TRY(up(&P.d_sdiag, P.sdiag_tasks, s));
   CH_TRY(up(&P.d_col, P.col_tasks, s));
+  {   // partition exchange lists (this rank's roots / the others' needed ones) and buffers
+    std::vector<int4> own, foreign, sown, sforeign;
+    const long long slot = std::max(P.xmax, 1LL);
+    if (P.part_size > 1 && (long long)P.part_size * std::max(P.xmax, P.xsol_max) >= (1LL << 31))
+      return hipErrorInvalidValue;   // int offsets
+    for (size_t q = 0; q < P.xroot.size(); q++) {
+      const int sr = P.xroot[q], r = P.xroot_rank[q], u = P.m[sr] - P.w[sr];
+      if (u == 0) continue;
+      if (r == P.part_rank) own.push_back(make_int4(sr, (int)P.xroot_off[q], u, 0));
+      else if (P.parent[sr] >= 0) foreign.push_back(make_int4(sr, (int)(r * slot + P.xroot_off[q]), u, 0));
+    }
+    for (const int4& rg : P.xsol_ranges) (rg.x == P.part_rank ? sown : sforeign).push_back(rg);
+    P.n_xown = (int)own.size();
+    P.n_xforeign = (int)foreign.size();
+    P.n_xsol_own = (int)sown.size();
+    P.n_xsol_foreign = (int)sforeign.size();
+    CH_TRY(up(&P.d_xown, own, s));
+    CH_TRY(up(&P.d_xforeign, foreign, s));
+    CH_TRY(up(&P.d_xsol_own, sown, s));
+    CH_TRY(up(&P.d_xsol_foreign, sforeign, s));
+    const long long xs = P.part_size > 1 ? std::max({P.xmax, P.xsol_max, 1LL}) : 1;
+    CH_TRY(hipMalloc((void**)&P.d_xsend, sizeof(double) * xs));
+    CH_TRY(hipMalloc((void**)&P.d_xrecv, sizeof(double) * xs * std::max(P.part_size, 1)));
+  }
   CH_TRY(up(&P.d_at_iptr, P.at_iptr, s));
   CH_TRY(up(&P.d_at_items, P.at_items, s));
   CH_TRY(alloc_numeric(P, std::max(P.batch, 1), s));
@@ -1689,7 +1754,7 @@ void chol_free(CholPlan& P) {
   void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
                   P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
                   P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
-                  P.d_syrk, P.d_ea_tasks, P.d_ea_pairs, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_at_iptr, P.d_at_items, P.d_col, P.d_stepflag};
+                  P.d_syrk, P.d_ea_tasks, P.d_ea_pairs, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_at_iptr, P.d_at_items, P.d_col, P.d_stepflag, P.d_xown, P.d_xforeign, P.d_xsol_own, P.d_xsol_foreign, P.d_xsend, P.d_xrecv};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : P.evs)
@@ -1728,7 +1793,7 @@ static void launch(LaunchProfile* prof, int fam, Cost cost, K kern, dim3 grid, d
 }
 
 hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
-                       hipStream_t s, LaunchProfile* prof, int nb) {
+                       hipStream_t s, LaunchProfile* prof, int nb, ExchangeHook* hook) {
   if (P.n == 0) return hipSuccess;
   if (nb < 1 || nb > P.batch) return hipErrorInvalidValue;
   const CholDev c = dev_view(P);
@@ -1738,9 +1803,22 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
          B256, 0, s, c, b, scale_b, P.n);
   CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int) * nb, s));
   CH_TRY(hipMemsetAsync(P.d_stepflag, 0, sizeof(int) * std::max(P.ns, 1) * nb, s));
+  const bool part = P.part_size > 1;
+  if (part && (nb != 1 || !hook)) return hipErrorInvalidValue;
+  auto exchange = [&]() -> hipError_t {   // subtree roots -> every rank
+    if (P.n_xown) k_xroots<true><<<P.n_xown, 256, 0, s>>>(c, P.d_xown, P.d_xsend);
+    CH_TRY(hipGetLastError());
+    if (hook->allgather(hook->ctx, P.d_xsend, P.d_xrecv, sizeof(double) * std::max(P.xmax, 1LL), s) != 0) {
+      hook->failed = true;
+      return hipErrorUnknown;
+    }
+    if (P.n_xforeign) k_xroots<false><<<P.n_xforeign, 256, 0, s>>>(c, P.d_xforeign, P.d_xrecv);
+    return hipGetLastError();
+  };
   for (size_t li = 0; li < P.levels.size(); li++) {
     const CholLevel& lv = P.levels[li];
     if (prof) prof->cur_tag = (int)li << 16;
+    if (part && (int)li == P.split) CH_TRY(exchange());
     if (lv.ea_cnt[0])
       launch(prof, kFamAssemble, [&] { return make_double2(0, lv.at_bytes * nb); },
              k_assemble_tile, dim3(lv.ea_cnt[0], nb), B256, 0, s, c, (const int4*)(P.d_ea_tasks + lv.ea_off[0]),
@@ -1811,6 +1889,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       CH_TRY(hipStreamWaitEvent(s, P.evs[1], 0));
     }
   }
+  if (part && P.split >= (int)P.levels.size()) CH_TRY(exchange());
   return hipGetLastError();
 }
 
@@ -1845,7 +1924,8 @@ hipError_t chol_marginals(const CholPlan& P, const int* poses, int n, double* ou
   return e;
 }
 
-hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb, long long xstride, LaunchProfile* prof) {
+hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb, long long xstride, LaunchProfile* prof,
+                      ExchangeHook* hook) {
   if (P.n == 0) return hipSuccess;
   if (nb < 1 || nb > P.batch) return hipErrorInvalidValue;
   const CholDev c = dev_view(P);
@@ -1867,6 +1947,18 @@ hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb, long 
         launch(prof, kFamBwdStep, [&] { return make_double2(0, 0); }, k_bwd_step, dim3(lv.bwd[q].cnt, nb), B256, 0,
                s, c, (const int4*)(P.d_bwd + lv.bwd[q].off), bb);
     }
+  }
+  if (P.part_size > 1) {   // every rank's subtree solutions -> every rank
+    if (nb != 1 || !hook) return hipErrorInvalidValue;
+    if (P.n_xsol_own) k_xsol<true><<<dim3(16, P.n_xsol_own), 256, 0, s>>>(c, P.d_xsol_own, P.d_xsend, 0);
+    CH_TRY(hipGetLastError());
+    if (hook->allgather(hook->ctx, P.d_xsend, P.d_xrecv, sizeof(double) * std::max(P.xsol_max, 1LL), s) != 0) {
+      hook->failed = true;
+      return hipErrorUnknown;
+    }
+    if (P.n_xsol_foreign)
+      k_xsol<false><<<dim3(16, P.n_xsol_foreign), 256, 0, s>>>(c, P.d_xsol_foreign, P.d_xrecv, std::max(P.xsol_max, 1LL));
+    CH_TRY(hipGetLastError());
   }
   launch(prof, kFamPerm, [&] { return make_double2(0, 48.0 * P.n * nb); }, k_perm_out, dim3(g, nb), B256, 0, s, c, x,
          P.n, xstride);

@@ -169,6 +169,31 @@ int comm_allgather(Comm* c, const double* mine, int count, double* all, hipStrea
   return PGO_OK;
 }
 
+int comm_allgather_device(Comm* c, const void* send, void* recv, size_t bytes, hipStream_t s, std::string* err) {
+  hipError_t he;
+  if (c->size == 1 && !force_collectives(c)) {
+    he = hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s);
+    return he == hipSuccess ? PGO_OK : hip_fail(he, "all-gather copy", err);
+  }
+  if (c->host) {   // stage through host memory, the caller's all-gather, back
+    c->stage.resize(bytes * (c->size + 1));
+    char* mine = c->stage.data() + bytes * c->size;
+    he = hipMemcpyAsync(mine, send, bytes, hipMemcpyDeviceToHost, s);
+    if (he == hipSuccess) he = hipStreamSynchronize(s);
+    if (he != hipSuccess) return hip_fail(he, "all-gather download", err);
+    if (c->hc.allgather(c->hc.ctx, mine, c->stage.data(), bytes) != 0) {
+      *err = "host all-gather callback failed";
+      return PGO_E_COMM;
+    }
+    he = hipMemcpyAsync(recv, c->stage.data(), bytes * c->size, hipMemcpyHostToDevice, s);
+    if (he == hipSuccess) he = hipStreamSynchronize(s);
+    return he == hipSuccess ? PGO_OK : hip_fail(he, "all-gather upload", err);
+  }
+  const ncclResult_t e = rccl().all_gather(send, recv, bytes, ncclUint8, static_cast<ncclComm_t>(c->nccl), s);
+  if (e != ncclSuccess) return nccl_fail(e, "ncclAllGather", err);
+  return PGO_OK;
+}
+
 int comm_broadcast_device(Comm* c, void* dptr, size_t bytes, int root, hipStream_t s, std::string* err) {
   if ((c->size == 1 && !force_collectives(c)) || bytes == 0) return PGO_OK;
   hipError_t he;

@@ -1,9 +1,11 @@
 // Inter-rank exchange of the multi-GPU path (internal to libpgo.so).
 //
-// The only data-path exchange of the speculative lambda search:
-// per lambda round an all-gather of every rank's try outcome (4 doubles) and a
-// broadcast of the accepted candidate values (N double4) from the rank that
-// computed them.  Two transports behind one interface:
+// The data-path exchanges of the multi-GPU modes: speculative
+// lambda search -- per lambda round an all-gather of every rank's try outcome
+// (4 doubles) and a broadcast of the accepted candidate values (N double4) from
+// the rank that computed them; partitioned factorisation -- per factorisation
+// an all-gather of the subtree roots' update matrices / vectors and one of the
+// subtrees' solutions.  Two transports behind one interface:
 //   * RCCL (librccl.so.1 resolved at run time with dlopen; device buffers, the
 //     handle's HIP stream) -- xGMI between the GPUs of one node;
 //   * host callbacks (pgo_host_comm) -- the caller's own transport on host
@@ -42,6 +44,11 @@ int comm_allgather(Comm* c, const double* mine, int count, double* all, hipStrea
 // device buffer dptr[bytes] of rank `root` -> every rank (in place); returns
 // after the data has arrived (stream synchronised)
 int comm_broadcast_device(Comm* c, void* dptr, size_t bytes, int root, hipStream_t s, std::string* err);
+
+// device all-gather: recv[size * bytes] = every rank's send[bytes], rank order;
+// RCCL: enqueued on s (ncclAllGather over xGMI); host transport: staged and
+// synchronised (the partitioned factorisation's exchanges)
+int comm_allgather_device(Comm* c, const void* send, void* recv, size_t bytes, hipStream_t s, std::string* err);
 
 // PGO_COMM_FORCE_COLLECTIVES=1 on an RCCL communicator: exchanges run even at size 1
 bool force_collectives(const Comm* c);

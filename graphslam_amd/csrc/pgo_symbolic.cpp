@@ -433,10 +433,80 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   for (auto& v : hitems) std::stable_sort(v.begin(), v.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
     return a.first < b.first;
   });
-  // ---- level schedules
-  const int nl = ns ? *std::max_element(P.height.begin(), P.height.end()) + 1 : 0;
-  std::vector<std::vector<int>> bylevel(nl);
-  for (int s = 0; s < ns; s++) bylevel[P.height[s]].push_back(s);
+  // ---- multi-GPU subtree partition (part_size > 1, DESIGN.md "Multi-GPU"):
+  // rank part_rank factorises the fronts of its subtrees (phase 1), then every
+  // rank the replicated top fronts (phase 2), after the subtree roots' update
+  // matrices / vectors have been exchanged.  Storage only for the fronts this
+  // rank touches: its own, the top, and the other ranks' subtree roots (their
+  // update matrices arrive in the exchange).  One rank: everything is phase 1.
+  const int psz = std::max(P.part_size, 1), prk = P.part_rank;
+  P.owner = partition_subtrees(P, psz);
+  P.subtree_cnt.assign(ns, 1);
+  for (int s = 0; s < ns; s++)
+    if (P.parent[s] >= 0) P.subtree_cnt[P.parent[s]] += P.subtree_cnt[s];
+  std::vector<char> need(ns, 0);
+  P.xroot.clear();
+  P.xroot_rank.clear();
+  for (int s = 0; s < ns; s++) {
+    const bool root = P.owner[s] >= 0 && (P.parent[s] < 0 || P.owner[P.parent[s]] < 0);
+    if (root) {
+      P.xroot.push_back(s);
+      P.xroot_rank.push_back(P.owner[s]);
+    }
+    need[s] = P.owner[s] == prk || P.owner[s] < 0 || (root && P.parent[s] >= 0);
+  }
+  if (psz > 1) {   // offsets over the needed fronts only
+    for (int s = 0; s < ns; s++) {
+      const long long mm = need[s] ? P.m[s] : 0;
+      P.foff[s + 1] = P.foff[s] + ((mm * mm + 7) / 8) * 8;
+      P.voff[s + 1] = P.voff[s] + (need[s] ? ((P.m[s] + 7) / 8) * 8 : 0);
+      P.toff[s + 1] = P.toff[s] + (need[s] ? (long long)((P.w[s] + 63) / 64) * 4096 : 0);
+    }
+    P.ftotal = P.foff[ns];
+    P.ttotal = P.toff[ns];
+    P.vtotal = P.voff[ns];
+  }
+  // exchange layout: per rank its roots' payloads (packed lower update matrix,
+  // then the update vector) back to back; the solve's: its subtrees' poses
+  P.xroot_off.assign(P.xroot.size(), 0);
+  P.xsize.assign(psz, 0);
+  P.xsol_size.assign(psz, 0);
+  P.xsol_ranges.clear();
+  for (size_t q = 0; q < P.xroot.size(); q++) {
+    const int sr = P.xroot[q], r = P.xroot_rank[q];
+    const long long u = P.m[sr] - P.w[sr];
+    P.xroot_off[q] = P.xsize[r];
+    P.xsize[r] += u * (u + 1) / 2 + u;
+    const int first = sr - P.subtree_cnt[sr] + 1;   // the subtree: postorder fronts [first, sr]
+    P.xsol_ranges.push_back(make_int4(r, 3 * P.sfirst[first], 3 * P.sfirst[sr + 1], (int)P.xsol_size[r]));
+    P.xsol_size[r] += 3LL * (P.sfirst[sr + 1] - P.sfirst[first]);
+  }
+  P.xmax = *std::max_element(P.xsize.begin(), P.xsize.end());
+  P.xsol_max = *std::max_element(P.xsol_size.begin(), P.xsol_size.end());
+  // ---- level schedules: phase 1 (this rank's subtree fronts) then phase 2 (top)
+  std::vector<std::vector<int>> bylevel;
+  for (int phase = 0; phase < 2; phase++) {
+    int hmax = -1;
+    for (int s = 0; s < ns; s++)
+      if ((phase == 0 ? P.owner[s] == prk : P.owner[s] < 0)) hmax = std::max(hmax, P.height[s]);
+    const size_t base = bylevel.size();
+    bylevel.resize(base + hmax + 1);
+    for (int s = 0; s < ns; s++)
+      if ((phase == 0 ? P.owner[s] == prk : P.owner[s] < 0)) bylevel[base + P.height[s]].push_back(s);
+    if (phase == 0) P.split = (int)bylevel.size();
+  }
+  {   // drop empty levels (a height with no front of this rank), keeping the split
+    std::vector<std::vector<int>> kept;
+    int split = 0;
+    for (size_t L = 0; L < bylevel.size(); L++)
+      if (!bylevel[L].empty()) {
+        kept.push_back(std::move(bylevel[L]));
+        if ((int)L < P.split) split++;
+      }
+    bylevel.swap(kept);
+    P.split = split;
+  }
+  const int nl = (int)bylevel.size();
   P.levels.assign(nl, CholLevel());
   P.small_list.clear();
   P.level_fronts.clear();
@@ -706,6 +776,67 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       lv.panels.push_back(ps);
     }
   }
+}
+
+}  // namespace pgo
+
+namespace pgo {
+
+// Subtree partition of the supernodal tree over `size` ranks (the partitioned
+// multi-GPU factorisation): starting from the tree roots, the heaviest
+// candidate subtree (by factorisation flops) is split -- its root joins the
+// replicated "top" and its children become candidates -- until every
+// candidate holds at most 1/(2 size) of the candidates' flops (or cannot be
+// split); the candidates are then dealt to ranks largest first, each to the
+// least-loaded rank.  owner[s] = rank of front s's subtree, -1 for top fronts.
+// Deterministic: every rank computes the same partition from the same plan.
+std::vector<int> partition_subtrees(const CholPlan& P, int size, std::vector<double>* rank_flops,
+                                    double* top_flops) {
+  const int ns = P.ns;
+  std::vector<double> f(ns, 0.0), sub(ns, 0.0);
+  for (int s = 0; s < ns; s++) {
+    for (int k = 0; k < P.w[s]; k++) {
+      const double r = P.m[s] - k - 1;
+      f[s] += 1 + r + r * (r + 1);
+    }
+    sub[s] += f[s];
+    if (P.parent[s] >= 0) sub[P.parent[s]] += sub[s];   // children precede parents (postorder)
+  }
+  std::vector<int> owner(ns, -1), cand;
+  for (int s = 0; s < ns; s++)
+    if (P.parent[s] < 0) cand.push_back(s);
+  if (size > 1) {
+    for (;;) {
+      double tot = 0;
+      int best = -1;
+      for (int c : cand) {
+        tot += sub[c];
+        if (best < 0 || sub[c] > sub[best]) best = c;
+      }
+      if (best < 0 || sub[best] <= tot / (2.0 * size) || P.cptr[best] == P.cptr[best + 1]) break;
+      cand.erase(std::find(cand.begin(), cand.end(), best));
+      for (int q = P.cptr[best]; q < P.cptr[best + 1]; q++) cand.push_back(P.children[q]);
+    }
+  }
+  std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) { return sub[a] > sub[b]; });
+  std::vector<double> load(size, 0.0);
+  std::vector<int> root_rank(ns, -1);
+  for (int c : cand) {
+    const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    load[r] += sub[c];
+    root_rank[c] = r;
+  }
+  for (int s = ns - 1; s >= 0; s--) {   // parents before children: inherit the subtree's rank
+    if (root_rank[s] >= 0) owner[s] = root_rank[s];
+    else if (P.parent[s] >= 0 && owner[P.parent[s]] >= 0) owner[s] = owner[P.parent[s]];
+  }
+  if (rank_flops) *rank_flops = load;
+  if (top_flops) {
+    *top_flops = 0;
+    for (int s = 0; s < ns; s++)
+      if (owner[s] < 0) *top_flops += f[s];
+  }
+  return owner;
 }
 
 }  // namespace pgo

@@ -169,6 +169,18 @@ class PoseGraph:
                     launches=int(out[f, 0]), ms=float(out[f, 1]), flops=float(out[f, 2]), bytes=float(out[f, 3]))
         return res
 
+    def debug_partition(self, size):
+        """Host-only: the PGO_MULTI_PARTITION subtree partition over `size`
+        ranks: (owner per supernode, -1 = replicated top; per-rank subtree
+        flops; top flops)."""
+        ns = self._check(self._L.pgo_debug_partition(self._h, int(size), None, None, 0))
+        cap = max(ns, size + 1)
+        owner = np.zeros(cap, np.int32)
+        out = np.zeros(cap)
+        self._check(self._L.pgo_debug_partition(self._h, int(size), owner.ctypes.data_as(C.POINTER(C.c_int)),
+                                                L.dptr(out), cap))
+        return owner[:ns], out[:size].copy(), float(out[size])
+
     def debug_ordering(self):
         """Host-only: the Cholesky solver's pose ordering (new -> insertion index)."""
         n = self.num_vertices

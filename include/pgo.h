@@ -107,7 +107,20 @@ typedef struct {
                                    about one pass for all lanes).  Speculative
                                    lambda search (see pgo_comm_*): results are
                                    those of 1 lane bit for bit [1] */
+  int multi_gpu;                /* with a communicator of size > 1 (pgo_comm_*):
+                                   PGO_MULTI_SPECULATIVE -- every rank solves
+                                   different lambda tries of GTSAM's sequence;
+                                   PGO_MULTI_PARTITION -- every try's
+                                   factorisation is split: each rank factors
+                                   its subtrees of the elimination tree, the
+                                   subtree roots' Schur complements are
+                                   all-gathered (the boundary reduction) and
+                                   the top separators factored on every rank
+                                   [PGO_MULTI_SPECULATIVE] */
 } pgo_params;
+
+#define PGO_MULTI_SPECULATIVE 0
+#define PGO_MULTI_PARTITION 1
 
 typedef struct {
   int status;                   /* PGO_OK / PGO_W_MAXITER / error                 */
@@ -300,6 +313,14 @@ int pgo_debug_solve(pgo_graph *g, double lambda, const pgo_params *params, doubl
  * trsm tasks, syrk tiles, small fronts; from out[16], 6 per level (leaves first):
  * fronts, max m, max 64-blocks, panel steps, small fronts, syrk tiles. */
 int pgo_debug_plan(pgo_graph *g, double *out, int cap);
+/* Host-only: the subtree partition the PGO_MULTI_PARTITION factorisation
+ * uses over `size` ranks: owner[s] per supernode (rank, -1 = replicated top;
+ * returns the supernode count, arrays filled up to cap) and out[0..size+1] =
+ * per-rank subtree flops, then the top's flops. */
+int pgo_debug_partition(pgo_graph *g, int size, int *owner, double *out, int cap);
+/* Host-only: the supernodal elimination tree (parent per supernode, -1 root);
+ * returns the supernode count. */
+int pgo_debug_parents(pgo_graph *g, int *parent, int cap);
 /* Host-only: the Cholesky solver's fill-reducing ordering of the poses
  * (perm[k] = insertion index of the k-th eliminated pose), n = vertex count.
  * bench.py hands it to the CPU restatement so both factor the same fill. */

@@ -76,5 +76,17 @@ int main(int argc, char** argv) {
     printf("level %2d: fronts %6d (small %6d) maxm %5d tiles %6d ea %6.1fM dbl, steps %3zu (inline %3d) potrf %5d trsm %6d syrk %7d\n",
            li++, lv.front_cnt, nsmall, lv.maxm, lv.ea_cnt[0], ea / 1e6, lv.panels.size(), nfused, npotrf, ntr, nsy);
   }
+  for (int size : {2, 4, 8}) {
+    std::vector<double> rf;
+    double top = 0;
+    const auto own = pgo::partition_subtrees(P, size, &rf, &top);
+    double mx = 0, sm = 0;
+    for (double v : rf) {
+      mx = std::max(mx, v);
+      sm += v;
+    }
+    printf("partition %d: top %.1f GFLOP (%.0f%%), subtrees %.1f GFLOP, max rank %.1f GFLOP -> bound %.2fx\n", size,
+           top / 1e9, 100 * top / P.flops, sm / 1e9, mx / 1e9, P.flops / (top + mx));
+  }
   return 0;
 }

@@ -72,6 +72,77 @@ def test_host_comm_selftest_gloo_world2():
         assert rs == (rank, 2)
 
 
+def _partition_worker(rank, world, port, q, case):
+    try:
+        dist = _init(rank, world, port)
+        import torch as _t
+        from graphslam_amd import datasets
+        from graphslam_amd.pose_graph import PoseGraph
+        pg = PoseGraph.from_dataset(datasets.make(case))
+        owner, rf, top = pg.debug_partition(world)
+        mine = _t.from_numpy(owner.astype(np.int64))
+        outs = [_t.empty_like(mine) for _ in range(world)]
+        dist.all_gather(outs, mine)
+        q.put((rank, [o.numpy() for o in outs], rf, top, None))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, None, None, repr(e)))
+
+
+@pytest.mark.parametrize("case", ["C1-nn", "C2"])
+def test_partition_plan_gloo_world2(case):
+    """PGO_MULTI_PARTITION's plan logic on CPU, two gloo ranks: both compute
+    the identical subtree partition of the elimination tree (every rank plans
+    for itself), every supernode is owned by exactly one rank or the
+    replicated top, the top is closed under parents, each rank's subtrees are
+    postorder ranges, and both ranks get work."""
+    out = _run(2, _partition_worker, (case,))
+    for rank, owners, rf, top, err in out:
+        assert err is None, err
+        assert np.array_equal(owners[0], owners[1])
+    owner = out[0][1][0]
+    from graphslam_amd import datasets
+    from graphslam_amd.pose_graph import PoseGraph
+    pg = PoseGraph.from_dataset(datasets.make(case))
+    w, m, lv = pg.debug_fronts()
+    assert len(owner) == len(w)
+    assert set(np.unique(owner)) <= {-1, 0, 1} and (owner == 0).any() and (owner == 1).any()
+    rf = out[0][2]
+    assert rf.min() > 0.25 * rf.max()                      # balanced within the LPT bound
+
+
+def test_partition_structure_sizes():
+    """Partition invariants for 2/4/8 ranks on C2 (host only): a front's rank
+    is its parent's unless the parent is top (subtrees are closed), the top is
+    closed under parents (an ancestor of a top front is top)."""
+    from graphslam_amd import datasets
+    from graphslam_amd.pose_graph import PoseGraph
+    g = datasets.make("C2")
+    pg = PoseGraph.from_dataset(g)
+    parent = _plan_parents(pg)
+    for size in (2, 4, 8):
+        owner, rf, top = pg.debug_partition(size)
+        for s, p in enumerate(parent):
+            if p < 0:
+                continue
+            if owner[p] >= 0:
+                assert owner[s] == owner[p]
+            if owner[s] < 0:
+                assert owner[p] < 0
+        assert top > 0 and len(rf) == size and (rf > 0).sum() >= min(size, 2)
+
+
+def _plan_parents(pg):
+    import ctypes as C
+    from graphslam_amd import _lib
+    L = _lib.lib()
+    ns = L.pgo_debug_fronts(pg._h, None, None, None, 0)
+    par = np.zeros(ns, np.int32)
+    rc = L.pgo_debug_parents(pg._h, par.ctypes.data_as(C.POINTER(C.c_int)), ns)
+    assert rc == ns
+    return par
+
+
 # ---------------------------------------------------------------- GPU
 def perturbed_c2():
     """C2 with heavy heading noise on the initial values: GTSAM's LM rejects
@@ -197,6 +268,24 @@ def test_speculative_lambda_oracle_trajectory():
     assert st["iterations"] == ref.stats["iterations"]
     assert st["inner_iterations"] == ref.stats["inner_iterations"]
     assert abs(st["final_error"] - ref.stats["final_error"]) <= 1e-8 * ref.stats["final_error"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,world", [("C2p", 2), ("C2p", 4), ("C3", 2)])
+def test_partitioned_factorisation_matches_one_rank(case, world):
+    """PGO_MULTI_PARTITION, ranks sharing cuda:0 over the host transport:
+    every try's factorisation split into the ranks' subtrees + the replicated
+    top, the subtree roots' Schur complements and the subtree solutions
+    all-gathered -- the LM trajectory and the final values are bitwise those
+    of one rank."""
+    st1, x1 = _single(case, {})
+    out = _run(world, _opt_worker, (case, dict(multi_gpu=1, lambda_lanes=1)), timeout=900)
+    for rank, st, x, err in out:
+        assert err is None, err
+        assert st["iterations"] == st1["iterations"]
+        assert st["inner_iterations"] == st1["inner_iterations"]
+        assert st["final_error"] == st1["final_error"]
+        np.testing.assert_array_equal(x, x1)
 
 
 @pytest.mark.gpu
