@@ -222,8 +222,9 @@ def main():
                     help="after the timed steps: time marginal covariances of this many poses (0: skip)")
     ap.add_argument("--lanes", type=int, default=2,
                     help="consecutive lambda tries per batched factorisation (pgo_params.lambda_lanes)")
-    ap.add_argument("--multi", choices=["spec", "replicas"], default="spec",
-                    help="N>1: speculative lambda search over RCCL (one job) or independent replicas")
+    ap.add_argument("--multi", choices=["spec", "partition", "replicas"], default="spec",
+                    help="N>1: speculative lambda search over RCCL (one job), partitioned factorisation "
+                         "(one job: subtrees per rank, Schur complements all-gathered) or independent replicas")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a one-GPU box: every rank on device 0, host (gloo) transport")
     ap.add_argument("--ordering", choices=["nd", "amd"], default="nd",
@@ -244,7 +245,8 @@ def main():
     from graphslam_amd import _lib
     ordering = _lib.PGO_ORDERING_AMD if args.ordering == "amd" else _lib.PGO_ORDERING_ND
     pg = PoseGraph.from_dataset(g, device=0 if args.same_device else r.local_rank, ordering=ordering)
-    spec = world > 1 and args.multi == "spec"
+    spec = world > 1 and args.multi in ("spec", "partition")   # one job over all ranks
+    part = world > 1 and args.multi == "partition"
     hc = None
     if spec:
         from graphslam_amd import multi_gpu
@@ -255,7 +257,8 @@ def main():
     pg.save_values()                     # upload graph + values once; snapshot the initial values
     params = default_params(profile_every=args.profile_every, max_outer=args.max_outer,
                             linear_solver=1 if args.solver == "cholesky" else 0,
-                            use_graphs=0 if args.no_graphs else 1, lambda_lanes=args.lanes)
+                            use_graphs=0 if args.no_graphs else 1, lambda_lanes=1 if part else args.lanes,
+                            multi_gpu=1 if part else 0)
 
     kprof = {}
 
@@ -331,8 +334,9 @@ def main():
             "config": {
                 "workload": f"{args.config}: {n} poses / {ne} between factors + 1 prior, Manhattan walk "
                             f"(seed {g.meta.get('seed')}), GTSAM-default LM from dead-reckoned values",
-                "poses": n, "edges": ne, "parallelism": (f"spec-lambda{world}" + ("-host" if args.same_device else "-rccl")) if spec
-                else f"replicas{world}",
+                "poses": n, "edges": ne,
+                "parallelism": ((f"partition{world}" if part else f"spec-lambda{world}") +
+                                ("-host" if args.same_device else "-rccl")) if spec else f"replicas{world}",
                 "lambda_lanes": args.lanes,
                 "solver": (f"GPU supernodal multifrontal Cholesky ({'nested-dissection' if args.ordering == 'nd' else 'AMD'} ordering, fp64 MFMA Schur updates)"
                            if args.solver == "cholesky" else
