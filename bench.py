@@ -174,6 +174,40 @@ def factor_roofline(kprof, totals, factor_flops):
     return out
 
 
+def live_resolve_bench(pg, g, k=5):
+    """The live node's per-registration re-solve (graph.cpp:180-200, :130):
+    starting at the optimum, k registrations, each appending one keyframe
+    (dead-reckoned initial value), its odometry factor and one loop closure
+    to an earlier keyframe (exact measurements), then optimize() on the same
+    handle -- the resident values, graph and solver plan are refreshed in place
+    (pgo_stats.plan_update).  Reports wall ms per registration (append +
+    optimize) and the plan work."""
+    import numpy as np
+    from graphslam_amd.datasets import between_xyt, compose_xyt
+    rng = np.random.default_rng(7)
+    n = g.num_poses
+    gt = np.array(g.ground_truth)
+    x = pg.poses()
+    cov = np.diag([0.05 ** 2, 0.05 ** 2, 0.00873 ** 2])
+    rows = []
+    for r in range(k):
+        v = n + r
+        step = np.array([1.0, 0.0, 0.0])
+        gt = np.vstack([gt, compose_xyt(gt[v - 1], step)])
+        x = np.vstack([x, compose_xyt(x[v - 1], step)])
+        j = int(rng.integers(0, v - 20))
+        t0 = time.perf_counter()
+        pg.add_vertex(v + 1, *x[v])
+        pg.add_edge(v, v + 1, between_xyt(gt[v - 1], gt[v]), cov)
+        pg.add_edge(v + 1, j + 1, between_xyt(gt[v], gt[j]), cov)
+        st = pg.optimize()
+        rows.append({"ms": 1e3 * (time.perf_counter() - t0), "plan_update": st["plan_update"],
+                     "ms_plan": st["ms_plan"], "ms_upload": st["ms_upload"], "linearizations": st["linearizations"],
+                     "lm_tries": st["inner_iterations"]})
+    return {"registrations": k, "ms_median": float(np.median([r["ms"] for r in rows])), "per_registration": rows,
+            "note": "append 1 keyframe + odometry + 1 loop closure, then optimize on the same handle"}
+
+
 def closest_keyframe_bench(pg, g, skip=10, reps=20):
     """closest_keyframe service (graph.cpp:146-178) at the optimum: one query
     over all keyframes (HBM scan: 16 B of (x, y) per candidate; the values are
@@ -231,6 +265,8 @@ def main():
                     help="fill-reducing ordering of the Cholesky solver (pgo_opts.ordering)")
     ap.add_argument("--search", type=int, default=1,
                     help="after the timed steps: time the closest_keyframe search at the optimum (0: skip)")
+    ap.add_argument("--live", type=int, default=5,
+                    help="after the timed steps: time this many per-registration re-solves (0: skip)")
     ap.add_argument("--max-outer", type=int, default=0,
                     help="profiling runs only: stop each optimize after this many linearisations")
     args = ap.parse_args()
@@ -288,6 +324,9 @@ def main():
     search = None
     if args.search and rank == 0:
         search = closest_keyframe_bench(pg, g)
+    live = None
+    if args.live and rank == 0 and not spec:
+        live = live_resolve_bench(pg, g, args.live)
     stats = [s for _, s in results]
     last = stats[-1]
     totals = dict(spmv_ms=sum(s["kernel_spmv_ms"] for s in stats), spmv_n=sum(s["kernel_spmv_count"] for s in stats),
@@ -367,6 +406,7 @@ def main():
             "cpu_baseline": None,
             "marginals": marg,
             "closest_keyframe": search,
+            "live_resolve": live,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(g, pg, out["per_step"], reps=args.cpu_reps)

@@ -69,7 +69,8 @@ class PgoStats(C.Structure):
                 ("kernel_syrk_launches", C.c_longlong), ("lambda_rounds", C.c_int), ("ranks", C.c_int),
                 ("solves", C.c_longlong), ("ms_comm", C.c_double),
                 ("ms_factor_profiled", C.c_double), ("ms_solve_profiled", C.c_double), ("stop_reason", C.c_int),
-                ("ms_factor_graph", C.c_double), ("factor_graph_flops", C.c_double)]
+                ("ms_factor_graph", C.c_double), ("factor_graph_flops", C.c_double),
+                ("plan_update", C.c_int), ("ms_plan", C.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}

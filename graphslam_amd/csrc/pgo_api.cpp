@@ -69,6 +69,9 @@ struct pgo_graph {
   pgo::CholPlan chol;
   int ordering = pgo::kOrderNd;             // fill-reducing ordering (pgo_opts.ordering)
   int part_size = 1;                        // subtree partition the plan must have (PGO_MULTI_PARTITION)
+  bool plan_stale = false;                  // the graph changed since the plan was built (kept, see ensure_chol)
+  int plan_update = 0;                      // how the last ensure_chol refreshed it (pgo_stats.plan_update)
+  double plan_ms = 0.0;
   pgo::ExchangeHook hook;                   // the partitioned factorisation's all-gathers (comm)
   bool chol_ready = false;
   // profiled factorisations (pgo_params.profile_every): every launch timed
@@ -184,7 +187,7 @@ void free_lanes(pgo_graph* g) {
     }
 }
 
-void free_device(pgo_graph* g) {
+void free_device(pgo_graph* g, bool keep_plan = false) {
   free_lanes(g);
   g->lane_cap = 8;
   DevGraph& d = g->d;
@@ -198,6 +201,10 @@ void free_device(pgo_graph* g) {
   g->dev_structure = false;
   g->dev_values = false;
   drop_graphs(g);
+  if (keep_plan && g->chol_ready) {   // the structure changed: ensure_chol decides what to keep
+    g->plan_stale = true;
+    return;
+  }
   if (g->chol_ready) pgo::chol_free(g->chol);
   g->chol_ready = false;
 }
@@ -248,15 +255,16 @@ int h2d(pgo_graph* g, T* dst, const T* src, size_t count) {
     if (rc_ != PGO_OK) return rc_; \
   } while (0)
 
-// Host values -> device pose (Pose2(x, y, theta): Rot2::fromAngle)
-int upload_values(pgo_graph* g) {
+// Host values -> device pose (Pose2(x, y, theta): Rot2::fromAngle), vertices
+// [first, n) (the ones before stay as they are on the device)
+int upload_values(pgo_graph* g, size_t first = 0) {
   const size_t n = g->keys.size();
-  std::vector<double4> h(n);
-  for (size_t i = 0; i < n; i++) {
+  std::vector<double4> h(n > first ? n - first : 0);
+  for (size_t i = first; i < n; i++) {
     const double th = g->xyt[3 * i + 2];
-    h[i] = make_double4(g->xyt[3 * i], g->xyt[3 * i + 1], std::cos(th), std::sin(th));
+    h[i - first] = make_double4(g->xyt[3 * i], g->xyt[3 * i + 1], std::cos(th), std::sin(th));
   }
-  RC_TRY(h2d(g, g->d.pose, h.data(), n));
+  RC_TRY(h2d(g, g->d.pose + first, h.data(), n - std::min(n, first)));
   HIP_TRY(g, hipStreamSynchronize(g->d.stream));
   g->dev_values = true;
   return PGO_OK;
@@ -438,7 +446,15 @@ int upload_structure(pgo_graph* g) {
     hpom[3 * t + 1] = make_double2(o[2], o[3]);
     hpom[3 * t + 2] = make_double2(o[4], o[5]);
   }
-  free_device(g);
+  // the values already resident stay bit for bit (no host atan2 -> cos / sin
+  // round trip): vertices are append-only, so the first n_old keep their index
+  double4* keep = nullptr;
+  const int n_old = g->dev_values && g->d.pose ? std::min(g->d.n, n) : 0;
+  if (n_old > 0) {
+    HIP_TRY(g, hipMalloc((void**)&keep, sizeof(double4) * n_old));
+    HIP_TRY(g, hipMemcpyAsync(keep, g->d.pose, sizeof(double4) * n_old, hipMemcpyDeviceToDevice, g->d.stream));
+  }
+  free_device(g, true);
   DevGraph& d = g->d;
   d.n = n;
   d.ne = ne;
@@ -533,7 +549,12 @@ int upload_structure(pgo_graph* g) {
   HIP_TRY(g, hipMemsetAsync(d.part, 0, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices, d.stream));
   HIP_TRY(g, hipStreamSynchronize(d.stream));
   g->dev_structure = true;
-  return upload_values(g);
+  if (n_old > 0) {
+    HIP_TRY(g, hipMemcpyAsync(d.pose, keep, sizeof(double4) * n_old, hipMemcpyDeviceToDevice, d.stream));
+    HIP_TRY(g, hipStreamSynchronize(d.stream));
+    (void)hipFree(keep);
+  }
+  return upload_values(g, n_old);
 }
 
 int ensure_device(pgo_graph* g) {
@@ -570,6 +591,8 @@ int exchange_allgather(void* ctx, const void* send, void* recv, size_t bytes, hi
   return rc == PGO_OK ? 0 : -1;
 }
 
+int bind_plan(pgo_graph* g, bool full);
+
 int ensure_chol(pgo_graph* g) {
   const int psz = g->part_size > 1 ? g->comm.size : 1, prk = psz > 1 ? g->comm.rank : 0;
   if (g->chol_ready && (g->chol.part_size != psz || g->chol.part_rank != prk)) {   // other partition: re-plan
@@ -580,16 +603,79 @@ int ensure_chol(pgo_graph* g) {
     g->chol_ready = false;
     g->lane_cap = 8;
   }
+  const auto t0 = std::chrono::steady_clock::now();
+  auto timed = [&](int kind) {
+    g->plan_update = kind;
+    g->plan_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  };
+  g->plan_update = 0;
+  g->plan_ms = 0.0;
+  std::vector<int> order_in;
+  if (g->chol_ready && g->plan_stale) {
+    // the graph grew since the plan (pgo_add_edge / pgo_add_vertex after an
+    // optimize: the live per-registration re-solve, graph.cpp:180-200).  Factors
+    // whose blocks fit the plan's fronts (a loop closure inside existing fill):
+    // keep the plan, rebuild only the H assembly lists.  New vertices / fill:
+    // re-plan on the previous ordering with the new poses inserted in front of
+    // their earliest-eliminated neighbour (no new nested dissection) while the
+    // appended part is small; otherwise a full analysis.
+    pgo::CholPlan& P = g->chol;
+    const int n = g->d.n;
+    if (pgo::chol_covers(P, n, g->h_row_ptr, g->h_slot_col)) {
+      pgo::chol_assembly(P, g->h_row_ptr, g->h_slot_col);
+      RC_TRY(bind_plan(g, false));
+      g->plan_stale = false;
+      timed(1);
+      return PGO_OK;
+    }
+    if (n >= P.n && n - P.n <= std::max(256, P.n / 10)) {
+      // (base, order): old pose k -> (iperm[k], 0); a new pose -> (min base of its
+      // already-placed neighbours, -(index)), so it is eliminated just before that
+      // neighbour, later new poses before earlier ones (leaves of the chain first)
+      const int n0 = P.n;
+      std::vector<long long> key(n);
+      for (int k = 0; k < n0; k++) key[k] = (long long)P.iperm[k] << 32;
+      for (int v = n0; v < n; v++) {
+        long long base = n;
+        for (int q = g->h_row_ptr[v]; q < g->h_row_ptr[v + 1]; q++) {
+          const int u = g->h_slot_col[q];
+          if (u < v) base = std::min(base, key[u] >> 32);
+        }
+        key[v] = (base << 32) | (0x7fffffffLL - (v - n0 + 1));   // below the old pose's 0x7fffffff
+      }
+      for (int k = 0; k < n0; k++) key[k] |= 0x7fffffffLL;
+      order_in.resize(n);
+      for (int k = 0; k < n; k++) order_in[k] = k;
+      std::stable_sort(order_in.begin(), order_in.end(), [&](int a, int b) { return key[a] < key[b]; });
+    }
+    (void)hipStreamSynchronize(g->d.stream);
+    free_lanes(g);
+    drop_graphs(g);
+    pgo::chol_free(P);
+    g->chol_ready = false;
+    g->lane_cap = 8;
+  }
+  g->plan_stale = false;
   if (g->chol_ready) return PGO_OK;
   g->chol.ordering = g->ordering;
   g->chol.part_size = psz;
   g->chol.part_rank = prk;
+  g->chol.order_in = order_in;
   g->hook.ctx = g;
   g->hook.allgather = exchange_allgather;
   pgo::chol_analyze(g->chol, g->d.n, g->h_row_ptr, g->h_slot_col);
-  // owner slot of every factor := its block in the lower triangle of the
-  // permuted matrix (the one the assembly reads); with write_all = 0 the
-  // linearisation writes only these
+  RC_TRY(bind_plan(g, true));
+  g->chol_ready = true;
+  timed(order_in.empty() ? 3 : 2);
+  return PGO_OK;
+}
+
+// Bind the plan to the device graph: owner slot of every factor := its block
+// in the lower triangle of the permuted matrix (the one the assembly reads;
+// with write_all = 0 the linearisation writes only these), the assembly's
+// sources remapped slot -> factor, and the plan (full) or its assembly lists
+// uploaded.
+int bind_plan(pgo_graph* g, bool full) {
   {
     const int n = g->d.n;
     std::vector<int> slot_edge = g->h_slot_edge;
@@ -605,7 +691,7 @@ int ensure_chol(pgo_graph* g) {
     for (size_t k = 0; k < slot_edge.size(); k++)
       if (slot_edge[k] & 2) eside[slot_edge[k] >> 2] = (unsigned char)(slot_edge[k] & 1);
     for (auto& src : g->chol.asm_src) src = slot_edge[src] >> 2;
-    const hipError_t e = pgo::chol_upload(g->chol, g->d.stream);
+    const hipError_t e = full ? pgo::chol_upload(g->chol, g->d.stream) : pgo::chol_upload_assembly(g->chol, g->d.stream);
     if (e != hipSuccess) {
       pgo::chol_free(g->chol);
       return fail(g, e == hipErrorOutOfMemory ? PGO_E_NOMEM : PGO_E_HIP,
@@ -618,7 +704,6 @@ int ensure_chol(pgo_graph* g) {
                                 hipMemcpyHostToDevice, g->d.stream));
     HIP_TRY(g, hipStreamSynchronize(g->d.stream));
   }
-  g->chol_ready = true;
   return PGO_OK;
 }
 
@@ -1250,7 +1335,11 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   g->part_size = partition ? g->comm.size : 1;
   // Cholesky: the plan (and the owner bits it assigns) first, then the
   // linearisation writes only the blocks the assembly reads
-  if (p.linear_solver != PGO_SOLVER_PCG && d.n > 0) RC_TRY(ensure_chol(g));
+  if (p.linear_solver != PGO_SOLVER_PCG && d.n > 0) {
+    RC_TRY(ensure_chol(g));
+    st.plan_update = g->plan_update;
+    st.ms_plan = g->plan_ms;
+  }
   d.write_all = p.linear_solver == PGO_SOLVER_PCG ? 1 : 0;
   // One lambda try (GTSAM tryLambda): solve (H + lam I) delta = -g, retract into
   // pose_cand, error there and the linear model decrease; one read-back.

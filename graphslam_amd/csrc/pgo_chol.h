@@ -75,6 +75,7 @@ enum { kOrderNd = 0, kOrderAmd = 1 };
 struct CholPlan {
   int ordering = kOrderNd;         // fill-reducing ordering of the pose graph (input of chol_analyze)
   int part_size = 1, part_rank = 0; // subtree partition over ranks (input of chol_analyze)
+  std::vector<int> order_in;       // optional given ordering (new -> old) instead of ND / AMD (input)
   int batch = 1;                   // lambda lanes with a numeric workspace (input of chol_upload)
   // ---- host symbolic result ----
   int n = 0, ns = 0;
@@ -172,7 +173,13 @@ std::vector<int> partition_subtrees(const CholPlan& P, int size, std::vector<dou
 
 // host: symbolic analysis from the block-CSR pattern (old pose indices)
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
+// host: (re)build the plan's H assembly lists for a pattern its fronts hold
+void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
+// host: does the plan's factor structure hold every block of this pattern?
+bool chol_covers(const CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
 hipError_t chol_upload(CholPlan& P, hipStream_t s);
+// device: re-upload the assembly lists after chol_assembly (same fronts)
+hipError_t chol_upload_assembly(CholPlan& P, hipStream_t s);
 void chol_free(CholPlan& P);
 // numeric workspaces for nb lambda lanes (P.batch); on failure one lane is kept
 // and the allocation error returned

@@ -1685,6 +1685,23 @@ hipError_t chol_set_batch(CholPlan& P, int nb, hipStream_t s) {
   return hipSuccess;
 }
 
+hipError_t chol_upload_assembly(CholPlan& P, hipStream_t s) {
+  CH_TRY(hipStreamSynchronize(s));
+  for (void** p : {(void**)&P.d_asm_front, (void**)&P.d_asm_li, (void**)&P.d_asm_lj, (void**)&P.d_asm_ptr,
+                   (void**)&P.d_asm_src, (void**)&P.d_at_iptr, (void**)&P.d_at_items}) {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+  }
+  CH_TRY(up(&P.d_asm_front, P.asm_front, s));
+  CH_TRY(up(&P.d_asm_li, P.asm_li, s));
+  CH_TRY(up(&P.d_asm_lj, P.asm_lj, s));
+  CH_TRY(up(&P.d_asm_ptr, P.asm_ptr, s));
+  CH_TRY(up(&P.d_asm_src, P.asm_src, s));
+  CH_TRY(up(&P.d_at_iptr, P.at_iptr, s));
+  CH_TRY(up(&P.d_at_items, P.at_items, s));
+  return hipStreamSynchronize(s);
+}
+
 hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(up(&P.d_toff, P.toff, s));
   CH_TRY(up(&P.d_m, P.m, s));

@@ -172,7 +172,10 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       xadj[i + 1] = (int)adj.size();
     }
   }
-  const std::vector<int> order0 = P.ordering == kOrderAmd ? order_amd(n, xadj, adj) : order_nd(n, xadj, adj);
+  // a caller-given ordering (the incremental re-plan: the previous ordering
+  // with the appended poses inserted) skips the fill-reducing ordering
+  const std::vector<int> order0 = (int)P.order_in.size() == n ? P.order_in
+                                  : P.ordering == kOrderAmd ? order_amd(n, xadj, adj) : order_nd(n, xadj, adj);
   std::vector<int> ip0(n);
   for (int k = 0; k < n; k++) ip0[order0[k]] = k;
   // ---- elimination tree of the permuted pattern (Liu, path compression)
@@ -378,61 +381,12 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.height.assign(ns, 0);
   for (int s = 0; s < ns; s++)  // children precede parents (postorder)
     if (P.parent[s] >= 0) P.height[P.parent[s]] = std::max(P.height[P.parent[s]], P.height[s] + 1);
-  // ---- assembly of H's lower blocks: block H_{i,j} (i > j, new) lives in the
-  // slots of block-CSR row perm[i] whose column is perm[j]; parallel factors
-  // between the same pair are summed in slot order.
-  struct Ent {
-    int j, i, k;
-  };
-  std::vector<Ent> ents;
-  ents.reserve(slot_col.size() / 2 + 1);
-  for (int r = 0; r < n; r++) {
-    const int i = P.iperm[r];
-    for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) {
-      const int j = P.iperm[slot_col[k]];
-      if (i > j) ents.push_back({j, i, k});
-    }
-  }
-  std::sort(ents.begin(), ents.end(), [&](const Ent& a, const Ent& b) {
-    return a.j != b.j ? a.j < b.j : (a.i != b.i ? a.i < b.i : a.k < b.k);
-  });
-  P.asm_front.clear();
-  P.asm_li.clear();
-  P.asm_lj.clear();
-  P.asm_ptr.assign(1, 0);
-  P.asm_src.clear();
-  for (size_t t = 0; t < ents.size(); t++) {
-    if (t == 0 || ents[t].i != ents[t - 1].i || ents[t].j != ents[t - 1].j) {
-      if (t) P.asm_ptr.push_back((int)P.asm_src.size());
-      const int s = snode[ents[t].j];
-      P.asm_front.push_back(s);
-      P.asm_lj.push_back(ents[t].j - P.sfirst[s]);
-      P.asm_li.push_back(local_of(s, ents[t].i));
-    }
-    P.asm_src.push_back(ents[t].k);
-  }
-  P.asm_ptr.push_back((int)P.asm_src.size());
-  if (ents.empty()) P.asm_ptr.assign(1, 0);
   P.dg_front.resize(n);
   P.dg_loc.resize(n);
   for (int j = 0; j < n; j++) {
     P.dg_front[j] = snode[j];
     P.dg_loc[j] = j - P.sfirst[snode[j]];
   }
-  // H entries by front tile: every 64x64 lower tile of a front lists the 3x3
-  // blocks of H (off-diagonal targets t >= 0, diagonal blocks ~pose) with an
-  // element in it (a block can straddle tile boundaries)
-  std::vector<std::vector<std::pair<int, int>>> hitems(ns);   // per front: (tile, item)
-  auto add_item = [&](int sf, int r0, int c0, int item) {
-    for (int ti = r0 / 64; ti <= (r0 + 2) / 64; ti++)
-      for (int tj = c0 / 64; tj <= (c0 + 2) / 64; tj++)
-        if (ti >= tj) hitems[sf].emplace_back(ti * (ti + 1) / 2 + tj, item);
-  };
-  for (size_t t = 0; t < P.asm_front.size(); t++) add_item(P.asm_front[t], 3 * P.asm_li[t], 3 * P.asm_lj[t], (int)t);
-  for (int j = 0; j < n; j++) add_item(P.dg_front[j], 3 * P.dg_loc[j], 3 * P.dg_loc[j], ~j);
-  for (auto& v : hitems) std::stable_sort(v.begin(), v.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
-    return a.first < b.first;
-  });
   // ---- multi-GPU subtree partition (part_size > 1, DESIGN.md "Multi-GPU"):
   // rank part_rank factorises the fronts of its subtrees (phase 1), then every
   // rank the replicated top fronts (phase 2), after the subtree roots' update
@@ -520,8 +474,6 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.npart = 0;
   P.ea_tasks.clear();
   P.ea_pairs.clear();
-  P.at_items.clear();
-  P.at_iptr.clear();
   for (int L = 0; L < nl; L++) {
     CholLevel& lv = P.levels[L];
     lv.front_off = (int)P.level_fronts.size();
@@ -595,38 +547,14 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
             tiles[(size_t)runs[i].x * (runs[i].x + 1) / 2 + runs[j].x].push_back(
                 make_int4(c, runs[i].y, runs[j].y, runs[i].z | (runs[j].z << 8)));
       }
-      const auto& hv = hitems[sp];
-      size_t hq = 0;
       for (int ti = 0; ti < nt; ti++)
         for (int tj = 0; tj <= ti; tj++) {
-          const int key = ti * (ti + 1) / 2 + tj;
-          const auto& v = tiles[key];
-          const int i0 = (int)P.at_items.size();
-          while (hq < hv.size() && hv[hq].first < key) hq++;
-          while (hq < hv.size() && hv[hq].first == key) P.at_items.push_back(hv[hq++].second);
-          P.at_iptr.push_back(make_int2(i0, (int)P.at_items.size() - i0));
+          const auto& v = tiles[ti * (ti + 1) / 2 + tj];
           P.ea_tasks.push_back(make_int4(sp, (ti << 16) | tj, (int)P.ea_pairs.size(), (int)v.size()));
           P.ea_pairs.insert(P.ea_pairs.end(), v.begin(), v.end());
         }
     }
     lv.ea_cnt.push_back((int)P.ea_tasks.size() - lv.ea_off.back());
-    for (int q = lv.ea_off[0]; q < lv.ea_off[0] + lv.ea_cnt[0]; q++) {   // algorithmic bytes (profiles)
-      const int4 t = P.ea_tasks[q];
-      double e = 0, h = 0;   // children's elements read + tile elements written; H slots read
-      for (int k = 0; k < t.w; k++) {
-        const int4 pr = P.ea_pairs[t.z + k];
-        const int nr = pr.w & 0xff, ncl = pr.w >> 8;
-        for (int r = 0; r < nr; r++) e += std::min(std::max(pr.y + r - pr.z + 1, 0), ncl);
-      }
-      const int2 it = P.at_iptr[q];
-      for (int k = 0; k < it.y; k++) {
-        const int code = P.at_items[it.x + k];
-        h += code >= 0 ? 72.0 * (P.asm_ptr[code + 1] - P.asm_ptr[code]) : 48.0;
-      }
-      const int mp = P.m[t.x], R0 = 64 * (t.y >> 16), C0 = 64 * (t.y & 0xffff);
-      for (int j = C0; j < std::min(C0 + 64, mp); j++) e += std::max(0, std::min(R0 + 64, mp) - std::max(R0, j));
-      lv.at_bytes += 8.0 * e + h;
-    }
     // small fronts (m <= kSmallFront): with w <= kWaveW one wavefront each (the
     // m x w panel in LDS, the rank-w Schur update streamed), largest first;
     // else one workgroup each with the whole front in LDS, launched per size
@@ -776,6 +704,123 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       lv.panels.push_back(ps);
     }
   }
+  chol_assembly(P, row_ptr, slot_col);
+}
+
+// Assembly of H into the plan's fronts (k_assemble_tile's H entries): the
+// targets (lower 3x3 blocks H_{i,j}, i > j, of the permuted pattern: front,
+// local row, local column, and their block-CSR slots -- parallel factors summed
+// in slot order) and, per tile task, the targets and diagonal blocks with an
+// element in the tile.  Depends on the pattern and the plan's fronts only: the
+// incremental path re-runs it alone when appended factors fit the fronts.
+void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
+  const int n = P.n, ns = P.ns;
+  P.nslots = (long long)slot_col.size();
+  auto local_of = [&](int s, int i) {  // local pose index of new pose i in front s (rows: own, then below)
+    const int f = P.sfirst[s], l = P.sfirst[s + 1];
+    if (i < l) return i - f;
+    const int* b0 = P.rows.data() + P.rptr[s] + (l - f);
+    const int* b1 = P.rows.data() + P.rptr[s + 1];
+    return (l - f) + (int)(std::lower_bound(b0, b1, i) - b0);
+  };
+  struct Ent {
+    int j, i, k;
+  };
+  std::vector<Ent> ents;
+  ents.reserve(slot_col.size() / 2 + 1);
+  for (int r = 0; r < n; r++) {
+    const int i = P.iperm[r];
+    for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) {
+      const int j = P.iperm[slot_col[k]];
+      if (i > j) ents.push_back({j, i, k});
+    }
+  }
+  std::sort(ents.begin(), ents.end(), [&](const Ent& a, const Ent& b) {
+    return a.j != b.j ? a.j < b.j : (a.i != b.i ? a.i < b.i : a.k < b.k);
+  });
+  P.asm_front.clear();
+  P.asm_li.clear();
+  P.asm_lj.clear();
+  P.asm_ptr.assign(1, 0);
+  P.asm_src.clear();
+  for (size_t t = 0; t < ents.size(); t++) {
+    if (t == 0 || ents[t].i != ents[t - 1].i || ents[t].j != ents[t - 1].j) {
+      if (t) P.asm_ptr.push_back((int)P.asm_src.size());
+      const int s = P.dg_front[ents[t].j];
+      P.asm_front.push_back(s);
+      P.asm_lj.push_back(ents[t].j - P.sfirst[s]);
+      P.asm_li.push_back(local_of(s, ents[t].i));
+    }
+    P.asm_src.push_back(ents[t].k);
+  }
+  P.asm_ptr.push_back((int)P.asm_src.size());
+  if (ents.empty()) P.asm_ptr.assign(1, 0);
+  // H entries by front tile: every 64x64 lower tile of a front lists the 3x3
+  // blocks of H (off-diagonal targets t >= 0, diagonal blocks ~pose) with an
+  // element in it (a block can straddle tile boundaries)
+  std::vector<std::vector<std::pair<int, int>>> hitems(ns);   // per front: (tile, item)
+  auto add_item = [&](int sf, int r0, int c0, int item) {
+    for (int ti = r0 / 64; ti <= (r0 + 2) / 64; ti++)
+      for (int tj = c0 / 64; tj <= (c0 + 2) / 64; tj++)
+        if (ti >= tj) hitems[sf].emplace_back(ti * (ti + 1) / 2 + tj, item);
+  };
+  for (size_t t = 0; t < P.asm_front.size(); t++) add_item(P.asm_front[t], 3 * P.asm_li[t], 3 * P.asm_lj[t], (int)t);
+  for (int j = 0; j < n; j++) add_item(P.dg_front[j], 3 * P.dg_loc[j], 3 * P.dg_loc[j], ~j);
+  for (auto& v : hitems) std::stable_sort(v.begin(), v.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
+    return a.first < b.first;
+  });
+  P.at_items.clear();
+  P.at_iptr.assign(P.ea_tasks.size(), make_int2(0, 0));
+  std::vector<size_t> hq(ns, 0);
+  for (size_t q = 0; q < P.ea_tasks.size(); q++) {   // a front's tile tasks come in key order
+    const int4 t = P.ea_tasks[q];
+    const int ti = t.y >> 16, tj = t.y & 0xffff, key = ti * (ti + 1) / 2 + tj;
+    const auto& hv = hitems[t.x];
+    size_t& h = hq[t.x];
+    const int i0 = (int)P.at_items.size();
+    while (h < hv.size() && hv[h].first < key) h++;
+    while (h < hv.size() && hv[h].first == key) P.at_items.push_back(hv[h++].second);
+    P.at_iptr[q] = make_int2(i0, (int)P.at_items.size() - i0);
+  }
+  for (CholLevel& lv : P.levels) {   // algorithmic bytes of the levels' k_assemble_tile (profiles)
+    lv.at_bytes = 0;
+    for (int q = lv.ea_off[0]; q < lv.ea_off[0] + lv.ea_cnt[0]; q++) {
+      const int4 t = P.ea_tasks[q];
+      double e = 0, h = 0;   // children's elements read + tile elements written; H slots read
+      for (int k = 0; k < t.w; k++) {
+        const int4 pr = P.ea_pairs[t.z + k];
+        const int nr = pr.w & 0xff, ncl = pr.w >> 8;
+        for (int r = 0; r < nr; r++) e += std::min(std::max(pr.y + r - pr.z + 1, 0), ncl);
+      }
+      const int2 it = P.at_iptr[q];
+      for (int k = 0; k < it.y; k++) {
+        const int code = P.at_items[it.x + k];
+        h += code >= 0 ? 72.0 * (P.asm_ptr[code + 1] - P.asm_ptr[code]) : 48.0;
+      }
+      const int mp = P.m[t.x], R0 = 64 * (t.y >> 16), C0 = 64 * (t.y & 0xffff);
+      for (int j = C0; j < std::min(C0 + 64, mp); j++) e += std::max(0, std::min(R0 + 64, mp) - std::max(R0, j));
+      lv.at_bytes += 8.0 * e + h;
+    }
+  }
+}
+
+// Does the plan's factor structure hold every block of the pattern (old pose
+// indices)?  Block (r, c) with new indices i < j must have row j in the front of
+// column i (its own poses or its below rows).
+bool chol_covers(const CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
+  if (n != P.n) return false;
+  for (int r = 0; r < n; r++)
+    for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) {
+      int i = P.iperm[r], j = P.iperm[slot_col[k]];
+      if (i == j) continue;
+      if (i > j) std::swap(i, j);
+      const int s = P.dg_front[i];
+      if (j < P.sfirst[s + 1]) continue;
+      const int* b0 = P.rows.data() + P.rptr[s] + (P.sfirst[s + 1] - P.sfirst[s]);
+      const int* b1 = P.rows.data() + P.rptr[s + 1];
+      if (!std::binary_search(b0, b1, j)) return false;
+    }
+  return true;
 }
 
 }  // namespace pgo

@@ -163,6 +163,12 @@ typedef struct {
      performed (lanes x one factorisation's flops) */
   double ms_factor_graph;
   double factor_graph_flops;
+  /* the solver's plan on this call (the per-registration re-solve): 0 reused,
+     1 same fronts / new H assembly (appended factors inside the existing fill),
+     2 re-planned on the previous ordering with the appended poses inserted,
+     3 full analysis (first call, or too much appended); ms_plan its host+upload ms */
+  int plan_update;
+  double ms_plan;
 } pgo_stats;
 
 /* pgo_stats.stop_reason.  GTSAM reports every one of these as convergence

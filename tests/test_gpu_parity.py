@@ -529,3 +529,84 @@ def test_c5_full_size_against_fixture(pg_cls):
     ea = float(gold["error_after"])
     assert abs(st["final_error"] - ea) <= 1e-8 * ea
     assert_poses(pg.poses()[idx], gold["poses_after_sample"], 1e-6, 1e-7)
+
+
+# ------------------------------------------------------------ incremental re-solve
+def _extend(g, x_now, new_pairs, n_new, rng):
+    """g plus `new_pairs` loop closures (exact ground-truth measurements) and
+    `n_new` appended poses continuing the walk (odometry + one closure each to an
+    old pose); returns (extended graph, its initial values = x_now + dead-reckoned
+    new poses, the appended vertices / edges)."""
+    from graphslam_amd.datasets import PoseGraph as DG, between_xyt, compose_xyt, _diag_cov, SIGMA
+    n = g.num_poses
+    gt = np.array(g.ground_truth)
+    init = np.array(x_now)
+    ei, ej = [], []
+    for i, j in new_pairs:
+        ei.append(i)
+        ej.append(j)
+    for k in range(n_new):
+        v = n + k
+        step = np.array([1.0, 0.0, (np.pi / 2) * (k % 3 == 2)])
+        gt = np.vstack([gt, compose_xyt(gt[v - 1], step)])
+        init = np.vstack([init, compose_xyt(init[v - 1], step)])
+        ei.append(v - 1)
+        ej.append(v)
+        ei.append(v)
+        ej.append(int(rng.integers(0, n - 20)))
+    ei, ej = np.array(ei), np.array(ej)
+    z = between_xyt(gt[ei], gt[ej])
+    keys = np.arange(1, n + n_new + 1, dtype=np.uint64)
+    ext = DG(name="ext", keys=keys, initial=init, ground_truth=gt,
+             edge_k1=np.concatenate([g.edge_k1, (ei + 1).astype(np.uint64)]),
+             edge_k2=np.concatenate([g.edge_k2, (ej + 1).astype(np.uint64)]),
+             edge_z=np.concatenate([g.edge_z, z]), edge_cov=np.concatenate([g.edge_cov, _diag_cov(SIGMA, len(ei))]),
+             prior_keys=g.prior_keys, prior_pose=g.prior_pose, prior_cov=g.prior_cov)
+    return ext, init, (ei, ej, z)
+
+
+@pytest.mark.parametrize("n_new", [0, 6])
+def test_incremental_append_matches_oracle(pg_cls, oracle_lib, n_new):
+    """graph.cpp:180-200 / :130: after an optimize, loop closures (parallel to
+    existing ones -- inside the plan's fill -- and new ones) and appended poses
+    are added to the same handle; the next optimize keeps the resident values
+    bit for bit, refreshes the solver plan incrementally (no full analysis) and
+    matches the oracle's optimize of the extended graph from the same values."""
+    g = datasets.make("C2")
+    pg = pg_cls.from_dataset(g)
+    pg.optimize()
+    x_now = pg.poses()
+    rng = np.random.default_rng(11)
+    i_lc, j_lc = g.edge_index()
+    par = [(int(i_lc[q]), int(j_lc[q])) for q in rng.choice(np.arange(g.num_poses - 1, g.num_edges), 8)]
+    newp = [(int(a), int(a) - 30 - int(rng.integers(0, 50))) for a in rng.integers(200, g.num_poses, 4)]
+    ext, init, (ei, ej, z) = _extend(g, x_now, par + newp, n_new, rng)
+    for v in range(g.num_poses, g.num_poses + n_new):
+        pg.add_vertex(v + 1, *init[v])
+    cov = np.diag(datasets.SIGMA ** 2)
+    for a, b, zz in zip(ei, ej, z):
+        pg.add_edge(int(a) + 1, int(b) + 1, zz, cov)
+    st = pg.optimize()
+    assert st["plan_update"] in (1, 2)                    # no new nested dissection
+    assert abs(st["initial_error"] - oracle_lib.Oracle(ext).error(init)) <= 1e-9 * st["initial_error"]
+    ref = oracle_lib.Oracle(ext).optimize(init=init)
+    assert st["iterations"] == ref.stats["iterations"]
+    assert abs(st["final_error"] - ref.stats["final_error"]) <= 1e-8 * ref.stats["final_error"]
+    assert_poses(pg.poses(), ref.poses, 1e-6, 1e-7)
+
+
+def test_incremental_loop_closure_inside_fill_keeps_plan(pg_cls):
+    """A loop closure parallel to an existing factor changes no fill: the plan's
+    fronts are kept (plan_update 1), only its H assembly is rebuilt; the values
+    already resident are kept bit for bit."""
+    g = datasets.make("C1-nn")
+    pg = pg_cls.from_dataset(g)
+    pg.optimize()
+    pg.save_values()
+    before = pg.poses()
+    i, j = g.edge_index()
+    cov = np.diag(datasets.SIGMA ** 2)
+    pg.add_edge(int(i[-1]) + 1, int(j[-1]) + 1, g.edge_z[-1], cov)
+    assert np.array_equal(pg.poses(), before)
+    st = pg.optimize(max_outer=1)
+    assert st["plan_update"] == 1 and st["ms_plan"] > 0
