@@ -85,6 +85,18 @@ class PgoHostComm(C.Structure):
                 ("allgather", ALLGATHER_FN), ("broadcast", BROADCAST_FN)]
 
 
+class PgoGicpParams(C.Structure):
+    _fields_ = [("max_iterations", C.c_int), ("k_correspondences", C.c_int), ("gicp_epsilon", C.c_double),
+                ("max_correspondence_distance", C.c_double), ("transformation_epsilon", C.c_double),
+                ("rotation_epsilon", C.c_double), ("max_inner_iterations", C.c_int)]
+
+
+class PgoGicpResult(C.Structure):
+    _fields_ = [("T", C.c_double * 16), ("converged", C.c_int), ("iterations", C.c_int),
+                ("fitness", C.c_double), ("delta", C.c_double * 3), ("cov", C.c_double * 9),
+                ("keyframe", C.c_int)]
+
+
 
 def build():
     subprocess.run(["make", "-s", "-C", os.path.join(HERE, "csrc")], check=True)
@@ -152,6 +164,14 @@ def lib():
         "pgo_debug_ordering": (C.c_int, [vp, C.POINTER(C.c_int32), C.c_size_t]),
         "pgo_debug_partition": (C.c_int, [vp, C.c_int, C.POINTER(C.c_int), dp, C.c_int]),
         "pgo_debug_parents": (C.c_int, [vp, C.POINTER(C.c_int), C.c_int]),
+        "pgo_gicp_default_params": (None, [C.POINTER(PgoGicpParams)]),
+        "pgo_gicp_create": (vp, [C.c_int]),
+        "pgo_gicp_destroy": (None, [vp]),
+        "pgo_gicp_last_error": (C.c_char_p, [vp]),
+        "pgo_gicp_align_batch": (C.c_int, [vp, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_int),
+                                           C.POINTER(C.c_float), C.POINTER(C.c_int), dp,
+                                           C.POINTER(PgoGicpParams), C.POINTER(PgoGicpResult)]),
+        "pgo_gicp_debug_ms": (C.c_int, [vp, dp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -338,3 +338,76 @@ def straight_chain(n=10, step=1.0):
     gt = np.zeros((n, 3))
     gt[:, 0] = step * np.arange(n)
     return noise_free(gt, [(k, k + 1) for k in range(n - 1)], name="chain")
+
+
+# ---------------------------------------------------------------- laser scans (scan registration, 8f row 4)
+def laser_world(seed=7, width=20.0, height=12.0, boxes=6):
+    """A rectangular room with `boxes` axis-aligned boxes: (m, 4) wall segments
+    (x0, y0, x1, y1) -- the kind of world the reference's Stage simulation scans."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    seg = [(0, 0, width, 0), (width, 0, width, height), (width, height, 0, height), (0, height, 0, 0)]
+    rects = []
+    for _ in range(boxes):
+        w, h = rng.uniform(0.5, 2.0, size=2)
+        x, y = rng.uniform(1.0, width - 3.0), rng.uniform(1.0, height - 3.0)
+        rects.append((x, y, x + w, y + h))
+        seg += [(x, y, x + w, y), (x + w, y, x + w, y + h), (x + w, y + h, x, y + h), (x, y + h, x, y)]
+    return np.array(seg, dtype=np.float64), np.array(rects, dtype=np.float64)
+
+
+def simulate_scan(segments, pose, n_beams=360, range_max=10.0, noise=0.01, rng=None):
+    """sensor_msgs/LaserScan ranges of a 360-degree laser at pose (x, y, theta):
+    beam i at angle_min + i * angle_increment (angle_min = -pi), the nearest wall
+    hit (+ N(0, noise^2)), range_max + 1 where nothing is hit within range_max."""
+    x, y, th = pose
+    inc = 2 * np.pi / n_beams
+    a = -np.pi + np.arange(n_beams) * inc
+    d = np.stack([np.cos(th + a), np.sin(th + a)], axis=1)                  # (n, 2)
+    p0, e = segments[:, :2], segments[:, 2:] - segments[:, :2]              # (m, 2)
+    ap = p0 - np.array([x, y])
+    den = d[:, None, 0] * e[None, :, 1] - d[:, None, 1] * e[None, :, 0]     # cross(d, e)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t = (ap[None, :, 0] * e[None, :, 1] - ap[None, :, 1] * e[None, :, 0]) / den
+        u = (ap[None, :, 0] * d[:, None, 1] - ap[None, :, 1] * d[:, None, 0]) / den
+    ok = (np.abs(den) > 1e-12) & (t > 1e-9) & (u >= 0) & (u <= 1)
+    r = np.where(ok, t, np.inf).min(axis=1)
+    if rng is not None and noise > 0:
+        r = r + rng.normal(0.0, noise, size=r.shape)
+    r = np.where(r < range_max, r, range_max + 1.0)
+    return r.astype(np.float32), -np.pi, inc, 0.05, range_max
+
+
+def _xyt_to_T(p):
+    c, s = np.cos(p[2]), np.sin(p[2])
+    T = np.eye(4)
+    T[:2, :2] = [[c, -s], [s, c]]
+    T[:2, 3] = p[:2]
+    return T
+
+
+def scan_pairs(count, seed=11, n_beams=360, motion=(0.3, 0.1, 0.05), noise=0.01, range_max=10.0):
+    """`count` registration pairs in one world: (source cloud = scan at pose B,
+    target cloud = scan at pose A, true T = A^-1 B) with B = A o motion (each
+    component scaled by U(0.5, 1.5) and a random sign), the scanner's
+    gicp(current, keyframe) shape (scanner.cpp:115)."""
+    from .scanner import scan_to_pointcloud
+    segs, rects = laser_world(seed)
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+
+    def free(p):
+        return not np.any((p[0] > rects[:, 0] - 0.3) & (p[0] < rects[:, 2] + 0.3) &
+                          (p[1] > rects[:, 1] - 0.3) & (p[1] < rects[:, 3] + 0.3))
+    out = []
+    while len(out) < count:
+        A = np.array([rng.uniform(1.5, 18.5), rng.uniform(1.5, 10.5), rng.uniform(-np.pi, np.pi)])
+        m = np.array(motion) * rng.uniform(0.5, 1.5, size=3) * rng.choice([-1.0, 1.0], size=3)
+        TB = _xyt_to_T(A) @ _xyt_to_T(m)
+        B = np.array([TB[0, 3], TB[1, 3], np.arctan2(TB[1, 0], TB[0, 0])])
+        if not (free(A) and free(B)):
+            continue
+        ca = scan_to_pointcloud(*simulate_scan(segs, A, n_beams, range_max, noise, rng))
+        cb = scan_to_pointcloud(*simulate_scan(segs, B, n_beams, range_max, noise, rng))
+        if len(ca) < 30 or len(cb) < 30:
+            continue
+        out.append((cb, ca, _xyt_to_T(m)))
+    return out

@@ -264,6 +264,48 @@ int pgo_closest_keyframes(pgo_graph *g, size_t q, const uint64_t *query_keys, in
 /* device time (ms) of the last scan / batch search kernel launch */
 int pgo_debug_search_ms(pgo_graph *g, double *scan_ms, double *batch_ms);
 
+/* ---- scan registration: Generalized-ICP -----------------
+   The scanner node's gicp() (scanner/src/scanner.cpp:35-74):
+   pcl::GeneralizedIterativeClosestPoint<PointXYZ, PointXYZ> with PCL's default
+   parameters, setInputSource(current scan) / setInputTarget(keyframe scan),
+   align(), hasConverged(), getFitnessScore(), getFinalTransformation(), then
+   make_Delta and compute_covariance (scanner.hpp) and the keyframe rule
+   (converged && fitness > converged_fitness_threshold = 0.1).  A batch of B
+   independent registrations (pair b: source cloud b -> target cloud b) runs as
+   one launch, one workgroup per registration.  Clouds are float xyz triplets,
+   concatenated (src: sum(src_n) x 3, tgt: sum(tgt_n) x 3), 1 .. 4096 points
+   each; guess: B x 16 row-major initial transforms (NULL = identity, as
+   align(output) without a guess).  The optimiser restates PCL's GICP with
+   Gauss-Newton where PCL runs BFGS (DESIGN.md "Scan registration"). */
+typedef struct pgo_gicp pgo_gicp;
+typedef struct {
+  int max_iterations;                 /* 200   (GICP's max_iterations_) */
+  int k_correspondences;              /* 20    neighbours per covariance, <= 32 */
+  double gicp_epsilon;                /* 1e-3  smallest covariance eigenvalue */
+  double max_correspondence_distance; /* 5     (squared: 25) */
+  double transformation_epsilon;      /* 5e-4  translation-column change to stop */
+  double rotation_epsilon;            /* 2e-3  rotation-element change to stop */
+  int max_inner_iterations;           /* 20    optimiser steps per correspondence set */
+} pgo_gicp_params;
+typedef struct {
+  double T[16];      /* getFinalTransformation(), row-major, source -> target frame */
+  int converged;     /* hasConverged() (PCL sets it at max_iterations too) */
+  int iterations;    /* correspondence rounds */
+  double fitness;    /* getFitnessScore(): mean squared nearest-target distance */
+  double delta[3];   /* make_Delta: T(0,3), T(1,3), atan(T(1,0) / T(0,0)) */
+  double cov[9];     /* compute_covariance(0.1, 0.1, 0.1, delta), row-major */
+  int keyframe;      /* converged && fitness > 0.1 (scanner.cpp:55-58) */
+} pgo_gicp_result;
+void pgo_gicp_default_params(pgo_gicp_params *p);
+pgo_gicp *pgo_gicp_create(int device);
+void pgo_gicp_destroy(pgo_gicp *h);
+const char *pgo_gicp_last_error(const pgo_gicp *h);
+int pgo_gicp_align_batch(pgo_gicp *h, int B, const float *src, const int *src_n, const float *tgt,
+                         const int *tgt_n, const double *guess, const pgo_gicp_params *params,
+                         pgo_gicp_result *out);
+/* device time (ms) of the last batch (covariance + registration kernels) */
+int pgo_gicp_debug_ms(const pgo_gicp *h, double *ms);
+
 /* ---- multi-GPU: speculative lambda search ---------------------
    One process per GPU, every rank holding the same graph and values.  Where
    GTSAM's LM (graph.cpp:119) tries lambda, lambda*f, lambda*f^2, ... one after

@@ -186,3 +186,64 @@ class Oracle:
     def error(self, poses=None):
         poses = self.initial if poses is None else np.ascontiguousarray(poses, dtype=np.float64)
         return lib().orc_error(self.h, _dp(poses))
+
+
+# ---------------------------------------------------------------- scan registration
+def gicp_align(src, tgt, guess=None, k=20, eps=1e-3, max_it=200, max_inner=20, max_dist=5.0,
+               trans_eps=5e-4, rot_eps=2e-3):
+    """C restatement of the scanner's PCL GICP (gicp_oracle.c; scanner.cpp:35-50).
+    Returns (T 4x4, iterations, converged, fitness)."""
+    L = lib()
+    L.orc_gicp_align.argtypes = [C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_float), C.c_int, C.c_int, C.c_double,
+                                 C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.POINTER(C.c_double),
+                                 C.POINTER(C.c_double)]
+    s = np.ascontiguousarray(src, dtype=np.float32).reshape(-1, 3)
+    t = np.ascontiguousarray(tgt, dtype=np.float32).reshape(-1, 3)
+    G = np.eye(4) if guess is None else np.asarray(guess, dtype=np.float64).reshape(4, 4)
+    T12 = np.ascontiguousarray(np.concatenate([G[:3, :3].reshape(9), G[:3, 3]]))
+    out = np.zeros(3)
+    fp = C.POINTER(C.c_float)
+    rc = L.orc_gicp_align(s.ctypes.data_as(fp), len(s), t.ctypes.data_as(fp), len(t), k, eps, max_it, max_inner,
+                          max_dist, trans_eps, rot_eps, _dp(T12), _dp(out))
+    if rc != 0:
+        raise ValueError(f"orc_gicp_align: {rc}")
+    T = np.eye(4)
+    T[:3, :3] = T12[:9].reshape(3, 3)
+    T[:3, 3] = T12[9:]
+    return T, int(out[0]), bool(out[1]), float(out[2])
+
+
+def gicp_covariances(points, k=20, eps=1e-3):
+    """computeCovariances restated: (n, 3, 3)."""
+    L = lib()
+    L.orc_gicp_covariances.argtypes = [C.POINTER(C.c_float), C.c_int, C.c_int, C.c_double, C.POINTER(C.c_double)]
+    p = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+    c = np.zeros((len(p), 6))
+    if L.orc_gicp_covariances(p.ctypes.data_as(C.POINTER(C.c_float)), len(p), k, eps, _dp(c)) != 0:
+        raise ValueError("orc_gicp_covariances")
+    out = np.empty((len(p), 3, 3))
+    for a, (i, j) in enumerate([(0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2)]):
+        out[:, i, j] = out[:, j, i] = c[:, a]
+    return out
+
+
+def make_delta(T):
+    """scanner.hpp:55-61 on the float transform: (T(0,3), T(1,3), atan(T(1,0) / T(0,0)))."""
+    Tf = np.asarray(T, dtype=np.float32)
+    return float(Tf[0, 3]), float(Tf[1, 3]), float(np.arctan(np.float64(Tf[1, 0] / Tf[0, 0])))
+
+
+def compute_covariance(k_dd, k_rd, k_rr, delta):
+    """scanner.hpp:64-80 (off-diagonals left 0; the reference leaves them uninitialised)."""
+    dl = np.sqrt(delta[0] ** 2 + delta[1] ** 2)
+    Q = np.zeros((3, 3))
+    Q[0, 0] = Q[1, 1] = k_dd * dl
+    Q[2, 2] = k_rd * dl + k_rr * delta[2]
+    return Q
+
+
+def registration(src, tgt, guess=None, **kw):
+    """gicp() of scanner.cpp:35-74 restated end to end: (keyframe_flag, delta, Q, T, fitness)."""
+    T, it, conv, fit = gicp_align(src, tgt, guess, **kw)
+    d = make_delta(T)
+    return conv and fit > 0.1, d, compute_covariance(0.1, 0.1, 0.1, d), T, fit, it
