@@ -240,6 +240,54 @@ def closest_keyframe_bench(pg, g, skip=10, reps=20):
     }
 
 
+def scan_registration_bench(batch=1024, reps=3, cpu_sample=64):
+    """The scanner's gicp() (scanner.cpp:35-74) on synthetic
+    360-beam laser scans of a room: `batch` registrations (current scan ->
+    keyframe scan) in one pgo_gicp_align_batch launch pair.  Reports
+    registrations/s (device time and call time), the nearest-neighbour distance
+    evaluations the batch performed (covariance kNN + correspondence rounds +
+    fitness: the kernel's algorithmic work) per second, and the C restatement
+    on one core over a sample of the same pairs."""
+    import numpy as np
+    from graphslam_amd.datasets import scan_pairs
+    from graphslam_amd.scanner import ScanRegistrar
+    pairs = scan_pairs(batch, seed=11)
+    S, T = [p[0] for p in pairs], [p[1] for p in pairs]
+    reg = ScanRegistrar(0)
+    reg.align_batch(S[:64], T[:64])                          # warm
+    dev, wall = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = reg.align_batch(S, T, arrays=True)
+        wall.append(1e3 * (time.perf_counter() - t0))
+        dev.append(reg.device_ms())
+    ns = np.array([len(s) for s in S], float)
+    nt = np.array([len(t) for t in T], float)
+    it = out["iterations"].astype(float)
+    evals = float(np.sum(ns * ns + nt * nt + (it + 1) * ns * nt))
+    dms = float(np.median(dev))
+    res = {"batch": batch, "points_per_cloud": float(np.mean(np.concatenate([ns, nt]))),
+           "mean_iterations": float(it.mean()), "mean_optimiser_steps": float(out["inner_iterations"].mean()),
+           "keyframes": int(out["keyframe"].sum()),
+           "device_ms": dms, "call_ms": float(np.median(wall)),
+           "registrations_per_s": batch / (dms * 1e-3), "registrations_per_s_call": batch / (np.median(wall) * 1e-3),
+           "nn_evals": evals, "gnn_evals_per_s": evals / (dms * 1e-3) / 1e9}
+    try:
+        from oracle import oracle as orc
+        k = min(cpu_sample, batch)
+        t0 = time.perf_counter()
+        for b in range(k):
+            orc.gicp_align(S[b], T[b])
+        cpu_s = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": k / cpu_s, "unit": "registrations/s", "cores": 1, "kind": "port",
+                               "sample": f"first {k} pairs, oracle/gicp_oracle.c (brute-force neighbours, gcc -O3)"}
+        res["gpu_over_cpu"] = res["registrations_per_s"] / res["cpu_baseline"]["value"]
+    except Exception as e:   # the oracle is optional on the GPU box
+        res["cpu_baseline"] = {"error": str(e)}
+    reg.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -265,6 +313,8 @@ def main():
                     help="fill-reducing ordering of the Cholesky solver (pgo_opts.ordering)")
     ap.add_argument("--search", type=int, default=1,
                     help="after the timed steps: time the closest_keyframe search at the optimum (0: skip)")
+    ap.add_argument("--gicp", type=int, default=1024,
+                    help="scan registrations in the GICP batch line (0: skip)")
     ap.add_argument("--live", type=int, default=5,
                     help="after the timed steps: time this many per-registration re-solves (0: skip)")
     ap.add_argument("--max-outer", type=int, default=0,
@@ -324,6 +374,9 @@ def main():
     search = None
     if args.search and rank == 0:
         search = closest_keyframe_bench(pg, g)
+    scan = None
+    if args.gicp and rank == 0:
+        scan = scan_registration_bench(args.gicp)
     live = None
     if args.live and rank == 0 and not spec:
         live = live_resolve_bench(pg, g, args.live)
@@ -407,6 +460,7 @@ def main():
             "marginals": marg,
             "closest_keyframe": search,
             "live_resolve": live,
+            "scan_registration": scan,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(g, pg, out["per_step"], reps=args.cpu_reps)

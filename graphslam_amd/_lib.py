@@ -94,7 +94,7 @@ class PgoGicpParams(C.Structure):
 class PgoGicpResult(C.Structure):
     _fields_ = [("T", C.c_double * 16), ("converged", C.c_int), ("iterations", C.c_int),
                 ("fitness", C.c_double), ("delta", C.c_double * 3), ("cov", C.c_double * 9),
-                ("keyframe", C.c_int)]
+                ("keyframe", C.c_int), ("inner_iterations", C.c_int)]
 
 
 

@@ -58,6 +58,7 @@ class Registration:
     fitness: float          # getFitnessScore()
     converged: bool         # hasConverged()
     iterations: int
+    inner_iterations: int = 0   # optimiser steps over all rounds
 
 
 def default_params(**kw) -> L.PgoGicpParams:
@@ -68,6 +69,13 @@ def default_params(**kw) -> L.PgoGicpParams:
             raise AttributeError(f"pgo_gicp_params has no field {k!r}")
         setattr(p, k, v)
     return p
+
+
+_RESULT_DTYPE = np.dtype({"names": [f[0] for f in L.PgoGicpResult._fields_],
+                          "formats": [(np.float64, 16), np.int32, np.int32, np.float64, (np.float64, 3),
+                                      (np.float64, 9), np.int32, np.int32],
+                          "offsets": [getattr(L.PgoGicpResult, f[0]).offset for f in L.PgoGicpResult._fields_],
+                          "itemsize": C.sizeof(L.PgoGicpResult)})
 
 
 class ScanRegistrar:
@@ -90,9 +98,12 @@ class ScanRegistrar:
         except Exception:
             pass
 
-    def align_batch(self, sources, targets, guesses=None, params=None):
+    def align_batch(self, sources, targets, guesses=None, params=None, arrays=False):
         """Register sources[b] -> targets[b] for every b in one launch; returns a
-        list of Registration.  guesses: B x 4 x 4 (None: identity)."""
+        list of Registration (arrays=True: a dict of numpy arrays over the whole
+        batch -- T (B, 4, 4), delta (B, 3), cov (B, 3, 3), fitness, iterations,
+        inner_iterations, converged, keyframe -- without per-pair objects).
+        guesses: B x 4 x 4 (None: identity)."""
         B = len(sources)
         if len(targets) != B:
             raise ValueError("sources and targets differ in length")
@@ -112,13 +123,18 @@ class ScanRegistrar:
                                           T.ctypes.data_as(fp), tn.ctypes.data_as(ip), L.dptr(g), C.byref(p), res)
         if rc != L.PGO_OK:
             raise PgoError(rc, self._L.pgo_gicp_last_error(self._h).decode())
+        if arrays:
+            rec = np.frombuffer(res, dtype=_RESULT_DTYPE, count=B)
+            return {k: rec[k].copy() for k in _RESULT_DTYPE.names} | {
+                "T": rec["T"].reshape(B, 4, 4).copy(), "cov": rec["cov"].reshape(B, 3, 3).copy()}
         out = []
         for b in range(B):
             r = res[b]
             out.append(Registration(keyframe_flag=bool(r.keyframe), delta=tuple(r.delta),
                                     covariance=np.array(r.cov[:]).reshape(3, 3),
                                     transform=np.array(r.T[:]).reshape(4, 4), fitness=r.fitness,
-                                    converged=bool(r.converged), iterations=r.iterations))
+                                    converged=bool(r.converged), iterations=r.iterations,
+                                    inner_iterations=r.inner_iterations))
         return out
 
     def device_ms(self):

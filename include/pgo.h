@@ -295,6 +295,7 @@ typedef struct {
   double delta[3];   /* make_Delta: T(0,3), T(1,3), atan(T(1,0) / T(0,0)) */
   double cov[9];     /* compute_covariance(0.1, 0.1, 0.1, delta), row-major */
   int keyframe;      /* converged && fitness > 0.1 (scanner.cpp:55-58) */
+  int inner_iterations; /* optimiser steps over all rounds */
 } pgo_gicp_result;
 void pgo_gicp_default_params(pgo_gicp_params *p);
 pgo_gicp *pgo_gicp_create(int device);

@@ -24,6 +24,9 @@
 
 #define GICP_MAXK 32
 
+/* squared distance in one fixed evaluation order (the GPU's too) */
+static inline float dist2(float dx, float dy, float dz) { return fmaf(dz, dz, fmaf(dy, dy, dx * dx)); }
+
 /* cyclic Jacobi on a symmetric 3x3: a -> diagonal, v columns = eigenvectors */
 static void sym_eigen3(double a[3][3], double v[3][3]) {
   for (int i = 0; i < 3; i++)
@@ -70,8 +73,7 @@ static void gicp_covariances(const float* P, int n, int k, double eps, double* c
     }
     for (int j = 0; j < n; j++) {
       const float* r = P + 3 * j;
-      const float dx = r[0] - q[0], dy = r[1] - q[1], dz = r[2] - q[2];
-      const float d = dx * dx + dy * dy + dz * dz;
+      const float d = dist2(r[0] - q[0], r[1] - q[1], r[2] - q[2]);
       if (!(d < bd[k - 1])) continue;
       int t = k - 1;
       while (t > 0 && d < bd[t - 1]) {
@@ -139,8 +141,7 @@ static int nearest(const float* Q, int nq, const double w[3], float* best_out) {
   float best = INFINITY;
   int bj = -1;
   for (int j = 0; j < nq; j++) {
-    const float dx = Q[3 * j] - q0, dy = Q[3 * j + 1] - q1, dz = Q[3 * j + 2] - q2;
-    const float d = dx * dx + dy * dy + dz * dz;
+    const float d = dist2(Q[3 * j] - q0, Q[3 * j + 1] - q1, Q[3 * j + 2] - q2);
     if (d < best) {
       best = d;
       bj = j;
@@ -155,7 +156,8 @@ static void apply(const double T[12], const float* p, double w[3]) {
 }
 
 /* One registration.  T (12: R row-major | t) holds the guess on entry and the
- * result on return; out[0] iterations, out[1] converged, out[2] fitness. */
+ * result on return; out[0] iterations, out[1] converged, out[2] fitness, out[3]
+ * optimiser steps in total. */
 int orc_gicp_align(const float* S, int ns, const float* Q, int nq, int k, double eps, int max_it, int max_inner,
                    double max_dist, double trans_eps, double rot_eps, double* T, double* out) {
   if (ns < 1 || nq < 1 || k < 1 || k > GICP_MAXK) return -1;
@@ -170,7 +172,7 @@ int orc_gicp_align(const float* S, int ns, const float* Q, int nq, int k, double
   gicp_covariances(S, ns, k, eps, cs);
   gicp_covariances(Q, nq, k, eps, ct);
   const double thr2 = max_dist * max_dist;
-  int it = 0, conv = 0;
+  int it = 0, conv = 0, inner_total = 0;
   while (!conv) {
     /* correspondences and Mahalanobis matrices at the current T */
     for (int i = 0; i < ns; i++) {
@@ -199,6 +201,7 @@ int orc_gicp_align(const float* S, int ns, const float* Q, int nq, int k, double
     memcpy(Tprev, T, sizeof(Tprev));
     /* minimise (1/n) sum d^T M d: Gauss-Newton, left perturbation T <- exp(dw, dt) T */
     for (int inner = 0; inner < max_inner; inner++) {
+      inner_total++;
       double acc[28] = {0};
       for (int i = 0; i < ns; i++) {
         if (nn[i] < 0) continue;
@@ -225,30 +228,28 @@ int orc_gicp_align(const float* S, int ns, const float* Q, int nq, int k, double
       for (int r = 0; r < 6; r++)
         for (int c = r; c < 6; c++) A[r][c] = A[c][r] = acc[q++];
       for (int r = 0; r < 6; r++) b[r] = -acc[21 + r];
-      for (int kk = 0; kk < 6 && ok; kk++) {
+      double inv[6];   /* reciprocal pivots (the GPU's arithmetic) */
+      for (int kk = 0; kk < 6; kk++) {
         double s = A[kk][kk];
         for (int j = 0; j < kk; j++) s -= A[kk][j] * A[kk][j];
-        if (!(s > 0)) {
-          ok = 0;
-          break;
-        }
-        A[kk][kk] = sqrt(s);
+        ok = ok && s > 0;
+        inv[kk] = 1.0 / sqrt(ok ? s : 1.0);
         for (int i = kk + 1; i < 6; i++) {
           double v = A[i][kk];
           for (int j = 0; j < kk; j++) v -= A[i][j] * A[kk][j];
-          A[i][kk] = v / A[kk][kk];
+          A[i][kk] = v * inv[kk];
         }
       }
       if (!ok) break;
       for (int i = 0; i < 6; i++) {
         double v = b[i];
         for (int j = 0; j < i; j++) v -= A[i][j] * x[j];
-        x[i] = v / A[i][i];
+        x[i] = v * inv[i];
       }
       for (int i = 5; i >= 0; i--) {
         double v = x[i];
         for (int j = i + 1; j < 6; j++) v -= A[j][i] * x[j];
-        x[i] = v / A[i][i];
+        x[i] = v * inv[i];
       }
       const double th = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
       double E[3][3];
@@ -257,7 +258,8 @@ int orc_gicp_align(const float* S, int ns, const float* Q, int nq, int k, double
         E[1][0] = x[2]; E[1][1] = 1; E[1][2] = -x[0];
         E[2][0] = -x[1]; E[2][1] = x[0]; E[2][2] = 1;
       } else {
-        const double k0 = x[0] / th, k1 = x[1] / th, k2 = x[2] / th, c = cos(th), s = sin(th), v = 1 - c;
+        const double ith = 1.0 / th, k0 = x[0] * ith, k1 = x[1] * ith, k2 = x[2] * ith, c = cos(th), s = sin(th),
+                     v = 1 - c;
         E[0][0] = c + k0 * k0 * v; E[0][1] = k0 * k1 * v - k2 * s; E[0][2] = k0 * k2 * v + k1 * s;
         E[1][0] = k1 * k0 * v + k2 * s; E[1][1] = c + k1 * k1 * v; E[1][2] = k1 * k2 * v - k0 * s;
         E[2][0] = k2 * k0 * v - k1 * s; E[2][1] = k2 * k1 * v + k0 * s; E[2][2] = c + k2 * k2 * v;
@@ -291,6 +293,7 @@ int orc_gicp_align(const float* S, int ns, const float* Q, int nq, int k, double
   out[0] = it;
   out[1] = 1.0;
   out[2] = fit / ns;
+  out[3] = inner_total;
   free(cs); free(ct); free(M); free(nn);
   return 0;
 }

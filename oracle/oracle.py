@@ -192,7 +192,8 @@ class Oracle:
 def gicp_align(src, tgt, guess=None, k=20, eps=1e-3, max_it=200, max_inner=20, max_dist=5.0,
                trans_eps=5e-4, rot_eps=2e-3):
     """C restatement of the scanner's PCL GICP (gicp_oracle.c; scanner.cpp:35-50).
-    Returns (T 4x4, iterations, converged, fitness)."""
+    Returns (T 4x4, iterations, converged, fitness); gicp_align.last_inner holds
+    the optimiser steps of the call."""
     L = lib()
     L.orc_gicp_align.argtypes = [C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_float), C.c_int, C.c_int, C.c_double,
                                  C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.POINTER(C.c_double),
@@ -201,7 +202,7 @@ def gicp_align(src, tgt, guess=None, k=20, eps=1e-3, max_it=200, max_inner=20, m
     t = np.ascontiguousarray(tgt, dtype=np.float32).reshape(-1, 3)
     G = np.eye(4) if guess is None else np.asarray(guess, dtype=np.float64).reshape(4, 4)
     T12 = np.ascontiguousarray(np.concatenate([G[:3, :3].reshape(9), G[:3, 3]]))
-    out = np.zeros(3)
+    out = np.zeros(4)
     fp = C.POINTER(C.c_float)
     rc = L.orc_gicp_align(s.ctypes.data_as(fp), len(s), t.ctypes.data_as(fp), len(t), k, eps, max_it, max_inner,
                           max_dist, trans_eps, rot_eps, _dp(T12), _dp(out))
@@ -210,6 +211,7 @@ def gicp_align(src, tgt, guess=None, k=20, eps=1e-3, max_it=200, max_inner=20, m
     T = np.eye(4)
     T[:3, :3] = T12[:9].reshape(3, 3)
     T[:3, 3] = T12[9:]
+    gicp_align.last_inner = int(out[3])
     return T, int(out[0]), bool(out[1]), float(out[2])
 
 

@@ -132,7 +132,7 @@ def test_abi_rejects_bad_arguments(pgo_lib):
 # ---------------------------------------------------------------- GPU
 def _check_against_oracle(r, src, tgt, oracle_lib, guess=None):
     T, it, conv, fit = oracle_lib.gicp_align(src, tgt, guess)
-    assert r.iterations == it
+    assert r.iterations == it and r.inner_iterations == oracle_lib.gicp_align.last_inner
     assert r.converged == conv
     assert np.abs(r.transform - T).max() < 1e-6, np.abs(r.transform - T).max()
     assert abs(r.fitness - fit) <= 1e-6 * max(fit, 1e-9) + 1e-12
@@ -151,6 +151,11 @@ def test_gpu_matches_oracle_batch(oracle_lib, pairs):
     for r, (src, tgt, _) in zip(out, pairs):
         _check_against_oracle(r, src, tgt, oracle_lib)
     assert any(r.keyframe_flag for r in out) and not all(r.keyframe_flag for r in out)
+    arr = reg.align_batch([s for s, _, _ in pairs], [t for _, t, _ in pairs], arrays=True)
+    assert np.array_equal(arr["T"], np.stack([r.transform for r in out]))
+    assert np.array_equal(arr["fitness"], [r.fitness for r in out])
+    assert np.array_equal(arr["keyframe"].astype(bool), [r.keyframe_flag for r in out])
+    assert np.array_equal(arr["cov"], np.stack([r.covariance for r in out]))
 
 
 @pytest.mark.gpu
