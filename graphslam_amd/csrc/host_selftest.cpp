@@ -1,0 +1,94 @@
+// Host self-test of the solver's planning code (test infrastructure, not part
+// of libpgo.so): drives the symbolic analysis on synthetic pose graphs so a host
+// AddressSanitizer / UndefinedBehaviorSanitizer build (`make -C
+// graphslam_amd/csrc asan-host`) exercises its memory accesses --
+// nested-dissection and AMD orderings, supernodes, level schedule, panel steps,
+// the assembly lists, the subtree partition for 2 and 4 ranks, the incremental
+// paths (chol_covers / chol_assembly, a caller-given ordering).  No GPU calls.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "pgo_chol.h"
+
+namespace {
+
+struct Pattern {
+  int n = 0;
+  std::vector<int> row_ptr, col;
+};
+
+// block pattern of H for a chain of n poses with `lc` random loop closures
+Pattern make_pattern(int n, int lc, unsigned seed, const std::vector<std::pair<int, int>>& extra = {}) {
+  std::mt19937 rng(seed);
+  std::vector<std::pair<int, int>> e;
+  for (int i = 0; i + 1 < n; i++) e.emplace_back(i, i + 1);
+  for (int q = 0; q < lc; q++) {
+    const int a = 20 + (int)(rng() % (unsigned)(n - 20));
+    e.emplace_back(a, (int)(rng() % (unsigned)(a - 10)));
+  }
+  e.insert(e.end(), extra.begin(), extra.end());
+  Pattern P;
+  P.n = n;
+  std::vector<std::vector<int>> adj(n);
+  for (auto& [a, b] : e) {
+    adj[a].push_back(b);
+    adj[b].push_back(a);
+  }
+  P.row_ptr.assign(1, 0);
+  for (int i = 0; i < n; i++) {
+    adj[i].push_back(i);
+    std::sort(adj[i].begin(), adj[i].end());
+    adj[i].erase(std::unique(adj[i].begin(), adj[i].end()), adj[i].end());
+    P.col.insert(P.col.end(), adj[i].begin(), adj[i].end());
+    P.row_ptr.push_back((int)P.col.size());
+  }
+  return P;
+}
+
+int fail(const char* m) {
+  std::fprintf(stderr, "host_selftest: %s\n", m);
+  return 1;
+}
+
+}  // namespace
+
+int main() {
+  for (int ordering : {pgo::kOrderNd, pgo::kOrderAmd}) {
+    const Pattern G = make_pattern(3000, 400, 7);
+    pgo::CholPlan P;
+    P.ordering = ordering;
+    pgo::chol_analyze(P, G.n, G.row_ptr, G.col);
+    if (P.ns <= 0 || P.flops <= 0) return fail("analysis");
+    if (!pgo::chol_covers(P, G.n, G.row_ptr, G.col)) return fail("plan does not cover its own pattern");
+    for (int size : {2, 4}) {
+      std::vector<double> rf;
+      double top = 0;
+      const auto own = pgo::partition_subtrees(P, size, &rf, &top);
+      if ((int)own.size() != P.ns) return fail("partition size");
+      for (int r = 0; r < size; r++) {
+        pgo::CholPlan Q;
+        Q.ordering = ordering;
+        Q.part_size = size;
+        Q.part_rank = r;
+        pgo::chol_analyze(Q, G.n, G.row_ptr, G.col);
+        if (Q.ns != P.ns) return fail("partitioned plan");
+      }
+    }
+    // a loop closure inside the existing fill: same fronts, new assembly lists
+    const Pattern G2 = make_pattern(3000, 400, 7, {{2, 0}});
+    if (pgo::chol_covers(P, G2.n, G2.row_ptr, G2.col)) pgo::chol_assembly(P, G2.row_ptr, G2.col);
+    // appended poses re-planned on a given ordering
+    const Pattern G3 = make_pattern(3010, 400, 7, {{3009, 5}});
+    pgo::CholPlan R;
+    R.ordering = ordering;
+    R.order_in.resize(G3.n);
+    for (int k = 0; k < G3.n; k++) R.order_in[k] = G3.n - 1 - k;
+    pgo::chol_analyze(R, G3.n, G3.row_ptr, G3.col);
+    if (!pgo::chol_covers(R, G3.n, G3.row_ptr, G3.col)) return fail("given ordering");
+  }
+  std::printf("host selftest ok\n");
+  return 0;
+}

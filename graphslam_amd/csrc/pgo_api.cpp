@@ -17,6 +17,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "pgo.h"
 #include "pgo_chol.h"
 #include "pgo_comm.h"
@@ -106,6 +108,18 @@ struct pgo_graph {
   hipEvent_t sev_scan[2] = {}, sev_batch[2] = {};
   bool scan_timed = false, batch_timed = false;
 };
+
+namespace {
+// roctx range over a host scope (rocprofv3 --marker-trace shows the LM
+// structure: optimize > plan / linearisation > lambda rounds; a no-op without
+// a profiler attached)
+struct RoctxRange {
+  explicit RoctxRange(const char* m) { roctxRangePush(m); }
+  ~RoctxRange() { roctxRangePop(); }
+  RoctxRange(const RoctxRange&) = delete;
+  RoctxRange& operator=(const RoctxRange&) = delete;
+};
+}  // namespace
 
 namespace {
 
@@ -1283,6 +1297,7 @@ int pgo_error(pgo_graph* g, double* err) {
 }
 
 int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
+  RoctxRange range_opt("pgo_optimize");
   if (!g) return PGO_E_ARG;
   pgo_params p;
   if (params) p = *params;
@@ -1336,6 +1351,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   // Cholesky: the plan (and the owner bits it assigns) first, then the
   // linearisation writes only the blocks the assembly reads
   if (p.linear_solver != PGO_SOLVER_PCG && d.n > 0) {
+    RoctxRange range_plan("plan");
     RC_TRY(ensure_chol(g));
     st.plan_update = g->plan_update;
     st.ms_plan = g->plan_ms;
@@ -1404,6 +1420,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
     double new_err = err;
     for (;;) {
       const double cur_err = new_err;
+      RoctxRange range_lin("linearisation");
       HIP_TRY(g, pgo::launch_linearize(d, ev[0], ev[1]));
       HIP_TRY(g, hipEventRecord(g->lin_done, d.stream));
       st.linearizations++;
@@ -1428,6 +1445,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
         // sequence order with GTSAM's rules, so the accepted step is the
         // sequential one.
         for (;;) {
+          RoctxRange range_round("lambda_round");
           lam_k[0] = lam;
           fac_k[0] = factor;
           valid[0] = 1;

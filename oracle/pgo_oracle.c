@@ -417,6 +417,8 @@ static chol_sym *sym_analyze(int n, int ne, const int32_t *ei, const int32_t *ej
       }
     }
   }
+  free(chead);
+  free(cnext);
   S->perm = (int *)malloc(n * sizeof(int));
   S->iperm = (int *)malloc(n * sizeof(int));
   int *pold = (int *)malloc(n * sizeof(int)); /* post position of old etree node */
@@ -503,6 +505,7 @@ static chol_sym *sym_analyze(int n, int ne, const int32_t *ei, const int32_t *ej
   free(sf);
   free(of);
   free(onz);
+  free(onb);
   free(ol);
   free(cc);
   free(nch);
@@ -550,7 +553,7 @@ static chol_sym *sym_analyze(int n, int ne, const int32_t *ei, const int32_t *ej
         }
       }
     }
-    qsort(rl[s].a, rl[s].n, sizeof(int), cmp_int);
+    if (rl[s].n > 1) qsort(rl[s].a, rl[s].n, sizeof(int), cmp_int);   /* (a root's list is empty: a == NULL) */
     total += rl[s].n;
   }
   S->rows = (int *)malloc((size_t)(total > 0 ? total : 1) * sizeof(int));
@@ -561,7 +564,7 @@ static chol_sym *sym_analyze(int n, int ne, const int32_t *ei, const int32_t *ej
   int maxfront = 0;
   for (int s = 0; s < no; s++) {
     S->rptr[s] = (int)pos;
-    memcpy(S->rows + pos, rl[s].a, rl[s].n * sizeof(int));
+    if (rl[s].n) memcpy(S->rows + pos, rl[s].a, rl[s].n * sizeof(int));
     pos += rl[s].n;
     int wd = 3 * (S->sfirst[s + 1] - S->sfirst[s]);
     int m = wd + 3 * rl[s].n;
@@ -987,8 +990,8 @@ void orc_destroy(void *h) {
   free(o->pz);
   free(o->eom);
   free(o->pom);
+  num_free(o->N);   /* reads the symbolic sizes: before sym_free */
   sym_free(o->S);
-  num_free(o->N);
   free(o->hdiag);
   free(o->hoff);
   free(o->g);

@@ -101,6 +101,15 @@ int orc_information(const double *cov, double *omega);
  * insertion order); index of the closest of the first n - skip, -1 if n <= skip */
 int orc_closest_keyframe(int n, const double *xy, double qx, double qy, int skip, double *dist);
 
+/* Scan registration (gicp_oracle.c; scanner.cpp:35-74): GICP of source S (ns
+ * float xyz) to target Q (nq).  T: 12 doubles (R row-major | t), the guess on
+ * entry and the result on return; out: iterations, converged, fitness,
+ * optimiser steps.  0 / negative on bad arguments. */
+int orc_gicp_align(const float *S, int ns, const float *Q, int nq, int k, double eps, int max_it, int max_inner,
+                   double max_dist, double trans_eps, double rot_eps, double *T, double *out);
+/* plane-regularised covariances (6 per point: 00 01 02 11 12 22) */
+int orc_gicp_covariances(const float *P, int n, int k, double eps, double *cov);
+
 #ifdef __cplusplus
 }
 #endif
