@@ -428,7 +428,8 @@ def main():
                             f"(seed {g.meta.get('seed')}), GTSAM-default LM from dead-reckoned values",
                 "poses": n, "edges": ne,
                 "parallelism": ((f"partition{world}" if part else f"spec-lambda{world}") +
-                                ("-host" if args.same_device else "-rccl")) if spec else f"replicas{world}",
+                                ("-host" if args.same_device else "-rccl")) if spec else
+                               (f"replicas{world}" if world > 1 else "single-gpu"),
                 "lambda_lanes": args.lanes,
                 "solver": (f"GPU supernodal multifrontal Cholesky ({'nested-dissection' if args.ordering == 'nd' else 'AMD'} ordering, fp64 MFMA Schur updates)"
                            if args.solver == "cholesky" else
