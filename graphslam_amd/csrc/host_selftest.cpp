@@ -62,6 +62,7 @@ int main() {
     P.ordering = ordering;
     pgo::chol_analyze(P, G.n, G.row_ptr, G.col);
     if (P.ns <= 0 || P.flops <= 0) return fail("analysis");
+    if (P.schedule_error) return fail("panel schedule bookkeeping");
     if (!pgo::chol_covers(P, G.n, G.row_ptr, G.col)) return fail("plan does not cover its own pattern");
     for (int size : {2, 4}) {
       std::vector<double> rf;
@@ -74,7 +75,7 @@ int main() {
         Q.part_size = size;
         Q.part_rank = r;
         pgo::chol_analyze(Q, G.n, G.row_ptr, G.col);
-        if (Q.ns != P.ns) return fail("partitioned plan");
+        if (Q.ns != P.ns || Q.schedule_error) return fail("partitioned plan");
       }
     }
     // a loop closure inside the existing fill: same fronts, new assembly lists
@@ -87,7 +88,38 @@ int main() {
     R.order_in.resize(G3.n);
     for (int k = 0; k < G3.n; k++) R.order_in[k] = G3.n - 1 - k;
     pgo::chol_analyze(R, G3.n, G3.row_ptr, G3.col);
-    if (!pgo::chol_covers(R, G3.n, G3.row_ptr, G3.col)) return fail("given ordering");
+    if (!pgo::chol_covers(R, G3.n, G3.row_ptr, G3.col) || R.schedule_error) return fail("given ordering");
+  }
+  {   // a 2-D grid of poses: nested dissection gives big separator fronts (many
+      // panels, kKB block boundaries, partial last panels) -- the look-ahead
+      // schedule's bookkeeping is checked on them
+    const int side = 60, n = side * side;
+    std::vector<std::pair<int, int>> e;
+    for (int y = 0; y < side; y++)
+      for (int x = 0; x < side; x++) {
+        if (x + 1 < side) e.emplace_back(y * side + x, y * side + x + 1);
+        if (y + 1 < side) e.emplace_back(y * side + x, (y + 1) * side + x);
+      }
+    std::vector<std::vector<int>> adj(n);
+    for (auto& [a, b] : e) {
+      adj[a].push_back(b);
+      adj[b].push_back(a);
+    }
+    Pattern G;
+    G.n = n;
+    G.row_ptr.assign(1, 0);
+    for (int i = 0; i < n; i++) {
+      adj[i].push_back(i);
+      std::sort(adj[i].begin(), adj[i].end());
+      G.col.insert(G.col.end(), adj[i].begin(), adj[i].end());
+      G.row_ptr.push_back((int)G.col.size());
+    }
+    pgo::CholPlan P;
+    pgo::chol_analyze(P, G.n, G.row_ptr, G.col);
+    int maxw = 0;
+    for (int s2 = 0; s2 < P.ns; s2++) maxw = std::max(maxw, P.w[s2]);
+    if (P.schedule_error) return fail("grid: panel schedule bookkeeping");
+    std::printf("grid plan: %d fronts, widest %d pivot columns\n", P.ns, maxw);
   }
   std::printf("host selftest ok\n");
   return 0;

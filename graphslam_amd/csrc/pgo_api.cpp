@@ -678,6 +678,7 @@ int ensure_chol(pgo_graph* g) {
   g->hook.ctx = g;
   g->hook.allgather = exchange_allgather;
   pgo::chol_analyze(g->chol, g->d.n, g->h_row_ptr, g->h_slot_col);
+  if (g->chol.schedule_error) return fail(g, PGO_E_HIP, "internal: inconsistent panel schedule");
   RC_TRY(bind_plan(g, true));
   g->chol_ready = true;
   timed(order_in.empty() ? 3 : 2);
@@ -1825,6 +1826,7 @@ int pgo_debug_plan(pgo_graph* g, double* out, int cap) {
   pgo::CholPlan P;
   P.ordering = g->ordering;
   pgo::chol_analyze(P, (int)g->keys.size(), H.row_ptr, H.slot_col);
+  if (P.schedule_error) return fail(g, PGO_E_HIP, "internal: inconsistent panel schedule");
   // launches: factor = memsets, assembly, rhs permutation, per level extend-add
   // ranks + vector assembly + small classes + per panel diag/trsm/Schur (+look-ahead);
   // solve (backward only) = per level partials + init + steps, perm out

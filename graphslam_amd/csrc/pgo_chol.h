@@ -28,6 +28,7 @@ constexpr int kTile = 64;          // Schur-update output tile
 constexpr int kBigTile = 128;      // Schur-update output tile of the LDS-pipelined kernel
 constexpr int kKB = 256;         // Schur updates deferred per kKB-column block (inner steps update the block only)
 constexpr int kInlineTiles = 512;
+constexpr int kLookaheadM = 2048;  // fronts this tall skip the next step's column block in their plain tiles
 constexpr int kMaxStampSlots = 256;  // PGO_STEP_STAMPS diagnostics // syrk tiles per step that ride inside k_step
 constexpr int kBwdRows = 512;      // rows per partial product of the backward solve           // Schur-update depth: trailing matrix updated once per kKB columns
 
@@ -45,6 +46,7 @@ struct PanelStep {                 // one 64-column panel kb of every big front 
   double plain_flops;              // ... of the syrk tiles alone
   double first_flops;              // algorithmic flops of k_panel_first (factor, inverse, trsm)
   double step_flops;               // ... of k_step (updates, factor, inverse, trsm, inline tiles)
+  int plain_lag = 0;               // apart plain tiles: joined before step +1 or (look-ahead skip) +2
 };
 
 struct SolveStep {                 // one launch of the blocked triangular solves
@@ -53,7 +55,7 @@ struct SolveStep {                 // one launch of the blocked triangular solve
 
 struct SmallClass {                // small fronts of one level with m <= mmax
   int off, cnt, mmax;
-  int wave;                        // 1: w <= kWaveW, one wavefront per front (k_front_wave)
+  int wave;                        // > 0: one wavefront per front (k_front_wave), panel width W (8, 16, kWaveW >= w)
   double flops = 0;                // algorithmic flops (factor + diagonal-block inverses)
 };
 
@@ -75,6 +77,7 @@ enum { kOrderNd = 0, kOrderAmd = 1 };
 struct CholPlan {
   int ordering = kOrderNd;         // fill-reducing ordering of the pose graph (input of chol_analyze)
   int part_size = 1, part_rank = 0; // subtree partition over ranks (input of chol_analyze)
+  bool schedule_error = false;     // the panel schedule's update bookkeeping failed (a bug: the plan is unusable)
   std::vector<int> order_in;       // optional given ordering (new -> old) instead of ND / AMD (input)
   int batch = 1;                   // lambda lanes with a numeric workspace (input of chol_upload)
   // ---- host symbolic result ----
@@ -145,6 +148,7 @@ struct CholPlan {
   int* d_stepflag = nullptr;       // [batch][ns]: last panel (kb / 64 + 1) whose diagonal inverse is published
   hipStream_t side = nullptr;      // look-ahead diagonal tiles
   hipStream_t side2 = nullptr;     // small fronts beside the blocked path
+  hipStream_t side3 = nullptr;     // the second wavefront class of small fronts, beside side2
   hipEvent_t evs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int4 *d_bwd = nullptr, *d_bwd_part = nullptr;
   int2* d_bwd_pref = nullptr;

@@ -314,12 +314,12 @@ __global__ __launch_bounds__(256) void k_front_small(CholDev c, const int* __res
 // Then the rank-w Schur update of the trailing block is streamed through global
 // memory (rows of L from registers, columns broadcast from an LDS copy), and
 // the w x w inverse for the backward solve is formed lane = column.
-template <bool kTwoRows>   // m > 64: lane also owns row l + 64
-__global__ __launch_bounds__(64) void k_front_wave(CholDev c, const int* __restrict__ list) {
-  lane_offset(c);
-  constexpr int W = kWaveW, LDP = kWaveW + 1;   // odd row stride: conflict-free per-lane rows
-  extern __shared__ __attribute__((aligned(16))) double S[];
-  const int s = list[blockIdx.x];
+// W: the compile-time panel width (8, 16 or kWaveW >= w): the pivot loop, the
+// per-pivot column updates and the trailing update's inner products run over W,
+// so narrow fronts (most leaves) do a quarter of the wide ones' work.
+template <int W, bool kTwoRows>   // m > 64: lane also owns row l + 64
+__device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double* S) {
+  constexpr int LDP = W + 1;   // odd row stride: conflict-free per-lane rows
   const int m = c.m[s], w = c.w[s];
   double* PR = S;                 // m x W row-major copy of L (after the factorisation)
   double* cb = S + m * LDP;       // 128 + 2: column k of the panel, then v[k]; then 1/L(k,k)
@@ -428,6 +428,13 @@ __global__ __launch_bounds__(64) void k_front_wave(CholDev c, const int* __restr
       if (r < w) M[r * 64 + l] = r >= l ? x[r] : 0.0;
   }
   DIAG_CLK(28);
+}
+
+template <int W, bool kTwoRows>
+__global__ __launch_bounds__(64) void k_front_wave(CholDev c, const int* __restrict__ list) {
+  lane_offset(c);
+  extern __shared__ __attribute__((aligned(16))) double S[];
+  front_wave_body<W, kTwoRows>(c, list[blockIdx.x], S);
 }
 
 // ------------------------------------------------------------ blocked path
@@ -1759,8 +1766,18 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(up(&P.d_at_iptr, P.at_iptr, s));
   CH_TRY(up(&P.d_at_items, P.at_items, s));
   CH_TRY(alloc_numeric(P, std::max(P.batch, 1), s));
-  CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
+  {   // PGO_SIDE_PRIORITY=1: the plain Schur tiles' stream at the lowest dispatch
+      // priority (measured on C3: 22.0 vs 26.0 it/s -- the starved tiles hold
+      // the level ends back more than the panel chain gains -- so off)
+    int least = 0, greatest = 0;
+    const char* pr = getenv("PGO_SIDE_PRIORITY");
+    if (pr && pr[0] == '1' && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      CH_TRY(hipStreamCreateWithPriority(&P.side, hipStreamNonBlocking, least));
+    else
+      CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
+  }
   CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
+  CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));
   for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   CH_TRY(up(&P.d_ea_tasks, P.ea_tasks, s));
   CH_TRY(up(&P.d_ea_pairs, P.ea_pairs, s));
@@ -1778,6 +1795,7 @@ void chol_free(CholPlan& P) {
     if (e) (void)hipEventDestroy(e);
   if (P.side) (void)hipStreamDestroy(P.side);
   if (P.side2) (void)hipStreamDestroy(P.side2);
+  if (P.side3) (void)hipStreamDestroy(P.side3);
   P = CholPlan();
 }
 
@@ -1845,28 +1863,56 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
            (size_t)lv.maxm * sizeof(double), s, c, (const int*)(P.d_level_fronts + lv.front_off));
     // small fronts on the second side stream, beside the blocked path of the
     // same level (disjoint fronts); joined before the next level
+    // (the two wavefront classes -- m <= 64, m > 64 -- on two side streams,
+    // concurrently: each is a grid of independent latency-bound waves)
     const bool fork_small = !lv.small.empty() && !lv.panels.empty();
+    bool lo = false, hi = false;   // wavefront classes with m <= 64 / m > 64
+    for (const SmallClass& sc : lv.small)
+      if (sc.wave) (sc.mmax > 64 ? hi : lo) = true;
+    const bool fork_wave = lo && hi;
     hipStream_t ss = s;
-    if (fork_small) {
+    if (fork_small || fork_wave) {
       CH_TRY(hipEventRecord(P.evs[0], s));
       CH_TRY(hipStreamWaitEvent(P.side2, P.evs[0], 0));
+      if (fork_wave) CH_TRY(hipStreamWaitEvent(P.side3, P.evs[0], 0));
       ss = P.side2;
     }
     for (const SmallClass& sc : lv.small) {
       auto small_cost = [&] { return make_double2(sc.flops * nb, 0); };
       const int* list = P.d_small + sc.off;
       if (sc.wave) {
-        const size_t lds = (size_t)(sc.mmax * (kWaveW + 1) + 130 + kWaveW) * sizeof(double);
-        if (sc.mmax > 64)
-          launch(prof, kFamFrontWave, small_cost, k_front_wave<true>, dim3(sc.cnt, nb), dim3(64), lds, ss, c, list);
-        else
-          launch(prof, kFamFrontWave, small_cost, k_front_wave<false>, dim3(sc.cnt, nb), dim3(64), lds, ss, c, list);
+        // classes by (m <= 64 | m > 64) x panel width W in {8, 16, 32}; the
+        // m > 64 ones on the third stream
+        const hipStream_t st = fork_wave && sc.mmax > 64 ? P.side3 : ss;
+        const size_t lds = (size_t)(sc.mmax * (sc.wave + 1) + 130 + sc.wave) * sizeof(double);
+        const dim3 g(sc.cnt, nb), b(64);
+        if (sc.mmax > 64) {
+          if (sc.wave == 8) launch(prof, kFamFrontWave, small_cost, k_front_wave<8, true>, g, b, lds, st, c, list);
+          else if (sc.wave == 16) launch(prof, kFamFrontWave, small_cost, k_front_wave<16, true>, g, b, lds, st, c, list);
+          else launch(prof, kFamFrontWave, small_cost, k_front_wave<kWaveW, true>, g, b, lds, st, c, list);
+        } else {
+          if (sc.wave == 8) launch(prof, kFamFrontWave, small_cost, k_front_wave<8, false>, g, b, lds, st, c, list);
+          else if (sc.wave == 16) launch(prof, kFamFrontWave, small_cost, k_front_wave<16, false>, g, b, lds, st, c, list);
+          else launch(prof, kFamFrontWave, small_cost, k_front_wave<kWaveW, false>, g, b, lds, st, c, list);
+        }
       } else {
         launch(prof, kFamFrontSmall, small_cost, k_front_small, dim3(sc.cnt, nb), B256,
                (size_t)(sc.mmax * sc.mmax + 64 + sc.mmax) * sizeof(double), ss, c, list);
       }
     }
-    for (const PanelStep& ps : lv.panels) {
+    // apart plain tiles run on P.side (in order, so two of them never touch a
+    // tile at once); plain(j) is joined before step j + plain_lag (1, or 2 when
+    // the look-ahead skip left the next step independent of it), and at the
+    // level's end.  Ring of two join events (evs[3], evs[5]).
+    bool side_pending = false;
+    std::vector<char> on_side(lv.panels.size(), 0);   // plain(j) went to P.side and recorded its event
+    for (size_t j = 0; j < lv.panels.size(); j++) {
+      const PanelStep& ps = lv.panels[j];
+      for (size_t back = 1; back <= 2 && back <= j; back++) {
+        const PanelStep& pp = lv.panels[j - back];
+        if (on_side[j - back] && pp.plain_lag == (int)back)
+          CH_TRY(hipStreamWaitEvent(s, P.evs[(j - back) & 1 ? 5 : 3], 0));
+      }
       if (prof) prof->cur_tag = ((int)li << 16) | (ps.kb / kNB + 1);
       const int4* cols = (const int4*)(P.d_col + ps.col_off);
       if (ps.potrf_cnt)
@@ -1882,7 +1928,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
         launch(prof, big ? kFamPanelSyrk128 : kFamPanelSyrk, [&] { return make_double2(ps.plain_flops * nb, 0); },
                big ? k_panel_syrk128 : k_panel_syrk_lds, dim3(ps.syrk_cnt, nb), B256, 0, st, c, tiles, ps.kb);
       };
-      if (apart && step) {   // beside k_step on the side stream, joined before the next step
+      if (apart) {   // on the side stream (beside k_step, behind the earlier plains)
         CH_TRY(hipEventRecord(P.evs[2], s));
         CH_TRY(hipStreamWaitEvent(P.side, P.evs[2], 0));
       }
@@ -1891,19 +1937,24 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
                dim3(ps.sdiag_cnt + ps.col_cnt + nin, nb), B256, 0, s, c, (const int4*)(P.d_sdiag + ps.sdiag_off),
                ps.sdiag_cnt, cols + ps.fcol_cnt, ps.col_cnt, tiles, ps.kb,
                stamps && li + 1 == P.levels.size() && ps.kb / kNB < kMaxStampSlots ? ps.kb / kNB : -1);
-      if (apart) {
-        if (step) {
-          plain(P.side);
-          CH_TRY(hipEventRecord(P.evs[3], P.side));
-          CH_TRY(hipStreamWaitEvent(s, P.evs[3], 0));
-        } else {
-          plain(s);
-        }
+      if (apart) {   // (never on the main stream: an earlier plain may still run on P.side)
+        plain(P.side);
+        CH_TRY(hipEventRecord(P.evs[j & 1 ? 5 : 3], P.side));
+        side_pending = true;
+        on_side[j] = 1;
       }
     }
-    if (fork_small) {
+    if (side_pending) {   // every apart plain of the level done before the next level
+      CH_TRY(hipEventRecord(P.evs[2], P.side));
+      CH_TRY(hipStreamWaitEvent(s, P.evs[2], 0));
+    }
+    if (fork_small || fork_wave) {
       CH_TRY(hipEventRecord(P.evs[1], P.side2));
       CH_TRY(hipStreamWaitEvent(s, P.evs[1], 0));
+      if (fork_wave) {
+        CH_TRY(hipEventRecord(P.evs[4], P.side3));
+        CH_TRY(hipStreamWaitEvent(s, P.evs[4], 0));
+      }
     }
   }
   if (part && P.split >= (int)P.levels.size()) CH_TRY(exchange());

@@ -579,16 +579,17 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
         while (P.m[s] > classes[q]) q++;
         bucket[q].push_back(s);
       }
-      for (int half = 0; half < 2; half++) {      // m <= 64 (one row per lane), m > 64
+      for (int cls = 0; cls < 6; cls++) {   // m <= 64 (one row per lane) | m > 64  x  w <= 8 | 16 | 32
+        const int half = cls / 3, W = cls % 3 == 0 ? 8 : cls % 3 == 1 ? 16 : kWaveW, Wlo = cls % 3 == 0 ? 0 : W / 2;
         std::vector<int> part;
         for (int s : wave)
-          if ((P.m[s] > 64) == (half == 1)) part.push_back(s);
+          if ((P.m[s] > 64) == (half == 1) && P.w[s] > Wlo && P.w[s] <= W) part.push_back(s);
         if (part.empty()) continue;
         std::stable_sort(part.begin(), part.end(), [&](int a, int b) {
           const double wa = (double)P.m[a] * P.m[a] * P.w[a], wb = (double)P.m[b] * P.m[b] * P.w[b];
           return wa > wb;
         });
-        SmallClass sc{(int)P.small_list.size(), (int)part.size(), 0, 1};
+        SmallClass sc{(int)P.small_list.size(), (int)part.size(), 0, W};
         for (int s : part) {
           P.small_list.push_back(s);
           sc.mmax = std::max(sc.mmax, P.m[s]);
@@ -619,6 +620,19 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     //               next panel's column block updated, then solved against that
     //               inverse (col); the other trailing tiles updated (syrk:
     //               inline, or a concurrent k_panel_syrk_lds / 128 launch)
+    // Look-ahead bookkeeping: applied[i][j] = the first panel column whose
+    // Schur update column j of big front i has not received yet (every task
+    // updates whole columns: rows from the column down).  A step's tasks must
+    // find their columns uniform; a violation drops the step's skip (below) or
+    // marks the plan invalid (schedule_error).
+    std::vector<std::vector<int>> applied(big.size());
+    for (size_t i = 0; i < big.size(); i++) applied[i].assign(P.m[big[i]], 0);
+    auto uniform = [&](size_t i, int c0, int c1, int k0) {
+      for (int j = c0; j < c1; j++)
+        if (applied[i][j] != k0) return false;
+      return true;
+    };
+    bool apart_chain = false;   // once a step's plain tiles go to their own launch, the later ones do too
     for (int kb = 0; kb < maxw; kb += kNB) {
       PanelStep ps;
       ps.kb = kb;
@@ -640,53 +654,110 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
           for (int r0 = kNB; r0 < P.m[s]; r0 += kNB) P.col_tasks.push_back(make_int4(s, r0, 0, -1));
       ps.fcol_cnt = (int)P.col_tasks.size() - ps.col_off;
       // this panel's Schur update, deferred by kKB-column blocks: inside a block
-      // only the block's remaining columns [kn, be) are updated (depth nb,
-      // "inner", bit 31 of k0); after the block's last panel the trailing
-      // columns [be, m) get one update of depth kn - bs <= kKB
-      std::vector<int4> plain;   // (front, first column, end column, k0): rows from the column down
-      for (int s : big) {
-        if (P.w[s] <= kb) continue;
-        const int nb = std::min(kNB, P.w[s] - kb), kn = kb + nb, m = P.m[s];
-        const int bs = kb & ~(kKB - 1), be = std::min(bs + kKB, P.w[s]);
+      // only the block's remaining columns [kn, be) are updated ("inner", bit 31
+      // of k0: tasks clip columns at the block end); after the block's last
+      // panel the trailing columns [be, m) get the whole block's update.
+      // With the plain tiles in their own launch (apart) the column block the
+      // next step prepares, [kn + 64, kn + 128), is skipped: the next step's
+      // diagonal / column tasks apply this panel's update with their own
+      // (depth 2 panels, or the deferred block + 1 panel), so the next step
+      // does not wait for this step's plain tiles (joined one step later).
+      // The skip is a property of the front alone (its size), never of the
+      // level it sits in: the update grouping -- hence the rounding -- of a
+      // front is the same in every plan (the partitioned plans' fronts are bit
+      // for bit the one-rank plan's).
+      const bool lookahead = !getenv("PGO_NO_LOOKAHEAD");
+      auto front_skip = [&](int s) { return lookahead && P.m[s] >= kLookaheadM; };
+      auto plain_range = [&](int s, bool skip, int& cstart, int& cend) {
+        const int w = P.w[s], m = P.m[s], nb = std::min(kNB, w - kb), kn = kb + nb;
+        const int bs = kb & ~(kKB - 1), be = std::min(bs + kKB, w);
         const bool inner = kn < be;
-        const int cend = inner ? be : m, depth = inner ? nb : kn - bs;
-        const int k0 = inner ? (kb | (int)0x80000000) : bs;
-        if (inner) {
-          for (int cc = kn; cc < be; cc++) ps.syrk_flops += 2.0 * nb * (m - cc);
-        } else if (be < m) {
-          const double t = m - be;
-          ps.syrk_flops += depth * t * (t + 1.0);
+        cend = inner ? be : m;
+        cstart = kn < w ? kn + kNB : kn;
+        if (skip && kn + kNB < w) {   // the next step prepares [kn2, kn2 + 64): only when it covers all of it
+          const int kn2 = kn + kNB, bs2 = kn & ~(kKB - 1), be2 = std::min(bs2 + kKB, w);
+          const int colend2 = kn2 < be2 ? be2 : m;
+          if (std::min(kn2 + kNB, colend2) == kn2 + kNB && cstart + kNB <= cend) cstart += kNB;
         }
-        int cstart = kn;
-        if (kn < P.w[s]) {   // next panel: its diagonal tile and the tiles below it
-          const int nb2 = std::min(kNB, P.w[s] - kn);
-          P.sdiag_tasks.push_back(make_int4(s, kn, kn, k0));
+      };
+      auto ntiles = [&](int T) {
+        long long cnt = 0;
+        for (int s : big) {
+          if (P.w[s] <= kb) continue;
+          int c0, c1;
+          plain_range(s, front_skip(s), c0, c1);
+          for (int cc = c0; cc < c1; cc += T) cnt += (P.m[s] - cc + T - 1) / T;
+        }
+        return cnt;
+      };
+      // plain tiles: 128x128 (LDS-pipelined kernel) when there are many rounds of
+      // them (measured: at <= ~500 tiles the 64x64 kernel's finer granularity
+      // wins, scripts/ubench_syrk.hip), else 64x64; few 64-tiles ride in k_step,
+      // many go to a concurrent launch (k_step's LDS request, sized for the
+      // diagonal workgroups, halves their occupancy)
+      const int tile0 = ntiles(kBigTile) >= 4096 ? kBigTile : kTile;
+      const bool apart = apart_chain || !(tile0 == kTile && ntiles(kTile) <= kInlineTiles);
+      std::vector<int4> plain;   // (front, first column, end column, k0): rows from the column down
+      bool conflict = false;   // a front's next step reads this step's plain tiles
+      for (size_t i = 0; i < big.size(); i++) {
+        const int s = big[i];
+        if (P.w[s] <= kb) continue;
+        const int w = P.w[s], m = P.m[s];
+        const int nb = std::min(kNB, w - kb), kn = kb + nb;
+        const int bs = kb & ~(kKB - 1), be = std::min(bs + kKB, w);
+        const bool inner = kn < be;
+        const int colend = inner ? be : m;   // the device's column clip
+        if (kn < w) {   // next panel: its diagonal tile and the tiles below it
+          const int nb2 = std::min(kNB, w - kn), c1 = std::min(kn + kNB, colend);
+          const int k0 = applied[i][kn];
+          if (!uniform(i, kn, c1, k0)) {
+            if (getenv("PGO_SCHED_DEBUG") && !P.schedule_error)
+              fprintf(stderr, "sched: sdiag front %d w %d m %d kb %d cols [%d,%d) k0 %d\n", s, w, m, kb, kn, c1, k0);
+            P.schedule_error = true;
+          }
+          for (int j = kn; j < c1; j++) applied[i][j] = kn;
+          const int depth = kn - k0, kw = inner ? (k0 | (int)0x80000000) : k0;
+          P.sdiag_tasks.push_back(make_int4(s, kn, kn, kw));
           ps.step_flops += (double)depth * kNB * (kNB + 1) + 2.0 * nb2 * nb2 * (double)nb2 / 3.0 +
                            (double)std::min(kNB - nb2, m - kn - nb2) * nb2 * nb2;
           for (int r0 = kn + kNB; r0 < m; r0 += kNB) {
-            P.col_tasks.push_back(make_int4(s, r0, kn, k0));
+            P.col_tasks.push_back(make_int4(s, r0, kn, kw));
             const int rows = std::min(kNB, m - r0);
-            ps.step_flops += 2.0 * depth * rows * std::min(kNB, cend - kn) + (double)rows * nb2 * nb2;
+            ps.step_flops += 2.0 * depth * rows * (c1 - kn) + (double)rows * nb2 * nb2;
           }
-          cstart = kn + kNB;
+          ps.syrk_flops += (double)depth * (c1 - kn) * (2.0 * m - kn - c1 + 1.0);
+        }
+        int cstart, cend;
+        plain_range(s, front_skip(s), cstart, cend);
+        if (kn + kNB < w && cstart < cend) {   // the next step prepares [kn2, c2) of this front
+          const int kn2 = kn + kNB, bs2 = kn & ~(kKB - 1), be2 = std::min(bs2 + kKB, w);
+          const int c2 = std::min(kn2 + kNB, kn2 < be2 ? be2 : m);
+          if (cstart < c2 && kn2 < cend) conflict = true;   // this step's plain tiles feed it: lag 1
         }
         if (cstart < cend) {
+          int k0 = applied[i][cstart];
+          if (!uniform(i, cstart, cend, k0)) {
+            if (getenv("PGO_SCHED_DEBUG") && !P.schedule_error) {
+              fprintf(stderr, "sched: plain front %d w %d m %d kb %d cols [%d,%d) k0 %d:", s, w, m, kb, cstart, cend, k0);
+              for (int j = cstart; j < cend; j += 16) fprintf(stderr, " %d", applied[i][j]);
+              fprintf(stderr, "\n");
+            }
+            P.schedule_error = true;
+            k0 = kb;
+          }
+          for (int j = cstart; j < cend; j++) applied[i][j] = kn;
+          const int depth = kn - k0;
           for (int cc = cstart; cc < cend; cc++) ps.plain_flops += 2.0 * depth * (m - cc);
-          plain.push_back(make_int4(s, cstart, cend, k0));
+          plain.push_back(make_int4(s, cstart, cend, inner ? (k0 | (int)0x80000000) : k0));
         }
       }
+      ps.syrk_flops += ps.plain_flops;
       ps.sdiag_cnt = (int)P.sdiag_tasks.size() - ps.sdiag_off;
       ps.col_cnt = (int)P.col_tasks.size() - ps.col_off - ps.fcol_cnt;
-      // plain tiles: 128x128 (LDS-pipelined kernel) when there are many rounds of
-      // them (measured: at <= ~500 tiles the 64x64 kernel's finer granularity
-      // wins, scripts/ubench_syrk.hip), else 64x64
-      auto ntiles = [&](int T) {
-        long long cnt = 0;
-        for (const int4& u : plain)
-          for (int c0 = u.y; c0 < u.z; c0 += T) cnt += (P.m[u.x] - c0 + T - 1) / T;
-        return cnt;
-      };
-      ps.syrk_tile = ntiles(kBigTile) >= 4096 ? kBigTile : kTile;
+      long long cnt128 = 0;
+      for (const int4& u : plain)
+        for (int c0 = u.y; c0 < u.z; c0 += kBigTile) cnt128 += (P.m[u.x] - c0 + kBigTile - 1) / kBigTile;
+      ps.syrk_tile = cnt128 >= 4096 ? kBigTile : kTile;
       for (const int4& u : plain)
         for (int c0 = u.y; c0 < u.z; c0 += ps.syrk_tile)
           for (int r0 = c0; r0 < P.m[u.x]; r0 += ps.syrk_tile) P.syrk_tasks.push_back(make_int4(u.x, r0, c0, u.w));
@@ -696,12 +767,25 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
         std::copy(mine.begin(), mine.end(), P.syrk_tasks.begin() + ps.syrk_off);
       }
       ps.syrk_cnt = (int)P.syrk_tasks.size() - ps.syrk_off;
-      // few 64-tiles ride in k_step; many go to a concurrent launch (k_step's
-      // LDS request, sized for the diagonal workgroups, halves their occupancy)
-      ps.syrk_inline = ps.syrk_tile == kTile && ps.syrk_cnt <= kInlineTiles;
+      ps.syrk_inline = !apart && ps.syrk_tile == kTile && ps.syrk_cnt <= kInlineTiles;
+      // an apart launch no front's next step reads is joined before the step after next
+      ps.plain_lag = ps.syrk_cnt > 0 && !ps.syrk_inline ? (conflict ? 1 : 2) : 0;
+      // (an inline plain after a lag-2 apart one could touch its tiles at once)
+      apart_chain = apart_chain || (ps.plain_lag == 2);
       if (ps.syrk_inline) ps.step_flops += ps.plain_flops;
       P.syrk_flops += ps.plain_flops;
       lv.panels.push_back(ps);
+    }
+    // every column has its updates: pivot columns up to their panel, the
+    // trailing ones from every panel
+    for (size_t i = 0; i < big.size(); i++) {
+      const int s = big[i], w = P.w[s];
+      for (int j = 0; j < P.m[s]; j++)
+        if (applied[i][j] != (j < w ? (j / kNB) * kNB : w)) {
+          if (getenv("PGO_SCHED_DEBUG") && !P.schedule_error)
+            fprintf(stderr, "sched: end front %d w %d m %d col %d applied %d\n", s, w, P.m[s], j, applied[i][j]);
+          P.schedule_error = true;
+        }
     }
   }
   chol_assembly(P, row_ptr, slot_col);
