@@ -67,7 +67,7 @@ def _host_info():
     return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model}
 
 
-def cpu_baseline(g, pg, per_step, reps=5, amd_reps=3):
+def cpu_baseline(g, nd_order, per_step, reps=5, amd_reps=3):
     """The C restatement (oracle/pgo_oracle.c: same LM, supernodal multifrontal
     Cholesky) on the host cores of this box, like-for-like with the GPU step
     (SURVEY 8d / BASELINE.md):
@@ -99,7 +99,7 @@ def cpu_baseline(g, pg, per_step, reps=5, amd_reps=3):
                 "ms_trajectory": 1e3 * t_traj, "factor_flops": runs[0]["factor_flops"], "nnz_l": runs[0]["nnz_l"],
                 "reps": n}
 
-    o_nd = Oracle(g, order=pg.debug_ordering())
+    o_nd = Oracle(g, order=nd_order)
     set_threads(threads)
     allc = unit(o_nd, reps)
     set_threads(1)
@@ -377,6 +377,8 @@ def main():
     scan = None
     if args.gicp and rank == 0:
         scan = scan_registration_bench(args.gicp)
+    # the GPU plan's ordering of g, taken before live_resolve appends to the handle
+    nd_order = pg.debug_ordering() if rank == 0 and not args.no_cpu_baseline and world == 1 else None
     live = None
     if args.live and rank == 0 and not spec:
         live = live_resolve_bench(pg, g, args.live)
@@ -464,7 +466,7 @@ def main():
             "scan_registration": scan,
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(g, pg, out["per_step"], reps=args.cpu_reps)
+            out["cpu_baseline"] = cpu_baseline(g, nd_order, out["per_step"], reps=args.cpu_reps)
             out["cpu_baseline"]["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
             out["cpu_baseline"]["gpu_over_cpu_one_core"] = out["value"] / out["cpu_baseline"]["one_core"]["value"]
         print(json.dumps(out))
