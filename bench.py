@@ -271,7 +271,12 @@ def scan_registration_bench(batch=1024, reps=3, cpu_sample=64):
            "keyframes": int(out["keyframe"].sum()),
            "device_ms": dms, "call_ms": float(np.median(wall)),
            "registrations_per_s": batch / (dms * 1e-3), "registrations_per_s_call": batch / (np.median(wall) * 1e-3),
-           "nn_evals": evals, "gnn_evals_per_s": evals / (dms * 1e-3) / 1e9}
+           "nn_evals": evals, "gnn_evals_per_s": evals / (dms * 1e-3) / 1e9,
+           # fp32 VALU bound: a distance evaluation is 3 sub + 1 mul + 2 fma = 8 flops
+           # (the fp64 Gauss-Newton steps are not counted), against the 157.3 TFLOP/s
+           # fp32 vector peak (MI355X_MICROARCH.md)
+           "roofline": {"bound": "valu", "achieved": 8.0 * evals / (dms * 1e-3) / 1e12, "peak": 157.3,
+                        "unit": "TFLOP/s", "frac": 8.0 * evals / (dms * 1e-3) / 1e12 / 157.3, "traffic": None}}
     try:
         from oracle import oracle as orc
         k = min(cpu_sample, batch)
