@@ -339,12 +339,30 @@ def main():
     spec = world > 1 and args.multi in ("spec", "partition")   # one job over all ranks
     part = world > 1 and args.multi == "partition"
     hc = None
+    transport = "host" if args.same_device else "rccl"
     if spec:
         from graphslam_amd import multi_gpu
         if args.same_device:
             hc = multi_gpu.attach_host(pg, r.dist, rank, world)
         else:
-            multi_gpu.attach_rccl(pg, r.dist, rank, world)
+            # RCCL over xGMI; should any rank fail to bring its communicator up,
+            # every rank falls back to the host transport (gloo) -- same results,
+            # slower exchange -- and the line says so
+            import torch
+            ok = 1
+            try:
+                multi_gpu.attach_rccl(pg, r.dist, rank, world)
+            except Exception as e:  # noqa: BLE001
+                ok = 0
+                print(f"rank {rank}: RCCL communicator failed ({e}); falling back to the host transport",
+                      file=sys.stderr)
+            flag = torch.tensor([ok], dtype=torch.int32)
+            r.dist.all_reduce(flag, op=r.dist.ReduceOp.MIN)
+            if int(flag.item()) == 0:
+                if ok:
+                    pg.comm_free()
+                hc = multi_gpu.attach_host(pg, r.dist, rank, world)
+                transport = "host-fallback"
     pg.save_values()                     # upload graph + values once; snapshot the initial values
     params = default_params(profile_every=args.profile_every, max_outer=args.max_outer,
                             linear_solver=1 if args.solver == "cholesky" else 0,
@@ -435,7 +453,7 @@ def main():
                             f"(seed {g.meta.get('seed')}), GTSAM-default LM from dead-reckoned values",
                 "poses": n, "edges": ne,
                 "parallelism": ((f"partition{world}" if part else f"spec-lambda{world}") +
-                                ("-host" if args.same_device else "-rccl")) if spec else
+                                "-" + transport) if spec else
                                (f"replicas{world}" if world > 1 else "single-gpu"),
                 "lambda_lanes": args.lanes,
                 "solver": (f"GPU supernodal multifrontal Cholesky ({'nested-dissection' if args.ordering == 'nd' else 'AMD'} ordering, fp64 MFMA Schur updates)"
