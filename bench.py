@@ -299,7 +299,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C3")
-    ap.add_argument("--profile-every", type=int, default=16)
+    ap.add_argument("--profile-every", type=int, default=8,
+                    help="in one extra untimed step, every k-th factorisation runs eagerly with per-launch events (0: none)")
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed CPU LM units per thread count (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--solver", choices=["cholesky", "pcg"], default="cholesky")
@@ -364,16 +365,20 @@ def main():
                 hc = multi_gpu.attach_host(pg, r.dist, rank, world)
                 transport = "host-fallback"
     pg.save_values()                     # upload graph + values once; snapshot the initial values
-    params = default_params(profile_every=args.profile_every, max_outer=args.max_outer,
-                            linear_solver=1 if args.solver == "cholesky" else 0,
-                            use_graphs=0 if args.no_graphs else 1, lambda_lanes=1 if part else args.lanes,
-                            multi_gpu=1 if part else 0)
+    # the timed steps run the production configuration (no per-launch
+    # profiling); one more, untimed step with every profile_every-th
+    # factorisation run eagerly with per-launch events feeds the kernel tables
+    common = dict(max_outer=args.max_outer, linear_solver=1 if args.solver == "cholesky" else 0,
+                  use_graphs=0 if args.no_graphs else 1, lambda_lanes=1 if part else args.lanes,
+                  multi_gpu=1 if part else 0)
+    params = default_params(profile_every=0, **common)
+    prof_params = default_params(profile_every=args.profile_every, **common)
 
     kprof = {}
 
-    def step():
+    def step(p=params):
         pg.restore_values()
-        st = pg.optimize(params)         # returns after the handle's stream has drained
+        st = pg.optimize(p)              # returns after the handle's stream has drained
         for k, v in pg.kernel_profile().items():   # profiled factorisations of this step (host copy)
             a = kprof.setdefault(k, dict(launches=0, ms=0.0, flops=0.0, bytes=0.0))
             for f in a:
@@ -383,6 +388,7 @@ def main():
     elapsed, lin_total, results = timed_steps(r, step, args.steps, args.warmup)
     if spec:   # one job: every rank walked the same linearisations
         lin_total /= world
+    prof_stats = [step(prof_params)[1]] if args.profile_every > 0 else []
     marg = None
     if args.marginals > 0 and rank == 0:
         import numpy as np
@@ -407,12 +413,13 @@ def main():
         live = live_resolve_bench(pg, g, args.live)
     stats = [s for _, s in results]
     last = stats[-1]
-    totals = dict(spmv_ms=sum(s["kernel_spmv_ms"] for s in stats), spmv_n=sum(s["kernel_spmv_count"] for s in stats),
-                  lin_ms=sum(s["kernel_linearize_ms"] for s in stats),
-                  lin_n=sum(s["kernel_linearize_count"] for s in stats),
-                  fac_n=sum(s["kernel_syrk_count"] for s in stats),
-                  fac_ms=sum(s["ms_factor_profiled"] for s in stats),
-                  sol_ms=sum(s["ms_solve_profiled"] for s in stats),
+    ps = prof_stats
+    totals = dict(spmv_ms=sum(s["kernel_spmv_ms"] for s in ps), spmv_n=sum(s["kernel_spmv_count"] for s in ps),
+                  lin_ms=sum(s["kernel_linearize_ms"] for s in ps),
+                  lin_n=sum(s["kernel_linearize_count"] for s in ps),
+                  fac_n=sum(s["kernel_syrk_count"] for s in ps),
+                  fac_ms=sum(s["ms_factor_profiled"] for s in ps),
+                  sol_ms=sum(s["ms_solve_profiled"] for s in ps),
                   gfac_ms=sum(s["ms_factor_graph"] for s in stats),
                   gfac_flops=sum(s["factor_graph_flops"] for s in stats))
 
