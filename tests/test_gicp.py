@@ -227,3 +227,33 @@ def test_gpu_pcl_mirror_and_gicp(pairs):
     g.setMaximumIterations(1)
     g.align()
     assert g.hasConverged()
+
+
+@pytest.mark.gpu
+def test_gpu_ties_params_and_errors(oracle_lib, pairs):
+    """Duplicate points (exact distance ties: lowest index on both sides),
+    non-default parameters, a far initial guess, and non-finite input."""
+    from graphslam_amd import _lib as L
+    from graphslam_amd.pose_graph import PgoError
+    from graphslam_amd.scanner import ScanRegistrar, default_params
+    reg = ScanRegistrar(0)
+    src, tgt, _ = pairs[4]
+    tgt_dup = np.concatenate([tgt, tgt[::3]])            # every 3rd target point twice
+    src_dup = np.concatenate([src[:50], src[:50], src])  # duplicated source points
+    r = reg.align_batch([src_dup], [tgt_dup])[0]
+    _check_against_oracle(r, src_dup, tgt_dup, oracle_lib)
+    # non-default parameters reach the kernels
+    p = default_params(max_iterations=3, k_correspondences=10, max_correspondence_distance=1.0)
+    r3 = reg.align_batch([src], [tgt], params=p)[0]
+    T, it, conv, fit = oracle_lib.gicp_align(src, tgt, None, k=10, max_it=3, max_dist=1.0)
+    assert r3.iterations == it <= 3 and np.abs(r3.transform - T).max() < 1e-6
+    # a far guess (a quarter turn): whatever the local minimum, the same as the restatement
+    G = np.eye(4)
+    G[:2, :2] = [[0, -1], [1, 0]]
+    r4 = reg.align_batch([src], [tgt], guesses=[G])[0]
+    _check_against_oracle(r4, src, tgt, oracle_lib, G)
+    bad = src.copy()
+    bad[7, 1] = np.nan
+    with pytest.raises(PgoError) as e:
+        reg.align_batch([bad], [tgt])
+    assert e.value.status == L.PGO_E_NONFINITE
