@@ -68,6 +68,7 @@ struct CholLevel {
   int maxblk = 0;                  // max 64-column blocks of a front's pivot columns
   std::vector<SolveStep> bwd;      // backward: [0] = init (all columns), then steps b = maxblk-1 .. 1
   SolveStep bwd_part{0, 0};        // partial products feeding the init tasks
+  SolveStep bwdc{0, 0};            // the backward steps as one chained launch (k_bwd_chain)
   double at_bytes = 0;             // algorithmic HBM bytes of the level's k_assemble_tile
   double bwd_part_flops = 0;       // ... flops of its k_bwd_part
 };
@@ -102,6 +103,7 @@ struct CholPlan {
   std::vector<int> small_list, level_fronts, potrf_list;
   std::vector<int4> syrk_tasks, sdiag_tasks, col_tasks;
   std::vector<int4> bwd_tasks;
+  std::vector<int4> bwdc_tasks;    // (front, c0, c1, block): k_bwd_chain, per level
   std::vector<int2> bwd_pref;      // per bwd task: first partial, partial count (init tasks)
   std::vector<int4> bwd_part_tasks;  // (front, c0, r0, partial slot)
   int npart = 0;
@@ -150,7 +152,7 @@ struct CholPlan {
   hipStream_t side2 = nullptr;     // small fronts beside the blocked path
   hipStream_t side3 = nullptr;     // the second wavefront class of small fronts, beside side2
   hipEvent_t evs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  int4 *d_bwd = nullptr, *d_bwd_part = nullptr;
+  int4 *d_bwd = nullptr, *d_bwd_part = nullptr, *d_bwdc = nullptr;
   int2* d_bwd_pref = nullptr;
   double* d_partial = nullptr;
   int4* d_ea_tasks = nullptr;

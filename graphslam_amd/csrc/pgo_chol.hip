@@ -1539,6 +1539,66 @@ __global__ __launch_bounds__(256) void k_bwd_step(CholDev c, const int4* __restr
   }
 }
 
+// All backward steps of a level in one launch (replacing one k_bwd_step launch
+// per block): the workgroup of block j of a front takes z_j from k_bwd_init,
+// then for b = nblk-1 down to j+1 -- as soon as block b's x is published by its
+// workgroup (in-launch hand-off: sc1 stores, flag, sc1 loads; the flags are the
+// factorisation's stepflag, zeroed per solve) -- z_j -= L[block b, j]' x_b with
+// k_bwd_step's arithmetic, then solves x_j = X_jj' z_j and publishes it.  The
+// same operations in the same order as the step launches: bitwise their result.
+// Tasks are ordered by distance from the front's last block, so a workgroup
+// waits only on workgroups dispatched before it; the waits are bounded.
+__global__ __launch_bounds__(256) void k_bwd_chain(CholDev c, const int4* __restrict__ tasks) {
+  lane_offset(c);
+  __shared__ double xbk[64];
+  __shared__ double z[64];
+  const int4 t = tasks[blockIdx.x];
+  const int s = t.x, c0 = t.y, c1 = t.z, jblk = t.w;
+  const int n2 = c1 - c0;
+  const int m = c.m[s], w = c.w[s], nblk = (w + 63) / 64;
+  const double* L = c.F + c.foff[s];
+  double* fv = c.fv + c.voff[s];
+  const int* rows = c.rows + c.rptr[s];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  TinvCol tc;
+  if (tid < 64) {
+    tinv_col_load(tc, c.Tinv + c.toff[s] + jblk * 4096, n2);   // in flight
+    z[tid] = tid < n2 ? fv[c0 + tid] : 0.0;                    // k_bwd_init's z (earlier launch)
+  }
+  for (int b = nblk - 1; b > jblk; b--) {
+    const int jb = b * 64, nbk = min(64, w - jb);
+    double acc[16];
+    const bool rin = lane < nbk;
+    const double* Lr = L + (jb + lane) + (size_t)(c0 + 16 * wv) * m;
+#pragma unroll
+    for (int q = 0; q < 16; q++) acc[q] = (rin && c0 + 16 * wv + q < c1) ? Lr[(size_t)q * m] : 0.0;
+    if (b < nblk - 1) wait_step(c, c.stepflag + s, nblk - 1 - b);   // x_b from its chain workgroup
+    if (tid < 64) xbk[tid] = tid < nbk ? ld_sc1(fv + jb + tid) : 0.0;
+    __syncthreads();
+    const double xl = xbk[lane];
+#pragma unroll
+    for (int q = 0; q < 16; q++) acc[q] *= xl;
+    halve<16>(acc, lane);
+    halve<8>(acc, lane);
+    halve<4>(acc, lane);
+    halve<2>(acc, lane);
+    double tsum = acc[0];
+    tsum += __shfl_xor(tsum, 16);
+    tsum += __shfl_xor(tsum, 32);
+    const int j = c0 + 16 * wv + lane;
+    if (lane < 16 && j < c1) z[j - c0] = z[j - c0] - tsum;
+    __syncthreads();
+  }
+  if (tid < 64) {
+    const double x = tinv_col_dot(tc, z, n2);
+    if (tid < n2) {
+      st_sc1(fv + c0 + tid, x);
+      c.xv[3 * rows[(c0 + tid) / 3] + (c0 + tid) % 3] = x;
+    }
+  }
+  publish_step(c.stepflag + s, nblk - 1 - jblk);
+}
+
 // ------------------------------------------------------------ marginals
 // Marginal covariance of one pose (GTSAM Marginals::marginalCovariance): with
 // H_perm = L L', the 3x3 block of H^-1 at the pose is Y'Y, Y = L^-1 [e_a e_b e_c]
@@ -1735,6 +1795,7 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(up(&P.d_level_fronts, P.level_fronts, s));
   CH_TRY(up(&P.d_potrf, P.potrf_list, s));
   CH_TRY(up(&P.d_bwd, P.bwd_tasks, s));
+  CH_TRY(up(&P.d_bwdc, P.bwdc_tasks, s));
   CH_TRY(up(&P.d_bwd_pref, P.bwd_pref, s));
   CH_TRY(up(&P.d_bwd_part, P.bwd_part_tasks, s));
   CH_TRY(up(&P.d_syrk, P.syrk_tasks, s));
@@ -1789,7 +1850,7 @@ void chol_free(CholPlan& P) {
   void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
                   P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
                   P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
-                  P.d_syrk, P.d_ea_tasks, P.d_ea_pairs, P.d_potrf, P.d_bwd, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_at_iptr, P.d_at_items, P.d_col, P.d_stepflag, P.d_xown, P.d_xforeign, P.d_xsol_own, P.d_xsol_foreign, P.d_xsend, P.d_xrecv};
+                  P.d_syrk, P.d_ea_tasks, P.d_ea_pairs, P.d_potrf, P.d_bwd, P.d_bwdc, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_at_iptr, P.d_at_items, P.d_col, P.d_stepflag, P.d_xown, P.d_xforeign, P.d_xsol_own, P.d_xsol_foreign, P.d_xsend, P.d_xrecv};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : P.evs)
@@ -2008,6 +2069,9 @@ hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb, long 
   const CholDev c = dev_view(P);
   const int g = (P.n + 255) / 256;
   const dim3 B256(256);
+  // backward steps chained in one launch per level (PGO_BWD_STEPS=1: one launch per step)
+  static const bool chain = !getenv("PGO_BWD_STEPS");
+  if (chain) CH_TRY(hipMemsetAsync(P.d_stepflag, 0, sizeof(int) * std::max(P.ns, 1) * nb, s));
   for (auto it = P.levels.rbegin(); it != P.levels.rend(); ++it) {
     const CholLevel& lv = *it;
     if (prof) prof->cur_tag = (int)(&lv - P.levels.data()) << 16;
@@ -2018,11 +2082,17 @@ hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb, long 
     launch(prof, kFamBwdInit, [&] { return make_double2(0, 0); }, k_bwd_init, dim3(lv.bwd[0].cnt, nb), B256, 0, s, c,
            (const int4*)(P.d_bwd + lv.bwd[0].off), (const int2*)(P.d_bwd_pref + lv.bwd[0].off),
            (const double*)P.d_partial);
-    for (size_t q = 1; q < lv.bwd.size(); q++) {
-      const int bb = lv.maxblk - (int)q;   // step b = maxblk-1 .. 1
-      if (lv.bwd[q].cnt)
-        launch(prof, kFamBwdStep, [&] { return make_double2(0, 0); }, k_bwd_step, dim3(lv.bwd[q].cnt, nb), B256, 0,
-               s, c, (const int4*)(P.d_bwd + lv.bwd[q].off), bb);
+    if (chain) {
+      if (lv.bwdc.cnt)
+        launch(prof, kFamBwdStep, [&] { return make_double2(0, 0); }, k_bwd_chain, dim3(lv.bwdc.cnt, nb), B256, 0,
+               s, c, (const int4*)(P.d_bwdc + lv.bwdc.off));
+    } else {
+      for (size_t q = 1; q < lv.bwd.size(); q++) {
+        const int bb = lv.maxblk - (int)q;   // step b = maxblk-1 .. 1
+        if (lv.bwd[q].cnt)
+          launch(prof, kFamBwdStep, [&] { return make_double2(0, 0); }, k_bwd_step, dim3(lv.bwd[q].cnt, nb), B256,
+                 0, s, c, (const int4*)(P.d_bwd + lv.bwd[q].off), bb);
+      }
     }
   }
   if (P.part_size > 1) {   // every rank's subtree solutions -> every rank

@@ -469,6 +469,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.potrf_list.clear();
   P.col_tasks.clear();
   P.bwd_tasks.clear();
+  P.bwdc_tasks.clear();
   P.bwd_pref.clear();
   P.bwd_part_tasks.clear();
   P.npart = 0;
@@ -508,6 +509,19 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       st.cnt = (int)P.bwd_tasks.size() - st.off;
       lv.bwd_part = sp;
       lv.bwd.push_back(st);
+    }
+    {   // the same steps as one chained launch (k_bwd_chain): block j of a front
+        // after the blocks above it, tasks ordered by distance from the last
+        // block so that every workgroup waits only on earlier-dispatched ones
+      lv.bwdc.off = (int)P.bwdc_tasks.size();
+      for (int d = 1; d < lv.maxblk; d++)
+        for (int s : bylevel[L]) {
+          const int w = P.w[s], nblk = (w + 63) / 64;
+          if (d >= nblk) continue;
+          const int j = nblk - 1 - d;
+          P.bwdc_tasks.push_back(make_int4(s, j * 64, j * 64 + 64, j));
+        }
+      lv.bwdc.cnt = (int)P.bwdc_tasks.size() - lv.bwdc.off;
     }
     for (int b = lv.maxblk - 1; b >= 1; b--) {   // backward step b: columns left of block b
       SolveStep st{(int)P.bwd_tasks.size(), 0};
