@@ -468,90 +468,160 @@ __device__ __forceinline__ void st16(double* C, d4 v, bool sub) {
   }
 }
 
+// 8x8 lower triangle packed row by row
+#define P8(i, j) ((i) * ((i) + 1) / 2 + (j))
+
+// Cholesky factor of an 8x8 SPD block held whole, the same values, in every
+// lane: the pivot chain (rsqrt, scale, rank-1 update of the next diagonal) runs
+// in registers with no cross-lane traffic.  a: lower, packed; iv[j] = 1 / L_jj.
+__device__ __forceinline__ bool chol8_lane(double (&a)[36], double (&iv)[8]) {
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    double d = a[P8(j, j)];
+    if (!(d > 0.0) || !isfinite(d)) {
+      bad = true;
+      d = 1.0;
+    }
+    const double inv = rsqrt_nr(d);
+    iv[j] = inv;
+    a[P8(j, j)] = d * inv;
+#pragma unroll
+    for (int i = j + 1; i < 8; i++) a[P8(i, j)] *= inv;
+#pragma unroll
+    for (int i = j + 1; i < 8; i++)
+#pragma unroll
+      for (int k = j + 1; k <= i; k++) a[P8(i, k)] = fma(-a[P8(i, j)], a[P8(k, j)], a[P8(i, k)]);
+  }
+  return bad;
+}
+
+// In place L -> L^-1 (8x8 lower, packed), columns right to left:
+// X_ij = -(1 / L_jj) sum_{k=j+1..i} X_ik L_kj.
+__device__ __forceinline__ void inv8_lane(double (&a)[36], const double (&iv)[8]) {
+#pragma unroll
+  for (int j = 7; j >= 0; j--) {
+#pragma unroll
+    for (int i = 7; i > j; i--) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = i; k > j; k--) s = fma(a[P8(i, k)], a[P8(k, j)], s);   // X_i,j+1 (newest) last
+      a[P8(i, j)] = -iv[j] * s;
+    }
+    a[P8(j, j)] = iv[j];
+  }
+}
+
+// Factor and inverse of the 16x16 diagonal block TJ (LDS, ld 65, lower valid)
+// by one wave, as 2x2 blocks of 8: A11 = L11 L11^T and X11 = L11^-1 lane-local
+// (chol8_lane, inv8_lane, every lane the same values), L21 = A21 X11^T and
+// A22 - L21 L21^T one element per lane, A22' lane-local again, then
+// X21 = -X22 (L21 X11).  Writes L to TJ (lower) and X to WJ (ld 65, lower,
+// zeros above); sc: LDS scratch of 64.  Same wave only: LDS accesses of one
+// wave complete in order, so no barrier between a lane's store and another's
+// load.  (Solving rows of L21 against a lane-held L11 instead, with A22' formed
+// in registers, measured slower: 34.4 k against 33.0 k cycles per 64x64.)
+__device__ __forceinline__ bool diag16_lane(double* TJ, double* WJ, double* sc) {
+  const int l = threadIdx.x & 63, r = l >> 3, c = l & 7;
+  double a[36], iv[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j <= i; j++) a[P8(i, j)] = TJ[i + j * 65];
+  // zeros above the diagonal of X (blocks (0,0), (1,1) upper, (0,1))
+  WJ[r + (8 + c) * 65] = 0.0;
+  if (c > r) {
+    WJ[r + c * 65] = 0.0;
+    WJ[(8 + r) + (8 + c) * 65] = 0.0;
+  }
+  bool bad = chol8_lane(a, iv);
+  if (l == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int j = 0; j <= i; j++) TJ[i + j * 65] = a[P8(i, j)];
+  }
+  inv8_lane(a, iv);
+  if (l == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int j = 0; j <= i; j++) WJ[i + j * 65] = a[P8(i, j)];
+  }
+  __builtin_amdgcn_wave_barrier();
+  // L21 (r, c) = sum_k A21(r, k) X11(c, k)   (X11 upper is zero)
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) s = fma(TJ[(8 + r) + k * 65], WJ[c + k * 65], s);
+  __builtin_amdgcn_wave_barrier();
+  TJ[(8 + r) + c * 65] = s;
+  __builtin_amdgcn_wave_barrier();
+  // A22 (r, c) -= sum_k L21(r, k) L21(c, k), lower part
+  double t = TJ[(8 + r) + (8 + c) * 65];
+#pragma unroll
+  for (int k = 0; k < 8; k++) t = fma(-TJ[(8 + r) + k * 65], TJ[(8 + c) + k * 65], t);
+  // Y = L21 X11 (X11 (k, c) zero for k < c)
+  double y = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) y = fma(TJ[(8 + r) + k * 65], WJ[k + c * 65], y);
+  __builtin_amdgcn_wave_barrier();
+  if (c <= r) TJ[(8 + r) + (8 + c) * 65] = t;
+  sc[r * 8 + c] = y;
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j <= i; j++) a[P8(i, j)] = TJ[(8 + i) + (8 + j) * 65];
+  bad = chol8_lane(a, iv) || bad;
+  if (l == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int j = 0; j <= i; j++) TJ[(8 + i) + (8 + j) * 65] = a[P8(i, j)];
+  }
+  inv8_lane(a, iv);
+  if (l == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int j = 0; j <= i; j++) WJ[(8 + i) + (8 + j) * 65] = a[P8(i, j)];
+  }
+  __builtin_amdgcn_wave_barrier();
+  // X21 (r, c) = -sum_k X22 (r, k) Y (k, c)   (X22 upper is zero)
+  double z = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) z = fma(WJ[(8 + r) + (8 + k) * 65], sc[k * 8 + c], z);
+  WJ[(8 + r) + c * 65] = -z;
+  return bad;
+}
+
 // Cholesky factor L and inverse X = L^-1 of the 64x64 SPD tile T (LDS,
 // column-major, ld 65, lower part valid, identity beyond the live size), by the
 // 4 waves of the workgroup: right-looking over 16-column blocks J; the 16x16
-// diagonal block is factored and inverted by wave 0 (lane (r, g): row r,
-// columns g, g+4, g+8, g+12; column j and row j of the inverse broadcast
-// through LDS), the rest are 16x16x16 MFMA products:
+// diagonal block is factored and inverted by wave 0 (diag16_lane), the rest
+// are 16x16x16 MFMA products:
 //   L_IJ = A_IJ X_JJ^T,  X_JK = X_JJ W_JK (K < J),
 //   A_IK -= L_IJ L_KJ^T (K > J),  W_IK -= L_IJ X_JK (K <= J)
 // where W (LDS, ld 65) must hold zeros below the diagonal blocks on entry
-// (the diagonal blocks are written here) and ends as X.
+// (the diagonal blocks are written here) and ends as X.  Look-ahead: of the
+// trailing updates of step J, wave 0 takes only the next diagonal block's and
+// goes straight on to factor it while waves 1-3 finish the others (they touch
+// neither that block nor its W block).
 // Returns (wave 0) whether a pivot was not positive and finite.
 __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double* bc) {
-  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int tid = threadIdx.x, wv = tid >> 6;
   DIAG_CLK(0);
   bool bad = false;
   for (int J = 0; J < 4; J++) {
     const int o = 16 * J;
     double* TJ = T + o + o * 65;
     if (wv == 0) {
-      const int r = l & 15, g = l >> 4;
-      double a[4], x[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int cu = 4 * u + g;
-        a[u] = cu <= r ? TJ[r + cu * 65] : 0.0;
-        x[u] = r == cu ? 1.0 : 0.0;
-      }
-      // pivot chain one step ahead in scalars: d_{j+1} = a(j+1,j+1) - l_{j+1}^2 from
-      // lane values before step j's broadcast, so the rsqrt overlaps the LDS round trip
-      double d = readlane_f64(a[0], 0);
-      if (!(d > 0.0) || !isfinite(d)) {
-        bad = true;
-        d = 1.0;
-      }
-      double inv = rsqrt_nr(d);
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const int gj = j & 3, uj = j >> 2;
-        double dn = 1.0, invn = 1.0;
-        if (j < 15) {
-          const int j1 = j + 1, g1 = j1 & 3, u1 = j1 >> 2;
-          const double l1 = readlane_f64(a[uj], j1 + 16 * gj) * inv;
-          dn = fma(-l1, l1, readlane_f64(a[u1], j1 + 16 * g1));
-          if (!(dn > 0.0) || !isfinite(dn)) {
-            bad = true;
-            dn = 1.0;
-          }
-          invn = rsqrt_nr(dn);
-        }
-        if (g == gj) {
-          const double lv = r > j ? a[uj] * inv : 0.0;
-          a[uj] = r == j ? d * inv : lv;
-          bc[r] = lv;
-        }
-        if (r == j) {
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            x[u] *= inv;
-            bc[16 + 4 * u + g] = x[u];
-          }
-        }
+      if (J > 0) {   // A_JJ -= L_J,J-1 L_J,J-1^T, the update left to this wave
+        const d4 v = mm16(T + o + (o - 16) * 65, 1, 65, T + o + (o - 16) * 65, 65, 1);
+        st16(TJ, v, true);
         __builtin_amdgcn_wave_barrier();
-        const double lr = bc[r];
-        double lk[4], xj[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          lk[u] = bc[4 * u + g];
-          xj[u] = bc[16 + 4 * u + g];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          a[u] = fma(-lr, lk[u], a[u]);
-          x[u] = fma(-lr, xj[u], x[u]);
-        }
-        __builtin_amdgcn_wave_barrier();
-        d = dn;
-        inv = invn;
       }
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int cu = 4 * u + g;
-        if (cu <= r) TJ[r + cu * 65] = a[u];
-        W[(o + r) + (o + cu) * 65] = cu <= r ? x[u] : 0.0;
-      }
+      bad = diag16_lane(TJ, W + o + o * 65, bc) || bad;
     }
     __syncthreads();
     DIAG_CLK(1 + 3 * J);
@@ -570,16 +640,17 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
     if (J == 3) break;
     __syncthreads();
     DIAG_CLK(2 + 3 * J);
-    // phase C: trailing updates of T and W.  A wave's (up to 3) products read
-    // only block column / row J and write blocks outside it: all products'
-    // loads and MFMAs first, then the read-modify-write stores, so their
-    // latencies overlap instead of adding up
+    // phase C on waves 1-3: trailing updates of T and W but the next diagonal
+    // block (pair 0).  A wave's (up to 3) products read only block column / row
+    // J and write blocks outside it: all products' loads and MFMAs first, then
+    // the read-modify-write stores, so their latencies overlap
+    if (wv == 0) continue;
     const int nA = (3 - J) * (4 - J) / 2, nW = (3 - J) * (J + 1);
     d4 acc[3];
     double* dst[3];
 #pragma unroll
     for (int u = 0; u < 3; u++) {
-      const int t = wv + 4 * u;
+      const int t = wv + 3 * u;
       dst[u] = nullptr;
       if (t >= nA + nW) continue;               // wave-uniform
       if (t < nA) {
@@ -602,8 +673,6 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
 #pragma unroll
     for (int u = 0; u < 3; u++)
       if (dst[u]) st16(dst[u], acc[u], true);
-    __syncthreads();
-    DIAG_CLK(3 + 3 * J);
   }
   __syncthreads();
   DIAG_CLK(12);
@@ -1147,7 +1216,7 @@ __device__ __forceinline__ void first_diag_body(const CholDev& c, int s, double*
 // First panel of every big front of a level: workgroups [0, np) factor the
 // fronts' first diagonal tiles (list), the others solve 64-row tiles below
 // them (col: (front, r0, 0, -1)) once the tile's inverse is published.
-__global__ __launch_bounds__(256) void k_panel_first(CholDev c, const int* __restrict__ list, int np,
+__global__ __launch_bounds__(256, 2) void k_panel_first(CholDev c, const int* __restrict__ list, int np,
                                                      const int4* __restrict__ col) {
   lane_offset(c);
   __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
@@ -1171,7 +1240,7 @@ __global__ __launch_bounds__(256) void k_panel_first(CholDev c, const int* __res
 //   the rest            the other Schur-update tiles (syrk_lds_body)
 // The diagonal workgroups come first in dispatch order, so every waiting
 // workgroup waits on a workgroup dispatched before it.
-__global__ __launch_bounds__(256) void k_step(CholDev c, const int4* __restrict__ sdiag, int nsd,
+__global__ __launch_bounds__(256, 2) void k_step(CholDev c, const int4* __restrict__ sdiag, int nsd,
                                               const int4* __restrict__ col, int ncol, const int4* __restrict__ tiles,
                                               int kb, int slot) {
   lane_offset(c);

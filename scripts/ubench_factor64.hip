@@ -1,17 +1,19 @@
 // Microbenchmark of diag_factor_invert (the 64x64 factor + inverse on the
 // panel chain): one workgroup, a random SPD tile, clock64 stamps at its phases
-// (PGO_DIAG_CLOCKS): per 16-column block J the wave-0 pivot chain (A), the
-// panel / inverse-row products (B) and the trailing updates (C).
+// (PGO_DIAG_CLOCKS): per 16-column block J the wave-0 diagonal block (A, beside
+// the previous block's trailing updates C) and the panel / inverse-row products (B).
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include scripts/ubench_factor64.hip -o graphslam_amd/build/ubench_factor64
 #define PGO_DIAG_CLOCKS 1
 #include "../graphslam_amd/csrc/pgo_chol.hip"
 
 #include <cstdio>
 #include <vector>
+#include <cmath>
+#include <algorithm>
 
 using namespace pgo;
 
-__global__ __launch_bounds__(256) void u_factor(const double* A, double* out, int reps) {
+__global__ __launch_bounds__(256) void u_factor(const double* A, double* out, int reps, double* LX = nullptr) {
   __shared__ double T[64 * 65], W[64 * 65], bc[64];
   for (int rep = 0; rep < reps; rep++) {
     for (int i = threadIdx.x; i < 64 * 65; i += 256) {
@@ -24,6 +26,11 @@ __global__ __launch_bounds__(256) void u_factor(const double* A, double* out, in
     __syncthreads();
     if (threadIdx.x == 0) out[0] += T[63 + 63 * 65] + W[63 + 63 * 65] + (bad ? 1 : 0);
   }
+  if (LX)
+    for (int i = threadIdx.x; i < 4096; i += 256) {
+      LX[i] = T[(i & 63) + (i >> 6) * 65];
+      LX[4096 + i] = W[(i & 63) + (i >> 6) * 65];
+    }
 }
 
 int main() {
@@ -35,20 +42,35 @@ int main() {
   hipMalloc(&dO, sizeof(double));
   hipMemcpy(dA, A.data(), sizeof(double) * 4096, hipMemcpyHostToDevice);
   hipMemset(dO, 0, sizeof(double));
-  u_factor<<<1, 256>>>(dA, dO, 3);
+  double* dLX;
+  hipMalloc(&dLX, sizeof(double) * 8192);
+  u_factor<<<1, 256>>>(dA, dO, 3, dLX);
   hipDeviceSynchronize();
+  {  // check: L L^T = A and X L = I (lower parts)
+    std::vector<double> LX(8192);
+    hipMemcpy(LX.data(), dLX, sizeof(double) * 8192, hipMemcpyDeviceToHost);
+    double e1 = 0, e2 = 0;
+    for (int i = 0; i < 64; i++)
+      for (int j = 0; j <= i; j++) {
+        double s = 0, t = 0;
+        for (int k = 0; k <= j; k++) s += LX[i + 64 * k] * LX[j + 64 * k];
+        for (int k = j; k <= i; k++) t += LX[4096 + i + 64 * k] * LX[k + 64 * j];
+        e1 = std::max(e1, std::fabs(s - A[i + 64 * j]));
+        e2 = std::max(e2, std::fabs(t - (i == j ? 1.0 : 0.0)));
+      }
+    double up = 0;
+    for (int i = 0; i < 64; i++)
+      for (int j = i + 1; j < 64; j++) up = std::max(up, std::fabs(LX[4096 + i + 64 * j]));
+    printf("max |LL^T - A| %.3g  max |XL - I| %.3g  max |X upper| %.3g\n", e1, e2, up);
+  }
   long long clk[32];
   hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_diag_clk), sizeof(clk));
   printf("total %lld cycles\n", clk[12] - clk[0]);
   long long prev = clk[0];
-  for (int J = 0; J < 4; J++) {
-    const int a = 1 + 3 * J, b = 2 + 3 * J, cq = 3 + 3 * J;
-    if (J < 3) {
-      printf("J%d chain %lld  B %lld  C %lld\n", J, clk[a] - prev, clk[b] - clk[a], clk[cq] - clk[b]);
-      prev = clk[cq];
-    } else {
-      printf("J%d chain %lld  B+end %lld\n", J, clk[a] - prev, clk[12] - clk[a]);
-    }
+  for (int J = 0; J < 4; J++) {   // A: wave 0's diagonal block (with phase C of J-1 beside it), B: panel products
+    const long long b = J < 3 ? clk[2 + 3 * J] : clk[12];
+    printf("J%d A(+C) %lld  B %lld\n", J, clk[1 + 3 * J] - prev, b - clk[1 + 3 * J]);
+    prev = b;
   }
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
