@@ -56,6 +56,10 @@ int fail(const char* m) {
 }  // namespace
 
 int main() {
+  // every front a look-ahead front (the skip and prep bookkeeping on small ones too), then the default
+  for (const char* la : {"64", "1000000000", ""}) {
+  if (*la) setenv("PGO_LOOKAHEAD_M", la, 1);
+  else unsetenv("PGO_LOOKAHEAD_M");
   for (int ordering : {pgo::kOrderNd, pgo::kOrderAmd}) {
     const Pattern G = make_pattern(3000, 400, 7);
     pgo::CholPlan P;
@@ -119,7 +123,9 @@ int main() {
     int maxw = 0;
     for (int s2 = 0; s2 < P.ns; s2++) maxw = std::max(maxw, P.w[s2]);
     if (P.schedule_error) return fail("grid: panel schedule bookkeeping");
-    std::printf("grid plan: %d fronts, widest %d pivot columns\n", P.ns, maxw);
+    std::printf("grid plan (look-ahead threshold %s): %d fronts, widest %d pivot columns\n", *la ? la : "default",
+                P.ns, maxw);
+  }
   }
   std::printf("host selftest ok\n");
   return 0;

@@ -37,7 +37,9 @@ struct PanelStep {                 // one 64-column panel kb of every big front 
   int potrf_off, potrf_cnt;        // first panel: fronts whose diagonal tile k_panel_first factors (potrf_list)
   int col_off, fcol_cnt, col_cnt;  // col_tasks [col_off, +fcol_cnt): first panel's trsm row tiles (front, r0, 0, -1);
                                    // then col_cnt (front, r0, kn, kb): next panel's column block below its
-                                   // diagonal tile, updated with panel kb then solved (k_step)
+                                   // diagonal tile, updated with panel kb then solved (k_step); then
+  int prep_cnt = 0;                // prep tiles (front, r0, kn + 64, k0): the block after next brought up
+                                   // to panel kb (k_step workgroups, look-ahead fronts)
   int sdiag_off, sdiag_cnt;        // next panel's diagonal tiles (front, kn, kn, kb) updated + factored (k_step)
   int syrk_off, syrk_cnt;          // the other Schur-update tiles (front, row0, col0, kb)
   int syrk_tile;                   // kTile or kBigTile

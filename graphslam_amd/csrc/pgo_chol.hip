@@ -1241,8 +1241,8 @@ __global__ __launch_bounds__(256, 2) void k_panel_first(CholDev c, const int* __
 // The diagonal workgroups come first in dispatch order, so every waiting
 // workgroup waits on a workgroup dispatched before it.
 __global__ __launch_bounds__(256, 2) void k_step(CholDev c, const int4* __restrict__ sdiag, int nsd,
-                                              const int4* __restrict__ col, int ncol, const int4* __restrict__ tiles,
-                                              int kb, int slot) {
+                                              const int4* __restrict__ col, int ncol, int nprep,
+                                              const int4* __restrict__ tiles, int kb, int slot) {
   lane_offset(c);
   __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
   const int b = blockIdx.x;
@@ -1264,7 +1264,11 @@ __global__ __launch_bounds__(256, 2) void k_step(CholDev c, const int4* __restri
     STAMP(sl, 8);
     return;
   }
-  syrk_lds_body(c, tiles[b - nsd - ncol], kb, smem);
+  if (b < nsd + ncol + nprep) {   // prep tiles follow the column tasks in col
+    syrk_lds_body(c, col[b - nsd], kb, smem);
+    return;
+  }
+  syrk_lds_body(c, tiles[b - nsd - ncol - nprep], kb, smem);
 }
 
 // Schur update of one 128x128 lower tile (same task format and semantics as
@@ -2061,7 +2065,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       const int4* tiles = (const int4*)(P.d_syrk + ps.syrk_off);
       const int nin = ps.syrk_inline && !off("plain") ? ps.syrk_cnt : 0;
       const bool apart = ps.syrk_cnt > 0 && !ps.syrk_inline && !off("plain");   // plain tiles in their own launch
-      const bool step = ps.sdiag_cnt + ps.col_cnt + nin > 0 && !off("step");
+      const bool step = ps.sdiag_cnt + ps.col_cnt + ps.prep_cnt + nin > 0 && !off("step");
       auto plain = [&](hipStream_t st) {
         const bool big = ps.syrk_tile == kBigTile;
         launch(prof, big ? kFamPanelSyrk128 : kFamPanelSyrk, [&] { return make_double2(ps.plain_flops * nb, 0); },
@@ -2073,8 +2077,9 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       }
       if (step)
         launch(prof, kFamStep, [&] { return make_double2(ps.step_flops * nb, 0); }, k_step,
-               dim3(ps.sdiag_cnt + ps.col_cnt + nin, nb), B256, 0, s, c, (const int4*)(P.d_sdiag + ps.sdiag_off),
-               ps.sdiag_cnt, cols + ps.fcol_cnt, ps.col_cnt, tiles, ps.kb,
+               dim3(ps.sdiag_cnt + ps.col_cnt + ps.prep_cnt + nin, nb), B256, 0, s, c,
+               (const int4*)(P.d_sdiag + ps.sdiag_off), ps.sdiag_cnt, cols + ps.fcol_cnt, ps.col_cnt, ps.prep_cnt,
+               tiles, ps.kb,
                stamps && li + 1 == P.levels.size() && ps.kb / kNB < kMaxStampSlots ? ps.kb / kNB : -1);
       if (apart) {   // (never on the main stream: an earlier plain may still run on P.side)
         plain(P.side);

@@ -681,7 +681,15 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       // front is the same in every plan (the partitioned plans' fronts are bit
       // for bit the one-rank plan's).
       const bool lookahead = !getenv("PGO_NO_LOOKAHEAD");
-      auto front_skip = [&](int s) { return lookahead && P.m[s] >= kLookaheadM; };
+      // (PGO_LOOKAHEAD_M: the front height threshold, a test knob)
+      const int la_m = getenv("PGO_LOOKAHEAD_M") ? atoi(getenv("PGO_LOOKAHEAD_M")) : kLookaheadM;
+      auto front_skip = [&](int s) { return lookahead && P.m[s] >= la_m; };
+      // Prep (look-ahead fronts): the step also brings the column block after
+      // the next one, [kn + 64, kn + 128), up to date with the panels before kn
+      // (k_step workgroups beside the diagonal chain), so the next step's
+      // diagonal and column tasks apply one panel only; the plain tiles skip
+      // that block too.  Only for whole 64-column pivot blocks.
+      auto has_prep = [&](int s, int kn_) { return front_skip(s) && kn_ + 2 * kNB <= P.w[s]; };
       auto plain_range = [&](int s, bool skip, int& cstart, int& cend) {
         const int w = P.w[s], m = P.m[s], nb = std::min(kNB, w - kb), kn = kb + nb;
         const int bs = kb & ~(kKB - 1), be = std::min(bs + kKB, w);
@@ -691,7 +699,10 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
         if (skip && kn + kNB < w) {   // the next step prepares [kn2, kn2 + 64): only when it covers all of it
           const int kn2 = kn + kNB, bs2 = kn & ~(kKB - 1), be2 = std::min(bs2 + kKB, w);
           const int colend2 = kn2 < be2 ? be2 : m;
-          if (std::min(kn2 + kNB, colend2) == kn2 + kNB && cstart + kNB <= cend) cstart += kNB;
+          if (std::min(kn2 + kNB, colend2) == kn2 + kNB && cstart + kNB <= cend) {
+            cstart += kNB;
+            if (has_prep(s, kn2)) cstart += kNB;   // the next step's prep block
+          }
         }
       };
       auto ntiles = [&](int T) {
@@ -712,6 +723,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       const int tile0 = ntiles(kBigTile) >= 4096 ? kBigTile : kTile;
       const bool apart = apart_chain || !(tile0 == kTile && ntiles(kTile) <= kInlineTiles);
       std::vector<int4> plain;   // (front, first column, end column, k0): rows from the column down
+      std::vector<int4> prep;    // prep tiles (front, r0, c0, k0), whole 64x64 tiles
       bool conflict = false;   // a front's next step reads this step's plain tiles
       for (size_t i = 0; i < big.size(); i++) {
         const int s = big[i];
@@ -741,6 +753,19 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
           }
           ps.syrk_flops += (double)depth * (c1 - kn) * (2.0 * m - kn - c1 + 1.0);
         }
+        if (has_prep(s, kn)) {
+          const int b0 = kn + kNB, b1 = b0 + kNB, k0 = applied[i][b0];
+          if (!uniform(i, b0, b1, k0) || k0 > kb) {
+            if (getenv("PGO_SCHED_DEBUG") && !P.schedule_error)
+              fprintf(stderr, "sched: prep front %d w %d m %d kb %d cols [%d,%d) k0 %d\n", s, w, m, kb, b0, b1, k0);
+            P.schedule_error = true;
+          }
+          for (int j = b0; j < b1; j++) applied[i][j] = kn;
+          for (int r0 = b0; r0 < m; r0 += kNB) prep.push_back(make_int4(s, r0, b0, k0));
+          const double f = (double)(kn - k0) * kNB * (2.0 * m - b0 - b1 + 1.0);
+          ps.step_flops += f;
+          ps.syrk_flops += f;
+        }
         int cstart, cend;
         plain_range(s, front_skip(s), cstart, cend);
         if (kn + kNB < w && cstart < cend) {   // the next step prepares [kn2, c2) of this front
@@ -768,6 +793,8 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       ps.syrk_flops += ps.plain_flops;
       ps.sdiag_cnt = (int)P.sdiag_tasks.size() - ps.sdiag_off;
       ps.col_cnt = (int)P.col_tasks.size() - ps.col_off - ps.fcol_cnt;
+      P.col_tasks.insert(P.col_tasks.end(), prep.begin(), prep.end());
+      ps.prep_cnt = (int)prep.size();
       long long cnt128 = 0;
       for (const int4& u : plain)
         for (int c0 = u.y; c0 < u.z; c0 += kBigTile) cnt128 += (P.m[u.x] - c0 + kBigTile - 1) / kBigTile;
