@@ -125,6 +125,19 @@ def cpu_baseline(g, nd_order, per_step, reps=5, amd_reps=3):
     }
 
 
+def _lane_traffic(pmc, kernel, fam):
+    """PMC HBM bytes per launch of `kernel` (profiles/pmc_traffic.json, measured
+    on one-lambda-lane launches) scaled to this run's launches by their
+    algorithmic flops per launch (the lane mix); None when not profiled."""
+    v = pmc.get(f"{kernel}_bytes_per_launch")
+    f1 = pmc.get(f"{kernel}_flops_per_launch")
+    if v is None:
+        return None
+    if f1 and fam.get("flops_per_launch"):
+        return v * fam["flops_per_launch"] / f1
+    return v
+
+
 def factor_roofline(kprof, totals, factor_flops):
     """Roofline of the dominant kernel family of the factor + solve (largest
     summed device time over the profiled factorisations, every launch timed
@@ -170,7 +183,7 @@ def factor_roofline(kprof, totals, factor_flops):
         t = fams[top]
         out.update(bound=t["bound"], achieved=t["achieved"], unit=t["unit"], frac=t["frac"],
                    peak=FP64_MFMA_PEAK_TFS if t["bound"] == "mfma" else HBM_PEAK_GBS,
-                   avg_launch_ms=t["avg_launch_ms"], traffic=pmc.get(f"{top}_bytes_per_launch"))
+                   avg_launch_ms=t["avg_launch_ms"], traffic=_lane_traffic(pmc, top, t))
     return out
 
 

@@ -691,6 +691,22 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// 16-byte forms (MI355X_MICROARCH.md: 8-byte accesses run at 0.54-0.70x the
+// 16-byte rate): buffer loads / stores with aux 16 = sc1, through a
+// wave-uniform descriptor of the payload
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p, unsigned bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ void st2_sc1(__amdgpu_buffer_rsrc_t r, int elem, double x, double y) {
+  const double2 v = make_double2(x, y);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, elem * 8, 0, 16);
+}
+__device__ __forceinline__ double2 ld2_sc1(__amdgpu_buffer_rsrc_t r, int elem) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, elem * 8, 0, 16));
+}
 __device__ __forceinline__ double ld_sc1(const double* p) {
   return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -743,10 +759,15 @@ __device__ __forceinline__ void panel_rhs(double* v, const double* X, int nb, do
 // trsm's lane l needs for k-step ks, column tile ct) -- the hand-off payload
 __device__ __forceinline__ void publish_inverse(double* __restrict__ Mf, const double* Ws, int nb) {
   const int tid = threadIdx.x;
-  for (int idx = tid; idx < 4096; idx += 256) {
+  const __amdgpu_buffer_rsrc_t r = wave_rsrc(Mf, 4096 * 8);
+#pragma unroll
+  for (int u = 0; u < 8; u++) {   // element pairs (idx, idx + 1): rows fa, fa + 1 of one column fb
+    const int idx = 2 * (tid + 256 * u);
     const int l = idx & 63, ct = (idx >> 6) & 3, ks = idx >> 8;
     const int fa = 16 * ct + (l & 15), fb = 4 * ks + (l >> 4);
-    st_sc1(Mf + idx, (fa < nb && fb < nb && fa >= fb) ? Ws[fa + fb * 65] : 0.0);
+    const double x0 = (fa < nb && fb < nb && fa >= fb) ? Ws[fa + fb * 65] : 0.0;
+    const double x1 = (fa + 1 < nb && fb < nb && fa + 1 >= fb) ? Ws[fa + 1 + fb * 65] : 0.0;
+    st2_sc1(r, idx, x0, x1);
   }
 }
 
@@ -821,12 +842,16 @@ __device__ __forceinline__ void trsm_rows(const CholDev& c, int s, int r0, int k
   const double* Mf = c.Tinv + c.tfo + c.toff[s] + (kn / 64) * 4096;
   double* fv = c.fv + c.voff[s];
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
-  {   // the inverse once per workgroup into LDS (xs: 4096 doubles), 16 coalesced sc1 loads per thread in flight
-    double t[16];
+  {   // the inverse once per workgroup into LDS (xs: 4096 doubles), 8 coalesced 16-byte sc1 loads per thread in flight
+    const __amdgpu_buffer_rsrc_t r = wave_rsrc(Mf, 4096 * 8);
+    double2 t[8];
 #pragma unroll
-    for (int u = 0; u < 16; u++) t[u] = ld_sc1(Mf + tid + 256 * u);
+    for (int u = 0; u < 8; u++) t[u] = ld2_sc1(r, 2 * (tid + 256 * u));
 #pragma unroll
-    for (int u = 0; u < 16; u++) xs[tid + 256 * u] = t[u];
+    for (int u = 0; u < 8; u++) {
+      xs[2 * (tid + 256 * u)] = t[u].x;
+      xs[2 * (tid + 256 * u) + 1] = t[u].y;
+    }
   }
   __syncthreads();
   const int rw = r0 + wv * 16;

@@ -74,10 +74,21 @@ def main():
     traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
     ent = traffic.get("C3", {})
     ent["source"] = f"{tag}_pmc.json"
-    for k in ("k_panel_syrk_lds", "k_panel_syrk", "k_linearize", "k_linearize_own", "k_linearize_side1", "k_pcg_spmv"):
-        v = summary["kernels"].get(k, {}).get("hbm_bytes_per_launch")
+    ent["lanes"] = 1   # the PMC passes run one lambda lane (gpu_profile.sh --lanes 1)
+    for k in sorted(summary["kernels"]):
+        v = summary["kernels"][k].get("hbm_bytes_per_launch")
         if v is not None:
             ent[f"{k}_bytes_per_launch"] = v
+    # the one-lane launches' algorithmic flops (the trace run's own table), so
+    # bench.py can scale the bytes to its launches' lane mix
+    tb = os.path.join(src, "trace_bench.log")
+    if os.path.exists(tb):
+        lines = [l for l in open(tb) if l.startswith("{")]
+        if lines:
+            fams = (json.loads(lines[-1]).get("roofline") or {}).get("families") or {}
+            for k, f in fams.items():
+                if f.get("flops_per_launch"):
+                    ent[f"{k}_flops_per_launch"] = f["flops_per_launch"]
     traffic["C3"] = ent
     with open(traffic_path, "w") as fh:
         json.dump(traffic, fh, indent=1)
