@@ -853,21 +853,29 @@ __device__ __forceinline__ void trsm_rows(const CholDev& c, int s, int r0, int k
       xs[2 * (tid + 256 * u) + 1] = t[u].y;
     }
   }
-  __syncthreads();
-  const int rw = r0 + wv * 16;
-  if (rw >= m) return;                                // (no barriers below)
-  double* Fc = c.F + c.foff[s] + (size_t)kn * m;
-  const int il = wv * 16 + (l & 15), arow = r0 + il, kl = l >> 4;
-  double a[16], tb[16][4], yc[4];   // A fragments, inverse fragments, y
-#pragma unroll
-  for (int ks = 0; ks < 16; ks++) {
-    const int k = 4 * ks + kl;
-    a[ks] = (arow < m && k < nb) ? A[il * ars + k * acs] : 0.0;
-  }
+  // the panel's y (handed off, sc1) and this lane's right-hand-side rows, in
+  // flight with the inverse's loads (one memory latency, not three)
+  const int rw = r0 + wv * 16, kl = l >> 4;
+  double yc[4], fvr[4];
 #pragma unroll
   for (int ct = 0; ct < 4; ct++) {
     const int col = 16 * ct + (l & 15);
     yc[ct] = col < nb ? ld_sc1(fv + kn + col) : 0.0;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int row = rw + kl + 4 * r;
+    fvr[r] = ((l & 15) == 0 && row < m) ? fv[row] : 0.0;
+  }
+  __syncthreads();
+  if (rw >= m) return;                                // (no barriers below)
+  double* Fc = c.F + c.foff[s] + (size_t)kn * m;
+  const int il = wv * 16 + (l & 15), arow = r0 + il;
+  double a[16], tb[16][4];   // A fragments, inverse fragments
+#pragma unroll
+  for (int ks = 0; ks < 16; ks++) {
+    const int k = 4 * ks + kl;
+    a[ks] = (arow < m && k < nb) ? A[il * ars + k * acs] : 0.0;
   }
 #pragma unroll
   for (int ks = 0; ks < 16; ks++)
@@ -901,7 +909,7 @@ __device__ __forceinline__ void trsm_rows(const CholDev& c, int s, int r0, int k
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o);
     const int row = rw + kl + 4 * r;
-    if ((l & 15) == 0 && row < m) fv[row] -= t;
+    if ((l & 15) == 0 && row < m) fv[row] = fvr[r] - t;
   }
 }
 
@@ -1106,12 +1114,18 @@ __device__ __forceinline__ void diag_tile_update(const CholDev& c, const int4 t,
       st[q] = (k < K && r0 + i < m) ? Fs[(r0 + i) + (size_t)(k0 + k) * m] : 0.0;
     }
   };
+  double cv[16];   // C, lower part of the updated region: its loads and the first chunk's in flight together
 #pragma unroll
-  for (int q = 0; q < 16; q++) {   // C, lower part of the updated region
+  for (int q = 0; q < 16; q++) {
     const int idx = tid + 256 * q, i = idx & 63, j = idx >> 6;
-    Ts[i + j * 65] = (i >= j && r0 + i < m && r0 + j < colend) ? Fs[(r0 + i) + (size_t)(r0 + j) * m] : 0.0;
+    cv[q] = (i >= j && r0 + i < m && r0 + j < colend) ? Fs[(r0 + i) + (size_t)(r0 + j) * m] : 0.0;
   }
   load(0);
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    const int idx = tid + 256 * q;
+    Ts[(idx & 63) + (idx >> 6) * 65] = cv[q];
+  }
   // lower 16x16 blocks (I, J) of this wave
   const int nblk = wv < 2 ? 3 : 2;
   const int bI0 = wv == 0 ? 0 : (wv == 1 ? 3 : 3), bJ0 = wv == 0 ? 0 : (wv == 1 ? 0 : (wv == 2 ? 1 : 2));
