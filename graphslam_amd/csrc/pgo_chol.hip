@@ -1547,12 +1547,18 @@ __global__ __launch_bounds__(256) void k_bwd_part(CholDev c, const int4* __restr
   double acc[64];
 #pragma unroll
   for (int q = 0; q < 64; q++) acc[q] = 0.0;
+  // Every column load is issued unconditionally (columns past ncol re-read the
+  // last one and are not accumulated): a predicated load per column made the
+  // compiler branch around each one and wait on it, 64 serial memory latencies.
   for (int r = r0 + tid; r < r1; r += 256) {
     const double xr = c.xv[3 * rows[r / 3] + r % 3];
     const double* Lr = L + r;
+    double lv[64];
+#pragma unroll
+    for (int q = 0; q < 64; q++) lv[q] = Lr[(size_t)min(q, ncol - 1) * m];
 #pragma unroll
     for (int q = 0; q < 64; q++)
-      if (q < ncol) acc[q] += Lr[(size_t)q * m] * xr;
+      if (q < ncol) acc[q] += lv[q] * xr;
   }
   halve<64>(acc, lane);
   halve<32>(acc, lane);
