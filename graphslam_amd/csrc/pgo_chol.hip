@@ -1530,6 +1530,46 @@ __device__ __forceinline__ void halve(double* acc, int lane) {
   }
 }
 
+// One wave's share of a backward partial product: lane = row (r, r + 256, ...
+// below r1), NC column accumulators, summed over the wave; lane q < NC returns
+// column q's sum.  Every column load is issued unconditionally (columns past
+// ncol re-read the last one and are not accumulated): a predicated load per
+// column made the compiler branch around each one and wait on it, NC serial
+// memory latencies.  NC = 16 serves the narrow fronts near the leaves with a
+// quarter of the reduction.
+template <int NC>
+__device__ __forceinline__ double bwd_part_wave(const CholDev& c, const double* L, const int* rows, int m,
+                                                int ncol, int rbeg, int r1, int lane) {
+  double acc[NC];
+#pragma unroll
+  for (int q = 0; q < NC; q++) acc[q] = 0.0;
+  for (int r = rbeg; r < r1; r += 256) {
+    const double xr = c.xv[3 * rows[r / 3] + r % 3];
+    const double* Lr = L + r;
+    double lv[NC];
+#pragma unroll
+    for (int q = 0; q < NC; q++) lv[q] = Lr[(size_t)min(q, ncol - 1) * m];
+#pragma unroll
+    for (int q = 0; q < NC; q++)
+      if (q < ncol) acc[q] += lv[q] * xr;
+  }
+  if constexpr (NC == 64) {
+    halve<64>(acc, lane);
+    halve<32>(acc, lane);
+  }
+  halve<16>(acc, lane);
+  halve<8>(acc, lane);
+  halve<4>(acc, lane);
+  halve<2>(acc, lane);
+  double v = acc[0];
+  if constexpr (NC == 16) {   // lane l: column l & 15 over its 16-lane group; add the 4 groups
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    v = lane < 16 ? v : 0.0;
+  }
+  return v;
+}
+
 // Backward partial product: part[slot][j] = sum over rows [r0, r0+kBwdRows) of
 // L[r, c0+j] x_r (rows below the pivot columns; x gathered from xv).
 __global__ __launch_bounds__(256) void k_bwd_part(CholDev c, const int4* __restrict__ tasks,
@@ -1544,29 +1584,12 @@ __global__ __launch_bounds__(256) void k_bwd_part(CholDev c, const int4* __restr
   const double* L = c.F + c.foff[s] + (size_t)c0 * m;
   const int* rows = c.rows + c.rptr[s];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  double acc[64];
-#pragma unroll
-  for (int q = 0; q < 64; q++) acc[q] = 0.0;
-  // Every column load is issued unconditionally (columns past ncol re-read the
-  // last one and are not accumulated): a predicated load per column made the
-  // compiler branch around each one and wait on it, 64 serial memory latencies.
-  for (int r = r0 + tid; r < r1; r += 256) {
-    const double xr = c.xv[3 * rows[r / 3] + r % 3];
-    const double* Lr = L + r;
-    double lv[64];
-#pragma unroll
-    for (int q = 0; q < 64; q++) lv[q] = Lr[(size_t)min(q, ncol - 1) * m];
-#pragma unroll
-    for (int q = 0; q < 64; q++)
-      if (q < ncol) acc[q] += lv[q] * xr;
-  }
-  halve<64>(acc, lane);
-  halve<32>(acc, lane);
-  halve<16>(acc, lane);
-  halve<8>(acc, lane);
-  halve<4>(acc, lane);
-  halve<2>(acc, lane);
-  red[wv][lane] = acc[0];
+  if (r0 + 64 * wv >= r1)
+    red[wv][lane] = 0.0;   // no rows for this wave (small fronts): skip the reduction
+  else if (ncol <= 16)
+    red[wv][lane] = bwd_part_wave<16>(c, L, rows, m, ncol, r0 + tid, r1, lane);
+  else
+    red[wv][lane] = bwd_part_wave<64>(c, L, rows, m, ncol, r0 + tid, r1, lane);
   __syncthreads();
   if (tid < 64) part[(size_t)slot * 64 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
 }
