@@ -2063,14 +2063,23 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
     const CholLevel& lv = P.levels[li];
     if (prof) prof->cur_tag = (int)li << 16;
     if (part && (int)li == P.split) CH_TRY(exchange());
+    // frontal vectors (fv) on the second side stream beside the tile assembly
+    // (F): disjoint data, both need only the previous levels; joined before the
+    // level's first factor launch
+    const bool vec = !off("vec");
+    if (vec) {
+      CH_TRY(hipEventRecord(P.evs[0], s));
+      CH_TRY(hipStreamWaitEvent(P.side2, P.evs[0], 0));
+      launch(prof, kFamVecAssemble, [&] { return make_double2(0, 0); }, k_vec_assemble, dim3(lv.front_cnt, nb), B256,
+             (size_t)lv.maxm * sizeof(double), P.side2, c, (const int*)(P.d_level_fronts + lv.front_off));
+      CH_TRY(hipEventRecord(P.evs[1], P.side2));
+    }
     if (lv.ea_cnt[0] && !off("assemble"))
       launch(prof, kFamAssemble, [&] { return make_double2(0, lv.at_bytes * nb); },
              k_assemble_tile, dim3(lv.ea_cnt[0], nb), B256, 0, s, c, (const int4*)(P.d_ea_tasks + lv.ea_off[0]),
              (const int2*)(P.d_at_iptr + lv.ea_off[0]), (const int*)P.d_at_items, (const int4*)P.d_ea_pairs, V,
              (long long)P.nslots, D, (const double*)P.d_lambda);
-    if (!off("vec"))
-      launch(prof, kFamVecAssemble, [&] { return make_double2(0, 0); }, k_vec_assemble, dim3(lv.front_cnt, nb), B256,
-           (size_t)lv.maxm * sizeof(double), s, c, (const int*)(P.d_level_fronts + lv.front_off));
+    if (vec) CH_TRY(hipStreamWaitEvent(s, P.evs[1], 0));
     // small fronts on the second side stream, beside the blocked path of the
     // same level (disjoint fronts); joined before the next level
     // (the two wavefront classes -- m <= 64, m > 64 -- on two side streams,
