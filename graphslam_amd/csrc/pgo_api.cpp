@@ -1417,6 +1417,13 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   std::vector<double> lam_k(T), fac_k(T), outs(4 * T);
   int last_outcome = PGO_STOP_CONVERGED;     // how the last linearisation's tries ended
   std::vector<char> valid(T);
+  // Lanes sized to the tries expected: a linearisation is taken to need as
+  // many tries as the previous one walked, so the round that should reach the
+  // accepted try runs only the lanes up to it (a one-lane round is cheaper than
+  // a batched one); more lanes again if that try fails.  The tries and their
+  // order are unchanged (PGO_LANES_ADAPT=0: every round runs all lanes).
+  static const bool adapt_lanes = !(getenv("PGO_LANES_ADAPT") && atoi(getenv("PGO_LANES_ADAPT")) == 0);
+  int prev_walked = 0;   // tries the previous linearisation walked (0: none yet)
   if (!(err <= p.error_tol) && iters < p.max_iterations && d.n > 0) {
     double new_err = err;
     for (;;) {
@@ -1445,6 +1452,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
         // round runs on rank k / L, lane k % L; the outcomes are walked in
         // sequence order with GTSAM's rules, so the accepted step is the
         // sequential one.
+        int walked = 0;   // tries of this linearisation walked so far
         for (;;) {
           RoctxRange range_round("lambda_round");
           lam_k[0] = lam;
@@ -1457,7 +1465,8 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
           }
           // a profiled factorisation (lane 0, eager, timed launches) runs alone
           const bool prof_next = p.profile_every > 0 && (g->factorizations % p.profile_every) == 0;
-          const int Lr = prof_next ? 1 : L;
+          int Lr = prof_next ? 1 : L;
+          if (adapt_lanes && !exchange && prev_walked > walked) Lr = std::min(Lr, prev_walked - walked);
           std::vector<double> mine(4 * L, 0.0);
           for (int l = 0; l < L; l++) mine[4 * l] = -1.0;  // -1: no try (past the bound / lane idle)
           int nb = 0;   // this rank's valid tries (a prefix of its lanes)
@@ -1507,6 +1516,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
               }
             }
             trace_row(iters, lam_k[k], o[0], lin_change, try_e, fidelity, success ? 1.0 : 0.0);
+            walked++;
             lam = lam_k[k];
             factor = fac_k[k];
             if (success) last_outcome = PGO_STOP_CONVERGED;
@@ -1555,6 +1565,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
           }
           if (done) break;
         }
+        prev_walked = walked;
       }
       if (status != PGO_OK) break;
       new_err = err;
