@@ -321,8 +321,10 @@ def main():
                     help="eager launches instead of the captured factor+solve hipGraph (rocprofv3 runs)")
     ap.add_argument("--marginals", type=int, default=64,
                     help="after the timed steps: time marginal covariances of this many poses (0: skip)")
-    ap.add_argument("--lanes", type=int, default=2,
-                    help="consecutive lambda tries per batched factorisation (pgo_params.lambda_lanes)")
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="consecutive lambda tries per batched factorisation (pgo_params.lambda_lanes; "
+                         "default 3 on one GPU -- the rounds are sized to the tries expected -- and 2 per "
+                         "rank in the speculative multi-GPU search, whose rounds run every lane)")
     ap.add_argument("--multi", choices=["spec", "partition", "replicas"], default="spec",
                     help="N>1: speculative lambda search over RCCL (one job), partitioned factorisation "
                          "(one job: subtrees per rank, Schur complements all-gathered) or independent replicas")
@@ -346,6 +348,8 @@ def main():
 
     r = init_from_env()
     world, rank = r.world, r.rank
+    if args.lanes is None:
+        args.lanes = 2 if world > 1 and args.multi == "spec" else 3
     g = datasets.make(args.config)
     from graphslam_amd import _lib
     ordering = _lib.PGO_ORDERING_AMD if args.ordering == "amd" else _lib.PGO_ORDERING_ND
