@@ -11,13 +11,15 @@ value = linearisations ("GN iterations": linearise + solve(s) + retract + chi^2)
 of the job (replicas: summed over ranks) / max-over-ranks wall time of the K
 timed steps.
 
-Multi-GPU (--gpus N, one process per GPU via torch.distributed.run): the
-default is the speculative lambda search: every rank holds the
-graph, the ranks solve consecutive lambda tries of GTSAM's sequence at once and
-exchange the outcomes and the accepted values over RCCL (xGMI).  One job,
-bitwise the one-GPU trajectory -> value = that job's linearisations / wall
-time, "strong" scaling.  --multi replicas runs N independent copies instead
-("weak").
+Multi-GPU (--gpus N, one process per GPU via torch.distributed.run), DESIGN.md
+§5: --multi auto (default) picks, by the plan-derived cost model of
+graphslam_amd/multi_model.py, between the speculative lambda search (every rank
+holds the graph, the ranks solve consecutive lambda tries of GTSAM's sequence at
+once and exchange the outcomes and the accepted values over RCCL / xGMI) and the
+partitioned factorisation (subtrees per rank, the top fronts' columns dealt to
+the ranks).  Either is one job, bitwise the one-GPU trajectory -> value = that
+job's linearisations / wall time, "strong" scaling.  --multi replicas runs N
+independent copies instead ("weak").
 
     python bench.py [--gpus N --steps K --warmup W --config C3 --no-cpu-baseline]
 """
@@ -306,6 +308,21 @@ def scan_registration_bench(batch=1024, reps=3, cpu_sample=64):
     return res
 
 
+def _partition_bounds(live):
+    """{config: {P: {bound, bound_replicated_top, est_speedup, exchange_points,
+    exchange_bytes}}}: profiles/r03_partition_bounds.json (host-computed for C3
+    and C5), plus this run's own rank count when it was computed live."""
+    path = os.path.join(ROOT, "profiles", "r03_partition_bounds.json")
+    keep = ("bound", "bound_replicated_top", "est_speedup", "exchange_points", "exchange_bytes")
+    out = {}
+    if os.path.exists(path):
+        for c, per in json.load(open(path)).items():
+            out[c] = {P: {k: v[k] for k in keep} for P, v in per.items()}
+    if live:
+        out["this_run"] = {P: {k: v[k] for k in keep} for P, v in live.items()}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -325,9 +342,11 @@ def main():
                     help="consecutive lambda tries per batched factorisation (pgo_params.lambda_lanes; "
                          "default 3 on one GPU -- the rounds are sized to the tries expected -- and 2 per "
                          "rank in the speculative multi-GPU search, whose rounds run every lane)")
-    ap.add_argument("--multi", choices=["spec", "partition", "replicas"], default="spec",
+    ap.add_argument("--multi", choices=["auto", "spec", "partition", "replicas"], default="auto",
                     help="N>1: speculative lambda search over RCCL (one job), partitioned factorisation "
-                         "(one job: subtrees per rank, Schur complements all-gathered) or independent replicas")
+                         "(one job: subtrees per rank, Schur complements all-gathered, the top fronts' columns "
+                         "dealt to the ranks), independent replicas, or auto: the partitioned mode when the "
+                         "cost model (graphslam_amd/multi_model.py) puts it above the speculative search")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a one-GPU box: every rank on device 0, host (gloo) transport")
     ap.add_argument("--ordering", choices=["nd", "amd"], default="nd",
@@ -348,12 +367,31 @@ def main():
 
     r = init_from_env()
     world, rank = r.world, r.rank
-    if args.lanes is None:
-        args.lanes = 2 if world > 1 and args.multi == "spec" else 3
     g = datasets.make(args.config)
     from graphslam_amd import _lib
     ordering = _lib.PGO_ORDERING_AMD if args.ordering == "amd" else _lib.PGO_ORDERING_ND
     pg = PoseGraph.from_dataset(g, device=0 if args.same_device else r.local_rank, ordering=ordering)
+    # plan-derived bounds of the partitioned factorisation (host only, before
+    # anything is timed): the auto mode's choice, the line's config
+    bounds = {}
+    mode_why = None
+    if world > 1 and args.multi == "auto":
+        from graphslam_amd import multi_model
+        obj = [None]
+        if rank == 0:
+            b = pg.debug_partition_bound(world)
+            b["rank_flops"] = [float(v) for v in b["rank_flops"]]
+            b.update(multi_model.partition_estimate(b))
+            obj = [(multi_model.choose_mode(b), b)]
+        r.dist.broadcast_object_list(obj, src=0)
+        args.multi, b = obj[0]
+        bounds[str(world)] = b
+        mode_why = (f"auto: partition est {b['est_speedup']:.2f}x vs speculative bound {multi_model.SPEC_GAIN}x "
+                    f"({b['model']})")
+    elif args.multi == "auto":
+        args.multi = "spec"
+    if args.lanes is None:
+        args.lanes = 2 if world > 1 and args.multi == "spec" else 3
     spec = world > 1 and args.multi in ("spec", "partition")   # one job over all ranks
     part = world > 1 and args.multi == "partition"
     hc = None
@@ -386,7 +424,7 @@ def main():
     # profiling); one more, untimed step with every profile_every-th
     # factorisation run eagerly with per-launch events feeds the kernel tables
     common = dict(max_outer=args.max_outer, linear_solver=1 if args.solver == "cholesky" else 0,
-                  use_graphs=0 if args.no_graphs else 1, lambda_lanes=1 if part else args.lanes,
+                  use_graphs=0 if args.no_graphs else 1, lambda_lanes=args.lanes,
                   multi_gpu=1 if part else 0)
     params = default_params(profile_every=0, **common)
     prof_params = default_params(profile_every=args.profile_every, **common)
@@ -480,6 +518,11 @@ def main():
                                 "-" + transport) if spec else
                                (f"replicas{world}" if world > 1 else "single-gpu"),
                 "lambda_lanes": args.lanes,
+                "multi_mode": mode_why or (args.multi if world > 1 else None),
+                # plan-derived flop bound of the partitioned factorisation (distributed top) and
+                # the cost model's estimate, per rank count -- scripts/partition_bounds.py;
+                # unmeasured on an 8-GPU node
+                "partition_bounds": _partition_bounds(bounds),
                 "solver": (f"GPU supernodal multifrontal Cholesky ({'nested-dissection' if args.ordering == 'nd' else 'AMD'} ordering, fp64 MFMA Schur updates)"
                            if args.solver == "cholesky" else
                            "block-Jacobi PCG, rel tol %.0e" % params.pcg_relative_tol),

@@ -8,6 +8,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <tuple>
 #include <random>
 #include <vector>
 
@@ -51,6 +53,89 @@ Pattern make_pattern(int n, int lc, unsigned seed, const std::vector<std::pair<i
 int fail(const char* m) {
   std::fprintf(stderr, "host_selftest: %s\n", m);
   return 1;
+}
+
+// Task coverage of one top level / panel step: (kind, front, row tile, column,
+// depth) -> how often.  Plain tiles count per (64-row tile, column) they
+// update (128-tiles split), clipped as the kernels clip them.
+using Key = std::tuple<int, int, int, int, int>;
+void step_keys(const pgo::CholPlan& P, const pgo::PanelStep& ps, std::map<Key, int>& out) {
+  for (int q = ps.syrk_off; q < ps.syrk_off + ps.syrk_cnt; q++) {
+    const int4 t = P.syrk_tasks[q];
+    const int s = t.x, row0 = t.y & pgo::kRowMask, clip = t.y >> pgo::kClipShift, c0 = t.z, m = P.m[s], w = P.w[s];
+    const int T = ps.syrk_tile;
+    int colend = t.w < 0 ? std::min((ps.kb & ~(pgo::kKB - 1)) + pgo::kKB, w) : m;
+    const int cend = std::min({colend, c0 + (clip ? clip : T), m});
+    for (int r0 = row0; r0 < std::min(row0 + T, m); r0 += 64)
+      for (int col = c0; col < cend; col++)
+        if (col <= r0 + 63) out[Key(0, s, r0, col, t.w)]++;
+  }
+  for (int q = ps.sdiag_off; q < ps.sdiag_off + ps.sdiag_cnt; q++) {
+    const int4 t = P.sdiag_tasks[q];
+    out[Key(1, t.x, t.y, t.z, t.w)]++;
+  }
+  for (int q = ps.col_off; q < ps.col_off + ps.fcol_cnt + ps.col_cnt + ps.prep_cnt; q++) {
+    const int4 t = P.col_tasks[q];
+    out[Key(2, t.x, t.y, t.z, t.w)]++;
+  }
+  for (int q = ps.potrf_off; q < ps.potrf_off + ps.potrf_cnt; q++) out[Key(3, P.potrf_list[q], 0, 0, 0)]++;
+}
+
+// The distributed top (part_size > 1): every rank's top tasks together are the
+// replicated plan's (PGO_DIST_TOP=0), each task on its column's rank (every
+// rank for the replicated columns); every factored panel is exchanged.
+int check_distributed(const Pattern& G, int ordering, int size) {
+  std::vector<pgo::CholPlan> D(size), R(size);
+  for (int r = 0; r < size; r++) {
+    for (int dist : {1, 0}) {
+      pgo::CholPlan& Q = dist ? D[r] : R[r];
+      if (!dist) setenv("PGO_DIST_TOP", "0", 1);
+      Q.ordering = ordering;
+      Q.part_size = size;
+      Q.part_rank = r;
+      pgo::chol_analyze(Q, G.n, G.row_ptr, G.col);
+      unsetenv("PGO_DIST_TOP");
+      if (Q.schedule_error) return fail("distributed: schedule");
+    }
+  }
+  const pgo::CholPlan& A = R[0];
+  long long tasks = 0, exch = 0;
+  for (size_t L = A.split; L < A.levels.size(); L++)
+    for (size_t j = 0; j < A.levels[L].panels.size(); j++) {
+      std::map<Key, int> full;
+      step_keys(A, A.levels[L].panels[j], full);
+      std::vector<std::map<Key, int>> got(size);
+      for (int r = 0; r < size; r++) {
+        const pgo::CholPlan& Q = D[r];
+        const size_t LQ = Q.split + (L - A.split);
+        if (LQ >= Q.levels.size() || Q.levels[LQ].panels.size() != A.levels[L].panels.size())
+          return fail("distributed: top levels differ");
+        step_keys(Q, Q.levels[LQ].panels[j], got[r]);
+        const pgo::PanelStep& ps = Q.levels[LQ].panels[j];
+        for (int xi : {ps.xfirst, ps.xstep})
+          if (xi >= 0) exch += Q.xchg[xi].cnt;
+      }
+      for (const auto& [k, cnt] : full) {
+        const int kind = std::get<0>(k), s = std::get<1>(k);
+        const int col = kind == 0 ? std::get<3>(k) : kind == 1 ? std::get<2>(k) : kind == 2 ? std::get<3>(k) : 0;
+        const int o = D[0].cown[D[0].cown_off[s] + col];
+        for (int r = 0; r < size; r++) {
+          const auto it = got[r].find(k);
+          const int want = (o < 0 || o == r) ? cnt : 0;
+          if ((it == got[r].end() ? 0 : it->second) != want) {
+            std::fprintf(stderr, "kind %d front %d row %d col %d depth %d: rank %d has %d, owner %d\n", kind, s,
+                         std::get<2>(k), std::get<3>(k), std::get<4>(k), r, it == got[r].end() ? 0 : it->second, o);
+            return fail("distributed: task coverage");
+          }
+          if (it != got[r].end()) got[r].erase(it);
+        }
+        tasks++;
+      }
+      for (int r = 0; r < size; r++)
+        if (!got[r].empty()) return fail("distributed: a rank has a task the replicated plan lacks");
+    }
+  std::printf("distributed top, %d ranks: %lld task keys checked, %lld panels exchanged\n", size, tasks, exch);
+  return 0;
 }
 
 }  // namespace
@@ -120,6 +205,8 @@ int main() {
     }
     pgo::CholPlan P;
     pgo::chol_analyze(P, G.n, G.row_ptr, G.col);
+    for (int size : {2, 3, 4, 8})
+      if (check_distributed(G, pgo::kOrderNd, size)) return 1;
     int maxw = 0;
     for (int s2 = 0; s2 < P.ns; s2++) maxw = std::max(maxw, P.w[s2]);
     if (P.schedule_error) return fail("grid: panel schedule bookkeeping");

@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -76,6 +77,7 @@ struct pgo_graph {
   double plan_ms = 0.0;
   pgo::ExchangeHook hook;                   // the partitioned factorisation's all-gathers (comm)
   bool chol_ready = false;
+  bool handoff_timeout = false;             // the last factorisation's in-launch hand-off gave up (retried once)
   // profiled factorisations (pgo_params.profile_every): every launch timed
   std::vector<hipEvent_t> sev;              // event pairs, one per launch
   std::vector<int> sev_fam;
@@ -462,11 +464,17 @@ int upload_structure(pgo_graph* g) {
   }
   // the values already resident stay bit for bit (no host atan2 -> cos / sin
   // round trip): vertices are append-only, so the first n_old keep their index
-  double4* keep = nullptr;
+  // (freed on every exit path: an early error return below must not leak it)
+  struct HipFree {
+    void operator()(double4* p) const { (void)hipFree(p); }
+  };
+  std::unique_ptr<double4, HipFree> keep;
   const int n_old = g->dev_values && g->d.pose ? std::min(g->d.n, n) : 0;
   if (n_old > 0) {
-    HIP_TRY(g, hipMalloc((void**)&keep, sizeof(double4) * n_old));
-    HIP_TRY(g, hipMemcpyAsync(keep, g->d.pose, sizeof(double4) * n_old, hipMemcpyDeviceToDevice, g->d.stream));
+    double4* k = nullptr;
+    HIP_TRY(g, hipMalloc((void**)&k, sizeof(double4) * n_old));
+    keep.reset(k);
+    HIP_TRY(g, hipMemcpyAsync(keep.get(), g->d.pose, sizeof(double4) * n_old, hipMemcpyDeviceToDevice, g->d.stream));
   }
   free_device(g, true);
   DevGraph& d = g->d;
@@ -564,9 +572,8 @@ int upload_structure(pgo_graph* g) {
   HIP_TRY(g, hipStreamSynchronize(d.stream));
   g->dev_structure = true;
   if (n_old > 0) {
-    HIP_TRY(g, hipMemcpyAsync(d.pose, keep, sizeof(double4) * n_old, hipMemcpyDeviceToDevice, d.stream));
+    HIP_TRY(g, hipMemcpyAsync(d.pose, keep.get(), sizeof(double4) * n_old, hipMemcpyDeviceToDevice, d.stream));
     HIP_TRY(g, hipStreamSynchronize(d.stream));
-    (void)hipFree(keep);
   }
   return upload_values(g, n_old);
 }
@@ -602,6 +609,22 @@ int exchange_allgather(void* ctx, const void* send, void* recv, size_t bytes, hi
   std::string why;
   const int rc = pgo::comm_allgather_device(&g->comm, send, recv, bytes, s, &why);
   if (rc != PGO_OK) g->last_error = "partition exchange: " + why;
+  return rc == PGO_OK ? 0 : -1;
+}
+
+int exchange_broadcast(void* ctx, void* buf, size_t bytes, int root, hipStream_t s) {
+  pgo_graph* g = static_cast<pgo_graph*>(ctx);
+  std::string why;
+  const int rc = pgo::comm_broadcast_device_async(&g->comm, buf, bytes, root, s, &why);
+  if (rc != PGO_OK) g->last_error = "panel exchange: " + why;
+  return rc == PGO_OK ? 0 : -1;
+}
+
+int exchange_group(void* ctx, int begin) {
+  pgo_graph* g = static_cast<pgo_graph*>(ctx);
+  std::string why;
+  const int rc = pgo::comm_group(&g->comm, begin, &why);
+  if (rc != PGO_OK) g->last_error = "panel exchange group: " + why;
   return rc == PGO_OK ? 0 : -1;
 }
 
@@ -677,6 +700,8 @@ int ensure_chol(pgo_graph* g) {
   g->chol.order_in = order_in;
   g->hook.ctx = g;
   g->hook.allgather = exchange_allgather;
+  g->hook.broadcast = exchange_broadcast;
+  g->hook.group = exchange_group;
   pgo::chol_analyze(g->chol, g->d.n, g->h_row_ptr, g->h_slot_col);
   if (g->chol.schedule_error) return fail(g, PGO_E_HIP, "internal: inconsistent panel schedule");
   RC_TRY(bind_plan(g, true));
@@ -854,7 +879,10 @@ int finish_solve(pgo_graph* g, pgo_stats* st, SolveState* ss) {
   }
   int flag = 0;
   HIP_TRY(g, hipMemcpy(&flag, g->chol.d_flag, sizeof(int), hipMemcpyDeviceToHost));
-  if (flag & 2) return fail(g, PGO_E_HIP, "factorisation: an in-launch hand-off timed out");
+  if (flag & 2) {
+    g->handoff_timeout = true;
+    return fail(g, PGO_E_HIP, "factorisation: an in-launch hand-off timed out");
+  }
   ss->solved = flag == 0;
   ss->known = true;
   if (st) st->factor_flops = g->chol.flops;
@@ -968,9 +996,16 @@ int run_lanes(pgo_graph* g, const pgo_params& p, int nb, const double* lams, dou
   HIP_TRY(g, hipEventRecord(ev[2], d.stream));
   HIP_TRY(g, hipMemcpyAsync(g->chol.d_lambda, g->h_lanes + 4 * 8, nb * sizeof(double), hipMemcpyHostToDevice,
                             d.stream));
-  if (!p.use_graphs) {
-    HIP_TRY(g, pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr, nb));
-    HIP_TRY(g, pgo::chol_solve(g->chol, g->xb, d.stream, nb, 3LL * d.n));
+  const bool part = g->chol.part_size > 1;
+  if (!p.use_graphs || part) {   // (partitioned: eager, the exchanges run between the phases)
+    pgo::ExchangeHook* hook = part ? &g->hook : nullptr;
+    g->hook.failed = false;
+    const hipError_t ef = pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr, nb, hook);
+    if (g->hook.failed) return fail(g, PGO_E_COMM, g->last_error);
+    HIP_TRY(g, ef);
+    const hipError_t es = pgo::chol_solve(g->chol, g->xb, d.stream, nb, 3LL * d.n, nullptr, hook);
+    if (g->hook.failed) return fail(g, PGO_E_COMM, g->last_error);
+    HIP_TRY(g, es);
   } else {
     RC_TRY(graph_factor_solve(g, nb, g->xb, 3LL * d.n));
   }
@@ -989,7 +1024,10 @@ int run_lanes(pgo_graph* g, const pgo_params& p, int nb, const double* lams, dou
   int flags[8];
   std::memcpy(flags, g->h_lanes + 4 * 8 + 8, nb * sizeof(int));
   for (int l = 0; l < nb; l++)
-    if (flags[l] & 2) return fail(g, PGO_E_HIP, "factorisation: an in-launch hand-off timed out");
+    if (flags[l] & 2) {
+      g->handoff_timeout = true;
+      return fail(g, PGO_E_HIP, "factorisation: an in-launch hand-off timed out");
+    }
   for (int l = 0; l < nb; l++) {
     out[4 * l] = flags[l] == 0 ? 1.0 : 0.0;
     out[4 * l + 1] = g->h_lanes[4 * l];
@@ -1000,7 +1038,7 @@ int run_lanes(pgo_graph* g, const pgo_params& p, int nb, const double* lams, dou
     st->ms_solve += ms_between(ev[2], ev[3]);
     st->ms_update += ms_between(ev[3], ev[4]);
     st->factor_flops = g->chol.flops;
-    if (p.use_graphs) {
+    if (p.use_graphs && !part) {   // (ev[5] is recorded by the graph replay only)
       st->ms_factor_graph += ms_between(ev[2], ev[5]);
       st->factor_graph_flops += nb * g->chol.flops;
     }
@@ -1020,7 +1058,10 @@ int ensure_search(pgo_graph* g) {
 
 double ms_between(hipEvent_t a, hipEvent_t b) {
   float ms = 0.f;
-  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+    (void)hipGetLastError();   // (an unrecorded event must not surface as the next launch's error)
+    return 0.0;
+  }
   return ms;
 }
 
@@ -1207,7 +1248,7 @@ int pgo_get_poses(pgo_graph* g, size_t n, const uint64_t* keys, double* out) {
   RC_TRY(download_values(g));
   if (!keys) {
     if (n != g->keys.size()) return fail(g, PGO_E_ARG, "n must equal the number of vertices when keys is NULL");
-    std::memcpy(out, g->xyt.data(), 3 * n * sizeof(double));
+    if (n) std::memcpy(out, g->xyt.data(), 3 * n * sizeof(double));
     return PGO_OK;
   }
   for (size_t i = 0; i < n; i++) {
@@ -1225,7 +1266,7 @@ int pgo_set_poses(pgo_graph* g, size_t n, const uint64_t* keys, const double* xy
     if (!std::isfinite(xyt[i])) return fail(g, PGO_E_NONFINITE, "non-finite value");
   if (!keys) {
     if (n != g->keys.size()) return fail(g, PGO_E_ARG, "n must equal the number of vertices when keys is NULL");
-    std::memcpy(g->xyt.data(), xyt, 3 * n * sizeof(double));
+    if (n) std::memcpy(g->xyt.data(), xyt, 3 * n * sizeof(double));
   } else {
     for (size_t i = 0; i < n; i++) {
       auto it = g->index.find(keys[i]);
@@ -1372,7 +1413,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
     }
     first_try = false;
   };
-  auto run_try = [&](double lam_try, double* out) -> int {
+  auto run_try_once = [&](double lam_try, double* out) -> int {
     SolveState ss;
     HIP_TRY(g, hipEventRecord(ev[2], d.stream));
     RC_TRY(linear_solve(g, p, lam_try, &st, &ss));
@@ -1395,6 +1436,21 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
     out[3] = g->h_scal[2];
     return PGO_OK;
   };
+  // a try whose in-launch hand-off timed out (a workgroup starved on a shared
+  // GPU) runs once more before the optimize fails (every rank of a partitioned
+  // run sees the same flags, so all retry together)
+  auto retried = [&](auto&& body) -> int {
+    g->handoff_timeout = false;
+    int rc = body();
+    if (rc == PGO_E_HIP && g->handoff_timeout) {
+      g->handoff_timeout = false;
+      rc = body();
+    }
+    return rc;
+  };
+  auto run_try = [&](double lam_try, double* out) -> int {
+    return retried([&] { return run_try_once(lam_try, out); });
+  };
   pgo::Comm& cm = g->comm;
   // the speculative search's ranks (a partitioned run is one search: P = 1 here)
   const int P = partition ? 1 : cm.size, me = partition ? 0 : cm.rank;
@@ -1402,11 +1458,12 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   st.ranks = cm.size;
   // lanes: concurrent tries on this GPU (Cholesky LM only)
   int L = 1;
-  if (!partition && p.algorithm != PGO_ALG_GN && p.linear_solver != PGO_SOLVER_PCG && p.lambda_lanes > 1 && d.n > 0)
+  if (p.algorithm != PGO_ALG_GN && p.linear_solver != PGO_SOLVER_PCG && p.lambda_lanes > 1 && d.n > 0)
     L = ensure_lanes(g, p.lambda_lanes);
-  // every rank must agree on the lanes per rank (a lane allocation may fail on one)
-  if (exchange) {
-    std::vector<double> all(P);
+  // every rank must agree on the lanes per rank (a lane allocation may fail on
+  // one); a partitioned run's ranks factor the same lanes together
+  if (exchange || (partition && cm.size > 1)) {
+    std::vector<double> all(cm.size);
     const double mineL = L;
     std::string why;
     const int rc = pgo::comm_allgather(&cm, &mineL, 1, all.data(), d.stream, &why);
@@ -1474,7 +1531,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
           if (nb == 1) {
             RC_TRY(run_try(lam_k[me * L], &mine[0]));
           } else if (nb > 1) {
-            RC_TRY(run_lanes(g, p, nb, &lam_k[me * L], mine.data(), &st));
+            RC_TRY(retried([&] { return run_lanes(g, p, nb, &lam_k[me * L], mine.data(), &st); }));
             st.solves += nb;
             account_linearize();
           }
@@ -1749,7 +1806,7 @@ int pgo_comm_selftest(pgo_graph* g) {
 int pgo_get_trace(const pgo_graph* g, double* out, int cap) {
   if (!g || cap < 0 || (cap > 0 && !out)) return PGO_E_ARG;
   const int rows = (int)(g->trace.size() / kTraceCols);
-  std::memcpy(out, g->trace.data(), sizeof(double) * kTraceCols * std::min(rows, cap));
+  if (cap > 0 && rows > 0) std::memcpy(out, g->trace.data(), sizeof(double) * kTraceCols * std::min(rows, cap));
   return rows;
 }
 
@@ -1794,6 +1851,26 @@ int pgo_debug_partition(pgo_graph* g, int size, int* owner, double* out, int cap
   for (int s = 0; s < P.ns && s < cap; s++) owner[s] = own[s];
   for (int r = 0; r < size && r < cap; r++) out[r] = rf[r];
   if (size < cap) out[size] = top;
+  if (cap >= 2 * size + 2) {
+    double rep = 0;
+    const std::vector<double> df = pgo::distributed_rank_flops(P, size, &rep);
+    for (int r = 0; r < size; r++) out[size + 1 + r] = df[r];
+    out[2 * size + 1] = rep;
+  }
+  if (cap >= 2 * size + 4 && size > 1) {   // the exchanges of the distributed top (rank 0's plan: all ranks share them)
+    pgo::CholPlan Q;
+    Q.ordering = g->ordering;
+    Q.part_size = size;
+    Q.part_rank = 0;
+    pgo::chol_analyze(Q, (int)g->keys.size(), H.row_ptr, H.slot_col);
+    double pts = 0, dbl = 0;
+    for (const pgo::XExchange& x : Q.xchg) {
+      pts++;
+      for (long long v : x.size) dbl += (double)v;
+    }
+    out[2 * size + 2] = pts;
+    out[2 * size + 3] = dbl;
+  }
   return P.ns;
 }
 
@@ -1801,7 +1878,7 @@ int pgo_debug_ordering(pgo_graph* g, int32_t* perm, size_t n) {
   if (!g || (n && !perm) || n != g->keys.size()) return PGO_E_ARG;
   RC_TRY(download_values(g));
   if (g->chol_ready) {
-    std::memcpy(perm, g->chol.perm.data(), n * sizeof(int32_t));
+    if (n) std::memcpy(perm, g->chol.perm.data(), n * sizeof(int32_t));
     return PGO_OK;
   }
   HostStructure H;
@@ -1809,7 +1886,7 @@ int pgo_debug_ordering(pgo_graph* g, int32_t* perm, size_t n) {
   pgo::CholPlan P;
   P.ordering = g->ordering;
   pgo::chol_analyze(P, (int)n, H.row_ptr, H.slot_col);
-  std::memcpy(perm, P.perm.data(), n * sizeof(int32_t));
+  if (n) std::memcpy(perm, P.perm.data(), n * sizeof(int32_t));
   return PGO_OK;
 }
 
@@ -1911,7 +1988,7 @@ int pgo_debug_linearize(pgo_graph* g, double* hdiag, double* hoff, double* grad,
   if (hoff)
     for (int e = 0; e < d.ne; e++)
       for (int q = 0; q < 9; q++) hoff[9 * (size_t)e + q] = V[q * (size_t)d.nslots + g->edge_slot0[e]];
-  if (grad) std::memcpy(grad, G.data(), G.size() * 8);
+  if (grad && !G.empty()) std::memcpy(grad, G.data(), G.size() * 8);
   return PGO_OK;
 }
 
@@ -1950,7 +2027,7 @@ int pgo_debug_linearize_cholesky(pgo_graph* g, double* hdiag, double* hoff, doub
         for (int c = 0; c < 3; c++)
           hoff[9 * (size_t)e + 3 * r + c] = V[(side0_owner ? 3 * r + c : 3 * c + r) * (size_t)d.nslots + de];
     }
-  if (grad) std::memcpy(grad, G.data(), G.size() * 8);
+  if (grad && !G.empty()) std::memcpy(grad, G.data(), G.size() * 8);
   return PGO_OK;
 }
 

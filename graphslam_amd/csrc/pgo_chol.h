@@ -30,7 +30,12 @@ constexpr int kKB = 256;         // Schur updates deferred per kKB-column block 
 constexpr int kInlineTiles = 512;
 constexpr int kLookaheadM = 2048;  // fronts this tall skip the next step's column block in their plain tiles
 constexpr int kMaxStampSlots = 256;  // PGO_STEP_STAMPS diagnostics // syrk tiles per step that ride inside k_step
-constexpr int kBwdRows = 512;      // rows per partial product of the backward solve           // Schur-update depth: trailing matrix updated once per kKB columns
+constexpr int kBwdRows = 512;      // rows per partial product of the backward solve
+// Schur-update tile tasks (front, row0 | clip << kClipShift, col0, k0): clip > 0
+// limits the tile to columns [col0, col0 + clip) (a distributed top front's
+// tile split where the column owner changes)
+constexpr int kClipShift = 20;
+constexpr int kRowMask = (1 << kClipShift) - 1;
 
 struct PanelStep {                 // one 64-column panel kb of every big front of a level
   int kb;
@@ -49,6 +54,15 @@ struct PanelStep {                 // one 64-column panel kb of every big front 
   double first_flops;              // algorithmic flops of k_panel_first (factor, inverse, trsm)
   double step_flops;               // ... of k_step (updates, factor, inverse, trsm, inline tiles)
   int plain_lag = 0;               // apart plain tiles: joined before step +1 or (look-ahead skip) +2
+  int xfirst = -1, xstep = -1;     // distributed top: exchanges after k_panel_first / k_step (index in xchg)
+};
+
+// Distributed top (part_size > 1): one exchange point -- the panels (or tails)
+// xp_tasks[off, off + cnt) go from their owners to every rank, one broadcast per
+// rank with a payload (size[r] doubles per lane, rank r's region of d_xprecv).
+struct XExchange {
+  int off = 0, cnt = 0;
+  std::vector<long long> size;
 };
 
 struct SolveStep {                 // one launch of the blocked triangular solves
@@ -71,6 +85,7 @@ struct CholLevel {
   std::vector<SolveStep> bwd;      // backward: [0] = init (all columns), then steps b = maxblk-1 .. 1
   SolveStep bwd_part{0, 0};        // partial products feeding the init tasks
   SolveStep bwdc{0, 0};            // the backward steps as one chained launch (k_bwd_chain)
+  int xtail = -1;                  // distributed top: the fronts' tail columns to every rank at the level's end
   double at_bytes = 0;             // algorithmic HBM bytes of the level's k_assemble_tile
   double bwd_part_flops = 0;       // ... flops of its k_bwd_part
 };
@@ -127,6 +142,14 @@ struct CholPlan {
   std::vector<long long> xsize, xsol_size;
   long long xmax = 0, xsol_max = 0;     // largest per-rank payload (all-gather slot)
   std::vector<int4> xsol_ranges;        // (rank, first, end, offset): solution entries (xv) of each subtree
+  // distributed top: column owners of the top fronts (cown[cown_off[s] + col]:
+  // rank, -1 every rank; cown_off -1 for subtree fronts) and the exchanges
+  std::vector<int> cown_off, cown;
+  std::vector<XExchange> xchg;
+  std::vector<int4> xp_tasks;           // (front, kn, nb | kind << 16, owner): kind 0 panel, 1 tail columns
+  std::vector<long long> xp_loff;       // offset of the item in its owner's payload (doubles)
+  std::vector<long long> xp_lstride;    // its owner's payload per lane at that exchange (doubles)
+  long long xp_rslot = 0;               // largest payload per rank and lane
   double flops = 0, nnzl = 0, syrk_flops = 0;
   long long ftotal = 0, ttotal = 0;
   int vtotal = 0;
@@ -148,7 +171,10 @@ struct CholPlan {
   int* d_at_items = nullptr;
   int4 *d_xown = nullptr, *d_xforeign = nullptr, *d_xsol_own = nullptr, *d_xsol_foreign = nullptr;
   int n_xown = 0, n_xforeign = 0, n_xsol_own = 0, n_xsol_foreign = 0;
-  double *d_xsend = nullptr, *d_xrecv = nullptr;   // exchange buffers (xmax / size x xmax doubles)
+  double *d_xsend = nullptr, *d_xrecv = nullptr;   // exchange buffers (xmax / size x xmax doubles, x lanes)
+  int4* d_xp = nullptr;            // xp_tasks
+  long long* d_xp_off = nullptr;   // (xp_loff, xp_lstride) pairs
+  double* d_xprecv = nullptr;      // panel exchange: size regions of xp_rslot x batch doubles
   int* d_stepflag = nullptr;       // [batch][ns]: last panel (kb / 64 + 1) whose diagonal inverse is published
   hipStream_t side = nullptr;      // look-ahead diagonal tiles
   hipStream_t side2 = nullptr;     // small fronts beside the blocked path
@@ -179,6 +205,11 @@ std::vector<int> order_nd(int n, const std::vector<int>& xadj, const std::vector
 std::vector<int> partition_subtrees(const CholPlan& P, int size, std::vector<double>* rank_flops = nullptr,
                                     double* top_flops = nullptr);
 
+// host: per-rank flops of the partitioned factorisation with the distributed
+// top (subtrees + the rank's top columns + the top work every rank repeats,
+// returned in *replicated)
+std::vector<double> distributed_rank_flops(const CholPlan& P, int size, double* replicated = nullptr);
+
 // host: symbolic analysis from the block-CSR pattern (old pose indices)
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
 // host: (re)build the plan's H assembly lists for a pattern its fronts hold
@@ -200,6 +231,11 @@ hipError_t chol_set_batch(CholPlan& P, int nb, hipStream_t s);
 struct ExchangeHook {
   void* ctx = nullptr;
   int (*allgather)(void* ctx, const void* send, void* recv, size_t bytes, hipStream_t s) = nullptr;
+  // distributed top: `bytes` at buf from rank root to every rank (in place),
+  // enqueued on stream s; several in a row form one group (group(ctx, 1) ...
+  // group(ctx, 0) around them, optional)
+  int (*broadcast)(void* ctx, void* buf, size_t bytes, int root, hipStream_t s) = nullptr;
+  int (*group)(void* ctx, int begin) = nullptr;
   bool failed = false;
 };
 

@@ -20,7 +20,10 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <algorithm>
 
 #include "pgo_chol.h"
 
@@ -44,6 +47,7 @@ struct CholDev {
   long long fst, tst;              // F, Tinv doubles per lane
   long long tfo;                   // Tinv + tfo: the inverses again, in the trsm's MFMA operand order
   int vst, xst, pst;               // fv, xv, backward partials per lane
+  unsigned long long poll_ticks;   // in-launch hand-off: give up after this many 10 ns ticks
 };
 
 // this workgroup's lane (blockIdx.y): every lane factors H + lambda_y I with
@@ -75,6 +79,10 @@ static CholDev dev_view(const CholPlan& P) {
   c.vst = P.vtotal;
   c.xst = 3 * P.n;
   c.pst = std::max(P.npart, 1) * 64;
+  // PGO_HANDOFF_TIMEOUT_MS (default 2000): a hand-off wait that long means a
+  // lost workgroup (a time-sliced queue on a shared GPU waits far less)
+  static const double tmo_ms = getenv("PGO_HANDOFF_TIMEOUT_MS") ? atof(getenv("PGO_HANDOFF_TIMEOUT_MS")) : 2000.0;
+  c.poll_ticks = (unsigned long long)(std::max(tmo_ms, 1.0) * 1e5);
   return c;
 }
 
@@ -717,14 +725,15 @@ __device__ __forceinline__ void publish_step(int* flag, int val) {
   if (threadIdx.x == 0) __hip_atomic_store(flag, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Waits (one lane polls, the workgroup joins a barrier) until *flag >= val;
-// gives up after ~0.2 s with bit 2 of the pivot flag set (reported as a HIP
-// failure by the host), so a lost hand-off can never hang the GPU.
+// gives up after c.poll_ticks (PGO_HANDOFF_TIMEOUT_MS, default 2 s) with bit 2
+// of the pivot flag set (the host retries the try once, then reports a HIP
+// failure), so a lost hand-off can never hang the GPU.
 __device__ __forceinline__ void wait_step(const CholDev& c, const int* flag, int val) {
   if (threadIdx.x == 0) {
     const unsigned long long t0 = wall_clock64();   // 100 MHz
     while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < val) {
       __builtin_amdgcn_s_sleep(2);
-      if (wall_clock64() - t0 > 20000000ull) {
+      if (wall_clock64() - t0 > c.poll_ticks) {
         __hip_atomic_fetch_or(c.flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -1001,12 +1010,13 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
   constexpr int LD = 64 + 4;
   double(*Sr)[16 * LD] = reinterpret_cast<double(*)[16 * LD]>(smem);
   double(*Sc)[16 * LD] = reinterpret_cast<double(*)[16 * LD]>(smem + 2 * 16 * LD);
-  const int s = t.x, row0 = t.y, col0 = t.z;
+  const int s = t.x, row0 = t.y & kRowMask, col0 = t.z, clip = t.y >> kClipShift;
   const bool inner = t.w < 0;
   const int k0 = t.w & 0x7fffffff;
   const int m = c.m[s], w = c.w[s];
   const int kend = min(kb + kNB, w);
-  const int colend = inner ? min((kb & ~(kKB - 1)) + kKB, w) : m;
+  int colend = inner ? min((kb & ~(kKB - 1)) + kKB, w) : m;
+  if (clip) colend = min(colend, col0 + clip);   // a split tile: its columns only
   const int K = kend - k0, nch = (K + 15) >> 4;
   double* Fs = c.F + c.foff[s];
   const double* P = Fs + (size_t)k0 * m;
@@ -1414,13 +1424,17 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
 // column by column (column j: rows j..u-1 at j u - j (j - 1) / 2), then the
 // update vector fv[w..m).  One workgroup per root, a wave per column.
 // tasks: (front, payload offset in buf, u, 0); unpack reverses it.
+// tasks: (front, payload offset, u, rank); lane y (grid y) at rank * rstride +
+// y * slot in buf (pack: rank 0, rstride 0 -- this rank's send buffer)
 template <bool kPack>
-__global__ __launch_bounds__(256) void k_xroots(CholDev c, const int4* __restrict__ tasks, double* __restrict__ buf) {
+__global__ __launch_bounds__(256) void k_xroots(CholDev c, const int4* __restrict__ tasks, double* __restrict__ buf,
+                                                long long slot, long long rstride) {
+  lane_offset(c);
   const int4 t = tasks[blockIdx.x];
   const int s = t.x, u = t.z, m = c.m[s], w = c.w[s];
   double* U = c.F + c.foff[s] + w + (size_t)w * m;
   double* v = c.fv + c.voff[s] + w;
-  double* b = buf + t.y;
+  double* b = buf + t.w * rstride + blockIdx.y * slot + t.y;
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
   for (int j = wv; j < u; j += 4) {
     double* col = b + (size_t)j * u - (size_t)j * (j - 1) / 2;
@@ -1436,16 +1450,78 @@ __global__ __launch_bounds__(256) void k_xroots(CholDev c, const int4* __restric
   }
 }
 
-// Solution ranges of the subtrees: (rank, first, end, offset) -- pack: buf[off +
-// k] = xv[first + k]; unpack: xv[first + k] = buf[rank * slot + off + k]
+// Solution ranges of the subtrees: (rank, first, end, offset), lane z: pack:
+// buf[z * slot + off + k] = xv[first + k]; unpack: xv[first + k] = buf[rank *
+// rstride + z * slot + off + k]
 template <bool kPack>
 __global__ __launch_bounds__(256) void k_xsol(CholDev c, const int4* __restrict__ ranges, double* __restrict__ buf,
-                                              long long slot) {
+                                              long long slot, long long rstride) {
   const int4 r = ranges[blockIdx.y];
   const int n = r.z - r.y;
+  double* xv = c.xv + blockIdx.z * c.xst;
+  const double* b = buf + (kPack ? 0 : r.x * rstride) + blockIdx.z * slot + r.w;
   for (int k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
-    if (kPack) buf[r.w + k] = c.xv[r.y + k];
-    else c.xv[r.y + k] = buf[r.x * slot + r.w + k];
+    if (kPack) buf[blockIdx.z * slot + r.w + k] = xv[r.y + k];
+    else xv[r.y + k] = b[k];
+  }
+}
+
+// Pivot flags through the solution exchange (every rank must take the same LM
+// decision: a bad pivot can be seen by one rank only): pack puts lane y's flag
+// at buf[y * slot + at]; reduce ORs every rank's into the flag.
+__global__ void k_xflag(CholDev c, double* __restrict__ buf, long long slot, long long at, long long rstride,
+                        int ranks, int pack) {
+  const int y = threadIdx.x;
+  if (pack) {
+    buf[y * slot + at] = (double)c.flag[y];
+    return;
+  }
+  int f = 0;
+  for (int r = 0; r < ranks; r++) f |= (int)buf[r * rstride + y * slot + at];
+  c.flag[y] = f;
+}
+
+// diagnostics (PGO_DEBUG_BAD_PIVOT=rank:count): a bad pivot reported by one rank
+__global__ void k_set_flag(int* flag, int v) { flag[threadIdx.x] |= v; }
+
+// Distributed top: panels / tail columns between ranks.  Task (front, kn, nb |
+// kind << 16, owner); its payload sits in the owner's region of buf (owner *
+// rstride), lane y at y * lstride, + loff.  kind 0 (a factored panel): F rows
+// [kn, m) x columns [kn, kn + nb), the panel's row-major inverse (backward
+// solve), the frontal vector [kn, m) (y and the rows below, forward
+// substitution so far); kind 1 (tail): F rows [kn, m) x columns [kn, kn + nb).
+// Pack: this rank's items (owner == me); unpack: the others'.
+template <bool kPack>
+__global__ __launch_bounds__(256) void k_xpanel(CholDev c, const int4* __restrict__ tasks,
+                                                const long long* __restrict__ offs, double* __restrict__ buf,
+                                                long long rstride, int me) {
+  lane_offset(c);
+  const int4 t = tasks[blockIdx.x];
+  if (kPack != (t.w == me)) return;
+  const int s = t.x, kn = t.y, nb = t.z & 0xffff, kind = t.z >> 16, m = c.m[s];
+  double* b = buf + t.w * rstride + blockIdx.y * offs[2 * blockIdx.x + 1] + offs[2 * blockIdx.x];
+  double* F = c.F + c.foff[s] + kn + (size_t)kn * m;
+  const int rows = m - kn, tid = threadIdx.x;
+  for (int cc = 0; cc < nb; cc++) {
+    double* col = F + (size_t)cc * m;
+    double* bc = b + (size_t)cc * rows;
+    for (int r = tid; r < rows; r += 256) {
+      if (kPack) bc[r] = col[r];
+      else col[r] = bc[r];
+    }
+  }
+  if (kind != 0) return;
+  b += (size_t)rows * nb;
+  double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;
+  for (int i = tid; i < 4096; i += 256) {
+    if (kPack) b[i] = M[i];
+    else M[i] = b[i];
+  }
+  b += 4096;
+  double* v = c.fv + c.voff[s] + kn;
+  for (int r = tid; r < rows; r += 256) {
+    if (kPack) b[r] = v[r];
+    else v[r] = b[r];
   }
 }
 
@@ -1858,13 +1934,20 @@ static hipError_t up(T** d, const std::vector<T>& h, hipStream_t s) {
 
 // numeric workspaces of nb lanes (fronts zeroed: the upper triangles stay zero)
 static void free_numeric(CholPlan& P) {
-  void* ptrs[] = {P.F, P.Tinv, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_partial, P.d_stepflag};
+  void* ptrs[] = {P.F, P.Tinv, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_partial, P.d_stepflag, P.d_xsend, P.d_xrecv,
+                  P.d_xprecv};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   P.F = P.Tinv = P.fv = P.xv = P.d_lambda = P.d_partial = nullptr;
+  P.d_xsend = P.d_xrecv = P.d_xprecv = nullptr;
   P.d_flag = P.d_stepflag = nullptr;
   P.batch = 0;
 }
+
+// partition exchange slots per lane (doubles): the subtree roots' payloads, the
+// solution ranges + the pivot flag (xsol_max), the largest of the two
+static long long xroot_slot(const CholPlan& P) { return std::max(P.xmax, 1LL); }
+static long long xsol_slot(const CholPlan& P) { return P.xsol_max + 1; }
 
 static hipError_t alloc_numeric(CholPlan& P, int nb, hipStream_t s) {
   CH_TRY(hipMalloc((void**)&P.F, nb * std::max<long long>(P.ftotal, 1) * sizeof(double)));
@@ -1876,6 +1959,13 @@ static hipError_t alloc_numeric(CholPlan& P, int nb, hipStream_t s) {
   CH_TRY(hipMalloc((void**)&P.d_lambda, nb * sizeof(double)));
   CH_TRY(hipMalloc((void**)&P.d_partial, (size_t)nb * std::max(P.npart, 1) * 64 * sizeof(double)));
   CH_TRY(hipMemsetAsync(P.F, 0, nb * std::max<long long>(P.ftotal, 1) * sizeof(double), s));
+  {   // partition exchange buffers, nb lanes per rank
+    const long long xs = P.part_size > 1 ? std::max(xroot_slot(P), xsol_slot(P)) : 1;
+    CH_TRY(hipMalloc((void**)&P.d_xsend, sizeof(double) * xs * nb));
+    CH_TRY(hipMalloc((void**)&P.d_xrecv, sizeof(double) * xs * nb * std::max(P.part_size, 1)));
+    const long long xp = P.part_size > 1 ? std::max(P.xp_rslot, 1LL) : 1;
+    CH_TRY(hipMalloc((void**)&P.d_xprecv, sizeof(double) * xp * nb * std::max(P.part_size, 1)));
+  }
   P.batch = nb;
   return hipStreamSynchronize(s);
 }
@@ -1951,7 +2041,7 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
       const int sr = P.xroot[q], r = P.xroot_rank[q], u = P.m[sr] - P.w[sr];
       if (u == 0) continue;
       if (r == P.part_rank) own.push_back(make_int4(sr, (int)P.xroot_off[q], u, 0));
-      else if (P.parent[sr] >= 0) foreign.push_back(make_int4(sr, (int)(r * slot + P.xroot_off[q]), u, 0));
+      else if (P.parent[sr] >= 0) foreign.push_back(make_int4(sr, (int)P.xroot_off[q], u, r));
     }
     for (const int4& rg : P.xsol_ranges) (rg.x == P.part_rank ? sown : sforeign).push_back(rg);
     P.n_xown = (int)own.size();
@@ -1962,9 +2052,14 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
     CH_TRY(up(&P.d_xforeign, foreign, s));
     CH_TRY(up(&P.d_xsol_own, sown, s));
     CH_TRY(up(&P.d_xsol_foreign, sforeign, s));
-    const long long xs = P.part_size > 1 ? std::max({P.xmax, P.xsol_max, 1LL}) : 1;
-    CH_TRY(hipMalloc((void**)&P.d_xsend, sizeof(double) * xs));
-    CH_TRY(hipMalloc((void**)&P.d_xrecv, sizeof(double) * xs * std::max(P.part_size, 1)));
+    (void)slot;
+    std::vector<long long> xo(2 * P.xp_tasks.size());
+    for (size_t q = 0; q < P.xp_tasks.size(); q++) {
+      xo[2 * q] = P.xp_loff[q];
+      xo[2 * q + 1] = P.xp_lstride[q];
+    }
+    CH_TRY(up(&P.d_xp, P.xp_tasks, s));
+    CH_TRY(up(&P.d_xp_off, xo, s));
   }
   CH_TRY(up(&P.d_at_iptr, P.at_iptr, s));
   CH_TRY(up(&P.d_at_items, P.at_items, s));
@@ -1991,7 +2086,7 @@ void chol_free(CholPlan& P) {
   void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
                   P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
                   P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
-                  P.d_syrk, P.d_ea_tasks, P.d_ea_pairs, P.d_potrf, P.d_bwd, P.d_bwdc, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_at_iptr, P.d_at_items, P.d_col, P.d_stepflag, P.d_xown, P.d_xforeign, P.d_xsol_own, P.d_xsol_foreign, P.d_xsend, P.d_xrecv};
+                  P.d_syrk, P.d_ea_tasks, P.d_ea_pairs, P.d_potrf, P.d_bwd, P.d_bwdc, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_at_iptr, P.d_at_items, P.d_col, P.d_stepflag, P.d_xown, P.d_xforeign, P.d_xsol_own, P.d_xsol_foreign, P.d_xsend, P.d_xrecv, P.d_xp, P.d_xp_off, P.d_xprecv};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : P.evs)
@@ -2043,15 +2138,39 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
   CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int) * nb, s));
   CH_TRY(hipMemsetAsync(P.d_stepflag, 0, sizeof(int) * std::max(P.ns, 1) * nb, s));
   const bool part = P.part_size > 1;
-  if (part && (nb != 1 || !hook)) return hipErrorInvalidValue;
+  if (part && (!hook || !hook->allgather || (!P.xchg.empty() && !hook->broadcast))) return hipErrorInvalidValue;
   auto exchange = [&]() -> hipError_t {   // subtree roots -> every rank
-    if (P.n_xown) k_xroots<true><<<P.n_xown, 256, 0, s>>>(c, P.d_xown, P.d_xsend);
+    const long long slot = xroot_slot(P);
+    if (P.n_xown) k_xroots<true><<<dim3(P.n_xown, nb), 256, 0, s>>>(c, P.d_xown, P.d_xsend, slot, 0);
     CH_TRY(hipGetLastError());
-    if (hook->allgather(hook->ctx, P.d_xsend, P.d_xrecv, sizeof(double) * std::max(P.xmax, 1LL), s) != 0) {
+    if (hook->allgather(hook->ctx, P.d_xsend, P.d_xrecv, sizeof(double) * slot * nb, s) != 0) {
       hook->failed = true;
       return hipErrorUnknown;
     }
-    if (P.n_xforeign) k_xroots<false><<<P.n_xforeign, 256, 0, s>>>(c, P.d_xforeign, P.d_xrecv);
+    if (P.n_xforeign) k_xroots<false><<<dim3(P.n_xforeign, nb), 256, 0, s>>>(c, P.d_xforeign, P.d_xrecv, slot, slot * nb);
+    return hipGetLastError();
+  };
+  // distributed top: the panels (tails) of exchange point xi from their owners
+  // to every rank -- pack, one broadcast per sending rank, unpack
+  auto xpanels = [&](int xi) -> hipError_t {
+    if (!part || xi < 0) return hipSuccess;
+    const XExchange& X = P.xchg[xi];
+    const long long rstride = std::max(P.xp_rslot, 1LL) * nb;
+    k_xpanel<true><<<dim3(X.cnt, nb), 256, 0, s>>>(c, P.d_xp + X.off, P.d_xp_off + 2 * X.off, P.d_xprecv, rstride,
+                                                   P.part_rank);
+    CH_TRY(hipGetLastError());
+    if (hook->group) hook->group(hook->ctx, 1);
+    bool bad = false;
+    for (int r = 0; r < P.part_size && !bad; r++)
+      if (X.size[r] > 0)
+        bad = hook->broadcast(hook->ctx, P.d_xprecv + r * rstride, sizeof(double) * X.size[r] * nb, r, s) != 0;
+    if (hook->group && hook->group(hook->ctx, 0) != 0) bad = true;
+    if (bad) {
+      hook->failed = true;
+      return hipErrorUnknown;
+    }
+    k_xpanel<false><<<dim3(X.cnt, nb), 256, 0, s>>>(c, P.d_xp + X.off, P.d_xp_off + 2 * X.off, P.d_xprecv, rstride,
+                                                    P.part_rank);
     return hipGetLastError();
   };
   // PGO_ABLATE (diagnostics only -- the factor is wrong): skip the named launch
@@ -2139,6 +2258,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
         launch(prof, kFamPanelFirst, [&] { return make_double2(ps.first_flops * nb, 0); }, k_panel_first,
                dim3(ps.potrf_cnt + ps.fcol_cnt, nb), B256, 0, s, c, (const int*)(P.d_potrf + ps.potrf_off),
                ps.potrf_cnt, cols);
+      CH_TRY(xpanels(ps.xfirst));
       const int4* tiles = (const int4*)(P.d_syrk + ps.syrk_off);
       const int nin = ps.syrk_inline && !off("plain") ? ps.syrk_cnt : 0;
       const bool apart = ps.syrk_cnt > 0 && !ps.syrk_inline && !off("plain");   // plain tiles in their own launch
@@ -2164,6 +2284,9 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
         side_pending = true;
         on_side[j] = 1;
       }
+      // the panel this step factored, to every rank (the apart plain tiles
+      // beside it neither read nor write its columns)
+      CH_TRY(xpanels(ps.xstep));
     }
     if (side_pending) {   // every apart plain of the level done before the next level
       CH_TRY(hipEventRecord(P.evs[2], P.side));
@@ -2177,8 +2300,18 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
         CH_TRY(hipStreamWaitEvent(s, P.evs[4], 0));
       }
     }
+    CH_TRY(xpanels(lv.xtail));
   }
   if (part && P.split >= (int)P.levels.size()) CH_TRY(exchange());
+  // PGO_DEBUG_BAD_PIVOT=r:k (tests): rank r's first k factorisations report a
+  // non-positive pivot that only it has seen -- the partitioned solve must
+  // still take the same decision on every rank
+  static const char* bad = getenv("PGO_DEBUG_BAD_PIVOT");
+  static int bad_left = bad && strchr(bad, ':') ? atoi(strchr(bad, ':') + 1) : 0;
+  if (bad && bad_left > 0 && atoi(bad) == P.part_rank) {
+    bad_left--;
+    k_set_flag<<<1, nb, 0, s>>>(P.d_flag, 1);
+  }
   return hipGetLastError();
 }
 
@@ -2246,16 +2379,19 @@ hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb, long 
       }
     }
   }
-  if (P.part_size > 1) {   // every rank's subtree solutions -> every rank
-    if (nb != 1 || !hook) return hipErrorInvalidValue;
-    if (P.n_xsol_own) k_xsol<true><<<dim3(16, P.n_xsol_own), 256, 0, s>>>(c, P.d_xsol_own, P.d_xsend, 0);
+  if (P.part_size > 1) {   // every rank's subtree solutions (and pivot flags) -> every rank
+    if (!hook) return hipErrorInvalidValue;
+    const long long slot = xsol_slot(P), rstride = slot * nb;
+    if (P.n_xsol_own) k_xsol<true><<<dim3(16, P.n_xsol_own, nb), 256, 0, s>>>(c, P.d_xsol_own, P.d_xsend, slot, 0);
+    k_xflag<<<1, nb, 0, s>>>(c, P.d_xsend, slot, P.xsol_max, 0, 1, 1);
     CH_TRY(hipGetLastError());
-    if (hook->allgather(hook->ctx, P.d_xsend, P.d_xrecv, sizeof(double) * std::max(P.xsol_max, 1LL), s) != 0) {
+    if (hook->allgather(hook->ctx, P.d_xsend, P.d_xrecv, sizeof(double) * rstride, s) != 0) {
       hook->failed = true;
       return hipErrorUnknown;
     }
     if (P.n_xsol_foreign)
-      k_xsol<false><<<dim3(16, P.n_xsol_foreign), 256, 0, s>>>(c, P.d_xsol_foreign, P.d_xrecv, std::max(P.xsol_max, 1LL));
+      k_xsol<false><<<dim3(16, P.n_xsol_foreign, nb), 256, 0, s>>>(c, P.d_xsol_foreign, P.d_xrecv, slot, rstride);
+    k_xflag<<<1, nb, 0, s>>>(c, P.d_xrecv, slot, P.xsol_max, rstride, P.part_size, 0);
     CH_TRY(hipGetLastError());
   }
   launch(prof, kFamPerm, [&] { return make_double2(0, 48.0 * P.n * nb); }, k_perm_out, dim3(g, nb), B256, 0, s, c, x,

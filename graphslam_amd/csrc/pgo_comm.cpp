@@ -22,6 +22,8 @@ struct Rccl {
   decltype(&::ncclAllGather) all_gather = nullptr;
   decltype(&::ncclBroadcast) broadcast = nullptr;
   decltype(&::ncclGetErrorString) error_string = nullptr;
+  decltype(&::ncclGroupStart) group_start = nullptr;
+  decltype(&::ncclGroupEnd) group_end = nullptr;
 };
 
 Rccl& rccl() {
@@ -47,6 +49,8 @@ Rccl& rccl() {
   PGO_SYM(all_gather, "ncclAllGather")
   PGO_SYM(broadcast, "ncclBroadcast")
   PGO_SYM(error_string, "ncclGetErrorString")
+  PGO_SYM(group_start, "ncclGroupStart")
+  PGO_SYM(group_end, "ncclGroupEnd")
 #undef PGO_SYM
   r.ok = true;
   return r;
@@ -220,6 +224,19 @@ int comm_broadcast_device(Comm* c, void* dptr, size_t bytes, int root, hipStream
   he = hipStreamSynchronize(s);
   if (he != hipSuccess) return hip_fail(he, "broadcast", err);
   return PGO_OK;
+}
+
+int comm_broadcast_device_async(Comm* c, void* dptr, size_t bytes, int root, hipStream_t s, std::string* err) {
+  if ((c->size == 1 && !force_collectives(c)) || bytes == 0 || c->host)
+    return comm_broadcast_device(c, dptr, bytes, root, s, err);   // (the host transport synchronises anyway)
+  const ncclResult_t e = rccl().broadcast(dptr, dptr, bytes, ncclUint8, root, static_cast<ncclComm_t>(c->nccl), s);
+  return e == ncclSuccess ? PGO_OK : nccl_fail(e, "ncclBroadcast", err);
+}
+
+int comm_group(Comm* c, int begin, std::string* err) {
+  if (c->host || !c->nccl || (c->size == 1 && !force_collectives(c))) return PGO_OK;
+  const ncclResult_t e = begin ? rccl().group_start() : rccl().group_end();
+  return e == ncclSuccess ? PGO_OK : nccl_fail(e, begin ? "ncclGroupStart" : "ncclGroupEnd", err);
 }
 
 }  // namespace pgo

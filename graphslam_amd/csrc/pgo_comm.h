@@ -45,6 +45,13 @@ int comm_allgather(Comm* c, const double* mine, int count, double* all, hipStrea
 // after the data has arrived (stream synchronised)
 int comm_broadcast_device(Comm* c, void* dptr, size_t bytes, int root, hipStream_t s, std::string* err);
 
+// as comm_broadcast_device, but the RCCL transport only enqueues it on s (the
+// distributed top's panel broadcasts, stream ordered with the kernels around
+// them); inside comm_group(c, 1) ... comm_group(c, 0) several broadcasts form one
+// RCCL group (ncclGroupStart / ncclGroupEnd; no-op on the host transport)
+int comm_broadcast_device_async(Comm* c, void* dptr, size_t bytes, int root, hipStream_t s, std::string* err);
+int comm_group(Comm* c, int begin, std::string* err);
+
 // device all-gather: recv[size * bytes] = every rank's send[bytes], rank order;
 // RCCL: enqueued on s (ncclAllGather over xGMI); host transport: staged and
 // synchronised (the partitioned factorisation's exchanges)

@@ -116,7 +116,7 @@ void xcd_order(std::vector<int4>& tasks, int tile) {
   const int span = tile * kBlk;
   std::vector<int> idx(tasks.size());
   for (size_t i = 0; i < idx.size(); i++) idx[i] = (int)i;
-  auto key = [&](const int4& t) { return std::make_tuple(t.x, t.z / span, t.y / span); };
+  auto key = [&](const int4& t) { return std::make_tuple(t.x, t.z / span, (t.y & kRowMask) / span); };
   std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return key(tasks[a]) < key(tasks[b]); });
   std::vector<std::vector<int4>> q(kXcd);
   int blk = -1;
@@ -150,6 +150,61 @@ static double front_flops(int m, int w) {
     f += 1 + r + r * (r + 1);
   }
   return f;
+}
+
+// blocked path (64-column panels) vs one workgroup / wavefront per front
+static bool is_blocked(const CholPlan& P, int s) {
+  return P.m[s] > kSmallFront || (P.w[s] > kWaveW && !getenv("PGO_SMALL_LDS"));
+}
+
+// Column owners of the distributed top (see chol_analyze): per top front s
+// (owner[s] < 0) its m columns at cown[off[s] ..]: rank, or -1 (every rank).
+static void column_owners(const CholPlan& P, const std::vector<int>& owner, int psz, std::vector<int>& off,
+                          std::vector<int>& cown) {
+  const int ns = P.ns;
+  off.assign(ns, -1);
+  cown.clear();
+  int rr = 0;   // round-robin position over the panels of the top fronts
+  for (int s = ns - 1; s >= 0; s--) {   // parents before children
+    if (owner[s] >= 0) continue;
+    const int m = P.m[s], w = P.w[s], p = P.parent[s];
+    off[s] = (int)cown.size();
+    cown.resize(cown.size() + m, -1);
+    int* own = cown.data() + off[s];
+    const bool blk = is_blocked(P, s);
+    const int wr = blk ? std::min(m, (w + kNB - 1) / kNB * kNB) : 0;
+    for (int col = 0; col < wr; col += kNB, rr++)
+      for (int j = col; j < std::min(col + kNB, wr); j++) own[j] = rr % psz;
+    for (int col = std::max(wr, w); col < m; col++) {
+      const int t = col - w;
+      own[col] = p >= 0 ? cown[off[p] + 3 * P.ea_rel[P.ea_ptr[s] + t / 3] + t % 3] : -1;
+    }
+    if (!blk)
+      for (int j = 0; j < m; j++) own[j] = -1;
+  }
+}
+
+std::vector<double> distributed_rank_flops(const CholPlan& P, int size, double* replicated) {
+  std::vector<double> rf;
+  double top = 0;
+  const std::vector<int> owner = partition_subtrees(P, size, &rf, &top);
+  std::vector<int> off, cown;
+  column_owners(P, owner, size, off, cown);
+  double rep = 0;
+  for (int s = 0; s < P.ns; s++) {
+    if (owner[s] >= 0) continue;
+    const int m = P.m[s], w = P.w[s];
+    for (int j = 0; j < m; j++) {
+      // column j: its scaling as a pivot, its update by every earlier pivot
+      const double f = 2.0 * std::min(j, w) * (m - j) + (j < w ? (double)(m - j) : 0.0);
+      const int o = cown[off[s] + j];
+      if (o < 0) rep += f;
+      else rf[o] += f;
+    }
+  }
+  for (double& v : rf) v += rep;
+  if (replicated) *replicated = rep;
+  return rf;
 }
 
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
@@ -460,6 +515,51 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     bylevel.swap(kept);
     P.split = split;
   }
+  auto blocked = [&](int s) { return is_blocked(P, s); };
+  // ---- distributed top (part_size > 1): the top fronts' columns are dealt to
+  // the ranks instead of every rank factoring every top front.  A blocked top
+  // front's pivot columns go by 64-column panel, round robin (continuing over
+  // the fronts); its columns past the last whole panel (the update matrix) take
+  // the rank of the parent column they extend-add into, so a rank's share of a
+  // parent's columns is assembled from its own shares of the children's update
+  // matrices (no exchange of update matrices between top fronts).  Small top
+  // fronts (one workgroup / wavefront each) are computed by every rank (-1),
+  // and so are the update columns of their children.  Each column's updates
+  // are applied by its rank only, with the same tasks (same depths, same
+  // order) as the one-rank plan: bitwise the one-rank factor.  A rank receives
+  // every panel (broadcast by its owner right after it is factored) for its own
+  // columns' updates and the replicated backward solve.
+  // (PGO_DIST_TOP=0: the top fronts replicated on every rank instead -- the
+  // previous scheme, kept as a reference for the host self-test)
+  const bool dtop = psz > 1 && !(getenv("PGO_DIST_TOP") && atoi(getenv("PGO_DIST_TOP")) == 0);
+  P.cown_off.assign(ns, -1);
+  P.cown.clear();
+  if (dtop) column_owners(P, P.owner, psz, P.cown_off, P.cown);
+  P.xchg.clear();
+  P.xp_tasks.clear();
+  P.xp_loff.clear();
+  P.xp_lstride.clear();
+  P.xp_rslot = 0;
+  // an exchange point: every panel / tail in `items` (front, kn, nb | kind << 16,
+  // owner) goes from its owner to every rank (one broadcast per sending rank)
+  auto add_exchange = [&](const std::vector<int4>& items) -> int {
+    if (items.empty()) return -1;
+    XExchange x;
+    x.off = (int)P.xp_tasks.size();
+    x.cnt = (int)items.size();
+    x.size.assign(psz, 0);
+    for (const int4& t : items) {
+      const int s = t.x, kn = t.y, nb = t.z & 0xffff, kind = t.z >> 16, m = P.m[s];
+      const long long sz = kind == 0 ? (long long)(m - kn) * nb + 4096 + (m - kn) : (long long)(m - kn) * nb;
+      P.xp_tasks.push_back(t);
+      P.xp_loff.push_back(x.size[t.w]);
+      x.size[t.w] += sz;
+    }
+    for (int q = x.off; q < x.off + x.cnt; q++) P.xp_lstride.push_back(x.size[P.xp_tasks[q].w]);
+    for (long long v : x.size) P.xp_rslot = std::max(P.xp_rslot, v);
+    P.xchg.push_back(x);
+    return (int)P.xchg.size() - 1;
+  };
   const int nl = (int)bylevel.size();
   P.levels.assign(nl, CholLevel());
   P.small_list.clear();
@@ -477,6 +577,14 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.ea_pairs.clear();
   for (int L = 0; L < nl; L++) {
     CholLevel& lv = P.levels[L];
+    // distributed top level: this rank generates only the tasks of its columns
+    const bool dist = dtop && L >= P.split;
+    auto mine = [&](int s, int col) {
+      if (!dist) return true;
+      const int o = P.cown[P.cown_off[s] + col];
+      return o < 0 || o == prk;
+    };
+    auto cowner = [&](int s, int col) { return dist ? P.cown[P.cown_off[s] + col] : -1; };
     lv.front_off = (int)P.level_fronts.size();
     lv.front_cnt = (int)bylevel[L].size();
     for (int s : bylevel[L]) {
@@ -581,7 +689,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
         // w > kWaveW: the blocked path (64-column panels, every front of the
         // level in the same launches) -- a whole-front-in-LDS workgroup runs
         // its w pivots one after the other at ~2 us each
-        if (P.m[s] > kSmallFront || (P.w[s] > kWaveW && !getenv("PGO_SMALL_LDS"))) {
+        if (blocked(s)) {
           big.push_back(s);
           continue;
         }
@@ -656,17 +764,21 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       ps.potrf_off = (int)P.potrf_list.size();
       ps.sdiag_off = (int)P.sdiag_tasks.size();
       // first panel of a front: k_panel_first (diagonal + trsm waiters)
+      std::vector<int4> xfirst, xstep;   // distributed top: panels factored by the first / the step launch
       for (int s : big) {
         if (kb != 0 || P.w[s] <= 0) continue;
-        P.potrf_list.push_back(s);
         const int nb = std::min(kNB, P.w[s]), m = P.m[s];
+        if (dist) xfirst.push_back(make_int4(s, 0, nb, cowner(s, 0)));
+        if (!mine(s, 0)) continue;
+        P.potrf_list.push_back(s);
         ps.first_flops += 2.0 * nb * nb * (double)nb / 3.0 + (double)std::max(0, m - nb) * nb * nb;
       }
       ps.potrf_cnt = (int)P.potrf_list.size() - ps.potrf_off;
       for (int s : big)
-        if (kb == 0 && P.w[s] > 0)
+        if (kb == 0 && P.w[s] > 0 && mine(s, 0))
           for (int r0 = kNB; r0 < P.m[s]; r0 += kNB) P.col_tasks.push_back(make_int4(s, r0, 0, -1));
       ps.fcol_cnt = (int)P.col_tasks.size() - ps.col_off;
+      ps.xfirst = add_exchange(xfirst);
       // this panel's Schur update, deferred by kKB-column blocks: inside a block
       // only the block's remaining columns [kn, be) are updated ("inner", bit 31
       // of k0: tasks clip columns at the block end); after the block's last
@@ -743,11 +855,13 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
           }
           for (int j = kn; j < c1; j++) applied[i][j] = kn;
           const int depth = kn - k0, kw = inner ? (k0 | (int)0x80000000) : k0;
-          P.sdiag_tasks.push_back(make_int4(s, kn, kn, kw));
+          if (dist) xstep.push_back(make_int4(s, kn, nb2, cowner(s, kn)));
+          const bool own = mine(s, kn);
+          if (own) P.sdiag_tasks.push_back(make_int4(s, kn, kn, kw));
           ps.step_flops += (double)depth * kNB * (kNB + 1) + 2.0 * nb2 * nb2 * (double)nb2 / 3.0 +
                            (double)std::min(kNB - nb2, m - kn - nb2) * nb2 * nb2;
           for (int r0 = kn + kNB; r0 < m; r0 += kNB) {
-            P.col_tasks.push_back(make_int4(s, r0, kn, kw));
+            if (own) P.col_tasks.push_back(make_int4(s, r0, kn, kw));
             const int rows = std::min(kNB, m - r0);
             ps.step_flops += 2.0 * depth * rows * (c1 - kn) + (double)rows * nb2 * nb2;
           }
@@ -761,7 +875,8 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
             P.schedule_error = true;
           }
           for (int j = b0; j < b1; j++) applied[i][j] = kn;
-          for (int r0 = b0; r0 < m; r0 += kNB) prep.push_back(make_int4(s, r0, b0, k0));
+          if (mine(s, b0))
+            for (int r0 = b0; r0 < m; r0 += kNB) prep.push_back(make_int4(s, r0, b0, k0));
           const double f = (double)(kn - k0) * kNB * (2.0 * m - b0 - b1 + 1.0);
           ps.step_flops += f;
           ps.syrk_flops += f;
@@ -798,10 +913,28 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       long long cnt128 = 0;
       for (const int4& u : plain)
         for (int c0 = u.y; c0 < u.z; c0 += kBigTile) cnt128 += (P.m[u.x] - c0 + kBigTile - 1) / kBigTile;
-      ps.syrk_tile = cnt128 >= 4096 ? kBigTile : kTile;
+      // (distributed top: 64-wide tiles, split where the column owner changes;
+      // a tile's elements are computed alike in either kernel, so this is
+      // bitwise the 128-tile update)
+      ps.syrk_tile = cnt128 >= 4096 && !dist ? kBigTile : kTile;
       for (const int4& u : plain)
-        for (int c0 = u.y; c0 < u.z; c0 += ps.syrk_tile)
-          for (int r0 = c0; r0 < P.m[u.x]; r0 += ps.syrk_tile) P.syrk_tasks.push_back(make_int4(u.x, r0, c0, u.w));
+        for (int c0 = u.y; c0 < u.z; c0 += ps.syrk_tile) {
+          if (!dist) {
+            for (int r0 = c0; r0 < P.m[u.x]; r0 += ps.syrk_tile) P.syrk_tasks.push_back(make_int4(u.x, r0, c0, u.w));
+            continue;
+          }
+          const int ce = std::min(c0 + kTile, u.z);
+          for (int a = c0; a < ce;) {   // runs of one column owner: (a, b)
+            int b = a + 1;
+            while (b < ce && cowner(u.x, b) == cowner(u.x, a)) b++;
+            if (mine(u.x, a)) {
+              const int clip = (a == c0 && b == ce) ? 0 : b - a;
+              for (int r0 = c0; r0 < P.m[u.x]; r0 += kTile)
+                P.syrk_tasks.push_back(make_int4(u.x, r0 | (clip << kClipShift), a, u.w));
+            }
+            a = b;
+          }
+        }
       {   // XCD-aware order of this step's Schur-update tiles
         std::vector<int4> mine(P.syrk_tasks.begin() + ps.syrk_off, P.syrk_tasks.end());
         xcd_order(mine, ps.syrk_tile);
@@ -815,7 +948,16 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       apart_chain = apart_chain || (ps.plain_lag == 2);
       if (ps.syrk_inline) ps.step_flops += ps.plain_flops;
       P.syrk_flops += ps.plain_flops;
+      ps.xstep = add_exchange(xstep);
       lv.panels.push_back(ps);
+    }
+    if (dist) {   // update columns past a front's last whole panel, factored with it: to every rank
+      std::vector<int4> tails;
+      for (int s : big) {
+        const int w = P.w[s], wr = std::min(P.m[s], (w + kNB - 1) / kNB * kNB);
+        if (wr > w) tails.push_back(make_int4(s, w, (wr - w) | (1 << 16), cowner(s, w)));
+      }
+      lv.xtail = add_exchange(tails);
     }
     // every column has its updates: pivot columns up to their panel, the
     // trailing ones from every panel

@@ -173,13 +173,31 @@ class PoseGraph:
         """Host-only: the PGO_MULTI_PARTITION subtree partition over `size`
         ranks: (owner per supernode, -1 = replicated top; per-rank subtree
         flops; top flops)."""
+        owner, out = self._partition(size)
+        return owner, out[:size].copy(), float(out[size])
+
+    def _partition(self, size):
         ns = self._check(self._L.pgo_debug_partition(self._h, int(size), None, None, 0))
-        cap = max(ns, size + 1)
+        cap = max(ns, 2 * size + 4)
         owner = np.zeros(cap, np.int32)
         out = np.zeros(cap)
         self._check(self._L.pgo_debug_partition(self._h, int(size), owner.ctypes.data_as(C.POINTER(C.c_int)),
                                                 L.dptr(out), cap))
-        return owner[:ns], out[:size].copy(), float(out[size])
+        return owner[:ns], out
+
+    def debug_partition_bound(self, size):
+        """Host-only: the partitioned factorisation's per-rank flops with the
+        distributed top (top fronts' columns dealt to the ranks), the work every
+        rank repeats, and the plan-derived flop bound on the speed-up
+        (factorisation flops / the busiest rank's)."""
+        _, out = self._partition(size)
+        total = self.debug_plan()["factor_flops"]
+        rank = out[size + 1:2 * size + 1].copy()
+        return {"ranks": int(size), "rank_flops": rank, "replicated_flops": float(out[2 * size + 1]),
+                "replicated_top_flops": float(out[size]), "total_flops": float(total),
+                "bound": float(total / rank.max()),
+                "bound_replicated_top": float(total / (out[size] + out[:size].max())),
+                "exchange_points": int(out[2 * size + 2]), "exchange_bytes": float(8.0 * out[2 * size + 3])}
 
     def debug_ordering(self):
         """Host-only: the Cholesky solver's pose ordering (new -> insertion index)."""

@@ -115,7 +115,9 @@ typedef struct {
                                    its subtrees of the elimination tree, the
                                    subtree roots' Schur complements are
                                    all-gathered (the boundary reduction) and
-                                   the top separators factored on every rank
+                                   the top separators' columns are dealt to
+                                   the ranks (each factored panel broadcast by
+                                   its rank); composes with lambda_lanes
                                    [PGO_MULTI_SPECULATIVE] */
 } pgo_params;
 
@@ -363,9 +365,14 @@ int pgo_debug_solve(pgo_graph *g, double lambda, const pgo_params *params, doubl
  * fronts, max m, max 64-blocks, panel steps, small fronts, syrk tiles. */
 int pgo_debug_plan(pgo_graph *g, double *out, int cap);
 /* Host-only: the subtree partition the PGO_MULTI_PARTITION factorisation
- * uses over `size` ranks: owner[s] per supernode (rank, -1 = replicated top;
+ * uses over `size` ranks: owner[s] per supernode (rank, -1 = top front;
  * returns the supernode count, arrays filled up to cap) and out[0..size+1] =
- * per-rank subtree flops, then the top's flops. */
+ * per-rank subtree flops, then the top's flops; then (as cap allows)
+ * out[size+1 .. 2 size+1] = per-rank flops with the distributed top (subtrees
+ * + the rank's top columns + the top work every rank repeats) and
+ * out[2 size+1] = that repeated work, out[2 size+2] = the exchange points
+ * (panel broadcast rounds) per factorisation and out[2 size+3] = the doubles
+ * they broadcast per lambda lane. */
 int pgo_debug_partition(pgo_graph *g, int size, int *owner, double *out, int cap);
 /* Host-only: the supernodal elimination tree (parent per supernode, -1 root);
  * returns the supernode count. */

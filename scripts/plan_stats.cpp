@@ -7,6 +7,7 @@
 #include <vector>
 #include <string>
 #include <chrono>
+#include <algorithm>
 
 #include "../graphslam_amd/csrc/pgo_chol.h"
 
@@ -34,6 +35,7 @@ int main(int argc, char** argv) {
     col[fill[e[2 * q]]++] = e[2 * q + 1];
     col[fill[e[2 * q + 1]]++] = e[2 * q];
   }
+  for (int i = 0; i < n; i++) std::sort(col.begin() + row_ptr[i], col.begin() + row_ptr[i + 1]);   // as build_structure
   pgo::CholPlan P;
   if (argc > 3 && std::string(argv[3]) == "amd") P.ordering = pgo::kOrderAmd;
   const auto t0 = std::chrono::steady_clock::now();

@@ -162,8 +162,9 @@ def _graph(case):
     return g, np.array(g.initial, copy=True)
 
 
-def _opt_worker(rank, world, port, q, case, kw):
+def _opt_worker(rank, world, port, q, case, kw, env=None):
     try:
+        os.environ.update(env or {})
         dist = _init(rank, world, port)
         from graphslam_amd import multi_gpu
         from graphslam_amd.pose_graph import PoseGraph
@@ -172,6 +173,7 @@ def _opt_worker(rank, world, port, q, case, kw):
         pg.set_poses(init)
         hc = multi_gpu.attach_host(pg, dist, rank, world)
         st = pg.optimize(**kw)
+        st["trace"] = pg.trace()
         q.put((rank, st, pg.poses(), None))
         del hc
         dist.destroy_process_group()
@@ -271,21 +273,52 @@ def test_speculative_lambda_oracle_trajectory():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case,world", [("C2p", 2), ("C2p", 4), ("C3", 2)])
-def test_partitioned_factorisation_matches_one_rank(case, world):
+@pytest.mark.parametrize("case,world,lanes,kw", [
+    ("C2p", 2, 1, {}), ("C2p", 3, 1, {}), ("C2p", 4, 1, {}),
+    ("C2p", 2, 2, {}), ("C2p", 4, 3, {}),                       # lambda lanes x partition
+    ("C3", 2, 1, {}), ("C3", 4, 1, {}),
+    ("C3", 4, 2, {"max_outer": 3}),
+    ("C3", 8, 1, {"max_outer": 2}),                             # BASELINE config C4 at 8 ranks
+])
+def test_partitioned_factorisation_matches_one_rank(case, world, lanes, kw):
     """PGO_MULTI_PARTITION, ranks sharing cuda:0 over the host transport:
-    every try's factorisation split into the ranks' subtrees + the replicated
-    top, the subtree roots' Schur complements and the subtree solutions
-    all-gathered -- the LM trajectory and the final values are bitwise those
-    of one rank."""
-    st1, x1 = _single(case, {})
-    out = _run(world, _opt_worker, (case, dict(multi_gpu=1, lambda_lanes=1)), timeout=900)
+    every try's factorisation split into the ranks' subtrees + the distributed
+    top (top fronts' columns dealt to the ranks, every factored panel
+    broadcast by its rank), the subtree roots' Schur complements and the
+    subtree solutions all-gathered -- the LM trajectory and the final values
+    are bitwise those of one rank, with and without lambda lanes (every rank
+    factors the same lanes).  The 8-rank C3 case stops after 2 linearisations
+    (its host-staged exchanges are slow on one shared GPU), both sides."""
+    st1, x1 = _single(case, kw)
+    out = _run(world, _opt_worker, (case, dict(kw, multi_gpu=1, lambda_lanes=lanes)), timeout=1200)
     for rank, st, x, err in out:
         assert err is None, err
         assert st["iterations"] == st1["iterations"]
         assert st["inner_iterations"] == st1["inner_iterations"]
+        assert st["linearizations"] == st1["linearizations"]
         assert st["final_error"] == st1["final_error"]
         np.testing.assert_array_equal(x, x1)
+        if lanes > 1 and st1["inner_iterations"] > st1["linearizations"]:
+            assert st["lambda_rounds"] < st1["lambda_rounds"]
+
+
+@pytest.mark.gpu
+def test_partitioned_bad_pivot_on_one_rank():
+    """A non-positive pivot that only one rank sees (PGO_DEBUG_BAD_PIVOT: rank
+    1's first two factorisations) is reduced over the ranks with the subtree
+    solutions: every rank rejects those tries and walks the same trace to the
+    same stop reason and values."""
+    env = {"PGO_DEBUG_BAD_PIVOT": "1:2"}
+    out = _run(2, _opt_worker, ("C2p", dict(multi_gpu=1, lambda_lanes=1), env), timeout=900)
+    for rank, st, x, err in out:
+        assert err is None, err
+    (_, st0, x0, _), (_, st1, x1, _) = out
+    np.testing.assert_array_equal(st0["trace"][:, :7], st1["trace"][:, :7])   # (column 7: wall ms)
+    assert st0["stop_reason"] == st1["stop_reason"]
+    np.testing.assert_array_equal(x0, x1)
+    tr = st0["trace"]
+    assert tr[0, 2] == 0.0 and tr[1, 2] == 0.0      # the first two tries: not solved
+    assert tr[2:, 2].min() == 1.0
 
 
 @pytest.mark.gpu
