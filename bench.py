@@ -66,13 +66,21 @@ def _host_info():
                 break
     except OSError:
         pass
-    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model}
+    quota = None
+    try:   # cgroup v2 CPU quota of this job ("max" = none)
+        quota = open("/sys/fs/cgroup/cpu.max").read().strip()
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model,
+            "cgroup_cpu_max": quota, "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
-def cpu_baseline(g, nd_order, per_step, reps=5, amd_reps=3):
+def cpu_baseline(g, nd_order, per_step, reps=5, curve_reps=3, amd_reps=3):
     """The C restatement (oracle/pgo_oracle.c: same LM, supernodal multifrontal
-    Cholesky) on the host cores of this box, like-for-like with the GPU step
-    (SURVEY 8d / BASELINE.md):
+    Cholesky, OpenMP: fronts of a level across the threads, a big front's
+    panel solve, Schur update, assembly and copies across the threads) on the
+    host cores of this box, like-for-like with the GPU step (SURVEY 8d /
+    BASELINE.md):
 
     * same fill: the CPU factorises on the GPU plan's nested-dissection
       ordering (handed over from pgo_debug_ordering); the oracle's own AMD is
@@ -83,11 +91,14 @@ def cpu_baseline(g, nd_order, per_step, reps=5, amd_reps=3):
       one warm-up, and the GPU trajectory's counts (per_step: L linearisations,
       T tries, both identical to the oracle's, tests/test_gpu_parity.py) are
       priced with it: t = t_err0 + L t_lin + T t_try;
-    * all host cores (OMP_NUM_THREADS) and 1 core.
+    * all host cores: every CPU of this process's affinity mask (the headline
+      value, `cores`); the thread-scaling curve at 1, 16, 64 and that count
+      (median of `curve_reps`); 1 core as one_core.  Results do not depend on
+      the thread count (bitwise).
     """
     import statistics
     from oracle.oracle import Oracle, set_threads
-    threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+    allc_threads = len(os.sched_getaffinity(0))
     L, T = per_step["linearizations"], per_step["lm_tries"]
 
     def unit(o, n):
@@ -99,29 +110,41 @@ def cpu_baseline(g, nd_order, per_step, reps=5, amd_reps=3):
         t_traj = t_err0 + L * t_lin + T * t_try
         return {"value": L / t_traj, "ms_per_try": 1e3 * t_try, "ms_per_linearization": 1e3 * t_lin,
                 "ms_trajectory": 1e3 * t_traj, "factor_flops": runs[0]["factor_flops"], "nnz_l": runs[0]["nnz_l"],
-                "reps": n}
+                "ms_factor": 1e3 * statistics.median(r["t_factor"] for r in runs),
+                "ms_solve": 1e3 * statistics.median(r["t_solve"] for r in runs), "reps": n}
 
     o_nd = Oracle(g, order=nd_order)
-    set_threads(threads)
+    set_threads(allc_threads)
     allc = unit(o_nd, reps)
-    set_threads(1)
-    one = unit(o_nd, reps)
+    curve = {str(allc_threads): allc}
+    for t in sorted({1, 16, 64} - {allc_threads}):
+        if t > allc_threads:
+            continue
+        set_threads(t)
+        curve[str(t)] = unit(o_nd, curve_reps if t > 1 else reps)
+    one = curve["1"] if "1" in curve else allc
     o_nd.close()
-    set_threads(threads)
+    set_threads(allc_threads)
     o_amd = Oracle(g)
     amd = unit(o_amd, amd_reps)
     o_amd.close()
+    best_t = max(curve, key=lambda k: curve[k]["value"])
     return {
         "value": allc["value"],
         "unit": "GN iterations/s",
-        "cores": threads,
+        "cores": allc_threads,
         "kind": "port",
         "sample": (f"{g.name}: median of {reps} LM units (initial error + 1 linearisation + 1 lambda try: "
                    f"{allc['factor_flops'] / 1e9:.1f} GFLOP supernodal Cholesky on the GPU plan's nested-dissection "
                    f"ordering, nnz(L) {allc['nnz_l'] / 1e6:.0f}M) after 1 warm-up, oracle/pgo_oracle.c, "
-                   f"{threads} OpenMP threads; priced on the GPU trajectory's {L} linearisations / {T} tries"),
+                   f"{allc_threads} OpenMP threads (every CPU of the affinity mask); priced on the GPU trajectory's "
+                   f"{L} linearisations / {T} tries"),
         "all_cores": allc,
         "one_core": one,
+        "thread_curve": {k: {"value": v["value"], "ms_per_try": v["ms_per_try"], "ms_factor": v["ms_factor"]}
+                         for k, v in sorted(curve.items(), key=lambda kv: int(kv[0]))},
+        "best_threads": int(best_t),
+        "best_value": curve[best_t]["value"],
         "amd_all_cores": amd,
         "host": _host_info(),
     }
@@ -221,6 +244,60 @@ def live_resolve_bench(pg, g, k=5):
                      "lm_tries": st["inner_iterations"]})
     return {"registrations": k, "ms_median": float(np.median([r["ms"] for r in rows])), "per_registration": rows,
             "note": "append 1 keyframe + odometry + 1 loop closure, then optimize on the same handle"}
+
+
+def gauss_newton_bench(pg, default_params, reps=3, **common):
+    """GTSAM's Gauss-Newton (PGO_ALG_GN) on the same graph from the same
+    dead-reckoned values: the GN-iterations/s of the metric's name taken
+    literally (one linearise + factor + solve + retract + chi^2 per iteration,
+    no lambda tries), the error trajectory and how it stopped (GTSAM's
+    relative-decrease test).  Median of `reps` after one warm-up; the oracle's
+    run is pinned in tests/golden/golden_C3-gn.npz."""
+    import numpy as np
+    from graphslam_amd import _lib
+    p = default_params(algorithm=1, **common)
+    runs = []
+    for k in range(reps + 1):
+        pg.restore_values()
+        t0 = time.perf_counter()
+        st = pg.optimize(p)
+        dt = time.perf_counter() - t0
+        if k:
+            runs.append((dt, st))
+    dt = float(np.median([r[0] for r in runs]))
+    st = runs[-1][1]
+    return {"iterations": st["iterations"], "linearizations": st["linearizations"], "ms_to_stop": 1e3 * dt,
+            "gn_iterations_per_s": st["linearizations"] / dt, "initial_error": st["initial_error"],
+            "final_error": st["final_error"], "errors": [float(v) for v in pg.trace()[:, 4]],
+            "stop_reason": _lib.STOP_REASONS.get(st["stop_reason"], str(st["stop_reason"])), "reps": reps}
+
+
+def converged_regime_bench(pg, g, default_params, reps=3, **common):
+    """ms-to-chi^2 convergence where GTSAM's convergence test is what stops LM:
+    GTSAM-default LM from the ground-truth poses (the values a warm-started
+    live solve holds, graph.cpp:130) to the optimum of the noisy measurements.
+    Values uploaded before each timed optimize (not timed); median of `reps`
+    after one warm-up."""
+    import numpy as np
+    from graphslam_amd import _lib
+    gt = np.asarray(g.ground_truth)
+    p = default_params(**common)
+    runs = []
+    for k in range(reps + 1):
+        pg.set_poses(gt)
+        pg.error()                                    # upload the values outside the timed region
+        t0 = time.perf_counter()
+        st = pg.optimize(p)
+        dt = time.perf_counter() - t0
+        if k:
+            runs.append((dt, st))
+    dt = float(np.median([r[0] for r in runs]))
+    st = runs[-1][1]
+    return {"start": "ground truth", "ms_to_convergence": 1e3 * dt, "iterations": st["iterations"],
+            "lm_tries": st["inner_iterations"], "linearizations": st["linearizations"],
+            "gn_iterations_per_s": st["linearizations"] / dt, "initial_error": st["initial_error"],
+            "final_error": st["final_error"],
+            "stop_reason": _lib.STOP_REASONS.get(st["stop_reason"], str(st["stop_reason"])), "reps": reps}
 
 
 def closest_keyframe_bench(pg, g, skip=10, reps=20):
@@ -357,6 +434,9 @@ def main():
                     help="scan registrations in the GICP batch line (0: skip)")
     ap.add_argument("--live", type=int, default=5,
                     help="after the timed steps: time this many per-registration re-solves (0: skip)")
+    ap.add_argument("--gn", type=int, default=1, help="after the timed steps: the Gauss-Newton line (0: skip)")
+    ap.add_argument("--converged", type=int, default=1,
+                    help="after the timed steps: LM from the ground truth to convergence (0: skip)")
     ap.add_argument("--max-outer", type=int, default=0,
                     help="profiling runs only: stop each optimize after this many linearisations")
     args = ap.parse_args()
@@ -461,6 +541,10 @@ def main():
     scan = None
     if args.gicp and rank == 0:
         scan = scan_registration_bench(args.gicp)
+    one = dict(linear_solver=common["linear_solver"], use_graphs=common["use_graphs"])
+    gn = gauss_newton_bench(pg, default_params, **one) if args.gn and rank == 0 and not spec else None
+    conv = (converged_regime_bench(pg, g, default_params, lambda_lanes=args.lanes, **one)
+            if args.converged and rank == 0 and not spec else None)
     # the GPU plan's ordering of g, taken before live_resolve appends to the handle
     nd_order = pg.debug_ordering() if rank == 0 and not args.no_cpu_baseline and world == 1 else None
     live = None
@@ -550,6 +634,8 @@ def main():
                             else None),
             },
             "cpu_baseline": None,
+            "gauss_newton": gn,
+            "converged_regime": conv,
             "marginals": marg,
             "closest_keyframe": search,
             "live_resolve": live,
@@ -558,6 +644,7 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(g, nd_order, out["per_step"], reps=args.cpu_reps)
             out["cpu_baseline"]["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+            out["cpu_baseline"]["gpu_over_cpu_best_threads"] = out["value"] / out["cpu_baseline"]["best_value"]
             out["cpu_baseline"]["gpu_over_cpu_one_core"] = out["value"] / out["cpu_baseline"]["one_core"]["value"]
         print(json.dumps(out))
     if spec:

@@ -688,27 +688,52 @@ static void syrk_lower(int m, int kk, const double *A, int lda, double *C, int l
  * leaves L11, L21 in F[:, :w] and the Schur complement in F[w:, w:].
  * Returns 0 or -1 on a non-positive / non-finite pivot. */
 #define NB 48
+/* Rows [r0, m) of the panel columns [kb, kb + nb) once the panel's diagonal
+ * block is factored: L21 = A21 L11^-T, column by column (left-looking inside
+ * the panel), in 64-row blocks spread over the threads.  Every element sees
+ * the same operations in the same order as a column sweep over all rows. */
+static void panel_trsm(double *F, int m, int kb, int nb, int r0) {
+  const int nblk = (m - r0 + 63) / 64;
+#pragma omp parallel for schedule(dynamic, 1) if ((double)(m - r0) * nb * nb > 1e6)
+  for (int bi = 0; bi < nblk; bi++) {
+    const int i0 = r0 + 64 * bi, i1 = i0 + 64 < m ? i0 + 64 : m;
+    for (int k = kb; k < kb + nb; k++) {
+      double *colk = F + (size_t)k * m;
+      for (int t = kb; t < k; t++) {
+        const double ljk = F[k + (size_t)t * m];
+        const double *colt = F + (size_t)t * m;
+        for (int i = i0; i < i1; i++) colk[i] -= colt[i] * ljk;
+      }
+      const double inv = 1.0 / colk[k];
+      for (int i = i0; i < i1; i++) colk[i] *= inv;
+    }
+  }
+}
+
 static int front_factor(double *F, int m, int w) {
   for (int kb = 0; kb < w; kb += NB) {
     int nb = w - kb < NB ? w - kb : NB;
-    /* unblocked on the panel F[kb:m, kb:kb+nb] (left-looking inside panel) */
-    for (int k = kb; k < kb + nb; k++) {
+    const int r0 = kb + nb;
+    /* unblocked on the panel's diagonal block (left-looking inside the panel) */
+    for (int k = kb; k < r0; k++) {
       double *colk = F + (size_t)k * m;
       for (int t = kb; t < k; t++) {
         double ljk = F[k + (size_t)t * m];
         const double *colt = F + (size_t)t * m;
-        for (int i = k; i < m; i++) colk[i] -= colt[i] * ljk;
+        for (int i = k; i < r0; i++) colk[i] -= colt[i] * ljk;
       }
       double d = colk[k];
       if (!(d > 0.0) || !isfinite(d)) return -1;
       d = sqrt(d);
       colk[k] = d;
       double inv = 1.0 / d;
-      for (int i = k + 1; i < m; i++) colk[i] *= inv;
+      for (int i = k + 1; i < r0; i++) colk[i] *= inv;
     }
-    /* trailing update of everything right of the panel (lower part) */
-    int r0 = kb + nb;
-    if (r0 < m) syrk_lower(m - r0, nb, F + r0 + (size_t)kb * m, m, F + r0 + (size_t)r0 * m, m);
+    /* the rows below it, then the trailing update (lower part) */
+    if (r0 < m) {
+      panel_trsm(F, m, kb, nb, r0);
+      syrk_lower(m - r0, nb, F + r0 + (size_t)kb * m, m, F + r0 + (size_t)r0 * m, m);
+    }
   }
   return 0;
 }
@@ -795,7 +820,12 @@ static int factor_one(chol_num *N, int s, const double *hdiag, const double *hof
   int wp = l - f, nb = S->rptr[s + 1] - S->rptr[s];
   const int *R = S->rows + S->rptr[s];
   int m = 3 * (wp + nb), wd = 3 * wp;
-  double *F = (double *)calloc((size_t)m * m > 0 ? (size_t)m * m : 1, sizeof(double));
+  /* a big front (run alone, see num_factor) is zeroed, extended and copied out
+   * by all the threads; the small ones by their own thread */
+  const int par = (double)wd * m * m > 2e7 && !omp_in_parallel();
+  double *F = (double *)malloc((size_t)m * m > 0 ? (size_t)m * m * sizeof(double) : sizeof(double));
+#pragma omp parallel for schedule(static) if (par)
+  for (int j = 0; j < m; j++) memset(F + (size_t)j * m, 0, (size_t)m * sizeof(double));
   for (int j = f; j < l; j++) rel[j] = j - f;
   for (int t = 0; t < nb; t++) rel[R[t]] = wp + t;
   for (int j = f; j < l; j++) {
@@ -824,7 +854,8 @@ static int factor_one(chol_num *N, int s, const double *hdiag, const double *hof
     int mc = 3 * nbc;
     const double *U = N->U[cs];
     if (U)
-      for (int b = 0; b < nbc; b++) {
+#pragma omp parallel for schedule(dynamic, 8) if (par)
+      for (int b = 0; b < nbc; b++) {   /* (b, y): column gb + y of F, one thread's */
         int gb = 3 * rel[Rc[b]];
         for (int y = 0; y < 3; y++) {
           int colU = 3 * b + y;
@@ -841,10 +872,13 @@ static int factor_one(chol_num *N, int s, const double *hdiag, const double *hof
   }
   int rc = front_factor(F, m, wd) != 0 ? ORC_E_INDETERMINANT : ORC_OK;
   if (rc == ORC_OK) {
-    memcpy(N->L + S->loff[s], F, (size_t)m * wd * sizeof(double));
+    double *Ls = N->L + S->loff[s];
+#pragma omp parallel for schedule(static) if (par)
+    for (int j = 0; j < wd; j++) memcpy(Ls + (size_t)j * m, F + (size_t)j * m, (size_t)m * sizeof(double));
     int mu = m - wd;
     if (S->sparent[s] >= 0 && mu > 0) {
       double *U = (double *)malloc((size_t)mu * mu * sizeof(double));
+#pragma omp parallel for schedule(static) if (par)
       for (int j = 0; j < mu; j++) memcpy(U + (size_t)j * mu, F + wd + (size_t)(wd + j) * m, mu * sizeof(double));
       N->U[s] = U;
     }
@@ -914,11 +948,18 @@ static void num_solve(chol_num *N, const double *b, double *x) {
       for (int i = j + 1; i < wd; i++) ys[i] -= P[i + (size_t)j * m] * v;
     }
     int mb = m - wd;
-    for (int i = 0; i < mb; i++) tmp[i] = 0;
-    for (int j = 0; j < wd; j++) {
-      double v = ys[j];
-      const double *col = P + wd + (size_t)j * m;
-      for (int i = 0; i < mb; i++) tmp[i] += col[i] * v;
+    /* tmp = L21 y: a big front's rows spread over the threads (every element
+     * summed over j in the same order) */
+    const int nrb = (mb + 255) / 256;
+#pragma omp parallel for schedule(static) if ((double)mb * wd > 1e6)
+    for (int rb = 0; rb < nrb; rb++) {
+      const int i0 = 256 * rb, i1 = i0 + 256 < mb ? i0 + 256 : mb;
+      for (int i = i0; i < i1; i++) tmp[i] = 0;
+      for (int j = 0; j < wd; j++) {
+        double v = ys[j];
+        const double *col = P + wd + (size_t)j * m;
+        for (int i = i0; i < i1; i++) tmp[i] += col[i] * v;
+      }
     }
     for (int t = 0; t < nb; t++)
       for (int a = 0; a < 3; a++) y[3 * R[t] + a] -= tmp[3 * t + a];
@@ -934,6 +975,7 @@ static void num_solve(chol_num *N, const double *b, double *x) {
     int mb = m - wd;
     for (int t = 0; t < nb; t++)
       for (int a = 0; a < 3; a++) tmp[3 * t + a] = y[3 * R[t] + a];
+#pragma omp parallel for schedule(static) if ((double)mb * wd > 1e6)
     for (int j = 0; j < wd; j++) {
       const double *col = P + wd + (size_t)j * m;
       double acc = 0;

@@ -11,7 +11,12 @@ output of the CPU restatements:
   counts, the error trace and every 100th final pose;
 * C3-numpy2 -- the numpy twin's first 2 linearisations of C3 (max_outer = 2),
   so the headline size is also pinned by a source independent of the C code
-  that provides the CPU baseline: trace, error and every 100th pose.
+  that provides the CPU baseline: trace, error and every 100th pose;
+* C3-gn -- the C oracle's Gauss-Newton run of C3 (error per step, final error,
+  every 100th final pose);
+* C5 -- the C oracle's first linearisation, first Cholesky step and first LM
+  linearisation (sampled); C5-numpy -- the numpy twin's first linearisation
+  (0.5 chi^2, sampled gradient and H diagonal blocks), a second source.
 
 Each fixture also records a SHA-256 of the generated inputs so a change of the
 generator is detected instead of silently comparing different graphs.
@@ -107,6 +112,59 @@ def c5_fixture(stride=1000):
           "GFLOP", s["factor_flops"] / 1e9, "t", time.time() - t0)
 
 
+def c5_numpy_fixture(stride=1000):
+    """C5's first linearisation pinned by the numpy twin (independent of the C
+    oracle that made golden_C5.npz): 0.5 chi^2 at the dead-reckoned values, and
+    at every 1000th pose the gradient g = J' Omega e and the diagonal block
+    H_ii = sum J' Omega J (oracle/pgo_numpy.py's residuals and Jacobians,
+    accumulated with np.add.at -- no sparse matrix at this size)."""
+    import time
+    from oracle import pgo_numpy as tw
+    g = graph_for("C5")
+    t0 = time.time()
+    prob = tw.problem_from_graph(g)
+    poses = tw.from_xyt(g.initial)
+    ee, ep, p1, p2, hx = tw.residuals(prob, poses)
+    J1 = tw.between_jacobian(p1, p2, hx)
+    om = prob.eom
+    B = np.einsum("eki,ekl->eil", J1, om)
+    D = np.zeros((g.num_poses, 3, 3))
+    np.add.at(D, prob.ei, np.einsum("eil,elj->eij", B, J1))
+    np.add.at(D, prob.ej, om)
+    np.add.at(D, prob.pi, prob.pom)
+    G = np.zeros((g.num_poses, 3))
+    np.add.at(G, prob.ei, np.einsum("eil,el->ei", B, ee))
+    np.add.at(G, prob.ej, np.einsum("eil,el->ei", om, ee))
+    np.add.at(G, prob.pi, np.einsum("pij,pj->pi", prob.pom, ep))
+    err0 = 0.5 * (np.einsum("ei,eij,ej->", ee, om, ee) + np.einsum("ei,eij,ej->", ep, prob.pom, ep))
+    idx = np.arange(0, g.num_poses, stride)
+    np.savez_compressed(os.path.join(HERE, "golden_C5-numpy.npz"), source="pgo_numpy", digest=input_digest(g),
+                        sample_index=idx, initial_error=err0, grad_sample=G[idx],
+                        hdiag_sample=D[idx].reshape(-1, 9))
+    print("C5 numpy err0", err0, "t", time.time() - t0)
+
+
+def gn_fixture(name, stride=100):
+    """GTSAM's GaussNewtonOptimizer (PGO_ALG_GN) from the dead-reckoned values:
+    the C oracle's error after every step, the iteration count, the final error
+    and every 100th final pose (the GPU plan's nested-dissection ordering)."""
+    from graphslam_amd.pose_graph import PoseGraph
+    from oracle.oracle import Oracle
+    g = graph_for(name)
+    pg = PoseGraph.from_dataset(g)
+    order = pg.debug_ordering()
+    pg.close()
+    o = Oracle(g, order=order)
+    r = o.optimize(algorithm=1)
+    s = r.stats
+    idx = np.arange(0, g.num_poses, stride)
+    np.savez_compressed(os.path.join(HERE, f"golden_{name}-gn.npz"), source="pgo_oracle.c", digest=input_digest(g),
+                        sample_index=idx, final_sample=r.poses[idx], errors=r.trace[:, 4],
+                        final_error=s["final_error"], initial_error=s["initial_error"],
+                        iterations=s["iterations"], linearizations=s["linearizations"])
+    print(name, "GN err", s["final_error"], "it", s["iterations"], "t", s["t_total"])
+
+
 def oracle_fixture(name, stride=100):
     from oracle.oracle import Oracle
     g = graph_for(name)
@@ -128,6 +186,10 @@ if __name__ == "__main__":
     for n in names:
         if n == "C5":
             c5_fixture()
+        elif n == "C5-numpy":
+            c5_numpy_fixture()
+        elif n.endswith("-gn"):
+            gn_fixture(n[: -len("-gn")])
         elif n.endswith("-numpy2"):
             numpy_truncated_fixture(n[: -len("-numpy2")], 2)
         elif n == "C3":

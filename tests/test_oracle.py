@@ -247,3 +247,32 @@ def test_oracle_given_ordering_same_solution(oracle_lib):
     assert pose_close(a.poses, b.poses, 1e-7, 1e-8)
     with pytest.raises(ValueError):
         oracle_lib.Oracle(g, order=np.zeros(g.num_poses, np.int32))   # not a permutation
+
+
+def test_c5_two_restatements_agree():
+    """C5's first linearisation from two independent restatements: the C oracle
+    (golden_C5.npz) and the numpy twin (golden_C5-numpy.npz) -- same inputs
+    (digest), 0.5 chi^2, sampled gradient and H diagonal blocks."""
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    a = np.load(os.path.join(here, "golden_C5.npz"), allow_pickle=False)
+    b = np.load(os.path.join(here, "golden_C5-numpy.npz"), allow_pickle=False)
+    assert str(a["digest"]) == str(b["digest"])
+    assert np.array_equal(a["sample_index"], b["sample_index"])
+    e0 = float(a["initial_error"])
+    assert abs(float(b["initial_error"]) - e0) <= 1e-11 * e0
+    ga, gb = a["grad_sample"], b["grad_sample"]
+    assert np.abs(ga - gb).max() <= 1e-11 * np.abs(ga).max()
+    ha, hb = np.asarray(a["hdiag_sample"]).reshape(-1, 9), np.asarray(b["hdiag_sample"]).reshape(-1, 9)
+    assert np.abs(ha - hb).max() <= 1e-11 * np.abs(ha).max()
+
+
+def test_c3_gauss_newton_fixture_consistent():
+    """golden_C3-gn.npz (the C oracle's Gauss-Newton run of C3): the per-step
+    errors, the stop (GTSAM's relative test: the last step raised the error),
+    the final error is the last step's."""
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    f = np.load(os.path.join(here, "golden_C3-gn.npz"), allow_pickle=False)
+    errs = np.asarray(f["errors"])
+    assert len(errs) == int(f["iterations"]) == int(f["linearizations"])
+    assert float(f["final_error"]) == errs[-1]
+    assert errs[0] < float(f["initial_error"])
