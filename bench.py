@@ -71,8 +71,24 @@ def _host_info():
         quota = open("/sys/fs/cgroup/cpu.max").read().strip()
     except OSError:
         pass
-    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model,
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "usable_cpus": usable_cpus(),
+            "cpu_model": model,
             "cgroup_cpu_max": quota, "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def usable_cpus():
+    """CPUs this process can actually run on: its affinity mask, capped by the
+    cgroup CPU quota (cpu.max "quota period": the GPU box grants each job a
+    share of a many-core host -- affinity alone shows every core of the host,
+    and OpenMP threads beyond the quota only oversubscribe it)."""
+    aff = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, min(aff, int(float(q) / float(per) + 0.5)))
+    except (OSError, ValueError):
+        pass
+    return aff
 
 
 def cpu_baseline(g, nd_order, per_step, reps=5, curve_reps=3, amd_reps=3):
@@ -91,19 +107,23 @@ def cpu_baseline(g, nd_order, per_step, reps=5, curve_reps=3, amd_reps=3):
       one warm-up, and the GPU trajectory's counts (per_step: L linearisations,
       T tries, both identical to the oracle's, tests/test_gpu_parity.py) are
       priced with it: t = t_err0 + L t_lin + T t_try;
-    * all host cores: every CPU of this process's affinity mask (the headline
-      value, `cores`); the thread-scaling curve at 1, 16, 64 and that count
-      (median of `curve_reps`); 1 core as one_core.  Results do not depend on
-      the thread count (bitwise).
+    * all the host cores this job can use (usable_cpus: the affinity mask
+      capped by the cgroup CPU quota; the headline value, `cores`); the
+      thread-scaling curve at 1, 4, 8, 16, 32, 64 up to that count (median of
+      `curve_reps`); 1 core as one_core.  Results do not depend on the thread
+      count (bitwise).
     """
     import statistics
     from oracle.oracle import Oracle, set_threads
-    allc_threads = len(os.sched_getaffinity(0))
+    allc_threads = usable_cpus()
     L, T = per_step["linearizations"], per_step["lm_tries"]
 
     def unit(o, n):
         o.optimize(max_outer=1)                           # warm-up
-        runs = [o.optimize(max_outer=1).stats for _ in range(n)]
+        runs = []
+        for k in range(n):
+            runs.append(o.optimize(max_outer=1).stats)
+            log(f"  cpu unit {k + 1}/{n}: {runs[-1]['t_total']:.2f} s")
         t_lin = statistics.median(r["t_linearize"] for r in runs)
         t_err0 = statistics.median(r["t_error"] for r in runs) / 2.0   # initial + candidate error
         t_try = statistics.median(r["t_total"] - r["t_linearize"] for r in runs) - t_err0
@@ -115,16 +135,19 @@ def cpu_baseline(g, nd_order, per_step, reps=5, curve_reps=3, amd_reps=3):
 
     o_nd = Oracle(g, order=nd_order)
     set_threads(allc_threads)
+    log(f"cpu baseline: {allc_threads} threads")
     allc = unit(o_nd, reps)
     curve = {str(allc_threads): allc}
-    for t in sorted({1, 16, 64} - {allc_threads}):
+    for t in sorted({1, 4, 8, 16, 32, 64} - {allc_threads}):
         if t > allc_threads:
             continue
         set_threads(t)
+        log(f"cpu baseline: {t} threads")
         curve[str(t)] = unit(o_nd, curve_reps if t > 1 else reps)
     one = curve["1"] if "1" in curve else allc
     o_nd.close()
     set_threads(allc_threads)
+    log("cpu baseline: AMD ordering")
     o_amd = Oracle(g)
     amd = unit(o_amd, amd_reps)
     o_amd.close()
@@ -137,7 +160,8 @@ def cpu_baseline(g, nd_order, per_step, reps=5, curve_reps=3, amd_reps=3):
         "sample": (f"{g.name}: median of {reps} LM units (initial error + 1 linearisation + 1 lambda try: "
                    f"{allc['factor_flops'] / 1e9:.1f} GFLOP supernodal Cholesky on the GPU plan's nested-dissection "
                    f"ordering, nnz(L) {allc['nnz_l'] / 1e6:.0f}M) after 1 warm-up, oracle/pgo_oracle.c, "
-                   f"{allc_threads} OpenMP threads (every CPU of the affinity mask); priced on the GPU trajectory's "
+                   f"{allc_threads} OpenMP threads (every CPU this job may use: affinity capped by the cgroup quota); "
+                   f"priced on the GPU trajectory's "
                    f"{L} linearisations / {T} tries"),
         "all_cores": allc,
         "one_core": one,
@@ -385,6 +409,11 @@ def scan_registration_bench(batch=1024, reps=3, cpu_sample=64):
     return res
 
 
+def log(msg):
+    """Progress on stderr (the JSON line is stdout's only output)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _partition_bounds(live):
     """{config: {P: {bound, bound_replicated_top, est_speedup, exchange_points,
     exchange_bytes}}}: profiles/r03_partition_bounds.json (host-computed for C3
@@ -520,7 +549,9 @@ def main():
                 a[f] += v[f]
         return st["linearizations"], st
 
+    log(f"timed steps: {args.warmup} warm-up + {args.steps}")
     elapsed, lin_total, results = timed_steps(r, step, args.steps, args.warmup)
+    log(f"timed steps done: {1e3 * elapsed / args.steps:.1f} ms per step")
     if spec:   # one job: every rank walked the same linearisations
         lin_total /= world
     prof_stats = [step(prof_params)[1]] if args.profile_every > 0 else []
@@ -541,14 +572,17 @@ def main():
     scan = None
     if args.gicp and rank == 0:
         scan = scan_registration_bench(args.gicp)
+    log("marginals / search / scan registration done")
     one = dict(linear_solver=common["linear_solver"], use_graphs=common["use_graphs"])
     gn = gauss_newton_bench(pg, default_params, **one) if args.gn and rank == 0 and not spec else None
     conv = (converged_regime_bench(pg, g, default_params, lambda_lanes=args.lanes, **one)
             if args.converged and rank == 0 and not spec else None)
+    log("Gauss-Newton and converged-regime lines done")
     # the GPU plan's ordering of g, taken before live_resolve appends to the handle
     nd_order = pg.debug_ordering() if rank == 0 and not args.no_cpu_baseline and world == 1 else None
     live = None
     if args.live and rank == 0 and not spec:
+        log("live re-solve line")
         live = live_resolve_bench(pg, g, args.live)
     stats = [s for _, s in results]
     last = stats[-1]

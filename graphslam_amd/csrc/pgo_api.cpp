@@ -2044,6 +2044,30 @@ int pgo_debug_spmv(pgo_graph* g, double lambda, const double* x, double* y) {
   return PGO_OK;
 }
 
+int pgo_debug_factor_time(pgo_graph* g, int lanes, int reps, double* ms) {
+  if (!g || lanes < 1 || lanes > 8 || reps < 1 || !ms) return PGO_E_ARG;
+  RC_TRY(ensure_device(g));
+  HIP_TRY(g, hipSetDevice(g->device));
+  DevGraph& d = g->d;
+  if (d.n == 0) return fail(g, PGO_E_ARG, "empty graph");
+  g->part_size = 1;
+  RC_TRY(ensure_chol(g));
+  d.write_all = 0;
+  HIP_TRY(g, pgo::launch_linearize(d));
+  const int L = lanes > 1 ? ensure_lanes(g, lanes) : 1;
+  if (L < lanes) return fail(g, PGO_E_NOMEM, "not enough memory for the lambda lanes");
+  for (int l = 0; l < L; l++) g->h_lanes[4 * 8 + l] = 1e-5 * std::pow(10.0, l);
+  HIP_TRY(g, hipMemcpyAsync(g->chol.d_lambda, g->h_lanes + 4 * 8, L * sizeof(double), hipMemcpyHostToDevice,
+                            d.stream));
+  RC_TRY(graph_factor_solve(g, L, L > 1 ? g->xb : d.x, L > 1 ? 3LL * d.n : 0));   // capture + warm
+  HIP_TRY(g, hipEventRecord(g->ev[0], d.stream));
+  for (int r = 0; r < reps; r++) HIP_TRY(g, hipGraphLaunch(g->fac_exec[L], d.stream));
+  HIP_TRY(g, hipEventRecord(g->ev[1], d.stream));
+  HIP_TRY(g, hipStreamSynchronize(d.stream));
+  *ms = ms_between(g->ev[0], g->ev[1]) / reps;
+  return PGO_OK;
+}
+
 int pgo_debug_solve(pgo_graph* g, double lambda, const pgo_params* params, double* delta, int* pcg_iterations) {
   if (!g || !delta) return PGO_E_ARG;
   pgo_params p;

@@ -319,6 +319,13 @@ class PoseGraph:
         self._check(fn(self._h, L.dptr(hd), L.dptr(ho), L.dptr(g), C.byref(e)))
         return hd, ho, g, e.value
 
+    def debug_factor_time(self, lanes=1, reps=10):
+        """Device ms of one replay of the captured factorisation graph with
+        `lanes` lambda lanes (diagnostics; PGO_ABLATE applies)."""
+        ms = C.c_double(0)
+        self._check(self._L.pgo_debug_factor_time(self._h, int(lanes), int(reps), C.byref(ms)))
+        return ms.value
+
     def debug_spmv(self, x, lam=0.0):
         x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1, 3)
         y = np.zeros_like(x)

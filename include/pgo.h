@@ -355,6 +355,11 @@ int pgo_debug_linearize(pgo_graph *g, double *hdiag, double *hoff, double *grad,
 int pgo_debug_linearize_cholesky(pgo_graph *g, double *hdiag, double *hoff, double *grad, double *err);
 /* y = (H + lambda I) x at the current linearisation (x, y: 3 per vertex) */
 int pgo_debug_spmv(pgo_graph *g, double lambda, const double *x, double *y);
+/* Diagnostics: device time of one replay of the captured factorisation graph
+ * of `lanes` lambda lanes (lambda_l = 1e-5 10^l) at the current linearisation,
+ * averaged over `reps` back-to-back replays (HIP events on the handle's
+ * stream); PGO_ABLATE (families to leave out) applies at capture. */
+int pgo_debug_factor_time(pgo_graph *g, int lanes, int reps, double *ms);
 /* delta = PCG solve of (H + lambda I) delta = -g at the current values */
 int pgo_debug_solve(pgo_graph *g, double lambda, const pgo_params *params, double *delta,
                     int *pcg_iterations);
