@@ -1043,7 +1043,18 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
       Sc[b][(idx >> 6) * LD + (idx & 63)] = st[4 + q];
     }
   };
-  d4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
+  // v_mfma_f64_4x4x4f64 (4 blocks of 4x4x4): the wave's 32x32 quadrant as 8
+  // column groups of 4 (p) x 2 row groups of 16 (h), 16 independent
+  // accumulators.  Block g of an instruction: A(i, k) at lane 16k + 4g + i,
+  // B(k, j) at lane 16k + 4g + j, D(i, j) at lane 16i + 4g + j (probed,
+  // scripts/ubench_mfma4.hip); here A = the column side (i: column 4p + i),
+  // B = the row side (g, j: row 16h + 4g + j), so lane l holds row 16h + (l & 15),
+  // column 4p + (l >> 4).  Each element is the same 4-term MFMA dot product in
+  // the same k order as with v_mfma_f64_16x16x4f64 (bitwise the same result,
+  // probed), at up to 69 instead of 48 TFLOP/s (independent chains).
+  double acc[8][2];
+#pragma unroll
+  for (int p = 0; p < 8; p++) acc[p][0] = acc[p][1] = 0.0;
   load(0);
   stash(0);
   __syncthreads();
@@ -1053,40 +1064,38 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
     if (active) {
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        const double* sr = Sr[b] + (4 * u + lk) * LD + qi + li;
-        const double* sc = Sc[b] + (4 * u + lk) * LD + qj + li;
-        const double ra = sr[0], rb = sr[16], ca = sc[0], cb = sc[16];
-        acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(ca, ra, acc00, 0, 0, 0);
-        acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(ca, rb, acc01, 0, 0, 0);
-        acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(cb, ra, acc10, 0, 0, 0);
-        acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(cb, rb, acc11, 0, 0, 0);
+        const double* sr = Sr[b] + (4 * u + lk) * LD + qi + (l & 15);
+        const double* sc = Sc[b] + (4 * u + lk) * LD + qj + (l & 3);
+        const double r0v = sr[0], r1v = sr[16];
+        double cv[8];
+#pragma unroll
+        for (int p = 0; p < 8; p++) cv[p] = sc[4 * p];
+#pragma unroll
+        for (int p = 0; p < 8; p++) {
+          acc[p][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(cv[p], r0v, acc[p][0], 0, 0, 0);
+          acc[p][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(cv[p], r1v, acc[p][1], 0, 0, 0);
+        }
       }
     }
     if (ch + 1 < nch) stash(b ^ 1);
     __syncthreads();
   }
   if (!active) return;
-  // C read-modify-write (layout: lane l, reg r -> column col0+qj+16mj+lk+4r, row row0+qi+16mi+li)
-  double cold[2][2][4];
+  // C read-modify-write: lane l holds (row row0 + qi + 16h + (l & 15), column col0 + qj + 4p + (l >> 4))
+  double cold[8][2];
 #pragma unroll
-  for (int mi = 0; mi < 2; mi++)
+  for (int p = 0; p < 8; p++)
 #pragma unroll
-    for (int mj = 0; mj < 2; mj++)
+    for (int h = 0; h < 2; h++) {
+      const int row = row0 + qi + 16 * h + (l & 15), col = col0 + qj + 4 * p + lk;
+      cold[p][h] = (row < m && col < colend && row >= col) ? Fs[row + (size_t)col * m] : 0.0;
+    }
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int row = row0 + qi + 16 * mi + li, col = col0 + qj + 16 * mj + lk + 4 * r;
-        cold[mi][mj][r] = (row < m && col < colend && row >= col) ? Fs[row + (size_t)col * m] : 0.0;
-      }
+  for (int p = 0; p < 8; p++)
 #pragma unroll
-  for (int mi = 0; mi < 2; mi++)
-#pragma unroll
-    for (int mj = 0; mj < 2; mj++) {
-      const d4 a = mj == 0 ? (mi == 0 ? acc00 : acc01) : (mi == 0 ? acc10 : acc11);
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int row = row0 + qi + 16 * mi + li, col = col0 + qj + 16 * mj + lk + 4 * r;
-        if (row < m && col < colend && row >= col) Fs[row + (size_t)col * m] = cold[mi][mj][r] - a[r];
-      }
+    for (int h = 0; h < 2; h++) {
+      const int row = row0 + qi + 16 * h + (l & 15), col = col0 + qj + 4 * p + lk;
+      if (row < m && col < colend && row >= col) Fs[row + (size_t)col * m] = cold[p][h] - acc[p][h];
     }
 }
 
@@ -1363,11 +1372,14 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
       Sc[buf][k * LD + r] = st[8 + q];
     }
   };
-  d4 acc[4][4];
+  // v_mfma_f64_4x4x4f64, as syrk_lds_body: the wave's 64x64 quarter as 16
+  // column groups of 4 (p) x 4 row groups of 16 (h), 64 accumulators; lane l
+  // holds (row 64wi + 16h + (l & 15), column 64wj + 4p + (l >> 4))
+  double acc[16][4];
 #pragma unroll
-  for (int bj = 0; bj < 4; bj++)
+  for (int p = 0; p < 16; p++)
 #pragma unroll
-    for (int bi = 0; bi < 4; bi++) acc[bj][bi] = d4{0, 0, 0, 0};
+    for (int h = 0; h < 4; h++) acc[p][h] = 0.0;
   load(0);
   stash(0);
   __syncthreads();
@@ -1376,45 +1388,39 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
     if (ch + 1 < nchunk) load(ch + 1);
     if (active) {
       const double* sr = Sr[buf] + 64 * wi + (l & 15);
-      const double* sc = Sc[buf] + 64 * wj + (l & 15);
+      const double* sc = Sc[buf] + 64 * wj + (l & 3);
 #pragma unroll
       for (int kk = 0; kk < 4; kk++) {
         const int ko = (4 * kk + (l >> 4)) * LD;
-        double ra[4], ca[4];
+        double rv[4];
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-          ra[b] = sr[ko + 16 * b];
-          ca[b] = sc[ko + 16 * b];
+        for (int h = 0; h < 4; h++) rv[h] = sr[ko + 16 * h];
+#pragma unroll
+        for (int p = 0; p < 16; p++) {
+          const double cv = sc[ko + 4 * p];
+#pragma unroll
+          for (int h = 0; h < 4; h++) acc[p][h] = __builtin_amdgcn_mfma_f64_4x4x4f64(cv, rv[h], acc[p][h], 0, 0, 0);
         }
-#pragma unroll
-        for (int bj = 0; bj < 4; bj++)
-#pragma unroll
-          for (int bi = 0; bi < 4; bi++)
-            acc[bj][bi] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[bj], ra[bi], acc[bj][bi], 0, 0, 0);
       }
     }
     if (ch + 1 < nchunk) stash(buf ^ 1);
     __syncthreads();
   }
   if (!active) return;
-  // lane l, reg r of acc[bj][bi] -> row row0+64wi+16bi+(l&15), col col0+64wj+16bj+(l>>4)+4r
 #pragma unroll
-  for (int bj = 0; bj < 4; bj++) {
-    double cold[4][4];
+  for (int p = 0; p < 16; p++) {
+    double cold[4];
+    const int col = col0 + 64 * wj + 4 * p + (l >> 4);
 #pragma unroll
-    for (int bi = 0; bi < 4; bi++)
+    for (int h = 0; h < 4; h++) {
+      const int row = row0 + 64 * wi + 16 * h + (l & 15);
+      cold[h] = (row < m && col < colend && row >= col) ? Fs[row + (size_t)col * m] : 0.0;
+    }
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int row = row0 + 64 * wi + 16 * bi + (l & 15), col = col0 + 64 * wj + 16 * bj + (l >> 4) + 4 * r;
-        cold[bi][r] = (row < m && col < colend && row >= col) ? Fs[row + (size_t)col * m] : 0.0;
-      }
-#pragma unroll
-    for (int bi = 0; bi < 4; bi++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int row = row0 + 64 * wi + 16 * bi + (l & 15), col = col0 + 64 * wj + 16 * bj + (l >> 4) + 4 * r;
-        if (row < m && col < colend && row >= col) Fs[row + (size_t)col * m] = cold[bi][r] - acc[bj][bi][r];
-      }
+    for (int h = 0; h < 4; h++) {
+      const int row = row0 + 64 * wi + 16 * h + (l & 15);
+      if (row < m && col < colend && row >= col) Fs[row + (size_t)col * m] = cold[h] - acc[p][h];
+    }
   }
 }
 

@@ -5,6 +5,7 @@
 //   ./graphslam_amd/build/ubench_syrk [m] [w]
 #include "../graphslam_amd/csrc/pgo_chol.hip"
 #include "../graphslam_amd/csrc/pgo_symbolic.cpp"
+#include "../graphslam_amd/csrc/pgo_order.cpp"
 
 #include <cstdio>
 #include <cstdlib>
@@ -130,7 +131,7 @@ int main(int argc, char** argv) {
   const int kb = 192, be = 256;
   const double flops = 256.0 * (M - be) * (M - be + 1.0);
   for (int T : {64, 65, 128}) {   // 65: the LDS-staged 64x64 kernel
-    const int TT = T >= 65 ? 64 : T;
+    const int TT = T == 65 ? 64 : T;
     std::vector<int4> tasks;
     for (int c0 = be; c0 < M; c0 += TT)
       for (int r0 = c0; r0 < M; r0 += TT) tasks.push_back(make_int4(0, r0, c0, 0));
