@@ -1289,6 +1289,94 @@ __global__ __launch_bounds__(256, 2) void k_panel_first(CholDev c, const int* __
   trsm_rows(c, s, t.y, 0, nb, c.F + c.foff[s] + t.y, 1, m, smem);
 }
 
+// The same first panel in two launches, for levels with many big fronts (the
+// lower levels: hundreds of fronts x lanes): k_first_diag factors and inverts
+// the first diagonal tiles (first_diag_body, one workgroup each), then
+// k_first_trsm solves the 64-row tiles below them against the inverses of the
+// previous launch -- a workgroup of ~64 VGPRs per lane and 32 KB of LDS, so
+// 4-5 fit a CU instead of k_panel_first's 2 (the in-launch waiters hold
+// k_step's LDS and registers).  Same arithmetic in the same order as
+// trsm_rows: bitwise k_panel_first's result.
+__global__ __launch_bounds__(256, 2) void k_first_diag(CholDev c, const int* __restrict__ list) {
+  lane_offset(c);
+  __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
+  first_diag_body(c, list[blockIdx.x], smem);
+}
+
+__global__ __launch_bounds__(256) void k_first_trsm(CholDev c, const int4* __restrict__ col) {
+  lane_offset(c);
+  __shared__ __attribute__((aligned(16))) double xs[4096];
+  const int4 t = col[blockIdx.x];
+  const int s = t.x, m = c.m[s], nb = min(kNB, c.w[s]), r0 = t.y;
+  const double* Mf = c.Tinv + c.tfo + c.toff[s];
+  double* fv = c.fv + c.voff[s];
+  const double* A = c.F + c.foff[s] + r0;   // A(i, k) = A[i + k m]
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  {
+    double2 tq[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) tq[u] = reinterpret_cast<const double2*>(Mf)[tid + 256 * u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      xs[2 * (tid + 256 * u)] = tq[u].x;
+      xs[2 * (tid + 256 * u) + 1] = tq[u].y;
+    }
+  }
+  const int rw = r0 + wv * 16, kl = l >> 4;
+  double yc[4], fvr[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ct++) {
+    const int col = 16 * ct + (l & 15);
+    yc[ct] = col < nb ? fv[col] : 0.0;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int row = rw + kl + 4 * r;
+    fvr[r] = ((l & 15) == 0 && row < m) ? fv[row] : 0.0;
+  }
+  const int il = wv * 16 + (l & 15), arow = r0 + il;
+  double a[16];
+#pragma unroll
+  for (int ks = 0; ks < 16; ks++) {
+    const int k = 4 * ks + kl;
+    a[ks] = (arow < m && k < nb) ? A[il + (size_t)k * m] : 0.0;
+  }
+  __syncthreads();
+  if (rw >= m) return;
+  double* Fc = c.F + c.foff[s];
+  d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0}, acc3 = {0, 0, 0, 0};
+#pragma unroll
+  for (int ks = 0; ks < 16; ks++) {
+    const double* x = xs + 4 * ks * 64 + l;
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], x[0], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], x[64], acc1, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], x[128], acc2, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], x[192], acc3, 0, 0, 0);
+  }
+  double part[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int ct = 0; ct < 4; ct++) {
+    const d4 v = ct == 0 ? acc0 : (ct == 1 ? acc1 : (ct == 2 ? acc2 : acc3));
+    const int col = 16 * ct + (l & 15);
+#pragma unroll
+    for (int r = 0; r < 4; r++) part[r] = fma(v[r], yc[ct], part[r]);
+    if (col >= nb) continue;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int row = rw + kl + 4 * r;
+      if (row < m) Fc[row + (size_t)col * m] = v[r];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    double t2 = part[r];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) t2 += __shfl_xor(t2, o);
+    const int row = rw + kl + 4 * r;
+    if ((l & 15) == 0 && row < m) fv[row] = fvr[r] - t2;
+  }
+}
+
 // One panel step kb of every big front of a level in one launch:
 //   [0, nsd)            the next panel's diagonal tiles (syrk_diag_body)
 //   [nsd, nsd + ncol)   64-row tiles of the next panel's column block below
@@ -2260,10 +2348,22 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       }
       if (prof) prof->cur_tag = ((int)li << 16) | (ps.kb / kNB + 1);
       const int4* cols = (const int4*)(P.d_col + ps.col_off);
-      if (ps.potrf_cnt && !off("first"))
-        launch(prof, kFamPanelFirst, [&] { return make_double2(ps.first_flops * nb, 0); }, k_panel_first,
-               dim3(ps.potrf_cnt + ps.fcol_cnt, nb), B256, 0, s, c, (const int*)(P.d_potrf + ps.potrf_off),
-               ps.potrf_cnt, cols);
+      // many first panels (x lanes): diagonal tiles, then the tiles below in a
+      // second launch of higher occupancy; few: one launch with in-launch
+      // hand-offs (PGO_FIRST_SPLIT: the fronts x lanes from which to split)
+      static const int first_split = getenv("PGO_FIRST_SPLIT") ? atoi(getenv("PGO_FIRST_SPLIT")) : 64;
+      if (ps.potrf_cnt && !off("first")) {
+        if (ps.potrf_cnt * nb >= first_split && ps.fcol_cnt > 0) {
+          launch(prof, kFamPanelFirst, [&] { return make_double2(ps.first_flops * nb, 0); }, k_first_diag,
+                 dim3(ps.potrf_cnt, nb), B256, 0, s, c, (const int*)(P.d_potrf + ps.potrf_off));
+          launch(prof, kFamPanelFirst, [&] { return make_double2(0, 0); }, k_first_trsm, dim3(ps.fcol_cnt, nb), B256,
+                 0, s, c, cols);
+        } else {
+          launch(prof, kFamPanelFirst, [&] { return make_double2(ps.first_flops * nb, 0); }, k_panel_first,
+                 dim3(ps.potrf_cnt + ps.fcol_cnt, nb), B256, 0, s, c, (const int*)(P.d_potrf + ps.potrf_off),
+                 ps.potrf_cnt, cols);
+        }
+      }
       CH_TRY(xpanels(ps.xfirst));
       const int4* tiles = (const int4*)(P.d_syrk + ps.syrk_off);
       const int nin = ps.syrk_inline && !off("plain") ? ps.syrk_cnt : 0;

@@ -34,16 +34,24 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--ablate", nargs="*", default=["small", "plain", "assemble", "vec", "first", "step",
                                                     "step,plain"])
+    ap.add_argument("--envs", nargs="*", default=None,
+                    help="instead of ablations: settings to compare, each 'tag:VAR=VAL[,VAR=VAL]'")
     ap.add_argument("--child", action="store_true")
     args = ap.parse_args()
     if args.child:
         print(json.dumps(one(args.config, args.lanes, args.reps)), flush=True)
         return
     res = {}
-    for ab in ["none"] + args.ablate:
+    runs = []
+    if args.envs is not None:
+        for e in ["default:"] + args.envs:
+            tag, _, kv = e.partition(":")
+            runs.append((tag, dict(x.split("=", 1) for x in kv.split(",") if x)))
+    else:
+        runs = [("none", {})] + [(a, {"PGO_ABLATE": a}) for a in args.ablate]
+    for ab, extra in runs:
         env = dict(os.environ)
-        if ab != "none":
-            env["PGO_ABLATE"] = ab
+        env.update(extra)
         cmd = [sys.executable, os.path.abspath(__file__), "--child", "--config", args.config, "--reps", str(args.reps),
                "--lanes"] + [str(l) for l in args.lanes]
         out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
