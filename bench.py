@@ -264,6 +264,7 @@ def live_resolve_bench(pg, g, k=5):
         pg.add_edge(v + 1, j + 1, between_xyt(gt[v], gt[j]), cov)
         st = pg.optimize()
         rows.append({"ms": 1e3 * (time.perf_counter() - t0), "plan_update": st["plan_update"],
+                     "upload_kind": st["upload_kind"],
                      "ms_plan": st["ms_plan"], "ms_upload": st["ms_upload"], "linearizations": st["linearizations"],
                      "lm_tries": st["inner_iterations"]})
     return {"registrations": k, "ms_median": float(np.median([r["ms"] for r in rows])), "per_registration": rows,

@@ -70,7 +70,7 @@ class PgoStats(C.Structure):
                 ("solves", C.c_longlong), ("ms_comm", C.c_double),
                 ("ms_factor_profiled", C.c_double), ("ms_solve_profiled", C.c_double), ("stop_reason", C.c_int),
                 ("ms_factor_graph", C.c_double), ("factor_graph_flops", C.c_double),
-                ("plan_update", C.c_int), ("ms_plan", C.c_double)]
+                ("plan_update", C.c_int), ("ms_plan", C.c_double), ("upload_kind", C.c_int)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
@@ -178,7 +178,7 @@ def lib():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.pgo_abi_version() != 4:
+    if L.pgo_abi_version() != 5:
         raise RuntimeError("libpgo.so ABI version mismatch")
     _lib = L
     return L

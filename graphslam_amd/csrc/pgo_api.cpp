@@ -40,6 +40,14 @@ struct Lane {
   double* scal = nullptr;
 };
 
+struct HostStructure {
+  std::vector<int2> eij;           // device order
+  std::vector<int> dorder;         // device factor -> user factor index
+  std::vector<int> pv, row_ptr, slot_edge, slot_col, prior_ptr, porder;
+  std::vector<int> uf;             // union-find parents over the vertices (gauge check)
+  bool gauge_free = false;
+};
+
 struct pgo_graph {
   int device = 0;
   std::string last_error;
@@ -98,6 +106,12 @@ struct pgo_graph {
   double* h_lanes = nullptr;                // pinned [48]: 4 scalars per lane, lambdas at 32, flags at 40
   hipEvent_t lin_done = nullptr;            // linearisation complete
   int lane_cap = 8;                         // 1 after a lane allocation failed (reset per plan)
+  // ---- incremental appends (append_structure, the live re-solve) ----
+  HostStructure hs;                         // the structure the device holds (host side)
+  std::vector<double> h_Dc;                 // its per-row sums of side-1 Omega
+  size_t cap_n = 0, cap_ne = 0;             // device capacities in vertices / factors
+  bool dev_complete = false;                // the device holds hs exactly (appendable)
+  int last_upload = 0;                      // 1 full upload, 2 append (diagnostics)
   // ---- closest-keyframe search scratch ----
   double* s_d = nullptr;                    // [kMaxBlocks + 1] partial / final distances
   int* s_i = nullptr;                       // [kMaxBlocks + 1] partial / final indices
@@ -204,6 +218,7 @@ void free_lanes(pgo_graph* g) {
 }
 
 void free_device(pgo_graph* g, bool keep_plan = false) {
+  g->dev_complete = false;
   free_lanes(g);
   g->lane_cap = 8;
   DevGraph& d = g->d;
@@ -308,12 +323,6 @@ int download_values(pgo_graph* g) {
 // optimize time for a factor on an unknown key), block-CSR slots, priors.
 // Host-side structure of the graph (no HIP): resolved factor endpoints,
 // block-CSR slots, priors by vertex, gauge freedom.
-struct HostStructure {
-  std::vector<int2> eij;           // device order
-  std::vector<int> dorder;         // device factor -> user factor index
-  std::vector<int> pv, row_ptr, slot_edge, slot_col, prior_ptr, porder;
-  bool gauge_free = false;
-};
 
 int build_structure(pgo_graph* g, HostStructure& H) {
   const int n = (int)g->keys.size();
@@ -383,7 +392,8 @@ int build_structure(pgo_graph* g, HostStructure& H) {
   // GTSAM's Cholesky throws IndeterminantLinearSystemException there (GN);
   // LM's damping keeps it solvable.
   {
-    std::vector<int> uf(n);
+    std::vector<int>& uf = H.uf;
+    uf.resize(n);
     for (int i = 0; i < n; i++) uf[i] = i;
     auto find = [&](int x) {
       while (uf[x] != x) x = uf[x] = uf[uf[x]];
@@ -482,6 +492,12 @@ int upload_structure(pgo_graph* g) {
   d.ne = ne;
   d.np = np;
   d.nslots = ns;
+  // room for appended vertices / factors (the live re-solve appends one
+  // keyframe and a few factors per registration: append_structure)
+  const size_t cn = (size_t)n + std::max<size_t>(1024, n / 8);
+  const size_t ce = (size_t)ne + std::max<size_t>(4096, ne / 8), cs = 2 * ce;
+  g->cap_n = cn;
+  g->cap_ne = ce;
   // lanes per row: smallest power of two >= mean degree, in [4, 32]
   const double mean_deg = n ? (double)ns / n : 0.0;
   d.G = 4;
@@ -521,38 +537,38 @@ int upload_structure(pgo_graph* g) {
     r = r1;
   }
   d.nlb = (int)brow.size() - 1;
-  RC_TRY(dev_alloc(g, &d.brow, brow.size()));
+  RC_TRY(dev_alloc(g, &d.brow, cn + 1));
   RC_TRY(h2d(g, d.brow, brow.data(), brow.size()));
-  RC_TRY(dev_alloc(g, &d.erow, n + 1));
-  RC_TRY(dev_alloc(g, &d.s1_ptr, n + 1));
-  RC_TRY(dev_alloc(g, &d.s1pos, ne));
-  RC_TRY(dev_alloc(g, &d.Dc, 6 * (size_t)n));
-  RC_TRY(dev_alloc(g, &d.W, ne));
+  RC_TRY(dev_alloc(g, &d.erow, cn + 1));
+  RC_TRY(dev_alloc(g, &d.s1_ptr, cn + 1));
+  RC_TRY(dev_alloc(g, &d.s1pos, ce));
+  RC_TRY(dev_alloc(g, &d.Dc, 6 * cn));
+  RC_TRY(dev_alloc(g, &d.W, ce));
   RC_TRY(h2d(g, d.erow, erow.data(), n + 1));
   RC_TRY(h2d(g, d.s1_ptr, s1_ptr.data(), n + 1));
   RC_TRY(h2d(g, d.s1pos, s1pos.data(), ne));
   RC_TRY(h2d(g, d.Dc, Dc.data(), 6 * (size_t)n));
-  RC_TRY(dev_alloc(g, &d.eij, ne));
-  RC_TRY(dev_alloc(g, &d.ez, ne));
-  RC_TRY(dev_alloc(g, &d.eom, 3 * (size_t)ne));
-  RC_TRY(dev_alloc(g, &d.prior_ptr, n + 1));
+  RC_TRY(dev_alloc(g, &d.eij, ce));
+  RC_TRY(dev_alloc(g, &d.ez, ce));
+  RC_TRY(dev_alloc(g, &d.eom, 3 * ce));
+  RC_TRY(dev_alloc(g, &d.prior_ptr, cn + 1));
   RC_TRY(dev_alloc(g, &d.prior_vtx, np));
   RC_TRY(dev_alloc(g, &d.pz, np));
   RC_TRY(dev_alloc(g, &d.pom, 3 * (size_t)np));
-  RC_TRY(dev_alloc(g, &d.row_ptr, n + 1));
-  RC_TRY(dev_alloc(g, &d.slot_edge, ns));
-  RC_TRY(dev_alloc(g, &d.slot_col, ns));
-  RC_TRY(dev_alloc(g, &d.V, 9 * (size_t)ns));
-  RC_TRY(dev_alloc(g, &d.D, 6 * (size_t)n));
-  RC_TRY(dev_alloc(g, &d.g, 3 * (size_t)n));
-  RC_TRY(dev_alloc(g, &d.pose, n));
-  RC_TRY(dev_alloc(g, &d.pose_cand, n));
-  RC_TRY(dev_alloc(g, &d.x, 3 * (size_t)n));
-  RC_TRY(dev_alloc(g, &d.r, 3 * (size_t)n));
-  RC_TRY(dev_alloc(g, &d.z, 3 * (size_t)n));
-  RC_TRY(dev_alloc(g, &d.p, 3 * (size_t)n));
-  RC_TRY(dev_alloc(g, &d.q, 3 * (size_t)n));
-  RC_TRY(dev_alloc(g, &d.Minv, 6 * (size_t)n));
+  RC_TRY(dev_alloc(g, &d.row_ptr, cn + 1));
+  RC_TRY(dev_alloc(g, &d.slot_edge, cs));
+  RC_TRY(dev_alloc(g, &d.slot_col, cs));
+  RC_TRY(dev_alloc(g, &d.V, 9 * cs));
+  RC_TRY(dev_alloc(g, &d.D, 6 * cn));
+  RC_TRY(dev_alloc(g, &d.g, 3 * cn));
+  RC_TRY(dev_alloc(g, &d.pose, cn));
+  RC_TRY(dev_alloc(g, &d.pose_cand, cn));
+  RC_TRY(dev_alloc(g, &d.x, 3 * cn));
+  RC_TRY(dev_alloc(g, &d.r, 3 * cn));
+  RC_TRY(dev_alloc(g, &d.z, 3 * cn));
+  RC_TRY(dev_alloc(g, &d.p, 3 * cn));
+  RC_TRY(dev_alloc(g, &d.q, 3 * cn));
+  RC_TRY(dev_alloc(g, &d.Minv, 6 * cn));
   RC_TRY(dev_alloc(g, &d.part, (size_t)pgo::kMaxBlocks * pgo::kPartSlices));
   RC_TRY(dev_alloc(g, &d.scal, 16));
   RC_TRY(dev_alloc(g, &d.ctrl, 4));
@@ -571,6 +587,10 @@ int upload_structure(pgo_graph* g) {
   HIP_TRY(g, hipMemsetAsync(d.part, 0, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices, d.stream));
   HIP_TRY(g, hipStreamSynchronize(d.stream));
   g->dev_structure = true;
+  g->h_Dc = std::move(Dc);
+  g->hs = std::move(H);
+  g->dev_complete = true;
+  g->last_upload = 1;
   if (n_old > 0) {
     HIP_TRY(g, hipMemcpyAsync(d.pose, keep.get(), sizeof(double4) * n_old, hipMemcpyDeviceToDevice, d.stream));
     HIP_TRY(g, hipStreamSynchronize(d.stream));
@@ -578,8 +598,196 @@ int upload_structure(pgo_graph* g) {
   return upload_values(g, n_old);
 }
 
+// Appended vertices and between factors (pgo_add_vertex / pgo_add_edge after
+// an upload -- the live re-solve, graph.cpp:180-200) extend the device graph in
+// place when the device holds the previous structure, no prior was added,
+// capacities suffice and the new factors sort after the old ones in device
+// order ((ei, ej): a new keyframe's odometry and loop closures do).  The host
+// structure is updated in step (block-CSR rows merged, side-1 lists, row
+// blocks); only the new factors, the per-row arrays and the slot arrays are
+// uploaded.  Returns 1 when the full upload must run instead.
+int append_structure(pgo_graph* g) {
+  DevGraph& d = g->d;
+  HostStructure& H = g->hs;
+  const int n_old = d.n, ne_old = d.ne;
+  const int n = (int)g->keys.size(), ne = (int)g->ek1.size(), np = (int)g->pk.size();
+  if (!g->dev_complete || !g->hip_ready || np != d.np || n < n_old || ne < ne_old || (n == n_old && ne == ne_old) ||
+      (size_t)n > g->cap_n || (size_t)ne > g->cap_ne || (int)H.eij.size() != ne_old || getenv("PGO_NO_APPEND"))
+    return 1;
+  // the new factors, resolved and in device order
+  std::vector<int> nd(ne - ne_old);
+  std::vector<int2> nij(ne - ne_old);
+  for (int e = ne_old; e < ne; e++) {
+    auto a = g->index.find(g->ek1[e]), b = g->index.find(g->ek2[e]);
+    if (a == g->index.end() || b == g->index.end()) return 1;   // the full path reports it
+    nij[e - ne_old] = make_int2(a->second, b->second);
+    nd[e - ne_old] = e;
+  }
+  {
+    std::vector<int> o(nd.size());
+    for (size_t q = 0; q < o.size(); q++) o[q] = (int)q;
+    std::stable_sort(o.begin(), o.end(), [&](int a, int b) {
+      return nij[a].x != nij[b].x ? nij[a].x < nij[b].x : nij[a].y < nij[b].y;
+    });
+    std::vector<int> nd2(nd.size());
+    std::vector<int2> nij2(nij.size());
+    for (size_t q = 0; q < o.size(); q++) {
+      nd2[q] = nd[o[q]];
+      nij2[q] = nij[o[q]];
+    }
+    nd.swap(nd2);
+    nij.swap(nij2);
+  }
+  if (!nij.empty() && ne_old > 0) {
+    const int2 last = H.eij.back(), f = nij.front();
+    if (f.x < last.x || (f.x == last.x && f.y < last.y)) return 1;   // not an append in device order
+  }
+  RC_TRY(download_values(g));
+  // host structure: device order, block-CSR rows (every row sorted by (column,
+  // code) as build_structure sorts them, codes in their pre-plan form)
+  H.eij.insert(H.eij.end(), nij.begin(), nij.end());
+  H.dorder.insert(H.dorder.end(), nd.begin(), nd.end());
+  std::vector<int> add(n, 0);
+  for (const int2& ij : nij) {
+    add[ij.x]++;
+    add[ij.y]++;
+  }
+  const int ns = 2 * ne;
+  std::vector<int> rp(n + 1, 0), sc(ns), se(ns);
+  for (int i = 0; i < n; i++) rp[i + 1] = rp[i] + (i < n_old ? H.row_ptr[i + 1] - H.row_ptr[i] : 0) + add[i];
+  std::vector<std::vector<std::pair<int, int>>> extra(n);
+  for (size_t q = 0; q < nij.size(); q++) {
+    const int de = ne_old + (int)q;
+    extra[nij[q].x].emplace_back(nij[q].y, (de << 2) | 2);
+    extra[nij[q].y].emplace_back(nij[q].x, (de << 2) | 1);
+  }
+  for (int i = 0; i < n; i++) {
+    const int b = i < n_old ? H.row_ptr[i] : 0, e0 = i < n_old ? H.row_ptr[i + 1] : 0;
+    int o = rp[i];
+    if (!add[i]) {
+      for (int k = b; k < e0; k++, o++) {
+        sc[o] = H.slot_col[k];
+        se[o] = ((H.slot_edge[k] >> 2) << 2) | ((H.slot_edge[k] & 1) ? 1 : 2);
+      }
+      continue;
+    }
+    std::vector<std::pair<int, int>> t;
+    for (int k = b; k < e0; k++) t.emplace_back(H.slot_col[k], ((H.slot_edge[k] >> 2) << 2) | ((H.slot_edge[k] & 1) ? 1 : 2));
+    t.insert(t.end(), extra[i].begin(), extra[i].end());
+    std::sort(t.begin(), t.end());
+    for (auto& [c, code] : t) {
+      sc[o] = c;
+      se[o++] = code;
+    }
+  }
+  H.row_ptr.swap(rp);
+  H.slot_col.swap(sc);
+  H.slot_edge.swap(se);
+  // gauge: the new factors join components; anchored roots from the priors
+  H.uf.resize(n);
+  for (int i = n_old; i < n; i++) H.uf[i] = i;
+  auto find = [&](int x) {
+    while (H.uf[x] != x) x = H.uf[x] = H.uf[H.uf[x]];
+    return x;
+  };
+  for (const int2& ij : nij) {
+    const int a = find(ij.x), b = find(ij.y);
+    if (a != b) H.uf[a] = b;
+  }
+  {
+    std::vector<char> anchored(n, 0);
+    for (int q = 0; q < np; q++) anchored[find(H.pv[q])] = 1;
+    g->gauge_free = false;
+    for (int i = 0; i < n; i++)
+      if (!anchored[find(i)]) g->gauge_free = true;
+    H.gauge_free = g->gauge_free;
+  }
+  H.prior_ptr.resize(n + 1, H.prior_ptr.empty() ? 0 : H.prior_ptr.back());
+  g->h_row_ptr = H.row_ptr;
+  g->h_slot_col = H.slot_col;
+  g->h_slot_edge = H.slot_edge;
+  g->edge_slot0.assign(ne, -1);
+  for (int k = 0; k < ns; k++)
+    if ((H.slot_edge[k] & 1) == 0) g->edge_slot0[H.dorder[H.slot_edge[k] >> 2]] = k;
+  // Cholesky-mode sweep structure (see upload_structure)
+  std::vector<int> erow(n + 1, 0), s1_ptr(n + 1, 0), s1pos(ne);
+  for (int e = 0; e < ne; e++) {
+    erow[H.eij[e].x + 1]++;
+    s1_ptr[H.eij[e].y + 1]++;
+  }
+  for (int i = 0; i < n; i++) {
+    erow[i + 1] += erow[i];
+    s1_ptr[i + 1] += s1_ptr[i];
+  }
+  {
+    std::vector<int> f(s1_ptr.begin(), s1_ptr.end() - 1);
+    for (int e = 0; e < ne; e++) s1pos[e] = f[H.eij[e].y]++;
+  }
+  g->h_Dc.resize(6 * (size_t)n, 0.0);
+  for (size_t q = 0; q < nij.size(); q++) {   // new side-1 terms, in device order after the old ones
+    const double* o = &g->eom[6 * (size_t)nd[q]];
+    for (int c = 0; c < 6; c++) g->h_Dc[6 * (size_t)nij[q].y + c] += o[c];
+  }
+  std::vector<int> brow(1, 0);
+  for (int r = 0; r < n;) {
+    int r1 = r + 1;
+    while (r1 < n && r1 - r < pgo::kThreads && erow[r1 + 1] - erow[r] <= pgo::kThreads) r1++;
+    brow.push_back(r1);
+    r = r1;
+  }
+  // the device: new factors, per-row arrays, slots
+  HIP_TRY(g, hipStreamSynchronize(d.stream));
+  free_lanes(g);
+  drop_graphs(g);
+  if (d.pose_saved) (void)hipFree(d.pose_saved);   // (a snapshot of the old structure's values)
+  d.pose_saved = nullptr;
+  std::vector<double4> hz(nij.size());
+  std::vector<double2> hom(3 * nij.size());
+  for (size_t q = 0; q < nij.size(); q++) {
+    const int e = nd[q];
+    const double th = g->ez[3 * e + 2];
+    hz[q] = make_double4(g->ez[3 * e], g->ez[3 * e + 1], std::cos(th), std::sin(th));
+    const double* o = &g->eom[6 * (size_t)e];
+    hom[3 * q] = make_double2(o[0], o[1]);
+    hom[3 * q + 1] = make_double2(o[2], o[3]);
+    hom[3 * q + 2] = make_double2(o[4], o[5]);
+  }
+  RC_TRY(h2d(g, d.eij + ne_old, nij.data(), nij.size()));
+  RC_TRY(h2d(g, d.ez + ne_old, hz.data(), hz.size()));
+  RC_TRY(h2d(g, d.eom + 3 * (size_t)ne_old, hom.data(), hom.size()));
+  RC_TRY(h2d(g, d.prior_ptr, H.prior_ptr.data(), n + 1));
+  RC_TRY(h2d(g, d.row_ptr, H.row_ptr.data(), n + 1));
+  RC_TRY(h2d(g, d.slot_edge, H.slot_edge.data(), ns));
+  RC_TRY(h2d(g, d.slot_col, H.slot_col.data(), ns));
+  RC_TRY(h2d(g, d.erow, erow.data(), n + 1));
+  RC_TRY(h2d(g, d.s1_ptr, s1_ptr.data(), n + 1));
+  RC_TRY(h2d(g, d.s1pos, s1pos.data(), ne));
+  RC_TRY(h2d(g, d.Dc, g->h_Dc.data(), 6 * (size_t)n));
+  RC_TRY(h2d(g, d.brow, brow.data(), brow.size()));
+  d.n = n;
+  d.ne = ne;
+  d.nslots = ns;
+  d.nlb = (int)brow.size() - 1;
+  const double mean_deg = n ? (double)ns / n : 0.0;
+  d.G = 4;
+  while (d.G < 32 && d.G < mean_deg) d.G *= 2;
+  d.G1 = 4;
+  while (d.G1 < 32 && d.G1 < (n ? (double)ne / n : 0.0)) d.G1 *= 2;
+  HIP_TRY(g, hipStreamSynchronize(d.stream));
+  g->dev_structure = true;
+  g->last_upload = 2;
+  if (g->chol_ready) g->plan_stale = true;   // ensure_chol decides what to keep
+  // the new vertices' values (the resident ones stay bit for bit, unless the
+  // caller set values since: then all of them)
+  return upload_values(g, g->dev_values ? n_old : 0);
+}
+
 int ensure_device(pgo_graph* g) {
-  if (!g->dev_structure) RC_TRY(upload_structure(g));
+  if (!g->dev_structure) {
+    const int rc = append_structure(g);
+    if (rc == 1) RC_TRY(upload_structure(g));
+    else if (rc != PGO_OK) return rc;
+  }
   else if (!g->dev_values) RC_TRY(upload_values(g));
   return PGO_OK;
 }
@@ -704,7 +912,11 @@ int ensure_chol(pgo_graph* g) {
   g->hook.group = exchange_group;
   pgo::chol_analyze(g->chol, g->d.n, g->h_row_ptr, g->h_slot_col);
   if (g->chol.schedule_error) return fail(g, PGO_E_HIP, "internal: inconsistent panel schedule");
+  const auto tb = std::chrono::steady_clock::now();
   RC_TRY(bind_plan(g, true));
+  if (getenv("PGO_PLAN_TIMING"))
+    fprintf(stderr, "ensure_chol bind_plan %8.2f ms\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count());
   g->chol_ready = true;
   timed(order_in.empty() ? 3 : 2);
   return PGO_OK;
@@ -737,7 +949,7 @@ int bind_plan(pgo_graph* g, bool full) {
       return fail(g, e == hipErrorOutOfMemory ? PGO_E_NOMEM : PGO_E_HIP,
                   std::string("Cholesky plan upload: ") + hipGetErrorString(e));
     }
-    if (!g->d.eside) RC_TRY(dev_alloc(g, &g->d.eside, g->d.ne));
+    if (!g->d.eside) RC_TRY(dev_alloc(g, &g->d.eside, std::max<size_t>(g->cap_ne, g->d.ne)));
     RC_TRY(h2d(g, g->d.eside, eside.data(), eside.size()));
     if (!slot_edge.empty())
       HIP_TRY(g, hipMemcpyAsync(g->d.slot_edge, slot_edge.data(), slot_edge.size() * sizeof(int),
@@ -956,7 +1168,10 @@ int ensure_lanes(pgo_graph* g, int want) {
   for (int l = 1; l < want && ok; l++) {
     g->lanes.emplace_back();
     Lane& ln = g->lanes.back();
-    ok = hipMalloc((void**)&ln.pose_cand, sizeof(double4) * std::max(d.n, 1)) == hipSuccess &&
+    // (capacity, not n: an accepted lane's buffer becomes the handle's pose
+    // array, which appended vertices extend in place)
+    ok = hipMalloc((void**)&ln.pose_cand, sizeof(double4) * std::max<size_t>({g->cap_n, (size_t)d.n, 1})) ==
+             hipSuccess &&
          hipMalloc((void**)&ln.part, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices) == hipSuccess &&
          hipMalloc((void**)&ln.scal, sizeof(double) * 16) == hipSuccess &&
          hipMemsetAsync(ln.part, 0, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices, d.stream) == hipSuccess;
@@ -1282,7 +1497,7 @@ int pgo_save_values(pgo_graph* g) {
   if (!g) return PGO_E_ARG;
   RC_TRY(ensure_device(g));
   DevGraph& d = g->d;
-  if (!d.pose_saved) RC_TRY(dev_alloc(g, &d.pose_saved, d.n));
+  if (!d.pose_saved) RC_TRY(dev_alloc(g, &d.pose_saved, std::max<size_t>(g->cap_n, d.n)));
   if (d.n)
     HIP_TRY(g, hipMemcpyAsync(d.pose_saved, d.pose, d.n * sizeof(double4), hipMemcpyDeviceToDevice, d.stream));
   HIP_TRY(g, hipStreamSynchronize(d.stream));
@@ -1362,9 +1577,11 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
     const double row[kTraceCols] = {it, lam_t, solved, lin_change, new_e, fid, acc, since_T0()};
     g->trace.insert(g->trace.end(), row, row + kTraceCols);
   };
+  g->last_upload = 0;
   int rc = ensure_device(g);
   if (rc != PGO_OK) return rc;
   st.ms_upload = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - upload0).count();
+  st.upload_kind = g->last_upload;
   DevGraph& d = g->d;
   HIP_TRY(g, hipSetDevice(g->device));
   double err = 0.0;

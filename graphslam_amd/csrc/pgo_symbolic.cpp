@@ -1,6 +1,7 @@
 // Host-side symbolic analysis for the GPU supernodal Cholesky (pgo_chol.h).
 // Runs once per graph structure (GTSAM recomputes COLAMD every solve).
 #include <algorithm>
+#include <chrono>
 #include <tuple>
 #include <cmath>
 #include <cstdlib>
@@ -208,6 +209,15 @@ std::vector<double> distributed_rank_flops(const CholPlan& P, int size, double* 
 }
 
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
+  // PGO_PLAN_TIMING: phase times of the analysis on stderr (diagnostics)
+  static const bool timing = getenv("PGO_PLAN_TIMING") != nullptr;
+  auto tlast = std::chrono::steady_clock::now();
+  auto phase = [&](const char* what) {
+    if (!timing) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "chol_analyze %-12s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - tlast).count());
+    tlast = t;
+  };
   P.nslots = (long long)slot_col.size();
   P.n = n;
   // ---- pose adjacency (old index), unique, no self loops
@@ -233,6 +243,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
                                   : P.ordering == kOrderAmd ? order_amd(n, xadj, adj) : order_nd(n, xadj, adj);
   std::vector<int> ip0(n);
   for (int k = 0; k < n; k++) ip0[order0[k]] = k;
+  phase("ordering");
   // ---- elimination tree of the permuted pattern (Liu, path compression)
   std::vector<int> et(n, -1), anc(n, -1);
   for (int j = 0; j < n; j++) {
@@ -251,6 +262,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
       }
     }
   }
+  phase("etree");
   // ---- postorder (children in increasing order)
   std::vector<int> chead(n, -1), cnext(n, -1), post;
   post.reserve(n);
@@ -286,6 +298,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   }
   for (int k = 0; k < n; k++) P.iperm[P.perm[k]] = k;
   for (int k = 0; k < n; k++) par[k] = et[post[k]] >= 0 ? pos[et[post[k]]] : -1;
+  phase("postorder");
   // ---- column counts (off-diagonal pose rows) via row subtrees
   std::vector<int> cc(n, 0), mark(n, -1), nch(n, 0);
   for (int i = 0; i < n; i++) {
@@ -303,6 +316,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   }
   for (int j = 0; j < n; j++)
     if (par[j] >= 0) nch[par[j]]++;
+  phase("colcounts");
   // ---- fundamental supernodes, then relaxed amalgamation of a child that
   // immediately precedes its parent when it adds few explicit zeros
   std::vector<int> fs;
@@ -361,6 +375,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     for (int s = 0; s < ns; s++)
       if (P.parent[s] >= 0) P.children[f[P.parent[s]]++] = s;
   }
+  phase("supernodes");
   // ---- front rows: own poses then sorted below rows (A's pattern + children's rows)
   std::vector<std::vector<int>> below(ns);
   std::fill(mark.begin(), mark.end(), -1);
@@ -423,6 +438,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     const auto& b = below[s];
     return (l - f) + (int)(std::lower_bound(b.begin(), b.end(), i) - b.begin());
   };
+  phase("frontrows");
   // ---- extend-add maps: each below row of s -> local pose index in parent's front
   P.ea_ptr.assign(ns + 1, 0);
   for (int s = 0; s < ns; s++) P.ea_ptr[s + 1] = P.ea_ptr[s] + (int)below[s].size();
@@ -492,6 +508,7 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   }
   P.xmax = *std::max_element(P.xsize.begin(), P.xsize.end());
   P.xsol_max = *std::max_element(P.xsol_size.begin(), P.xsol_size.end());
+  phase("partition");
   // ---- level schedules: phase 1 (this rank's subtree fronts) then phase 2 (top)
   std::vector<std::vector<int>> bylevel;
   for (int phase = 0; phase < 2; phase++) {
@@ -971,7 +988,9 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
         }
     }
   }
+  phase("schedule");
   chol_assembly(P, row_ptr, slot_col);
+  phase("assembly");
 }
 
 // Assembly of H into the plan's fronts (k_assemble_tile's H entries): the
@@ -983,92 +1002,142 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
 void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
   const int n = P.n, ns = P.ns;
   P.nslots = (long long)slot_col.size();
-  auto local_of = [&](int s, int i) {  // local pose index of new pose i in front s (rows: own, then below)
-    const int f = P.sfirst[s], l = P.sfirst[s + 1];
-    if (i < l) return i - f;
-    const int* b0 = P.rows.data() + P.rptr[s] + (l - f);
-    const int* b1 = P.rows.data() + P.rptr[s + 1];
-    return (l - f) + (int)(std::lower_bound(b0, b1, i) - b0);
-  };
-  struct Ent {
-    int j, i, k;
-  };
-  std::vector<Ent> ents;
-  ents.reserve(slot_col.size() / 2 + 1);
+  // entries (j, i, k) of the permuted lower triangle (new indices i > j, slot
+  // k), ordered by (j, i, k): a counting sort by j (slot order within a
+  // bucket), then each bucket -- a column's few blocks -- by (i, k)
+  std::vector<int> jcnt(n + 1, 0);
   for (int r = 0; r < n; r++) {
     const int i = P.iperm[r];
     for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) {
       const int j = P.iperm[slot_col[k]];
-      if (i > j) ents.push_back({j, i, k});
+      if (i > j) jcnt[j + 1]++;
     }
   }
-  std::sort(ents.begin(), ents.end(), [&](const Ent& a, const Ent& b) {
-    return a.j != b.j ? a.j < b.j : (a.i != b.i ? a.i < b.i : a.k < b.k);
-  });
+  for (int j = 0; j < n; j++) jcnt[j + 1] += jcnt[j];
+  std::vector<int2> eik(jcnt[n]);   // (i, k) per entry, bucketed by j
+  {
+    std::vector<int> fill(jcnt.begin(), jcnt.end() - 1);
+    for (int r = 0; r < n; r++) {
+      const int i = P.iperm[r];
+      for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) {
+        const int j = P.iperm[slot_col[k]];
+        if (i > j) eik[fill[j]++] = make_int2(i, k);
+      }
+    }
+  }
+  for (int j = 0; j < n; j++)
+    std::sort(eik.begin() + jcnt[j], eik.begin() + jcnt[j + 1],
+              [](const int2& a, const int2& b) { return a.x != b.x ? a.x < b.x : a.y < b.y; });
   P.asm_front.clear();
   P.asm_li.clear();
   P.asm_lj.clear();
   P.asm_ptr.assign(1, 0);
   P.asm_src.clear();
-  for (size_t t = 0; t < ents.size(); t++) {
-    if (t == 0 || ents[t].i != ents[t - 1].i || ents[t].j != ents[t - 1].j) {
-      if (t) P.asm_ptr.push_back((int)P.asm_src.size());
-      const int s = P.dg_front[ents[t].j];
-      P.asm_front.push_back(s);
-      P.asm_lj.push_back(ents[t].j - P.sfirst[s]);
-      P.asm_li.push_back(local_of(s, ents[t].i));
+  P.asm_src.reserve(eik.size());
+  for (int j = 0; j < n; j++) {
+    const int s = P.dg_front[j], f = P.sfirst[s], l = P.sfirst[s + 1];
+    const int* b0 = P.rows.data() + P.rptr[s] + (l - f);
+    const int* b1 = P.rows.data() + P.rptr[s + 1];
+    const int* cur = b0;   // the bucket's rows come in increasing order: a forward scan finds them
+    for (int q = jcnt[j]; q < jcnt[j + 1]; q++) {
+      const int i = eik[q].x;
+      if (q == jcnt[j] || i != eik[q - 1].x) {
+        if (!P.asm_front.empty()) P.asm_ptr.push_back((int)P.asm_src.size());
+        P.asm_front.push_back(s);
+        P.asm_lj.push_back(j - f);
+        int li;
+        if (i < l) {
+          li = i - f;
+        } else {
+          cur = std::lower_bound(cur, b1, i);
+          li = (l - f) + (int)(cur - b0);
+        }
+        P.asm_li.push_back(li);
+      }
+      P.asm_src.push_back(eik[q].y);
     }
-    P.asm_src.push_back(ents[t].k);
   }
   P.asm_ptr.push_back((int)P.asm_src.size());
-  if (ents.empty()) P.asm_ptr.assign(1, 0);
+  if (P.asm_front.empty()) P.asm_ptr.assign(1, 0);
   // H entries by front tile: every 64x64 lower tile of a front lists the 3x3
   // blocks of H (off-diagonal targets t >= 0, diagonal blocks ~pose) with an
-  // element in it (a block can straddle tile boundaries)
-  std::vector<std::vector<std::pair<int, int>>> hitems(ns);   // per front: (tile, item)
-  auto add_item = [&](int sf, int r0, int c0, int item) {
+  // element in it (a block can straddle tile boundaries); items of a tile in
+  // the order they are added (off-diagonal targets, then diagonal blocks) --
+  // a counting sort by (front, tile key)
+  std::vector<long long> tbase(ns + 1, 0);   // first tile key slot of each front
+  for (int s2 = 0; s2 < ns; s2++) {
+    const long long nt = (P.m[s2] + 63) / 64;
+    tbase[s2 + 1] = tbase[s2] + nt * (nt + 1) / 2;
+  }
+  std::vector<int> tcnt(tbase[ns] + 1, 0);
+  auto for_item = [&](int sf, int r0, int c0, auto&& fn) {
     for (int ti = r0 / 64; ti <= (r0 + 2) / 64; ti++)
       for (int tj = c0 / 64; tj <= (c0 + 2) / 64; tj++)
-        if (ti >= tj) hitems[sf].emplace_back(ti * (ti + 1) / 2 + tj, item);
+        if (ti >= tj) fn(tbase[sf] + ti * (ti + 1) / 2 + tj);
   };
-  for (size_t t = 0; t < P.asm_front.size(); t++) add_item(P.asm_front[t], 3 * P.asm_li[t], 3 * P.asm_lj[t], (int)t);
-  for (int j = 0; j < n; j++) add_item(P.dg_front[j], 3 * P.dg_loc[j], 3 * P.dg_loc[j], ~j);
-  for (auto& v : hitems) std::stable_sort(v.begin(), v.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
-    return a.first < b.first;
-  });
+  for (size_t t = 0; t < P.asm_front.size(); t++)
+    for_item(P.asm_front[t], 3 * P.asm_li[t], 3 * P.asm_lj[t], [&](long long key) { tcnt[key + 1]++; });
+  for (int j = 0; j < n; j++)
+    for_item(P.dg_front[j], 3 * P.dg_loc[j], 3 * P.dg_loc[j], [&](long long key) { tcnt[key + 1]++; });
+  for (size_t q = 0; q + 1 < tcnt.size(); q++) tcnt[q + 1] += tcnt[q];
+  std::vector<int> titems(tcnt.back());
+  {
+    std::vector<int> fill(tcnt.begin(), tcnt.end() - 1);
+    for (size_t t = 0; t < P.asm_front.size(); t++)
+      for_item(P.asm_front[t], 3 * P.asm_li[t], 3 * P.asm_lj[t], [&](long long key) { titems[fill[key]++] = (int)t; });
+    for (int j = 0; j < n; j++)
+      for_item(P.dg_front[j], 3 * P.dg_loc[j], 3 * P.dg_loc[j], [&](long long key) { titems[fill[key]++] = ~j; });
+  }
   P.at_items.clear();
+  P.at_items.reserve(titems.size());
   P.at_iptr.assign(P.ea_tasks.size(), make_int2(0, 0));
-  std::vector<size_t> hq(ns, 0);
-  for (size_t q = 0; q < P.ea_tasks.size(); q++) {   // a front's tile tasks come in key order
+  for (size_t q = 0; q < P.ea_tasks.size(); q++) {
     const int4 t = P.ea_tasks[q];
-    const int ti = t.y >> 16, tj = t.y & 0xffff, key = ti * (ti + 1) / 2 + tj;
-    const auto& hv = hitems[t.x];
-    size_t& h = hq[t.x];
+    const int ti = t.y >> 16, tj = t.y & 0xffff;
+    const long long key = tbase[t.x] + ti * (ti + 1) / 2 + tj;
     const int i0 = (int)P.at_items.size();
-    while (h < hv.size() && hv[h].first < key) h++;
-    while (h < hv.size() && hv[h].first == key) P.at_items.push_back(hv[h++].second);
+    P.at_items.insert(P.at_items.end(), titems.begin() + tcnt[key], titems.begin() + tcnt[key + 1]);
     P.at_iptr[q] = make_int2(i0, (int)P.at_items.size() - i0);
   }
+  static const bool timing = getenv("PGO_PLAN_TIMING") != nullptr;
+  const auto ta = std::chrono::steady_clock::now();
+  // sum_{t=A..B} clamp(t, 0, c) in closed form (G(x) = sum_{t=1..x} min(t, c))
+  auto G = [](long long x, long long c) -> long long {
+    if (x <= 0) return 0;
+    return x <= c ? x * (x + 1) / 2 : c * (c + 1) / 2 + (x - c) * c;
+  };
   for (CholLevel& lv : P.levels) {   // algorithmic bytes of the levels' k_assemble_tile (profiles)
     lv.at_bytes = 0;
     for (int q = lv.ea_off[0]; q < lv.ea_off[0] + lv.ea_cnt[0]; q++) {
       const int4 t = P.ea_tasks[q];
       double e = 0, h = 0;   // children's elements read + tile elements written; H slots read
-      for (int k = 0; k < t.w; k++) {
+      for (int k = 0; k < t.w; k++) {   // rows r < nr of a child rectangle: min(max(a0 + r - b0 + 1, 0), nc) columns
         const int4 pr = P.ea_pairs[t.z + k];
-        const int nr = pr.w & 0xff, ncl = pr.w >> 8;
-        for (int r = 0; r < nr; r++) e += std::min(std::max(pr.y + r - pr.z + 1, 0), ncl);
+        const long long nr = pr.w & 0xff, ncl = pr.w >> 8, d = pr.y - pr.z + 1;
+        e += (double)(G(d + nr - 1, ncl) - G(d - 1, ncl));
       }
       const int2 it = P.at_iptr[q];
       for (int k = 0; k < it.y; k++) {
         const int code = P.at_items[it.x + k];
         h += code >= 0 ? 72.0 * (P.asm_ptr[code + 1] - P.asm_ptr[code]) : 48.0;
       }
-      const int mp = P.m[t.x], R0 = 64 * (t.y >> 16), C0 = 64 * (t.y & 0xffff);
-      for (int j = C0; j < std::min(C0 + 64, mp); j++) e += std::max(0, std::min(R0 + 64, mp) - std::max(R0, j));
+      const long long mp = P.m[t.x], R0 = 64 * (t.y >> 16), C0 = 64 * (t.y & 0xffff);
+      const long long R1 = std::min(R0 + 64, mp), C1 = std::min(C0 + 64, mp);
+      // tile elements: columns j in [C0, C1), rows [max(R0, j), R1)
+      const long long jd = std::min(std::max(R0, C0), C1);   // columns below jd see all R1 - R0 rows
+      e += (double)((jd - C0) * std::max(0LL, R1 - R0));
+      for (long long a = std::max(jd, C0); a < C1; a++) e += (double)std::max(0LL, R1 - a);
       lv.at_bytes += 8.0 * e + h;
     }
   }
+  if (timing) {
+    double tot = 0;
+    for (const CholLevel& lv : P.levels) tot += lv.at_bytes;
+    fprintf(stderr, "chol_assembly at_bytes total %.0f\n", tot);
+  }
+  if (timing)
+    fprintf(stderr, "chol_assembly at_bytes %8.2f ms\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count());
 }
 
 // Does the plan's factor structure hold every block of the pattern (old pose

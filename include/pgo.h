@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PGO_ABI_VERSION 4
+#define PGO_ABI_VERSION 5
 
 /* ---- status codes (GTSAM exception each one replaces) -------------------- */
 #define PGO_OK 0
@@ -171,6 +171,10 @@ typedef struct {
      3 full analysis (first call, or too much appended); ms_plan its host+upload ms */
   int plan_update;
   double ms_plan;
+  /* how the device graph was brought up to date on this call: 0 resident, 1
+     full upload, 2 appended in place (new keyframes / factors after the
+     previous ones: the live re-solve); its host+upload time is ms_upload */
+  int upload_kind;
 } pgo_stats;
 
 /* pgo_stats.stop_reason.  GTSAM reports every one of these as convergence

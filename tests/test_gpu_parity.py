@@ -641,6 +641,50 @@ def test_incremental_append_matches_oracle(pg_cls, oracle_lib, n_new):
     assert_poses(pg.poses(), ref.poses, 1e-6, 1e-7)
 
 
+def _registrations(pg_cls, g, k, seed=7, lanes=1):
+    """The live node's per-registration re-solve on one handle: k times a new
+    keyframe (dead-reckoned), its odometry factor and one loop closure to an
+    earlier keyframe, then optimize; returns the stats and the final values."""
+    from graphslam_amd.datasets import between_xyt, compose_xyt
+    pg = pg_cls.from_dataset(g)
+    pg.optimize(lambda_lanes=lanes)
+    rng = np.random.default_rng(seed)
+    n = g.num_poses
+    gt = np.array(g.ground_truth)
+    x = pg.poses()
+    cov = np.diag(datasets.SIGMA ** 2)
+    sts = []
+    for r in range(k):
+        v = n + r
+        step = np.array([1.0, 0.0, 0.0])
+        gt = np.vstack([gt, compose_xyt(gt[v - 1], step)])
+        x = np.vstack([x, compose_xyt(x[v - 1], step)])
+        j = int(rng.integers(0, v - 20))
+        pg.add_vertex(v + 1, *x[v])
+        pg.add_edge(v, v + 1, between_xyt(gt[v - 1], gt[v]), cov)
+        pg.add_edge(v + 1, j + 1, between_xyt(gt[v], gt[j]), cov)
+        sts.append(pg.optimize(lambda_lanes=lanes))
+    return sts, pg.poses()
+
+
+@pytest.mark.parametrize("lanes", [1, 3])
+def test_append_in_place_matches_full_upload(pg_cls, monkeypatch, lanes):
+    """A registration's keyframe, odometry and loop closure are appended to the
+    device graph in place (pgo_stats.upload_kind 2: only the new factors, the
+    per-row arrays and the slots uploaded) -- bitwise the same optimisations as
+    the full re-upload of the grown graph (PGO_NO_APPEND=1, upload_kind 1)."""
+    g = datasets.make("C2")
+    monkeypatch.delenv("PGO_NO_APPEND", raising=False)
+    a, xa = _registrations(pg_cls, g, 3, lanes=lanes)
+    monkeypatch.setenv("PGO_NO_APPEND", "1")
+    b, xb = _registrations(pg_cls, g, 3, lanes=lanes)
+    assert [s["upload_kind"] for s in a] == [2, 2, 2] and [s["upload_kind"] for s in b] == [1, 1, 1]
+    for sa, sb in zip(a, b):
+        assert sa["plan_update"] == sb["plan_update"] and sa["iterations"] == sb["iterations"]
+        assert sa["inner_iterations"] == sb["inner_iterations"] and sa["final_error"] == sb["final_error"]
+    np.testing.assert_array_equal(xa, xb)
+
+
 def test_incremental_loop_closure_inside_fill_keeps_plan(pg_cls):
     """A loop closure parallel to an existing factor changes no fill: the plan's
     fronts are kept (plan_update 1), only its H assembly is rebuilt; the values
