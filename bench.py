@@ -236,16 +236,18 @@ def factor_roofline(kprof, totals, factor_flops):
     return out
 
 
-def live_resolve_bench(pg, g, k=5):
+def live_resolve_bench(pg, g, k=5, params=None):
     """The live node's per-registration re-solve (graph.cpp:180-200, :130):
     starting at the optimum, k registrations, each appending one keyframe
     (dead-reckoned initial value), its odometry factor and one loop closure
     to an earlier keyframe (exact measurements), then optimize() on the same
     handle -- the resident values, graph and solver plan are refreshed in place
     (pgo_stats.plan_update).  Reports wall ms per registration (append +
-    optimize) and the plan work."""
+    optimize) and the plan work; `params` are the headline run's (lambda lanes,
+    graphs)."""
     import numpy as np
     from graphslam_amd.datasets import between_xyt, compose_xyt
+    from graphslam_amd import _lib
     rng = np.random.default_rng(7)
     n = g.num_poses
     gt = np.array(g.ground_truth)
@@ -262,11 +264,13 @@ def live_resolve_bench(pg, g, k=5):
         pg.add_vertex(v + 1, *x[v])
         pg.add_edge(v, v + 1, between_xyt(gt[v - 1], gt[v]), cov)
         pg.add_edge(v + 1, j + 1, between_xyt(gt[v], gt[j]), cov)
-        st = pg.optimize()
+        st = pg.optimize(params)
         rows.append({"ms": 1e3 * (time.perf_counter() - t0), "plan_update": st["plan_update"],
                      "upload_kind": st["upload_kind"],
                      "ms_plan": st["ms_plan"], "ms_upload": st["ms_upload"], "linearizations": st["linearizations"],
-                     "lm_tries": st["inner_iterations"]})
+                     "lm_tries": st["inner_iterations"], "initial_error": st["initial_error"],
+                     "final_error": st["final_error"],
+                     "stop_reason": _lib.STOP_REASONS.get(st["stop_reason"], str(st["stop_reason"]))})
     return {"registrations": k, "ms_median": float(np.median([r["ms"] for r in rows])), "per_registration": rows,
             "note": "append 1 keyframe + odometry + 1 loop closure, then optimize on the same handle"}
 
@@ -584,7 +588,7 @@ def main():
     live = None
     if args.live and rank == 0 and not spec:
         log("live re-solve line")
-        live = live_resolve_bench(pg, g, args.live)
+        live = live_resolve_bench(pg, g, args.live, params)
     stats = [s for _, s in results]
     last = stats[-1]
     ps = prof_stats

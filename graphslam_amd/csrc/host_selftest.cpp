@@ -138,6 +138,64 @@ int check_distributed(const Pattern& G, int ordering, int size) {
   return 0;
 }
 
+// the pattern restricted to poses [0, n)
+Pattern restrict_pattern(const Pattern& G, int n) {
+  Pattern R;
+  R.n = n;
+  R.row_ptr.assign(1, 0);
+  for (int i = 0; i < n; i++) {
+    for (int k = G.row_ptr[i]; k < G.row_ptr[i + 1]; k++)
+      if (G.col[k] < n) R.col.push_back(G.col[k]);
+    R.row_ptr.push_back((int)R.col.size());
+  }
+  return R;
+}
+
+// The incremental symbolic update (chol_append): poses appended one at a time
+// to a plan of the first n0 poses.  After each: the schedule is consistent,
+// every front's below rows sit in its parent at the extend-add map's index, the
+// sizes match the row lists, and the structure holds the exact fill of the
+// plan's own ordering (a fresh analysis on P.perm) and the whole pattern.
+int check_append(const Pattern& G, int n0, int ordering) {
+  pgo::CholPlan P;
+  P.ordering = ordering;
+  const Pattern B = restrict_pattern(G, n0);
+  pgo::chol_analyze(P, n0, B.row_ptr, B.col);
+  for (int n = n0 + 1; n <= G.n; n++) {
+    const Pattern Gn = restrict_pattern(G, n);
+    std::vector<int2> pairs;
+    for (int k = Gn.row_ptr[n - 1]; k < Gn.row_ptr[n]; k++) pairs.push_back(make_int2(n - 1, Gn.col[k]));
+    if (!pgo::chol_append(P, n, Gn.row_ptr, Gn.col, pairs, 1 << 30, 1e30)) return fail("append: refused");
+    if (P.schedule_error) return fail("append: panel schedule bookkeeping");
+    if (P.n != n || !pgo::chol_covers(P, n, Gn.row_ptr, Gn.col)) return fail("append: pattern not covered");
+    for (int s = 0; s < P.ns; s++) {
+      const int wp = P.sfirst[s + 1] - P.sfirst[s], nr = P.rptr[s + 1] - P.rptr[s];
+      if (P.m[s] != 3 * nr || P.w[s] != 3 * wp || P.ea_ptr[s + 1] - P.ea_ptr[s] != nr - wp)
+        return fail("append: front sizes");
+      const int p = P.parent[s];
+      for (int t = 0; t < nr - wp; t++) {
+        const int r = P.rows[P.rptr[s] + wp + t];
+        if (t > 0 && r <= P.rows[P.rptr[s] + wp + t - 1]) return fail("append: rows unsorted");
+        if (p < 0 || P.rows[P.rptr[p] + P.ea_rel[P.ea_ptr[s] + t]] != r) return fail("append: extend-add map");
+      }
+    }
+    pgo::CholPlan Q;
+    Q.order_in = P.perm;
+    pgo::chol_analyze(Q, n, Gn.row_ptr, Gn.col);
+    for (int q = 0; q < Q.ns; q++)
+      for (int a = Q.rptr[q]; a < Q.rptr[q + 1]; a++)
+        for (int j = Q.sfirst[q]; j < Q.sfirst[q + 1]; j++) {
+          const int i = Q.rows[a];
+          if (i > j) {
+            std::vector<int2> one{make_int2(Q.perm[i], Q.perm[j])};
+            if (!pgo::chol_covers(P, one)) return fail("append: fill of the ordering not covered");
+          }
+        }
+  }
+  std::printf("append: %d poses onto %d, %d fronts, flops %.3g\n", G.n - n0, n0, P.ns, P.flops);
+  return 0;
+}
+
 }  // namespace
 
 int main() {
@@ -178,6 +236,8 @@ int main() {
     for (int k = 0; k < G3.n; k++) R.order_in[k] = G3.n - 1 - k;
     pgo::chol_analyze(R, G3.n, G3.row_ptr, G3.col);
     if (!pgo::chol_covers(R, G3.n, G3.row_ptr, G3.col) || R.schedule_error) return fail("given ordering");
+    // appended poses: the incremental symbolic update
+    if (check_append(make_pattern(1500, 200, 9), 1490, ordering)) return 1;
   }
   {   // a 2-D grid of poses: nested dissection gives big separator fronts (many
       // panels, kKB block boundaries, partial last panels) -- the look-ahead

@@ -16,6 +16,7 @@
 #include <memory>
 #include <string>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -81,6 +82,7 @@ struct pgo_graph {
   int ordering = pgo::kOrderNd;             // fill-reducing ordering (pgo_opts.ordering)
   int part_size = 1;                        // subtree partition the plan must have (PGO_MULTI_PARTITION)
   bool plan_stale = false;                  // the graph changed since the plan was built (kept, see ensure_chol)
+  size_t plan_edges = 0;                    // between factors (user order) the plan holds: later ones are new
   int plan_update = 0;                      // how the last ensure_chol refreshed it (pgo_stats.plan_update)
   double plan_ms = 0.0;
   pgo::ExchangeHook hook;                   // the partitioned factorisation's all-gathers (comm)
@@ -103,6 +105,7 @@ struct pgo_graph {
   pgo::Comm comm;
   std::vector<Lane> lanes;                  // lanes 1..L-1 (speculative tries on this GPU)
   double* xb = nullptr;                     // [L x 3n] solutions of a batched factor + solve
+  size_t xb_n = 0;                          // ... allocated for this many vertices (capacity)
   double* h_lanes = nullptr;                // pinned [48]: 4 scalars per lane, lambdas at 32, flags at 40
   hipEvent_t lin_done = nullptr;            // linearisation complete
   int lane_cap = 8;                         // 1 after a lane allocation failed (reset per plan)
@@ -304,7 +307,8 @@ int upload_values(pgo_graph* g, size_t first = 0) {
 // Device pose -> host values (Values::at<Pose2>(k).x()/y()/theta(), graph.cpp:123-125)
 int download_values(pgo_graph* g) {
   if (g->host_values) return PGO_OK;
-  const size_t n = g->keys.size();
+  // the device-resident vertices (vertices appended since keep their host values)
+  const size_t n = std::min(g->keys.size(), (size_t)g->d.n);
   std::vector<double4> h(n);
   if (n) {
     HIP_TRY(g, hipMemcpyAsync(h.data(), g->d.pose, n * sizeof(double4), hipMemcpyDeviceToHost, g->d.stream));
@@ -606,7 +610,35 @@ int upload_structure(pgo_graph* g) {
 // structure is updated in step (block-CSR rows merged, side-1 lists, row
 // blocks); only the new factors, the per-row arrays and the slot arrays are
 // uploaded.  Returns 1 when the full upload must run instead.
+// fn(begin, end) over contiguous chunks of [0, n) on up to 16 host threads
+// (the live re-solve's per-registration host work; chunk results independent)
+template <class F>
+void host_parallel(int n, F&& fn) {
+  static const int hw = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+  const int nth = std::max(1, std::min(hw, n / 16384));
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nth; t++)
+    pool.emplace_back([&fn, t, n, nth] { fn((int)((long long)n * t / nth), (int)((long long)n * (t + 1) / nth)); });
+  fn(0, (int)((long long)n / nth));
+  for (auto& th : pool) th.join();
+}
+
+// PGO_PLAN_TIMING: phase times of the plan / append paths on stderr
+struct PhaseTimer {
+  const char* who;
+  bool on = getenv("PGO_PLAN_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  explicit PhaseTimer(const char* w) : who(w) {}
+  void operator()(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "%s %-14s %8.2f ms\n", who, what, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
+
 int append_structure(pgo_graph* g) {
+  PhaseTimer phase("append_structure");
   DevGraph& d = g->d;
   HostStructure& H = g->hs;
   const int n_old = d.n, ne_old = d.ne;
@@ -642,7 +674,7 @@ int append_structure(pgo_graph* g) {
     const int2 last = H.eij.back(), f = nij.front();
     if (f.x < last.x || (f.x == last.x && f.y < last.y)) return 1;   // not an append in device order
   }
-  RC_TRY(download_values(g));
+  phase("resolve");
   // host structure: device order, block-CSR rows (every row sorted by (column,
   // code) as build_structure sorts them, codes in their pre-plan form)
   H.eij.insert(H.eij.end(), nij.begin(), nij.end());
@@ -655,31 +687,50 @@ int append_structure(pgo_graph* g) {
   const int ns = 2 * ne;
   std::vector<int> rp(n + 1, 0), sc(ns), se(ns);
   for (int i = 0; i < n; i++) rp[i + 1] = rp[i] + (i < n_old ? H.row_ptr[i + 1] - H.row_ptr[i] : 0) + add[i];
-  std::vector<std::vector<std::pair<int, int>>> extra(n);
+  // the new slots (row, column, code), by row then (column, code): merged
+  // into the old rows (sorted by (column, code), as build_structure sorts them)
+  std::vector<int3> extra;
+  extra.reserve(2 * nij.size());
   for (size_t q = 0; q < nij.size(); q++) {
     const int de = ne_old + (int)q;
-    extra[nij[q].x].emplace_back(nij[q].y, (de << 2) | 2);
-    extra[nij[q].y].emplace_back(nij[q].x, (de << 2) | 1);
+    extra.push_back(make_int3(nij[q].x, nij[q].y, (de << 2) | 2));
+    extra.push_back(make_int3(nij[q].y, nij[q].x, (de << 2) | 1));
   }
-  for (int i = 0; i < n; i++) {
+  std::sort(extra.begin(), extra.end(), [](const int3& a, const int3& b) {
+    return a.x != b.x ? a.x < b.x : a.y != b.y ? a.y < b.y : a.z < b.z;
+  });
+  int prev = 0;   // rows [prev, r) copied whole (H.slot_edge holds pre-plan codes)
+  auto copy_rows = [&](int r) {
+    if (prev >= n_old) return;
+    const int b = H.row_ptr[prev], e0 = H.row_ptr[std::min(r, n_old)];
+    if (e0 > b) {
+      std::copy(H.slot_col.begin() + b, H.slot_col.begin() + e0, sc.begin() + rp[prev]);
+      std::copy(H.slot_edge.begin() + b, H.slot_edge.begin() + e0, se.begin() + rp[prev]);
+    }
+  };
+  for (size_t q = 0; q < extra.size();) {
+    const int i = extra[q].x;
+    size_t q1 = q;
+    while (q1 < extra.size() && extra[q1].x == i) q1++;
+    copy_rows(i);
     const int b = i < n_old ? H.row_ptr[i] : 0, e0 = i < n_old ? H.row_ptr[i + 1] : 0;
-    int o = rp[i];
-    if (!add[i]) {
-      for (int k = b; k < e0; k++, o++) {
+    int o = rp[i], k = b;
+    for (size_t t = q; t < q1; t++) {   // merge: old slots before an equal (column, code) stay first
+      while (k < e0 && (H.slot_col[k] < extra[t].y || (H.slot_col[k] == extra[t].y && H.slot_edge[k] <= extra[t].z))) {
         sc[o] = H.slot_col[k];
-        se[o] = ((H.slot_edge[k] >> 2) << 2) | ((H.slot_edge[k] & 1) ? 1 : 2);
+        se[o++] = H.slot_edge[k++];
       }
-      continue;
+      sc[o] = extra[t].y;
+      se[o++] = extra[t].z;
     }
-    std::vector<std::pair<int, int>> t;
-    for (int k = b; k < e0; k++) t.emplace_back(H.slot_col[k], ((H.slot_edge[k] >> 2) << 2) | ((H.slot_edge[k] & 1) ? 1 : 2));
-    t.insert(t.end(), extra[i].begin(), extra[i].end());
-    std::sort(t.begin(), t.end());
-    for (auto& [c, code] : t) {
-      sc[o] = c;
-      se[o++] = code;
+    for (; k < e0; k++) {
+      sc[o] = H.slot_col[k];
+      se[o++] = H.slot_edge[k];
     }
+    prev = i + 1;
+    q = q1;
   }
+  copy_rows(n);
   H.row_ptr.swap(rp);
   H.slot_col.swap(sc);
   H.slot_edge.swap(se);
@@ -703,6 +754,7 @@ int append_structure(pgo_graph* g) {
     H.gauge_free = g->gauge_free;
   }
   H.prior_ptr.resize(n + 1, H.prior_ptr.empty() ? 0 : H.prior_ptr.back());
+  phase("rows");
   g->h_row_ptr = H.row_ptr;
   g->h_slot_col = H.slot_col;
   g->h_slot_edge = H.slot_edge;
@@ -735,9 +787,10 @@ int append_structure(pgo_graph* g) {
     brow.push_back(r1);
     r = r1;
   }
+  phase("per-row");
   // the device: new factors, per-row arrays, slots
   HIP_TRY(g, hipStreamSynchronize(d.stream));
-  free_lanes(g);
+  if (g->xb && (size_t)n > g->xb_n) free_lanes(g);   // (else the lanes hold the grown graph too)
   drop_graphs(g);
   if (d.pose_saved) (void)hipFree(d.pose_saved);   // (a snapshot of the old structure's values)
   d.pose_saved = nullptr;
@@ -777,6 +830,7 @@ int append_structure(pgo_graph* g) {
   g->dev_structure = true;
   g->last_upload = 2;
   if (g->chol_ready) g->plan_stale = true;   // ensure_chol decides what to keep
+  phase("upload");
   // the new vertices' values (the resident ones stay bit for bit, unless the
   // caller set values since: then all of them)
   return upload_values(g, g->dev_values ? n_old : 0);
@@ -866,11 +920,27 @@ int ensure_chol(pgo_graph* g) {
     // appended part is small; otherwise a full analysis.
     pgo::CholPlan& P = g->chol;
     const int n = g->d.n;
-    if (pgo::chol_covers(P, n, g->h_row_ptr, g->h_slot_col)) {
+    std::vector<int2> pairs;   // the factors added since the plan (vertex indices)
+    for (size_t e = g->plan_edges; e < g->ek1.size(); e++)
+      pairs.push_back(make_int2(g->index.at(g->ek1[e]), g->index.at(g->ek2[e])));
+    if (n == P.n && pgo::chol_covers(P, pairs)) {
       pgo::chol_assembly(P, g->h_row_ptr, g->h_slot_col);
       RC_TRY(bind_plan(g, false));
       g->plan_stale = false;
+      g->plan_edges = g->ek1.size();
       timed(1);
+      return PGO_OK;
+    }
+    // appended poses: into the plan incrementally while the tail is short and
+    // the factor has not grown much (then a re-plan below)
+    constexpr int kMaxTail = 64;
+    if (!getenv("PGO_NO_PLAN_APPEND") && pgo::chol_append(P, n, g->h_row_ptr, g->h_slot_col, pairs, kMaxTail, 1.05)) {
+      if (P.schedule_error) return fail(g, PGO_E_HIP, "internal: inconsistent panel schedule");
+      drop_graphs(g);
+      RC_TRY(bind_plan(g, true));
+      g->plan_stale = false;
+      g->plan_edges = g->ek1.size();
+      timed(4);
       return PGO_OK;
     }
     if (n >= P.n && n - P.n <= std::max(256, P.n / 10)) {
@@ -918,6 +988,7 @@ int ensure_chol(pgo_graph* g) {
     fprintf(stderr, "ensure_chol bind_plan %8.2f ms\n",
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count());
   g->chol_ready = true;
+  g->plan_edges = g->ek1.size();
   timed(order_in.empty() ? 3 : 2);
   return PGO_OK;
 }
@@ -928,33 +999,40 @@ int ensure_chol(pgo_graph* g) {
 // sources remapped slot -> factor, and the plan (full) or its assembly lists
 // uploaded.
 int bind_plan(pgo_graph* g, bool full) {
+  PhaseTimer phase("bind_plan");
   {
     const int n = g->d.n;
-    std::vector<int> slot_edge = g->h_slot_edge;
-    for (int r = 0; r < n; r++)
-      for (int k = g->h_row_ptr[r]; k < g->h_row_ptr[r + 1]; k++) {
-        const bool own = g->chol.iperm[r] > g->chol.iperm[g->h_slot_col[k]];
-        slot_edge[k] = (slot_edge[k] & ~2) | (own ? 2 : 0);
-      }
-    g->h_slot_edge = slot_edge;
+    std::vector<int>& slot_edge = g->h_slot_edge;
+    std::vector<unsigned char> eside(g->d.ne, 0);
     // Cholesky-mode linearisation writes each factor's owner block at its
     // device factor index (coalesced), so the assembly reads V[q*S + e]
-    std::vector<unsigned char> eside(g->d.ne, 0);
-    for (size_t k = 0; k < slot_edge.size(); k++)
-      if (slot_edge[k] & 2) eside[slot_edge[k] >> 2] = (unsigned char)(slot_edge[k] & 1);
-    for (auto& src : g->chol.asm_src) src = slot_edge[src] >> 2;
+    host_parallel(n, [&](int r0, int r1) {
+      for (int r = r0; r < r1; r++)
+        for (int k = g->h_row_ptr[r]; k < g->h_row_ptr[r + 1]; k++) {
+          const bool own = g->chol.iperm[r] > g->chol.iperm[g->h_slot_col[k]];
+          slot_edge[k] = (slot_edge[k] & ~2) | (own ? 2 : 0);
+          if (own) eside[slot_edge[k] >> 2] = (unsigned char)(slot_edge[k] & 1);   // one owner slot per factor
+        }
+    });
+    std::vector<int>& src = g->chol.asm_src;
+    host_parallel((int)src.size(), [&](int q0, int q1) {
+      for (int q = q0; q < q1; q++) src[q] = slot_edge[src[q]] >> 2;
+    });
+    phase("owners");
     const hipError_t e = full ? pgo::chol_upload(g->chol, g->d.stream) : pgo::chol_upload_assembly(g->chol, g->d.stream);
     if (e != hipSuccess) {
       pgo::chol_free(g->chol);
       return fail(g, e == hipErrorOutOfMemory ? PGO_E_NOMEM : PGO_E_HIP,
                   std::string("Cholesky plan upload: ") + hipGetErrorString(e));
     }
+    phase("chol_upload");
     if (!g->d.eside) RC_TRY(dev_alloc(g, &g->d.eside, std::max<size_t>(g->cap_ne, g->d.ne)));
     RC_TRY(h2d(g, g->d.eside, eside.data(), eside.size()));
     if (!slot_edge.empty())
       HIP_TRY(g, hipMemcpyAsync(g->d.slot_edge, slot_edge.data(), slot_edge.size() * sizeof(int),
                                 hipMemcpyHostToDevice, g->d.stream));
     HIP_TRY(g, hipStreamSynchronize(g->d.stream));
+    phase("slots");
   }
   return PGO_OK;
 }
@@ -1015,6 +1093,7 @@ int graph_factor_solve(pgo_graph* g, int nb, double* x, long long xstride) {
   DevGraph& d = g->d;
   auto capture = [&](hipGraphExec_t* exec, bool factor) -> int {
     if (*exec) return PGO_OK;
+    PhaseTimer phase("graph_capture");
     hipGraph_t graph = nullptr;
     HIP_TRY(g, hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal));
     const hipError_t e1 = factor ? pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr, nb)
@@ -1023,6 +1102,7 @@ int graph_factor_solve(pgo_graph* g, int nb, double* x, long long xstride) {
     HIP_TRY(g, e1);
     HIP_TRY(g, hipGraphInstantiate(exec, graph, nullptr, nullptr, 0));
     HIP_TRY(g, hipGraphDestroy(graph));
+    phase(factor ? "factor" : "solve");
     return PGO_OK;
   };
   RC_TRY(capture(&g->fac_exec[nb], true));
@@ -1164,7 +1244,8 @@ int ensure_lanes(pgo_graph* g, int want) {
       return 1;
     }
   }
-  bool ok = hipMalloc((void**)&g->xb, sizeof(double) * 3 * std::max(d.n, 1) * want) == hipSuccess;
+  g->xb_n = std::max<size_t>({g->cap_n, (size_t)d.n, 1});   // appended vertices keep the lanes
+  bool ok = hipMalloc((void**)&g->xb, sizeof(double) * 3 * g->xb_n * want) == hipSuccess;
   for (int l = 1; l < want && ok; l++) {
     g->lanes.emplace_back();
     Lane& ln = g->lanes.back();
@@ -1391,7 +1472,8 @@ int pgo_add_vertex(pgo_graph* g, uint64_t key, double x, double y, double theta)
   if (!std::isfinite(x) || !std::isfinite(y) || !std::isfinite(theta))
     return fail(g, PGO_E_NONFINITE, "non-finite initial value for key " + std::to_string(key));
   if (g->index.count(key)) return fail(g, PGO_E_DUP_KEY, "key " + std::to_string(key) + " already inserted");
-  RC_TRY(download_values(g));
+  // (no download: the resident values stay on the device, the new one is host-side
+  // until the next upload -- download_values reads back the resident ones only)
   g->index.emplace(key, (int32_t)g->keys.size());
   g->keys.push_back(key);
   g->xyt.insert(g->xyt.end(), {x, y, theta});

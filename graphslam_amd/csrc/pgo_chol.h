@@ -92,6 +92,10 @@ struct CholLevel {
 
 enum { kOrderNd = 0, kOrderAmd = 1 };
 
+struct NumericCap {                // element counts of the numeric workspaces (all lanes)
+  long long F = 0, T = 0, v = 0, x = 0, sf = 0, part = 0;
+};
+
 struct CholPlan {
   int ordering = kOrderNd;         // fill-reducing ordering of the pose graph (input of chol_analyze)
   int part_size = 1, part_rank = 0; // subtree partition over ranks (input of chol_analyze)
@@ -100,6 +104,8 @@ struct CholPlan {
   int batch = 1;                   // lambda lanes with a numeric workspace (input of chol_upload)
   // ---- host symbolic result ----
   int n = 0, ns = 0;
+  int n_analyzed = 0;              // poses at the last full analysis (chol_append's tail starts there)
+  double flops_analyzed = 0;       // ... and its factorisation flops
   long long nslots = 0;            // block-CSR slots of the analysed pattern (stride of V)
   std::vector<int> perm, iperm;    // pose level: new -> old, old -> new
   std::vector<int> sfirst;         // [ns+1] first pose (new index) of each supernode
@@ -155,6 +161,11 @@ struct CholPlan {
   int vtotal = 0;
 
   // ---- device copies ----
+  void* d_blob = nullptr;          // every index array below (d_m ... d_ea_pairs) in one allocation
+  size_t blob_cap = 0;
+  void* h_blob = nullptr;          // its pinned staging copy
+  size_t h_blob_cap = 0;
+  NumericCap num_cap;              // allocated workspaces (room for appended poses)
   double* F = nullptr;             // fronts
   double* Tinv = nullptr;          // inverses of the diagonal 64-blocks, column-major 64x64 each
   double* fv = nullptr;            // frontal vectors (solve)
@@ -216,6 +227,13 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
 void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
 // host: does the plan's factor structure hold every block of this pattern?
 bool chol_covers(const CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
+// ... every given block (old pose index pairs)?
+bool chol_covers(const CholPlan& P, const std::vector<int2>& pairs);
+// host: incremental symbolic update for poses P.n .. n-1 appended to the pattern
+// (eliminated last, rows added along their fill paths); false = not applicable,
+// plan unchanged (pgo_symbolic.cpp)
+bool chol_append(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col,
+                 const std::vector<int2>& new_pairs, int max_tail, double max_growth);
 hipError_t chol_upload(CholPlan& P, hipStream_t s);
 // device: re-upload the assembly lists after chol_assembly (same fronts)
 hipError_t chol_upload_assembly(CholPlan& P, hipStream_t s);

@@ -2012,14 +2012,6 @@ __global__ __launch_bounds__(256) void k_marginals(CholDev c, const int2* __rest
 }
 
 // ------------------------------------------------------------ host drivers
-template <class T>
-static hipError_t up(T** d, const std::vector<T>& h, hipStream_t s) {
-  hipError_t e = hipMalloc((void**)d, std::max<size_t>(h.size(), 1) * sizeof(T));
-  if (e != hipSuccess) return e;
-  if (!h.empty()) e = hipMemcpyAsync(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s);
-  return e;
-}
-
 #define CH_TRY(x)                       \
   do {                                  \
     hipError_t e_ = (x);                \
@@ -2036,6 +2028,7 @@ static void free_numeric(CholPlan& P) {
   P.d_xsend = P.d_xrecv = P.d_xprecv = nullptr;
   P.d_flag = P.d_stepflag = nullptr;
   P.batch = 0;
+  P.num_cap = NumericCap();
 }
 
 // partition exchange slots per lane (doubles): the subtree roots' payloads, the
@@ -2043,16 +2036,34 @@ static void free_numeric(CholPlan& P) {
 static long long xroot_slot(const CholPlan& P) { return std::max(P.xmax, 1LL); }
 static long long xsol_slot(const CholPlan& P) { return P.xsol_max + 1; }
 
+// The workspaces' element counts for nb lanes of the plan as it is
+static NumericCap numeric_need(const CholPlan& P, int nb) {
+  NumericCap c;
+  c.F = nb * std::max<long long>(P.ftotal, 1);
+  c.T = nb * std::max<long long>(2 * P.ttotal, 1);
+  c.v = (long long)nb * std::max(P.vtotal, 1);
+  c.x = (long long)nb * std::max(3 * P.n, 1);
+  c.sf = (long long)nb * std::max(P.ns, 1);
+  c.part = (long long)nb * std::max(P.npart, 1) * 64;
+  return c;
+}
+
+// With room_for_growth (the appendable one-rank plan, chol_append), every
+// workspace gets 1/32 more than it needs, so the next appended poses reuse it.
 static hipError_t alloc_numeric(CholPlan& P, int nb, hipStream_t s) {
-  CH_TRY(hipMalloc((void**)&P.F, nb * std::max<long long>(P.ftotal, 1) * sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.Tinv, nb * std::max<long long>(2 * P.ttotal, 1) * sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.fv, (size_t)nb * std::max(P.vtotal, 1) * sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.xv, (size_t)nb * std::max(3 * P.n, 1) * sizeof(double)));
+  NumericCap need = numeric_need(P, nb), cap = need;
+  if (P.part_size <= 1) {
+    for (long long* v : {&cap.F, &cap.T, &cap.v, &cap.x, &cap.sf, &cap.part}) *v += *v / 32 + 4096;
+  }
+  CH_TRY(hipMalloc((void**)&P.F, cap.F * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.Tinv, cap.T * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.fv, cap.v * sizeof(double)));
+  CH_TRY(hipMalloc((void**)&P.xv, cap.x * sizeof(double)));
   CH_TRY(hipMalloc((void**)&P.d_flag, nb * sizeof(int)));
-  CH_TRY(hipMalloc((void**)&P.d_stepflag, (size_t)nb * std::max(P.ns, 1) * sizeof(int)));
+  CH_TRY(hipMalloc((void**)&P.d_stepflag, cap.sf * sizeof(int)));
   CH_TRY(hipMalloc((void**)&P.d_lambda, nb * sizeof(double)));
-  CH_TRY(hipMalloc((void**)&P.d_partial, (size_t)nb * std::max(P.npart, 1) * 64 * sizeof(double)));
-  CH_TRY(hipMemsetAsync(P.F, 0, nb * std::max<long long>(P.ftotal, 1) * sizeof(double), s));
+  CH_TRY(hipMalloc((void**)&P.d_partial, cap.part * sizeof(double)));
+  CH_TRY(hipMemsetAsync(P.F, 0, need.F * sizeof(double), s));
   {   // partition exchange buffers, nb lanes per rank
     const long long xs = P.part_size > 1 ? std::max(xroot_slot(P), xsol_slot(P)) : 1;
     CH_TRY(hipMalloc((void**)&P.d_xsend, sizeof(double) * xs * nb));
@@ -2061,7 +2072,23 @@ static hipError_t alloc_numeric(CholPlan& P, int nb, hipStream_t s) {
     CH_TRY(hipMalloc((void**)&P.d_xprecv, sizeof(double) * xp * nb * std::max(P.part_size, 1)));
   }
   P.batch = nb;
+  P.num_cap = cap;
   return hipStreamSynchronize(s);
+}
+
+// The plan changed shape (chol_append): keep the workspaces when they hold it
+// (the fronts zeroed again: their layout moved), else allocate anew.
+static hipError_t refresh_numeric(CholPlan& P, int nb, hipStream_t s) {
+  const NumericCap need = numeric_need(P, nb), &cap = P.num_cap;
+  if (P.F && P.part_size <= 1 && nb <= P.batch && need.F <= cap.F && need.T <= cap.T && need.v <= cap.v &&
+      need.x <= cap.x && need.sf <= cap.sf && need.part <= cap.part) {
+    CH_TRY(hipMemsetAsync(P.F, 0, need.F * sizeof(double), s));
+    P.batch = nb;
+    return hipSuccess;
+  }
+  CH_TRY(hipStreamSynchronize(s));
+  free_numeric(P);
+  return alloc_numeric(P, nb, s);
 }
 
 hipError_t chol_set_batch(CholPlan& P, int nb, hipStream_t s) {
@@ -2078,111 +2105,142 @@ hipError_t chol_set_batch(CholPlan& P, int nb, hipStream_t s) {
   return hipSuccess;
 }
 
-hipError_t chol_upload_assembly(CholPlan& P, hipStream_t s) {
-  CH_TRY(hipStreamSynchronize(s));
-  for (void** p : {(void**)&P.d_asm_front, (void**)&P.d_asm_li, (void**)&P.d_asm_lj, (void**)&P.d_asm_ptr,
-                   (void**)&P.d_asm_src, (void**)&P.d_at_iptr, (void**)&P.d_at_items}) {
-    if (*p) (void)hipFree(*p);
-    *p = nullptr;
+// The plan's index arrays live in one device allocation, filled by one copy
+// from a pinned staging buffer (a plan refresh is one upload, not ~45
+// allocations and pageable copies).
+namespace {
+struct BlobItem {
+  void** dptr;
+  const void* src;
+  size_t bytes, off;
+};
+template <class T>
+void blob_add(std::vector<BlobItem>& items, T** dptr, const std::vector<T>& h) {
+  items.push_back({(void**)dptr, h.data(), h.size() * sizeof(T), 0});
+}
+}  // namespace
+
+static hipError_t upload_index(CholPlan& P, hipStream_t s) {
+  std::vector<int4> own, foreign, sown, sforeign;   // partition exchange lists (this rank's roots / the others')
+  std::vector<long long> xo(2 * P.xp_tasks.size());
+  if (P.part_size > 1 && (long long)P.part_size * std::max(P.xmax, P.xsol_max) >= (1LL << 31))
+    return hipErrorInvalidValue;   // int offsets
+  for (size_t q = 0; q < P.xroot.size(); q++) {
+    const int sr = P.xroot[q], r = P.xroot_rank[q], u = P.m[sr] - P.w[sr];
+    if (u == 0) continue;
+    if (r == P.part_rank) own.push_back(make_int4(sr, (int)P.xroot_off[q], u, 0));
+    else if (P.parent[sr] >= 0) foreign.push_back(make_int4(sr, (int)P.xroot_off[q], u, r));
   }
-  CH_TRY(up(&P.d_asm_front, P.asm_front, s));
-  CH_TRY(up(&P.d_asm_li, P.asm_li, s));
-  CH_TRY(up(&P.d_asm_lj, P.asm_lj, s));
-  CH_TRY(up(&P.d_asm_ptr, P.asm_ptr, s));
-  CH_TRY(up(&P.d_asm_src, P.asm_src, s));
-  CH_TRY(up(&P.d_at_iptr, P.at_iptr, s));
-  CH_TRY(up(&P.d_at_items, P.at_items, s));
+  for (const int4& rg : P.xsol_ranges) (rg.x == P.part_rank ? sown : sforeign).push_back(rg);
+  P.n_xown = (int)own.size();
+  P.n_xforeign = (int)foreign.size();
+  P.n_xsol_own = (int)sown.size();
+  P.n_xsol_foreign = (int)sforeign.size();
+  for (size_t q = 0; q < P.xp_tasks.size(); q++) {
+    xo[2 * q] = P.xp_loff[q];
+    xo[2 * q + 1] = P.xp_lstride[q];
+  }
+  std::vector<BlobItem> it;
+  blob_add(it, &P.d_toff, P.toff);
+  blob_add(it, &P.d_m, P.m);
+  blob_add(it, &P.d_w, P.w);
+  blob_add(it, &P.d_voff, P.voff);
+  blob_add(it, &P.d_rptr, P.rptr);
+  blob_add(it, &P.d_rows, P.rows);
+  blob_add(it, &P.d_foff, P.foff);
+  blob_add(it, &P.d_cptr, P.cptr);
+  blob_add(it, &P.d_children, P.children);
+  blob_add(it, &P.d_ea_rel, P.ea_rel);
+  blob_add(it, &P.d_ea_ptr, P.ea_ptr);
+  blob_add(it, &P.d_parent, P.parent);
+  blob_add(it, &P.d_asm_front, P.asm_front);
+  blob_add(it, &P.d_asm_li, P.asm_li);
+  blob_add(it, &P.d_asm_lj, P.asm_lj);
+  blob_add(it, &P.d_asm_ptr, P.asm_ptr);
+  blob_add(it, &P.d_asm_src, P.asm_src);
+  blob_add(it, &P.d_dg_front, P.dg_front);
+  blob_add(it, &P.d_dg_loc, P.dg_loc);
+  blob_add(it, &P.d_perm, P.perm);
+  blob_add(it, &P.d_small, P.small_list);
+  blob_add(it, &P.d_level_fronts, P.level_fronts);
+  blob_add(it, &P.d_potrf, P.potrf_list);
+  blob_add(it, &P.d_bwd, P.bwd_tasks);
+  blob_add(it, &P.d_bwdc, P.bwdc_tasks);
+  blob_add(it, &P.d_bwd_pref, P.bwd_pref);
+  blob_add(it, &P.d_bwd_part, P.bwd_part_tasks);
+  blob_add(it, &P.d_syrk, P.syrk_tasks);
+  blob_add(it, &P.d_sdiag, P.sdiag_tasks);
+  blob_add(it, &P.d_col, P.col_tasks);
+  blob_add(it, &P.d_xown, own);
+  blob_add(it, &P.d_xforeign, foreign);
+  blob_add(it, &P.d_xsol_own, sown);
+  blob_add(it, &P.d_xsol_foreign, sforeign);
+  blob_add(it, &P.d_xp, P.xp_tasks);
+  blob_add(it, &P.d_xp_off, xo);
+  blob_add(it, &P.d_at_iptr, P.at_iptr);
+  blob_add(it, &P.d_at_items, P.at_items);
+  blob_add(it, &P.d_ea_tasks, P.ea_tasks);
+  blob_add(it, &P.d_ea_pairs, P.ea_pairs);
+  size_t total = 0;
+  for (BlobItem& b : it) {
+    b.off = total;
+    total += (std::max<size_t>(b.bytes, 1) + 255) / 256 * 256;
+  }
+  CH_TRY(hipStreamSynchronize(s));   // the staging buffer and the old blob are idle
+  if (total > P.blob_cap) {
+    if (P.d_blob) (void)hipFree(P.d_blob);
+    P.d_blob = nullptr;
+    P.blob_cap = 0;
+    const size_t cap = total + total / 8;
+    CH_TRY(hipMalloc(&P.d_blob, cap));
+    P.blob_cap = cap;
+  }
+  if (total > P.h_blob_cap) {
+    if (P.h_blob) (void)hipHostFree(P.h_blob);
+    P.h_blob = nullptr;
+    P.h_blob_cap = 0;
+    const size_t cap = total + total / 8;
+    CH_TRY(hipHostMalloc(&P.h_blob, cap, hipHostMallocDefault));
+    P.h_blob_cap = cap;
+  }
+  char* h = static_cast<char*>(P.h_blob);
+  char* d = static_cast<char*>(P.d_blob);
+  for (const BlobItem& b : it) {
+    if (b.bytes) memcpy(h + b.off, b.src, b.bytes);
+    *b.dptr = d + b.off;
+  }
+  CH_TRY(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, s));
+  return hipSuccess;
+}
+
+hipError_t chol_upload_assembly(CholPlan& P, hipStream_t s) {
+  CH_TRY(upload_index(P, s));
   return hipStreamSynchronize(s);
 }
 
 hipError_t chol_upload(CholPlan& P, hipStream_t s) {
-  CH_TRY(up(&P.d_toff, P.toff, s));
-  CH_TRY(up(&P.d_m, P.m, s));
-  CH_TRY(up(&P.d_w, P.w, s));
-  CH_TRY(up(&P.d_voff, P.voff, s));
-  CH_TRY(up(&P.d_rptr, P.rptr, s));
-  CH_TRY(up(&P.d_rows, P.rows, s));
-  CH_TRY(up(&P.d_foff, P.foff, s));
-  CH_TRY(up(&P.d_cptr, P.cptr, s));
-  CH_TRY(up(&P.d_children, P.children, s));
-  CH_TRY(up(&P.d_ea_rel, P.ea_rel, s));
-  CH_TRY(up(&P.d_ea_ptr, P.ea_ptr, s));
-  CH_TRY(up(&P.d_parent, P.parent, s));
-  CH_TRY(up(&P.d_asm_front, P.asm_front, s));
-  CH_TRY(up(&P.d_asm_li, P.asm_li, s));
-  CH_TRY(up(&P.d_asm_lj, P.asm_lj, s));
-  CH_TRY(up(&P.d_asm_ptr, P.asm_ptr, s));
-  CH_TRY(up(&P.d_asm_src, P.asm_src, s));
-  CH_TRY(up(&P.d_dg_front, P.dg_front, s));
-  CH_TRY(up(&P.d_dg_loc, P.dg_loc, s));
-  CH_TRY(up(&P.d_perm, P.perm, s));
-  CH_TRY(up(&P.d_small, P.small_list, s));
-  CH_TRY(up(&P.d_level_fronts, P.level_fronts, s));
-  CH_TRY(up(&P.d_potrf, P.potrf_list, s));
-  CH_TRY(up(&P.d_bwd, P.bwd_tasks, s));
-  CH_TRY(up(&P.d_bwdc, P.bwdc_tasks, s));
-  CH_TRY(up(&P.d_bwd_pref, P.bwd_pref, s));
-  CH_TRY(up(&P.d_bwd_part, P.bwd_part_tasks, s));
-  CH_TRY(up(&P.d_syrk, P.syrk_tasks, s));
-  CH_TRY(up(&P.d_sdiag, P.sdiag_tasks, s));
-  CH_TRY(up(&P.d_col, P.col_tasks, s));
-  {   // partition exchange lists (this rank's roots / the others' needed ones) and buffers
-    std::vector<int4> own, foreign, sown, sforeign;
-    const long long slot = std::max(P.xmax, 1LL);
-    if (P.part_size > 1 && (long long)P.part_size * std::max(P.xmax, P.xsol_max) >= (1LL << 31))
-      return hipErrorInvalidValue;   // int offsets
-    for (size_t q = 0; q < P.xroot.size(); q++) {
-      const int sr = P.xroot[q], r = P.xroot_rank[q], u = P.m[sr] - P.w[sr];
-      if (u == 0) continue;
-      if (r == P.part_rank) own.push_back(make_int4(sr, (int)P.xroot_off[q], u, 0));
-      else if (P.parent[sr] >= 0) foreign.push_back(make_int4(sr, (int)P.xroot_off[q], u, r));
-    }
-    for (const int4& rg : P.xsol_ranges) (rg.x == P.part_rank ? sown : sforeign).push_back(rg);
-    P.n_xown = (int)own.size();
-    P.n_xforeign = (int)foreign.size();
-    P.n_xsol_own = (int)sown.size();
-    P.n_xsol_foreign = (int)sforeign.size();
-    CH_TRY(up(&P.d_xown, own, s));
-    CH_TRY(up(&P.d_xforeign, foreign, s));
-    CH_TRY(up(&P.d_xsol_own, sown, s));
-    CH_TRY(up(&P.d_xsol_foreign, sforeign, s));
-    (void)slot;
-    std::vector<long long> xo(2 * P.xp_tasks.size());
-    for (size_t q = 0; q < P.xp_tasks.size(); q++) {
-      xo[2 * q] = P.xp_loff[q];
-      xo[2 * q + 1] = P.xp_lstride[q];
-    }
-    CH_TRY(up(&P.d_xp, P.xp_tasks, s));
-    CH_TRY(up(&P.d_xp_off, xo, s));
-  }
-  CH_TRY(up(&P.d_at_iptr, P.at_iptr, s));
-  CH_TRY(up(&P.d_at_items, P.at_items, s));
-  CH_TRY(alloc_numeric(P, std::max(P.batch, 1), s));
-  {   // PGO_SIDE_PRIORITY=1: the plain Schur tiles' stream at the lowest dispatch
-      // priority (measured on C3: 22.0 vs 26.0 it/s -- the starved tiles hold
-      // the level ends back more than the panel chain gains -- so off)
+  CH_TRY(upload_index(P, s));
+  CH_TRY(P.F ? refresh_numeric(P, std::max(P.batch, 1), s) : alloc_numeric(P, std::max(P.batch, 1), s));
+  if (!P.side) {   // PGO_SIDE_PRIORITY=1: the plain Schur tiles' stream at the lowest dispatch
+                   // priority (measured on C3: 22.0 vs 26.0 it/s -- the starved tiles hold
+                   // the level ends back more than the panel chain gains -- so off)
     int least = 0, greatest = 0;
     const char* pr = getenv("PGO_SIDE_PRIORITY");
     if (pr && pr[0] == '1' && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
       CH_TRY(hipStreamCreateWithPriority(&P.side, hipStreamNonBlocking, least));
     else
       CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
+    CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
+    CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));
+    for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
-  CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
-  CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));
-  for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  CH_TRY(up(&P.d_ea_tasks, P.ea_tasks, s));
-  CH_TRY(up(&P.d_ea_pairs, P.ea_pairs, s));
   return hipStreamSynchronize(s);
 }
 
 void chol_free(CholPlan& P) {
-  void* ptrs[] = {P.F, P.Tinv, P.d_toff, P.fv, P.xv, P.d_flag, P.d_lambda, P.d_m, P.d_w, P.d_voff, P.d_rptr, P.d_rows, P.d_foff, P.d_cptr,
-                  P.d_children, P.d_ea_rel, P.d_ea_ptr, P.d_parent, P.d_asm_front, P.d_asm_li, P.d_asm_lj,
-                  P.d_asm_ptr, P.d_asm_src, P.d_dg_front, P.d_dg_loc, P.d_perm, P.d_small, P.d_level_fronts,
-                  P.d_syrk, P.d_ea_tasks, P.d_ea_pairs, P.d_potrf, P.d_bwd, P.d_bwdc, P.d_bwd_pref, P.d_bwd_part, P.d_partial, P.d_sdiag, P.d_at_iptr, P.d_at_items, P.d_col, P.d_stepflag, P.d_xown, P.d_xforeign, P.d_xsol_own, P.d_xsol_foreign, P.d_xsend, P.d_xrecv, P.d_xp, P.d_xp_off, P.d_xprecv};
-  for (void* p : ptrs)
-    if (p) (void)hipFree(p);
+  free_numeric(P);
+  if (P.d_blob) (void)hipFree(P.d_blob);
+  if (P.h_blob) (void)hipHostFree(P.h_blob);
   for (hipEvent_t e : P.evs)
     if (e) (void)hipEventDestroy(e);
   if (P.side) (void)hipStreamDestroy(P.side);

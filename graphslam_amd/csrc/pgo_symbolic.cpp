@@ -1,9 +1,12 @@
 // Host-side symbolic analysis for the GPU supernodal Cholesky (pgo_chol.h).
 // Runs once per graph structure (GTSAM recomputes COLAMD every solve).
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <tuple>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -208,6 +211,686 @@ std::vector<double> distributed_rank_flops(const CholPlan& P, int size, double* 
   return rf;
 }
 
+// Front storage offsets (F, Tinv, frontal vectors) and the factor's flops /
+// nonzeros from the fronts' sizes m, w.
+static void size_fronts(CholPlan& P) {
+  const int ns = P.ns;
+  P.foff.assign(ns + 1, 0);
+  P.toff.assign(ns + 1, 0);
+  P.voff.assign(ns + 1, 0);
+  P.flops = 0;
+  P.nnzl = 0;
+  for (int s = 0; s < ns; s++) {
+    const long long mm = P.m[s];
+    P.foff[s + 1] = P.foff[s] + ((mm * mm + 7) / 8) * 8;   // 64-byte aligned fronts
+    P.voff[s + 1] = P.voff[s] + ((P.m[s] + 7) / 8) * 8;
+    P.toff[s + 1] = P.toff[s] + (long long)((P.w[s] + 63) / 64) * 4096;
+    for (int k = 0; k < P.w[s]; k++) {
+      const double r = P.m[s] - k - 1;
+      P.flops += 1 + r + r * (r + 1);
+      P.nnzl += r + 1;
+    }
+  }
+  P.ftotal = P.foff[ns];
+  P.ttotal = P.toff[ns];
+  P.vtotal = P.voff[ns];
+}
+
+// Threads of the host planning (PGO_PLAN_THREADS, default: the hardware's, at
+// most 16); parallel_chunks runs fn(t, begin, end) on nth contiguous chunks of
+// [0, n), chunk t on thread t (the results are independent of nth).
+static int plan_threads() {
+  static const int t = [] {
+    if (const char* e = getenv("PGO_PLAN_THREADS")) return std::max(1, atoi(e));
+    return (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+  }();
+  return t;
+}
+
+template <class F>
+static void parallel_chunks(int n, int nth, F&& fn) {
+  nth = std::max(1, std::min(nth, n));
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nth; t++)
+    pool.emplace_back([&fn, t, n, nth] { fn(t, (int)((long long)n * t / nth), (int)((long long)n * (t + 1) / nth)); });
+  fn(0, 0, (int)((long long)n / nth));
+  for (auto& th : pool) th.join();
+}
+
+// One level's share of the schedule lists (chol_schedule builds the levels
+// concurrently, then appends them to the plan's lists in level order).
+struct LevelLists {
+  std::vector<int> small_list, level_fronts, potrf_list;
+  std::vector<int4> syrk_tasks, sdiag_tasks, col_tasks, bwd_tasks, bwdc_tasks, bwd_part_tasks, ea_tasks, ea_pairs;
+  std::vector<int2> bwd_pref;
+  std::vector<XExchange> xchg;
+  std::vector<int4> xp_tasks;
+  std::vector<long long> xp_loff, xp_lstride;
+  long long xp_rslot = 0;
+  int npart = 0;
+  bool schedule_error = false;
+};
+
+// The plan's schedules from its fronts (chol_analyze's second half; the
+// incremental append re-runs it on the updated fronts): the subtree partition,
+// the level schedules and task lists, then the H assembly lists.
+static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
+  static const bool timing = getenv("PGO_PLAN_TIMING") != nullptr;
+  auto tlast = std::chrono::steady_clock::now();
+  auto phase = [&](const char* what) {
+    if (!timing) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "chol_schedule %-12s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - tlast).count());
+    tlast = t;
+  };
+  const int ns = P.ns;
+  P.schedule_error = false;
+  // ---- multi-GPU subtree partition (part_size > 1, DESIGN.md "Multi-GPU"):
+  // rank part_rank factorises the fronts of its subtrees (phase 1), then every
+  // rank the replicated top fronts (phase 2), after the subtree roots' update
+  // matrices / vectors have been exchanged.  Storage only for the fronts this
+  // rank touches: its own, the top, and the other ranks' subtree roots (their
+  // update matrices arrive in the exchange).  One rank: everything is phase 1.
+  const int psz = std::max(P.part_size, 1), prk = P.part_rank;
+  P.owner = partition_subtrees(P, psz);
+  P.subtree_cnt.assign(ns, 1);
+  for (int s = 0; s < ns; s++)
+    if (P.parent[s] >= 0) P.subtree_cnt[P.parent[s]] += P.subtree_cnt[s];
+  std::vector<char> need(ns, 0);
+  P.xroot.clear();
+  P.xroot_rank.clear();
+  for (int s = 0; s < ns; s++) {
+    const bool root = P.owner[s] >= 0 && (P.parent[s] < 0 || P.owner[P.parent[s]] < 0);
+    if (root) {
+      P.xroot.push_back(s);
+      P.xroot_rank.push_back(P.owner[s]);
+    }
+    need[s] = P.owner[s] == prk || P.owner[s] < 0 || (root && P.parent[s] >= 0);
+  }
+  if (psz > 1) {   // offsets over the needed fronts only
+    for (int s = 0; s < ns; s++) {
+      const long long mm = need[s] ? P.m[s] : 0;
+      P.foff[s + 1] = P.foff[s] + ((mm * mm + 7) / 8) * 8;
+      P.voff[s + 1] = P.voff[s] + (need[s] ? ((P.m[s] + 7) / 8) * 8 : 0);
+      P.toff[s + 1] = P.toff[s] + (need[s] ? (long long)((P.w[s] + 63) / 64) * 4096 : 0);
+    }
+    P.ftotal = P.foff[ns];
+    P.ttotal = P.toff[ns];
+    P.vtotal = P.voff[ns];
+  }
+  // exchange layout: per rank its roots' payloads (packed lower update matrix,
+  // then the update vector) back to back; the solve's: its subtrees' poses
+  P.xroot_off.assign(P.xroot.size(), 0);
+  P.xsize.assign(psz, 0);
+  P.xsol_size.assign(psz, 0);
+  P.xsol_ranges.clear();
+  for (size_t q = 0; q < P.xroot.size(); q++) {
+    const int sr = P.xroot[q], r = P.xroot_rank[q];
+    const long long u = P.m[sr] - P.w[sr];
+    P.xroot_off[q] = P.xsize[r];
+    P.xsize[r] += u * (u + 1) / 2 + u;
+    const int first = sr - P.subtree_cnt[sr] + 1;   // the subtree: postorder fronts [first, sr]
+    P.xsol_ranges.push_back(make_int4(r, 3 * P.sfirst[first], 3 * P.sfirst[sr + 1], (int)P.xsol_size[r]));
+    P.xsol_size[r] += 3LL * (P.sfirst[sr + 1] - P.sfirst[first]);
+  }
+  P.xmax = *std::max_element(P.xsize.begin(), P.xsize.end());
+  P.xsol_max = *std::max_element(P.xsol_size.begin(), P.xsol_size.end());
+  phase("partition");
+  // ---- level schedules: phase 1 (this rank's subtree fronts) then phase 2 (top)
+  std::vector<std::vector<int>> bylevel;
+  for (int phase = 0; phase < 2; phase++) {
+    int hmax = -1;
+    for (int s = 0; s < ns; s++)
+      if ((phase == 0 ? P.owner[s] == prk : P.owner[s] < 0)) hmax = std::max(hmax, P.height[s]);
+    const size_t base = bylevel.size();
+    bylevel.resize(base + hmax + 1);
+    for (int s = 0; s < ns; s++)
+      if ((phase == 0 ? P.owner[s] == prk : P.owner[s] < 0)) bylevel[base + P.height[s]].push_back(s);
+    if (phase == 0) P.split = (int)bylevel.size();
+  }
+  {   // drop empty levels (a height with no front of this rank), keeping the split
+    std::vector<std::vector<int>> kept;
+    int split = 0;
+    for (size_t L = 0; L < bylevel.size(); L++)
+      if (!bylevel[L].empty()) {
+        kept.push_back(std::move(bylevel[L]));
+        if ((int)L < P.split) split++;
+      }
+    bylevel.swap(kept);
+    P.split = split;
+  }
+  auto blocked = [&](int s) { return is_blocked(P, s); };
+  // ---- distributed top (part_size > 1): the top fronts' columns are dealt to
+  // the ranks instead of every rank factoring every top front.  A blocked top
+  // front's pivot columns go by 64-column panel, round robin (continuing over
+  // the fronts); its columns past the last whole panel (the update matrix) take
+  // the rank of the parent column they extend-add into, so a rank's share of a
+  // parent's columns is assembled from its own shares of the children's update
+  // matrices (no exchange of update matrices between top fronts).  Small top
+  // fronts (one workgroup / wavefront each) are computed by every rank (-1),
+  // and so are the update columns of their children.  Each column's updates
+  // are applied by its rank only, with the same tasks (same depths, same
+  // order) as the one-rank plan: bitwise the one-rank factor.  A rank receives
+  // every panel (broadcast by its owner right after it is factored) for its own
+  // columns' updates and the replicated backward solve.
+  // (PGO_DIST_TOP=0: the top fronts replicated on every rank instead -- the
+  // previous scheme, kept as a reference for the host self-test)
+  const bool dtop = psz > 1 && !(getenv("PGO_DIST_TOP") && atoi(getenv("PGO_DIST_TOP")) == 0);
+  P.cown_off.assign(ns, -1);
+  P.cown.clear();
+  if (dtop) column_owners(P, P.owner, psz, P.cown_off, P.cown);
+  P.xchg.clear();
+  P.xp_tasks.clear();
+  P.xp_loff.clear();
+  P.xp_lstride.clear();
+  P.xp_rslot = 0;
+  // an exchange point: every panel / tail in `items` (front, kn, nb | kind << 16,
+  // owner) goes from its owner to every rank (one broadcast per sending rank)
+  auto add_exchange = [&](LevelLists& S, const std::vector<int4>& items) -> int {
+    if (items.empty()) return -1;
+    XExchange x;
+    x.off = (int)S.xp_tasks.size();
+    x.cnt = (int)items.size();
+    x.size.assign(psz, 0);
+    for (const int4& t : items) {
+      const int s = t.x, kn = t.y, nb = t.z & 0xffff, kind = t.z >> 16, m = P.m[s];
+      const long long sz = kind == 0 ? (long long)(m - kn) * nb + 4096 + (m - kn) : (long long)(m - kn) * nb;
+      S.xp_tasks.push_back(t);
+      S.xp_loff.push_back(x.size[t.w]);
+      x.size[t.w] += sz;
+    }
+    for (int q = x.off; q < x.off + x.cnt; q++) S.xp_lstride.push_back(x.size[S.xp_tasks[q].w]);
+    for (long long v : x.size) S.xp_rslot = std::max(S.xp_rslot, v);
+    S.xchg.push_back(x);
+    return (int)S.xchg.size() - 1;
+  };
+  const int nl = (int)bylevel.size();
+  P.levels.assign(nl, CholLevel());
+  // one level's schedule into its own lists (offsets level-relative; merged
+  // below in level order, so the plan is the same for any thread count)
+  auto schedule_level = [&](int L, LevelLists& S) {
+    CholLevel& lv = P.levels[L];
+    // distributed top level: this rank generates only the tasks of its columns
+    const bool dist = dtop && L >= P.split;
+    auto mine = [&](int s, int col) {
+      if (!dist) return true;
+      const int o = P.cown[P.cown_off[s] + col];
+      return o < 0 || o == prk;
+    };
+    auto cowner = [&](int s, int col) { return dist ? P.cown[P.cown_off[s] + col] : -1; };
+    lv.front_off = (int)S.level_fronts.size();
+    lv.front_cnt = (int)bylevel[L].size();
+    for (int s : bylevel[L]) {
+      S.level_fronts.push_back(s);
+      lv.maxm = std::max(lv.maxm, P.m[s]);
+      if (P.m[s] <= kSmallFront) lv.small_maxm = std::max(lv.small_maxm, P.m[s]);
+    }
+    // blocked backward solve (64-column blocks of each front's pivot columns);
+    // the forward substitution is carried by the factorisation
+    for (int s : bylevel[L]) lv.maxblk = std::max(lv.maxblk, (P.w[s] + 63) / 64);
+    {                                            // backward init: all columns vs the rows below w
+      // partial products L21[r0:r0+kBwdRows, block]' x_below, one task each,
+      // reduced in fixed order by the init task of the block
+      SolveStep sp{(int)S.bwd_part_tasks.size(), 0};
+      SolveStep st{(int)S.bwd_tasks.size(), 0};
+      for (int s : bylevel[L]) {
+        const int w = P.w[s], m = P.m[s], nblk = (w + 63) / 64;
+        for (int b = 0; b < nblk; b++) {
+          const int p0 = S.npart;
+          for (int r0 = w; r0 < m; r0 += kBwdRows) S.bwd_part_tasks.push_back(make_int4(s, b * 64, r0, S.npart++));
+          S.bwd_tasks.push_back(make_int4(s, b * 64, std::min(b * 64 + 64, w), b == nblk - 1 ? b : -1));
+          S.bwd_pref.push_back(make_int2(p0, S.npart - p0));
+        }
+      }
+      sp.cnt = (int)S.bwd_part_tasks.size() - sp.off;
+      for (int q = sp.off; q < sp.off + sp.cnt; q++) {
+        const int4 t = S.bwd_part_tasks[q];
+        lv.bwd_part_flops += 2.0 * std::min(64, P.w[t.x] - t.y) * std::min(kBwdRows, P.m[t.x] - t.z);
+      }
+      st.cnt = (int)S.bwd_tasks.size() - st.off;
+      lv.bwd_part = sp;
+      lv.bwd.push_back(st);
+    }
+    {   // the same steps as one chained launch (k_bwd_chain): block j of a front
+        // after the blocks above it, tasks ordered by distance from the last
+        // block so that every workgroup waits only on earlier-dispatched ones
+      lv.bwdc.off = (int)S.bwdc_tasks.size();
+      for (int d = 1; d < lv.maxblk; d++)
+        for (int s : bylevel[L]) {
+          const int w = P.w[s], nblk = (w + 63) / 64;
+          if (d >= nblk) continue;
+          const int j = nblk - 1 - d;
+          S.bwdc_tasks.push_back(make_int4(s, j * 64, j * 64 + 64, j));
+        }
+      lv.bwdc.cnt = (int)S.bwdc_tasks.size() - lv.bwdc.off;
+    }
+    for (int b = lv.maxblk - 1; b >= 1; b--) {   // backward step b: columns left of block b
+      SolveStep st{(int)S.bwd_tasks.size(), 0};
+      for (int s : bylevel[L]) {
+        const int w = P.w[s], nblk = (w + 63) / 64;
+        if (b >= nblk) continue;
+        for (int c = 0; c < b; c++)
+        {
+          S.bwd_tasks.push_back(make_int4(s, c * 64, c * 64 + 64, c == b - 1 ? c : -1));
+          S.bwd_pref.push_back(make_int2(0, 0));
+        }
+      }
+      st.cnt = (int)S.bwd_tasks.size() - st.off;
+      lv.bwd.push_back(st);
+    }
+    // assembly: one task per 64x64 tile of every front's lower triangle, which
+    // it writes whole: its H entries (+ lambda on the diagonal), then the
+    // update-matrix elements of the front's children in order (fixed
+    // summation order, no atomics), each child contributing a rectangle of its
+    // update matrix (child rows [a0, a0+nr) x columns [b0, b0+nc), the rows /
+    // columns whose parent index falls in the tile).  No front is zeroed.
+    lv.ea_off.push_back((int)S.ea_tasks.size());
+    std::vector<int> tcnt, tpos;
+    std::vector<int4> runs;   // (child, tile, first child row, rows) of every child, children in order
+    for (int sp : bylevel[L]) {
+      const int nt = (P.m[sp] + 63) / 64;
+      tcnt.assign((size_t)nt * (nt + 1) / 2, 0);
+      runs.clear();
+      std::vector<int> cr(1, 0);   // runs of child q: [cr[q], cr[q + 1])
+      for (int q = P.cptr[sp]; q < P.cptr[sp + 1]; q++) {
+        const int c = P.children[q];
+        const int u = P.m[c] - P.w[c];
+        const size_t r0 = runs.size();
+        for (int a = 0; a < u; a++) {
+          const int t = (3 * P.ea_rel[P.ea_ptr[c] + a / 3] + a % 3) / 64;
+          if (runs.size() == r0 || runs.back().y != t) runs.push_back(make_int4(c, t, a, 0));
+          runs.back().w++;
+        }
+        for (size_t i = r0; i < runs.size(); i++)   // a child's runs are in increasing tiles: one pair per tile
+          for (size_t j = r0; j <= i; j++) tcnt[(size_t)runs[i].y * (runs[i].y + 1) / 2 + runs[j].y]++;
+        cr.push_back((int)runs.size());
+      }
+      const int base = (int)S.ea_pairs.size();
+      tpos.assign(tcnt.size(), 0);
+      for (size_t k = 1; k < tcnt.size(); k++) tpos[k] = tpos[k - 1] + tcnt[k - 1];
+      for (int ti = 0; ti < nt; ti++)
+        for (int tj = 0; tj <= ti; tj++) {
+          const size_t k = (size_t)ti * (ti + 1) / 2 + tj;
+          S.ea_tasks.push_back(make_int4(sp, (ti << 16) | tj, base + tpos[k], tcnt[k]));
+        }
+      S.ea_pairs.resize(base + (tcnt.empty() ? 0 : tpos.back() + tcnt.back()));
+      for (size_t q = 0; q + 1 < cr.size(); q++)   // children in order: their pairs in order within every tile
+        for (int i = cr[q]; i < cr[q + 1]; i++)
+          for (int j = cr[q]; j <= i; j++) {
+            const size_t k = (size_t)runs[i].y * (runs[i].y + 1) / 2 + runs[j].y;
+            S.ea_pairs[base + tpos[k]++] = make_int4(runs[i].x, runs[i].z, runs[j].z, runs[i].w | (runs[j].w << 8));
+          }
+    }
+    lv.ea_cnt.push_back((int)S.ea_tasks.size() - lv.ea_off.back());
+    // small fronts (m <= kSmallFront): with w <= kWaveW one wavefront each (the
+    // m x w panel in LDS, the rank-w Schur update streamed), largest first;
+    // else one workgroup each with the whole front in LDS, launched per size
+    // class so the LDS request (m^2 doubles) does not cap the occupancy
+    std::vector<int> big;
+    {
+      const int classes[4] = {32, 64, 96, kSmallFront};
+      std::vector<int> bucket[4], wave;
+      for (int s : bylevel[L]) {
+        // w > kWaveW: the blocked path (64-column panels, every front of the
+        // level in the same launches) -- a whole-front-in-LDS workgroup runs
+        // its w pivots one after the other at ~2 us each
+        if (blocked(s)) {
+          big.push_back(s);
+          continue;
+        }
+        if (P.w[s] <= kWaveW) {
+          wave.push_back(s);
+          continue;
+        }
+        int q = 0;
+        while (P.m[s] > classes[q]) q++;
+        bucket[q].push_back(s);
+      }
+      for (int cls = 0; cls < 6; cls++) {   // m <= 64 (one row per lane) | m > 64  x  w <= 8 | 16 | 32
+        const int half = cls / 3, W = cls % 3 == 0 ? 8 : cls % 3 == 1 ? 16 : kWaveW, Wlo = cls % 3 == 0 ? 0 : W / 2;
+        std::vector<int> part;
+        for (int s : wave)
+          if ((P.m[s] > 64) == (half == 1) && P.w[s] > Wlo && P.w[s] <= W) part.push_back(s);
+        if (part.empty()) continue;
+        std::stable_sort(part.begin(), part.end(), [&](int a, int b) {
+          const double wa = (double)P.m[a] * P.m[a] * P.w[a], wb = (double)P.m[b] * P.m[b] * P.w[b];
+          return wa > wb;
+        });
+        SmallClass sc{(int)S.small_list.size(), (int)part.size(), 0, W};
+        for (int s : part) {
+          S.small_list.push_back(s);
+          sc.mmax = std::max(sc.mmax, P.m[s]);
+          sc.flops += front_flops(P.m[s], P.w[s]);
+        }
+        lv.small.push_back(sc);
+      }
+      for (int q = 0; q < 4; q++) {
+        if (bucket[q].empty()) continue;
+        SmallClass sc{(int)S.small_list.size(), (int)bucket[q].size(), 0, 0};
+        for (int s : bucket[q]) {
+          S.small_list.push_back(s);
+          sc.mmax = std::max(sc.mmax, P.m[s]);
+          sc.flops += front_flops(P.m[s], P.w[s]);
+        }
+        lv.small.push_back(sc);
+      }
+    }
+    int maxw = 0;
+    for (int s : big) maxw = std::max(maxw, P.w[s]);
+    // Blocked path, one step per 64-column panel kb of every big front of the
+    // level (right-looking, look-ahead 1, Schur updates of depth 64):
+    //   first step  k_panel_first: the front's first diagonal tile factored +
+    //               inverted, the rows below it solved (trsm) by workgroups that
+    //               wait for that inverse (in-launch hand-off)
+    //   each step   k_step: the next panel's diagonal tile updated with panel kb,
+    //               factored and inverted (sdiag); the tiles below it in the
+    //               next panel's column block updated, then solved against that
+    //               inverse (col); the other trailing tiles updated (syrk:
+    //               inline, or a concurrent k_panel_syrk_lds / 128 launch)
+    // Look-ahead bookkeeping: applied[i][j] = the first panel column whose
+    // Schur update column j of big front i has not received yet (every task
+    // updates whole columns: rows from the column down).  A step's tasks must
+    // find their columns uniform; a violation drops the step's skip (below) or
+    // marks the plan invalid (schedule_error).
+    std::vector<std::vector<int>> applied(big.size());
+    for (size_t i = 0; i < big.size(); i++) applied[i].assign(P.m[big[i]], 0);
+    auto uniform = [&](size_t i, int c0, int c1, int k0) {
+      for (int j = c0; j < c1; j++)
+        if (applied[i][j] != k0) return false;
+      return true;
+    };
+    bool apart_chain = false;   // once a step's plain tiles go to their own launch, the later ones do too
+    for (int kb = 0; kb < maxw; kb += kNB) {
+      PanelStep ps;
+      ps.kb = kb;
+      ps.syrk_flops = ps.plain_flops = ps.step_flops = ps.first_flops = 0;
+      ps.col_off = (int)S.col_tasks.size();
+      ps.syrk_off = (int)S.syrk_tasks.size();
+      ps.potrf_off = (int)S.potrf_list.size();
+      ps.sdiag_off = (int)S.sdiag_tasks.size();
+      // first panel of a front: k_panel_first (diagonal + trsm waiters)
+      std::vector<int4> xfirst, xstep;   // distributed top: panels factored by the first / the step launch
+      for (int s : big) {
+        if (kb != 0 || P.w[s] <= 0) continue;
+        const int nb = std::min(kNB, P.w[s]), m = P.m[s];
+        if (dist) xfirst.push_back(make_int4(s, 0, nb, cowner(s, 0)));
+        if (!mine(s, 0)) continue;
+        S.potrf_list.push_back(s);
+        ps.first_flops += 2.0 * nb * nb * (double)nb / 3.0 + (double)std::max(0, m - nb) * nb * nb;
+      }
+      ps.potrf_cnt = (int)S.potrf_list.size() - ps.potrf_off;
+      for (int s : big)
+        if (kb == 0 && P.w[s] > 0 && mine(s, 0))
+          for (int r0 = kNB; r0 < P.m[s]; r0 += kNB) S.col_tasks.push_back(make_int4(s, r0, 0, -1));
+      ps.fcol_cnt = (int)S.col_tasks.size() - ps.col_off;
+      ps.xfirst = add_exchange(S, xfirst);
+      // this panel's Schur update, deferred by kKB-column blocks: inside a block
+      // only the block's remaining columns [kn, be) are updated ("inner", bit 31
+      // of k0: tasks clip columns at the block end); after the block's last
+      // panel the trailing columns [be, m) get the whole block's update.
+      // With the plain tiles in their own launch (apart) the column block the
+      // next step prepares, [kn + 64, kn + 128), is skipped: the next step's
+      // diagonal / column tasks apply this panel's update with their own
+      // (depth 2 panels, or the deferred block + 1 panel), so the next step
+      // does not wait for this step's plain tiles (joined one step later).
+      // The skip is a property of the front alone (its size), never of the
+      // level it sits in: the update grouping -- hence the rounding -- of a
+      // front is the same in every plan (the partitioned plans' fronts are bit
+      // for bit the one-rank plan's).
+      const bool lookahead = !getenv("PGO_NO_LOOKAHEAD");
+      // (PGO_LOOKAHEAD_M: the front height threshold, a test knob)
+      const int la_m = getenv("PGO_LOOKAHEAD_M") ? atoi(getenv("PGO_LOOKAHEAD_M")) : kLookaheadM;
+      auto front_skip = [&](int s) { return lookahead && P.m[s] >= la_m; };
+      // Prep (look-ahead fronts): the step also brings the column block after
+      // the next one, [kn + 64, kn + 128), up to date with the panels before kn
+      // (k_step workgroups beside the diagonal chain), so the next step's
+      // diagonal and column tasks apply one panel only; the plain tiles skip
+      // that block too.  Only for whole 64-column pivot blocks.
+      auto has_prep = [&](int s, int kn_) { return front_skip(s) && kn_ + 2 * kNB <= P.w[s]; };
+      auto plain_range = [&](int s, bool skip, int& cstart, int& cend) {
+        const int w = P.w[s], m = P.m[s], nb = std::min(kNB, w - kb), kn = kb + nb;
+        const int bs = kb & ~(kKB - 1), be = std::min(bs + kKB, w);
+        const bool inner = kn < be;
+        cend = inner ? be : m;
+        cstart = kn < w ? kn + kNB : kn;
+        if (skip && kn + kNB < w) {   // the next step prepares [kn2, kn2 + 64): only when it covers all of it
+          const int kn2 = kn + kNB, bs2 = kn & ~(kKB - 1), be2 = std::min(bs2 + kKB, w);
+          const int colend2 = kn2 < be2 ? be2 : m;
+          if (std::min(kn2 + kNB, colend2) == kn2 + kNB && cstart + kNB <= cend) {
+            cstart += kNB;
+            if (has_prep(s, kn2)) cstart += kNB;   // the next step's prep block
+          }
+        }
+      };
+      auto ntiles = [&](int T) {
+        long long cnt = 0;
+        for (int s : big) {
+          if (P.w[s] <= kb) continue;
+          int c0, c1;
+          plain_range(s, front_skip(s), c0, c1);
+          for (int cc = c0; cc < c1; cc += T) cnt += (P.m[s] - cc + T - 1) / T;
+        }
+        return cnt;
+      };
+      // plain tiles: 128x128 (LDS-pipelined kernel) when there are many rounds of
+      // them (measured: at <= ~500 tiles the 64x64 kernel's finer granularity
+      // wins, scripts/ubench_syrk.hip), else 64x64; few 64-tiles ride in k_step,
+      // many go to a concurrent launch (k_step's LDS request, sized for the
+      // diagonal workgroups, halves their occupancy)
+      const int tile0 = ntiles(kBigTile) >= 4096 ? kBigTile : kTile;
+      const bool apart = apart_chain || !(tile0 == kTile && ntiles(kTile) <= kInlineTiles);
+      std::vector<int4> plain;   // (front, first column, end column, k0): rows from the column down
+      std::vector<int4> prep;    // prep tiles (front, r0, c0, k0), whole 64x64 tiles
+      bool conflict = false;   // a front's next step reads this step's plain tiles
+      for (size_t i = 0; i < big.size(); i++) {
+        const int s = big[i];
+        if (P.w[s] <= kb) continue;
+        const int w = P.w[s], m = P.m[s];
+        const int nb = std::min(kNB, w - kb), kn = kb + nb;
+        const int bs = kb & ~(kKB - 1), be = std::min(bs + kKB, w);
+        const bool inner = kn < be;
+        const int colend = inner ? be : m;   // the device's column clip
+        if (kn < w) {   // next panel: its diagonal tile and the tiles below it
+          const int nb2 = std::min(kNB, w - kn), c1 = std::min(kn + kNB, colend);
+          const int k0 = applied[i][kn];
+          if (!uniform(i, kn, c1, k0)) {
+            if (getenv("PGO_SCHED_DEBUG") && !S.schedule_error)
+              fprintf(stderr, "sched: sdiag front %d w %d m %d kb %d cols [%d,%d) k0 %d\n", s, w, m, kb, kn, c1, k0);
+            S.schedule_error = true;
+          }
+          for (int j = kn; j < c1; j++) applied[i][j] = kn;
+          const int depth = kn - k0, kw = inner ? (k0 | (int)0x80000000) : k0;
+          if (dist) xstep.push_back(make_int4(s, kn, nb2, cowner(s, kn)));
+          const bool own = mine(s, kn);
+          if (own) S.sdiag_tasks.push_back(make_int4(s, kn, kn, kw));
+          ps.step_flops += (double)depth * kNB * (kNB + 1) + 2.0 * nb2 * nb2 * (double)nb2 / 3.0 +
+                           (double)std::min(kNB - nb2, m - kn - nb2) * nb2 * nb2;
+          for (int r0 = kn + kNB; r0 < m; r0 += kNB) {
+            if (own) S.col_tasks.push_back(make_int4(s, r0, kn, kw));
+            const int rows = std::min(kNB, m - r0);
+            ps.step_flops += 2.0 * depth * rows * (c1 - kn) + (double)rows * nb2 * nb2;
+          }
+          ps.syrk_flops += (double)depth * (c1 - kn) * (2.0 * m - kn - c1 + 1.0);
+        }
+        if (has_prep(s, kn)) {
+          const int b0 = kn + kNB, b1 = b0 + kNB, k0 = applied[i][b0];
+          if (!uniform(i, b0, b1, k0) || k0 > kb) {
+            if (getenv("PGO_SCHED_DEBUG") && !S.schedule_error)
+              fprintf(stderr, "sched: prep front %d w %d m %d kb %d cols [%d,%d) k0 %d\n", s, w, m, kb, b0, b1, k0);
+            S.schedule_error = true;
+          }
+          for (int j = b0; j < b1; j++) applied[i][j] = kn;
+          if (mine(s, b0))
+            for (int r0 = b0; r0 < m; r0 += kNB) prep.push_back(make_int4(s, r0, b0, k0));
+          const double f = (double)(kn - k0) * kNB * (2.0 * m - b0 - b1 + 1.0);
+          ps.step_flops += f;
+          ps.syrk_flops += f;
+        }
+        int cstart, cend;
+        plain_range(s, front_skip(s), cstart, cend);
+        if (kn + kNB < w && cstart < cend) {   // the next step prepares [kn2, c2) of this front
+          const int kn2 = kn + kNB, bs2 = kn & ~(kKB - 1), be2 = std::min(bs2 + kKB, w);
+          const int c2 = std::min(kn2 + kNB, kn2 < be2 ? be2 : m);
+          if (cstart < c2 && kn2 < cend) conflict = true;   // this step's plain tiles feed it: lag 1
+        }
+        if (cstart < cend) {
+          int k0 = applied[i][cstart];
+          if (!uniform(i, cstart, cend, k0)) {
+            if (getenv("PGO_SCHED_DEBUG") && !S.schedule_error) {
+              fprintf(stderr, "sched: plain front %d w %d m %d kb %d cols [%d,%d) k0 %d:", s, w, m, kb, cstart, cend, k0);
+              for (int j = cstart; j < cend; j += 16) fprintf(stderr, " %d", applied[i][j]);
+              fprintf(stderr, "\n");
+            }
+            S.schedule_error = true;
+            k0 = kb;
+          }
+          for (int j = cstart; j < cend; j++) applied[i][j] = kn;
+          const int depth = kn - k0;
+          for (int cc = cstart; cc < cend; cc++) ps.plain_flops += 2.0 * depth * (m - cc);
+          plain.push_back(make_int4(s, cstart, cend, inner ? (k0 | (int)0x80000000) : k0));
+        }
+      }
+      ps.syrk_flops += ps.plain_flops;
+      ps.sdiag_cnt = (int)S.sdiag_tasks.size() - ps.sdiag_off;
+      ps.col_cnt = (int)S.col_tasks.size() - ps.col_off - ps.fcol_cnt;
+      S.col_tasks.insert(S.col_tasks.end(), prep.begin(), prep.end());
+      ps.prep_cnt = (int)prep.size();
+      long long cnt128 = 0;
+      for (const int4& u : plain)
+        for (int c0 = u.y; c0 < u.z; c0 += kBigTile) cnt128 += (P.m[u.x] - c0 + kBigTile - 1) / kBigTile;
+      // (distributed top: 64-wide tiles, split where the column owner changes;
+      // a tile's elements are computed alike in either kernel, so this is
+      // bitwise the 128-tile update)
+      ps.syrk_tile = cnt128 >= 4096 && !dist ? kBigTile : kTile;
+      for (const int4& u : plain)
+        for (int c0 = u.y; c0 < u.z; c0 += ps.syrk_tile) {
+          if (!dist) {
+            for (int r0 = c0; r0 < P.m[u.x]; r0 += ps.syrk_tile) S.syrk_tasks.push_back(make_int4(u.x, r0, c0, u.w));
+            continue;
+          }
+          const int ce = std::min(c0 + kTile, u.z);
+          for (int a = c0; a < ce;) {   // runs of one column owner: (a, b)
+            int b = a + 1;
+            while (b < ce && cowner(u.x, b) == cowner(u.x, a)) b++;
+            if (mine(u.x, a)) {
+              const int clip = (a == c0 && b == ce) ? 0 : b - a;
+              for (int r0 = c0; r0 < P.m[u.x]; r0 += kTile)
+                S.syrk_tasks.push_back(make_int4(u.x, r0 | (clip << kClipShift), a, u.w));
+            }
+            a = b;
+          }
+        }
+      {   // XCD-aware order of this step's Schur-update tiles
+        std::vector<int4> mine(S.syrk_tasks.begin() + ps.syrk_off, S.syrk_tasks.end());
+        xcd_order(mine, ps.syrk_tile);
+        std::copy(mine.begin(), mine.end(), S.syrk_tasks.begin() + ps.syrk_off);
+      }
+      ps.syrk_cnt = (int)S.syrk_tasks.size() - ps.syrk_off;
+      ps.syrk_inline = !apart && ps.syrk_tile == kTile && ps.syrk_cnt <= kInlineTiles;
+      // an apart launch no front's next step reads is joined before the step after next
+      ps.plain_lag = ps.syrk_cnt > 0 && !ps.syrk_inline ? (conflict ? 1 : 2) : 0;
+      // (an inline plain after a lag-2 apart one could touch its tiles at once)
+      apart_chain = apart_chain || (ps.plain_lag == 2);
+      if (ps.syrk_inline) ps.step_flops += ps.plain_flops;
+      ps.xstep = add_exchange(S, xstep);
+      lv.panels.push_back(ps);
+    }
+    if (dist) {   // update columns past a front's last whole panel, factored with it: to every rank
+      std::vector<int4> tails;
+      for (int s : big) {
+        const int w = P.w[s], wr = std::min(P.m[s], (w + kNB - 1) / kNB * kNB);
+        if (wr > w) tails.push_back(make_int4(s, w, (wr - w) | (1 << 16), cowner(s, w)));
+      }
+      lv.xtail = add_exchange(S, tails);
+    }
+    // every column has its updates: pivot columns up to their panel, the
+    // trailing ones from every panel
+    for (size_t i = 0; i < big.size(); i++) {
+      const int s = big[i], w = P.w[s];
+      for (int j = 0; j < P.m[s]; j++)
+        if (applied[i][j] != (j < w ? (j / kNB) * kNB : w)) {
+          if (getenv("PGO_SCHED_DEBUG") && !S.schedule_error)
+            fprintf(stderr, "sched: end front %d w %d m %d col %d applied %d\n", s, w, P.m[s], j, applied[i][j]);
+          S.schedule_error = true;
+        }
+    }
+  };
+  std::vector<LevelLists> out(nl);
+  {
+    const int nth = std::min(plan_threads(), nl);
+    std::atomic<int> next(0);
+    auto work = [&] {
+      for (int L; (L = next.fetch_add(1)) < nl;) schedule_level(L, out[L]);
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nth; t++) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+  }
+  P.small_list.clear();
+  P.level_fronts.clear();
+  P.syrk_tasks.clear();
+  P.sdiag_tasks.clear();
+  P.potrf_list.clear();
+  P.col_tasks.clear();
+  P.bwd_tasks.clear();
+  P.bwdc_tasks.clear();
+  P.bwd_pref.clear();
+  P.bwd_part_tasks.clear();
+  P.npart = 0;
+  P.ea_tasks.clear();
+  P.ea_pairs.clear();
+  P.syrk_flops = 0;
+  for (int L = 0; L < nl; L++) {   // merge: level-relative offsets and indices made absolute
+    LevelLists& S = out[L];
+    CholLevel& lv = P.levels[L];
+    const int bx = (int)P.xchg.size(), npart0 = P.npart;
+    lv.front_off += (int)P.level_fronts.size();
+    lv.bwd_part.off += (int)P.bwd_part_tasks.size();
+    for (int4& t : S.bwd_part_tasks) t.w += npart0;
+    for (int q = lv.bwd[0].off; q < lv.bwd[0].off + lv.bwd[0].cnt; q++) S.bwd_pref[q].x += npart0;   // init tasks
+    for (SolveStep& st : lv.bwd) st.off += (int)P.bwd_tasks.size();
+    lv.bwdc.off += (int)P.bwdc_tasks.size();
+    for (int& o : lv.ea_off) o += (int)P.ea_tasks.size();
+    for (int4& t : S.ea_tasks) t.z += (int)P.ea_pairs.size();
+    for (SmallClass& sc : lv.small) sc.off += (int)P.small_list.size();
+    for (PanelStep& ps : lv.panels) {
+      ps.potrf_off += (int)P.potrf_list.size();
+      ps.col_off += (int)P.col_tasks.size();
+      ps.syrk_off += (int)P.syrk_tasks.size();
+      ps.sdiag_off += (int)P.sdiag_tasks.size();
+      if (ps.xfirst >= 0) ps.xfirst += bx;
+      if (ps.xstep >= 0) ps.xstep += bx;
+      P.syrk_flops += ps.plain_flops;
+    }
+    if (lv.xtail >= 0) lv.xtail += bx;
+    for (XExchange& x : S.xchg) x.off += (int)P.xp_tasks.size();
+    auto cat = [](auto& dst, const auto& src) { dst.insert(dst.end(), src.begin(), src.end()); };
+    cat(P.small_list, S.small_list);
+    cat(P.level_fronts, S.level_fronts);
+    cat(P.potrf_list, S.potrf_list);
+    cat(P.syrk_tasks, S.syrk_tasks);
+    cat(P.sdiag_tasks, S.sdiag_tasks);
+    cat(P.col_tasks, S.col_tasks);
+    cat(P.bwd_tasks, S.bwd_tasks);
+    cat(P.bwdc_tasks, S.bwdc_tasks);
+    cat(P.bwd_pref, S.bwd_pref);
+    cat(P.bwd_part_tasks, S.bwd_part_tasks);
+    cat(P.ea_tasks, S.ea_tasks);
+    cat(P.ea_pairs, S.ea_pairs);
+    cat(P.xchg, S.xchg);
+    cat(P.xp_tasks, S.xp_tasks);
+    cat(P.xp_loff, S.xp_loff);
+    cat(P.xp_lstride, S.xp_lstride);
+    P.xp_rslot = std::max(P.xp_rslot, S.xp_rslot);
+    P.npart += S.npart;
+    P.schedule_error = P.schedule_error || S.schedule_error;
+  }
+  phase("schedule");
+  chol_assembly(P, row_ptr, slot_col);
+  phase("assembly");
+}
+
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
   // PGO_PLAN_TIMING: phase times of the analysis on stderr (diagnostics)
   static const bool timing = getenv("PGO_PLAN_TIMING") != nullptr;
@@ -403,29 +1086,13 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   P.rptr.assign(ns + 1, 0);
   P.m.resize(ns);
   P.w.resize(ns);
-  P.foff.assign(ns + 1, 0);
-  P.toff.assign(ns + 1, 0);
-  P.voff.assign(ns + 1, 0);
-  P.flops = 0;
-  P.nnzl = 0;
   for (int s = 0; s < ns; s++) {
     const int wp = P.sfirst[s + 1] - P.sfirst[s];
     P.w[s] = 3 * wp;
     P.m[s] = 3 * (wp + (int)below[s].size());
     P.rptr[s + 1] = P.rptr[s] + wp + (int)below[s].size();
-    const long long mm = P.m[s];
-    P.foff[s + 1] = P.foff[s] + ((mm * mm + 7) / 8) * 8;   // 64-byte aligned fronts
-    P.voff[s + 1] = P.voff[s] + ((P.m[s] + 7) / 8) * 8;
-    P.toff[s + 1] = P.toff[s] + (long long)((P.w[s] + 63) / 64) * 4096;
-    for (int k = 0; k < P.w[s]; k++) {
-      const double r = P.m[s] - k - 1;
-      P.flops += 1 + r + r * (r + 1);
-      P.nnzl += r + 1;
-    }
   }
-  P.ftotal = P.foff[ns];
-  P.ttotal = P.toff[ns];
-  P.vtotal = P.voff[ns];
+  size_fronts(P);
   P.rows.resize(P.rptr[ns]);
   for (int s = 0; s < ns; s++) {
     int q = P.rptr[s];
@@ -458,539 +1125,9 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
     P.dg_front[j] = snode[j];
     P.dg_loc[j] = j - P.sfirst[snode[j]];
   }
-  // ---- multi-GPU subtree partition (part_size > 1, DESIGN.md "Multi-GPU"):
-  // rank part_rank factorises the fronts of its subtrees (phase 1), then every
-  // rank the replicated top fronts (phase 2), after the subtree roots' update
-  // matrices / vectors have been exchanged.  Storage only for the fronts this
-  // rank touches: its own, the top, and the other ranks' subtree roots (their
-  // update matrices arrive in the exchange).  One rank: everything is phase 1.
-  const int psz = std::max(P.part_size, 1), prk = P.part_rank;
-  P.owner = partition_subtrees(P, psz);
-  P.subtree_cnt.assign(ns, 1);
-  for (int s = 0; s < ns; s++)
-    if (P.parent[s] >= 0) P.subtree_cnt[P.parent[s]] += P.subtree_cnt[s];
-  std::vector<char> need(ns, 0);
-  P.xroot.clear();
-  P.xroot_rank.clear();
-  for (int s = 0; s < ns; s++) {
-    const bool root = P.owner[s] >= 0 && (P.parent[s] < 0 || P.owner[P.parent[s]] < 0);
-    if (root) {
-      P.xroot.push_back(s);
-      P.xroot_rank.push_back(P.owner[s]);
-    }
-    need[s] = P.owner[s] == prk || P.owner[s] < 0 || (root && P.parent[s] >= 0);
-  }
-  if (psz > 1) {   // offsets over the needed fronts only
-    for (int s = 0; s < ns; s++) {
-      const long long mm = need[s] ? P.m[s] : 0;
-      P.foff[s + 1] = P.foff[s] + ((mm * mm + 7) / 8) * 8;
-      P.voff[s + 1] = P.voff[s] + (need[s] ? ((P.m[s] + 7) / 8) * 8 : 0);
-      P.toff[s + 1] = P.toff[s] + (need[s] ? (long long)((P.w[s] + 63) / 64) * 4096 : 0);
-    }
-    P.ftotal = P.foff[ns];
-    P.ttotal = P.toff[ns];
-    P.vtotal = P.voff[ns];
-  }
-  // exchange layout: per rank its roots' payloads (packed lower update matrix,
-  // then the update vector) back to back; the solve's: its subtrees' poses
-  P.xroot_off.assign(P.xroot.size(), 0);
-  P.xsize.assign(psz, 0);
-  P.xsol_size.assign(psz, 0);
-  P.xsol_ranges.clear();
-  for (size_t q = 0; q < P.xroot.size(); q++) {
-    const int sr = P.xroot[q], r = P.xroot_rank[q];
-    const long long u = P.m[sr] - P.w[sr];
-    P.xroot_off[q] = P.xsize[r];
-    P.xsize[r] += u * (u + 1) / 2 + u;
-    const int first = sr - P.subtree_cnt[sr] + 1;   // the subtree: postorder fronts [first, sr]
-    P.xsol_ranges.push_back(make_int4(r, 3 * P.sfirst[first], 3 * P.sfirst[sr + 1], (int)P.xsol_size[r]));
-    P.xsol_size[r] += 3LL * (P.sfirst[sr + 1] - P.sfirst[first]);
-  }
-  P.xmax = *std::max_element(P.xsize.begin(), P.xsize.end());
-  P.xsol_max = *std::max_element(P.xsol_size.begin(), P.xsol_size.end());
-  phase("partition");
-  // ---- level schedules: phase 1 (this rank's subtree fronts) then phase 2 (top)
-  std::vector<std::vector<int>> bylevel;
-  for (int phase = 0; phase < 2; phase++) {
-    int hmax = -1;
-    for (int s = 0; s < ns; s++)
-      if ((phase == 0 ? P.owner[s] == prk : P.owner[s] < 0)) hmax = std::max(hmax, P.height[s]);
-    const size_t base = bylevel.size();
-    bylevel.resize(base + hmax + 1);
-    for (int s = 0; s < ns; s++)
-      if ((phase == 0 ? P.owner[s] == prk : P.owner[s] < 0)) bylevel[base + P.height[s]].push_back(s);
-    if (phase == 0) P.split = (int)bylevel.size();
-  }
-  {   // drop empty levels (a height with no front of this rank), keeping the split
-    std::vector<std::vector<int>> kept;
-    int split = 0;
-    for (size_t L = 0; L < bylevel.size(); L++)
-      if (!bylevel[L].empty()) {
-        kept.push_back(std::move(bylevel[L]));
-        if ((int)L < P.split) split++;
-      }
-    bylevel.swap(kept);
-    P.split = split;
-  }
-  auto blocked = [&](int s) { return is_blocked(P, s); };
-  // ---- distributed top (part_size > 1): the top fronts' columns are dealt to
-  // the ranks instead of every rank factoring every top front.  A blocked top
-  // front's pivot columns go by 64-column panel, round robin (continuing over
-  // the fronts); its columns past the last whole panel (the update matrix) take
-  // the rank of the parent column they extend-add into, so a rank's share of a
-  // parent's columns is assembled from its own shares of the children's update
-  // matrices (no exchange of update matrices between top fronts).  Small top
-  // fronts (one workgroup / wavefront each) are computed by every rank (-1),
-  // and so are the update columns of their children.  Each column's updates
-  // are applied by its rank only, with the same tasks (same depths, same
-  // order) as the one-rank plan: bitwise the one-rank factor.  A rank receives
-  // every panel (broadcast by its owner right after it is factored) for its own
-  // columns' updates and the replicated backward solve.
-  // (PGO_DIST_TOP=0: the top fronts replicated on every rank instead -- the
-  // previous scheme, kept as a reference for the host self-test)
-  const bool dtop = psz > 1 && !(getenv("PGO_DIST_TOP") && atoi(getenv("PGO_DIST_TOP")) == 0);
-  P.cown_off.assign(ns, -1);
-  P.cown.clear();
-  if (dtop) column_owners(P, P.owner, psz, P.cown_off, P.cown);
-  P.xchg.clear();
-  P.xp_tasks.clear();
-  P.xp_loff.clear();
-  P.xp_lstride.clear();
-  P.xp_rslot = 0;
-  // an exchange point: every panel / tail in `items` (front, kn, nb | kind << 16,
-  // owner) goes from its owner to every rank (one broadcast per sending rank)
-  auto add_exchange = [&](const std::vector<int4>& items) -> int {
-    if (items.empty()) return -1;
-    XExchange x;
-    x.off = (int)P.xp_tasks.size();
-    x.cnt = (int)items.size();
-    x.size.assign(psz, 0);
-    for (const int4& t : items) {
-      const int s = t.x, kn = t.y, nb = t.z & 0xffff, kind = t.z >> 16, m = P.m[s];
-      const long long sz = kind == 0 ? (long long)(m - kn) * nb + 4096 + (m - kn) : (long long)(m - kn) * nb;
-      P.xp_tasks.push_back(t);
-      P.xp_loff.push_back(x.size[t.w]);
-      x.size[t.w] += sz;
-    }
-    for (int q = x.off; q < x.off + x.cnt; q++) P.xp_lstride.push_back(x.size[P.xp_tasks[q].w]);
-    for (long long v : x.size) P.xp_rslot = std::max(P.xp_rslot, v);
-    P.xchg.push_back(x);
-    return (int)P.xchg.size() - 1;
-  };
-  const int nl = (int)bylevel.size();
-  P.levels.assign(nl, CholLevel());
-  P.small_list.clear();
-  P.level_fronts.clear();
-  P.syrk_tasks.clear();
-  P.sdiag_tasks.clear();
-  P.potrf_list.clear();
-  P.col_tasks.clear();
-  P.bwd_tasks.clear();
-  P.bwdc_tasks.clear();
-  P.bwd_pref.clear();
-  P.bwd_part_tasks.clear();
-  P.npart = 0;
-  P.ea_tasks.clear();
-  P.ea_pairs.clear();
-  for (int L = 0; L < nl; L++) {
-    CholLevel& lv = P.levels[L];
-    // distributed top level: this rank generates only the tasks of its columns
-    const bool dist = dtop && L >= P.split;
-    auto mine = [&](int s, int col) {
-      if (!dist) return true;
-      const int o = P.cown[P.cown_off[s] + col];
-      return o < 0 || o == prk;
-    };
-    auto cowner = [&](int s, int col) { return dist ? P.cown[P.cown_off[s] + col] : -1; };
-    lv.front_off = (int)P.level_fronts.size();
-    lv.front_cnt = (int)bylevel[L].size();
-    for (int s : bylevel[L]) {
-      P.level_fronts.push_back(s);
-      lv.maxm = std::max(lv.maxm, P.m[s]);
-      if (P.m[s] <= kSmallFront) lv.small_maxm = std::max(lv.small_maxm, P.m[s]);
-    }
-    // blocked backward solve (64-column blocks of each front's pivot columns);
-    // the forward substitution is carried by the factorisation
-    for (int s : bylevel[L]) lv.maxblk = std::max(lv.maxblk, (P.w[s] + 63) / 64);
-    {                                            // backward init: all columns vs the rows below w
-      // partial products L21[r0:r0+kBwdRows, block]' x_below, one task each,
-      // reduced in fixed order by the init task of the block
-      SolveStep sp{(int)P.bwd_part_tasks.size(), 0};
-      SolveStep st{(int)P.bwd_tasks.size(), 0};
-      for (int s : bylevel[L]) {
-        const int w = P.w[s], m = P.m[s], nblk = (w + 63) / 64;
-        for (int b = 0; b < nblk; b++) {
-          const int p0 = P.npart;
-          for (int r0 = w; r0 < m; r0 += kBwdRows) P.bwd_part_tasks.push_back(make_int4(s, b * 64, r0, P.npart++));
-          P.bwd_tasks.push_back(make_int4(s, b * 64, std::min(b * 64 + 64, w), b == nblk - 1 ? b : -1));
-          P.bwd_pref.push_back(make_int2(p0, P.npart - p0));
-        }
-      }
-      sp.cnt = (int)P.bwd_part_tasks.size() - sp.off;
-      for (int q = sp.off; q < sp.off + sp.cnt; q++) {
-        const int4 t = P.bwd_part_tasks[q];
-        lv.bwd_part_flops += 2.0 * std::min(64, P.w[t.x] - t.y) * std::min(kBwdRows, P.m[t.x] - t.z);
-      }
-      st.cnt = (int)P.bwd_tasks.size() - st.off;
-      lv.bwd_part = sp;
-      lv.bwd.push_back(st);
-    }
-    {   // the same steps as one chained launch (k_bwd_chain): block j of a front
-        // after the blocks above it, tasks ordered by distance from the last
-        // block so that every workgroup waits only on earlier-dispatched ones
-      lv.bwdc.off = (int)P.bwdc_tasks.size();
-      for (int d = 1; d < lv.maxblk; d++)
-        for (int s : bylevel[L]) {
-          const int w = P.w[s], nblk = (w + 63) / 64;
-          if (d >= nblk) continue;
-          const int j = nblk - 1 - d;
-          P.bwdc_tasks.push_back(make_int4(s, j * 64, j * 64 + 64, j));
-        }
-      lv.bwdc.cnt = (int)P.bwdc_tasks.size() - lv.bwdc.off;
-    }
-    for (int b = lv.maxblk - 1; b >= 1; b--) {   // backward step b: columns left of block b
-      SolveStep st{(int)P.bwd_tasks.size(), 0};
-      for (int s : bylevel[L]) {
-        const int w = P.w[s], nblk = (w + 63) / 64;
-        if (b >= nblk) continue;
-        for (int c = 0; c < b; c++)
-        {
-          P.bwd_tasks.push_back(make_int4(s, c * 64, c * 64 + 64, c == b - 1 ? c : -1));
-          P.bwd_pref.push_back(make_int2(0, 0));
-        }
-      }
-      st.cnt = (int)P.bwd_tasks.size() - st.off;
-      lv.bwd.push_back(st);
-    }
-    // assembly: one task per 64x64 tile of every front's lower triangle, which
-    // it writes whole: its H entries (+ lambda on the diagonal), then the
-    // update-matrix elements of the front's children in order (fixed
-    // summation order, no atomics), each child contributing a rectangle of its
-    // update matrix (child rows [a0, a0+nr) x columns [b0, b0+nc), the rows /
-    // columns whose parent index falls in the tile).  No front is zeroed.
-    lv.ea_off.push_back((int)P.ea_tasks.size());
-    for (int sp : bylevel[L]) {
-      const int nt = (P.m[sp] + 63) / 64;
-      std::vector<std::vector<int4>> tiles((size_t)nt * (nt + 1) / 2);
-      for (int q = P.cptr[sp]; q < P.cptr[sp + 1]; q++) {
-        const int c = P.children[q];
-        const int u = P.m[c] - P.w[c];
-        std::vector<int3> runs;   // (tile, first child row, rows)
-        for (int a = 0; a < u; a++) {
-          const int t = (3 * P.ea_rel[P.ea_ptr[c] + a / 3] + a % 3) / 64;
-          if (runs.empty() || runs.back().x != t) runs.push_back(make_int3(t, a, 0));
-          runs.back().z++;
-        }
-        for (size_t i = 0; i < runs.size(); i++)
-          for (size_t j = 0; j <= i; j++)
-            tiles[(size_t)runs[i].x * (runs[i].x + 1) / 2 + runs[j].x].push_back(
-                make_int4(c, runs[i].y, runs[j].y, runs[i].z | (runs[j].z << 8)));
-      }
-      for (int ti = 0; ti < nt; ti++)
-        for (int tj = 0; tj <= ti; tj++) {
-          const auto& v = tiles[ti * (ti + 1) / 2 + tj];
-          P.ea_tasks.push_back(make_int4(sp, (ti << 16) | tj, (int)P.ea_pairs.size(), (int)v.size()));
-          P.ea_pairs.insert(P.ea_pairs.end(), v.begin(), v.end());
-        }
-    }
-    lv.ea_cnt.push_back((int)P.ea_tasks.size() - lv.ea_off.back());
-    // small fronts (m <= kSmallFront): with w <= kWaveW one wavefront each (the
-    // m x w panel in LDS, the rank-w Schur update streamed), largest first;
-    // else one workgroup each with the whole front in LDS, launched per size
-    // class so the LDS request (m^2 doubles) does not cap the occupancy
-    std::vector<int> big;
-    {
-      const int classes[4] = {32, 64, 96, kSmallFront};
-      std::vector<int> bucket[4], wave;
-      for (int s : bylevel[L]) {
-        // w > kWaveW: the blocked path (64-column panels, every front of the
-        // level in the same launches) -- a whole-front-in-LDS workgroup runs
-        // its w pivots one after the other at ~2 us each
-        if (blocked(s)) {
-          big.push_back(s);
-          continue;
-        }
-        if (P.w[s] <= kWaveW) {
-          wave.push_back(s);
-          continue;
-        }
-        int q = 0;
-        while (P.m[s] > classes[q]) q++;
-        bucket[q].push_back(s);
-      }
-      for (int cls = 0; cls < 6; cls++) {   // m <= 64 (one row per lane) | m > 64  x  w <= 8 | 16 | 32
-        const int half = cls / 3, W = cls % 3 == 0 ? 8 : cls % 3 == 1 ? 16 : kWaveW, Wlo = cls % 3 == 0 ? 0 : W / 2;
-        std::vector<int> part;
-        for (int s : wave)
-          if ((P.m[s] > 64) == (half == 1) && P.w[s] > Wlo && P.w[s] <= W) part.push_back(s);
-        if (part.empty()) continue;
-        std::stable_sort(part.begin(), part.end(), [&](int a, int b) {
-          const double wa = (double)P.m[a] * P.m[a] * P.w[a], wb = (double)P.m[b] * P.m[b] * P.w[b];
-          return wa > wb;
-        });
-        SmallClass sc{(int)P.small_list.size(), (int)part.size(), 0, W};
-        for (int s : part) {
-          P.small_list.push_back(s);
-          sc.mmax = std::max(sc.mmax, P.m[s]);
-          sc.flops += front_flops(P.m[s], P.w[s]);
-        }
-        lv.small.push_back(sc);
-      }
-      for (int q = 0; q < 4; q++) {
-        if (bucket[q].empty()) continue;
-        SmallClass sc{(int)P.small_list.size(), (int)bucket[q].size(), 0, 0};
-        for (int s : bucket[q]) {
-          P.small_list.push_back(s);
-          sc.mmax = std::max(sc.mmax, P.m[s]);
-          sc.flops += front_flops(P.m[s], P.w[s]);
-        }
-        lv.small.push_back(sc);
-      }
-    }
-    int maxw = 0;
-    for (int s : big) maxw = std::max(maxw, P.w[s]);
-    // Blocked path, one step per 64-column panel kb of every big front of the
-    // level (right-looking, look-ahead 1, Schur updates of depth 64):
-    //   first step  k_panel_first: the front's first diagonal tile factored +
-    //               inverted, the rows below it solved (trsm) by workgroups that
-    //               wait for that inverse (in-launch hand-off)
-    //   each step   k_step: the next panel's diagonal tile updated with panel kb,
-    //               factored and inverted (sdiag); the tiles below it in the
-    //               next panel's column block updated, then solved against that
-    //               inverse (col); the other trailing tiles updated (syrk:
-    //               inline, or a concurrent k_panel_syrk_lds / 128 launch)
-    // Look-ahead bookkeeping: applied[i][j] = the first panel column whose
-    // Schur update column j of big front i has not received yet (every task
-    // updates whole columns: rows from the column down).  A step's tasks must
-    // find their columns uniform; a violation drops the step's skip (below) or
-    // marks the plan invalid (schedule_error).
-    std::vector<std::vector<int>> applied(big.size());
-    for (size_t i = 0; i < big.size(); i++) applied[i].assign(P.m[big[i]], 0);
-    auto uniform = [&](size_t i, int c0, int c1, int k0) {
-      for (int j = c0; j < c1; j++)
-        if (applied[i][j] != k0) return false;
-      return true;
-    };
-    bool apart_chain = false;   // once a step's plain tiles go to their own launch, the later ones do too
-    for (int kb = 0; kb < maxw; kb += kNB) {
-      PanelStep ps;
-      ps.kb = kb;
-      ps.syrk_flops = ps.plain_flops = ps.step_flops = ps.first_flops = 0;
-      ps.col_off = (int)P.col_tasks.size();
-      ps.syrk_off = (int)P.syrk_tasks.size();
-      ps.potrf_off = (int)P.potrf_list.size();
-      ps.sdiag_off = (int)P.sdiag_tasks.size();
-      // first panel of a front: k_panel_first (diagonal + trsm waiters)
-      std::vector<int4> xfirst, xstep;   // distributed top: panels factored by the first / the step launch
-      for (int s : big) {
-        if (kb != 0 || P.w[s] <= 0) continue;
-        const int nb = std::min(kNB, P.w[s]), m = P.m[s];
-        if (dist) xfirst.push_back(make_int4(s, 0, nb, cowner(s, 0)));
-        if (!mine(s, 0)) continue;
-        P.potrf_list.push_back(s);
-        ps.first_flops += 2.0 * nb * nb * (double)nb / 3.0 + (double)std::max(0, m - nb) * nb * nb;
-      }
-      ps.potrf_cnt = (int)P.potrf_list.size() - ps.potrf_off;
-      for (int s : big)
-        if (kb == 0 && P.w[s] > 0 && mine(s, 0))
-          for (int r0 = kNB; r0 < P.m[s]; r0 += kNB) P.col_tasks.push_back(make_int4(s, r0, 0, -1));
-      ps.fcol_cnt = (int)P.col_tasks.size() - ps.col_off;
-      ps.xfirst = add_exchange(xfirst);
-      // this panel's Schur update, deferred by kKB-column blocks: inside a block
-      // only the block's remaining columns [kn, be) are updated ("inner", bit 31
-      // of k0: tasks clip columns at the block end); after the block's last
-      // panel the trailing columns [be, m) get the whole block's update.
-      // With the plain tiles in their own launch (apart) the column block the
-      // next step prepares, [kn + 64, kn + 128), is skipped: the next step's
-      // diagonal / column tasks apply this panel's update with their own
-      // (depth 2 panels, or the deferred block + 1 panel), so the next step
-      // does not wait for this step's plain tiles (joined one step later).
-      // The skip is a property of the front alone (its size), never of the
-      // level it sits in: the update grouping -- hence the rounding -- of a
-      // front is the same in every plan (the partitioned plans' fronts are bit
-      // for bit the one-rank plan's).
-      const bool lookahead = !getenv("PGO_NO_LOOKAHEAD");
-      // (PGO_LOOKAHEAD_M: the front height threshold, a test knob)
-      const int la_m = getenv("PGO_LOOKAHEAD_M") ? atoi(getenv("PGO_LOOKAHEAD_M")) : kLookaheadM;
-      auto front_skip = [&](int s) { return lookahead && P.m[s] >= la_m; };
-      // Prep (look-ahead fronts): the step also brings the column block after
-      // the next one, [kn + 64, kn + 128), up to date with the panels before kn
-      // (k_step workgroups beside the diagonal chain), so the next step's
-      // diagonal and column tasks apply one panel only; the plain tiles skip
-      // that block too.  Only for whole 64-column pivot blocks.
-      auto has_prep = [&](int s, int kn_) { return front_skip(s) && kn_ + 2 * kNB <= P.w[s]; };
-      auto plain_range = [&](int s, bool skip, int& cstart, int& cend) {
-        const int w = P.w[s], m = P.m[s], nb = std::min(kNB, w - kb), kn = kb + nb;
-        const int bs = kb & ~(kKB - 1), be = std::min(bs + kKB, w);
-        const bool inner = kn < be;
-        cend = inner ? be : m;
-        cstart = kn < w ? kn + kNB : kn;
-        if (skip && kn + kNB < w) {   // the next step prepares [kn2, kn2 + 64): only when it covers all of it
-          const int kn2 = kn + kNB, bs2 = kn & ~(kKB - 1), be2 = std::min(bs2 + kKB, w);
-          const int colend2 = kn2 < be2 ? be2 : m;
-          if (std::min(kn2 + kNB, colend2) == kn2 + kNB && cstart + kNB <= cend) {
-            cstart += kNB;
-            if (has_prep(s, kn2)) cstart += kNB;   // the next step's prep block
-          }
-        }
-      };
-      auto ntiles = [&](int T) {
-        long long cnt = 0;
-        for (int s : big) {
-          if (P.w[s] <= kb) continue;
-          int c0, c1;
-          plain_range(s, front_skip(s), c0, c1);
-          for (int cc = c0; cc < c1; cc += T) cnt += (P.m[s] - cc + T - 1) / T;
-        }
-        return cnt;
-      };
-      // plain tiles: 128x128 (LDS-pipelined kernel) when there are many rounds of
-      // them (measured: at <= ~500 tiles the 64x64 kernel's finer granularity
-      // wins, scripts/ubench_syrk.hip), else 64x64; few 64-tiles ride in k_step,
-      // many go to a concurrent launch (k_step's LDS request, sized for the
-      // diagonal workgroups, halves their occupancy)
-      const int tile0 = ntiles(kBigTile) >= 4096 ? kBigTile : kTile;
-      const bool apart = apart_chain || !(tile0 == kTile && ntiles(kTile) <= kInlineTiles);
-      std::vector<int4> plain;   // (front, first column, end column, k0): rows from the column down
-      std::vector<int4> prep;    // prep tiles (front, r0, c0, k0), whole 64x64 tiles
-      bool conflict = false;   // a front's next step reads this step's plain tiles
-      for (size_t i = 0; i < big.size(); i++) {
-        const int s = big[i];
-        if (P.w[s] <= kb) continue;
-        const int w = P.w[s], m = P.m[s];
-        const int nb = std::min(kNB, w - kb), kn = kb + nb;
-        const int bs = kb & ~(kKB - 1), be = std::min(bs + kKB, w);
-        const bool inner = kn < be;
-        const int colend = inner ? be : m;   // the device's column clip
-        if (kn < w) {   // next panel: its diagonal tile and the tiles below it
-          const int nb2 = std::min(kNB, w - kn), c1 = std::min(kn + kNB, colend);
-          const int k0 = applied[i][kn];
-          if (!uniform(i, kn, c1, k0)) {
-            if (getenv("PGO_SCHED_DEBUG") && !P.schedule_error)
-              fprintf(stderr, "sched: sdiag front %d w %d m %d kb %d cols [%d,%d) k0 %d\n", s, w, m, kb, kn, c1, k0);
-            P.schedule_error = true;
-          }
-          for (int j = kn; j < c1; j++) applied[i][j] = kn;
-          const int depth = kn - k0, kw = inner ? (k0 | (int)0x80000000) : k0;
-          if (dist) xstep.push_back(make_int4(s, kn, nb2, cowner(s, kn)));
-          const bool own = mine(s, kn);
-          if (own) P.sdiag_tasks.push_back(make_int4(s, kn, kn, kw));
-          ps.step_flops += (double)depth * kNB * (kNB + 1) + 2.0 * nb2 * nb2 * (double)nb2 / 3.0 +
-                           (double)std::min(kNB - nb2, m - kn - nb2) * nb2 * nb2;
-          for (int r0 = kn + kNB; r0 < m; r0 += kNB) {
-            if (own) P.col_tasks.push_back(make_int4(s, r0, kn, kw));
-            const int rows = std::min(kNB, m - r0);
-            ps.step_flops += 2.0 * depth * rows * (c1 - kn) + (double)rows * nb2 * nb2;
-          }
-          ps.syrk_flops += (double)depth * (c1 - kn) * (2.0 * m - kn - c1 + 1.0);
-        }
-        if (has_prep(s, kn)) {
-          const int b0 = kn + kNB, b1 = b0 + kNB, k0 = applied[i][b0];
-          if (!uniform(i, b0, b1, k0) || k0 > kb) {
-            if (getenv("PGO_SCHED_DEBUG") && !P.schedule_error)
-              fprintf(stderr, "sched: prep front %d w %d m %d kb %d cols [%d,%d) k0 %d\n", s, w, m, kb, b0, b1, k0);
-            P.schedule_error = true;
-          }
-          for (int j = b0; j < b1; j++) applied[i][j] = kn;
-          if (mine(s, b0))
-            for (int r0 = b0; r0 < m; r0 += kNB) prep.push_back(make_int4(s, r0, b0, k0));
-          const double f = (double)(kn - k0) * kNB * (2.0 * m - b0 - b1 + 1.0);
-          ps.step_flops += f;
-          ps.syrk_flops += f;
-        }
-        int cstart, cend;
-        plain_range(s, front_skip(s), cstart, cend);
-        if (kn + kNB < w && cstart < cend) {   // the next step prepares [kn2, c2) of this front
-          const int kn2 = kn + kNB, bs2 = kn & ~(kKB - 1), be2 = std::min(bs2 + kKB, w);
-          const int c2 = std::min(kn2 + kNB, kn2 < be2 ? be2 : m);
-          if (cstart < c2 && kn2 < cend) conflict = true;   // this step's plain tiles feed it: lag 1
-        }
-        if (cstart < cend) {
-          int k0 = applied[i][cstart];
-          if (!uniform(i, cstart, cend, k0)) {
-            if (getenv("PGO_SCHED_DEBUG") && !P.schedule_error) {
-              fprintf(stderr, "sched: plain front %d w %d m %d kb %d cols [%d,%d) k0 %d:", s, w, m, kb, cstart, cend, k0);
-              for (int j = cstart; j < cend; j += 16) fprintf(stderr, " %d", applied[i][j]);
-              fprintf(stderr, "\n");
-            }
-            P.schedule_error = true;
-            k0 = kb;
-          }
-          for (int j = cstart; j < cend; j++) applied[i][j] = kn;
-          const int depth = kn - k0;
-          for (int cc = cstart; cc < cend; cc++) ps.plain_flops += 2.0 * depth * (m - cc);
-          plain.push_back(make_int4(s, cstart, cend, inner ? (k0 | (int)0x80000000) : k0));
-        }
-      }
-      ps.syrk_flops += ps.plain_flops;
-      ps.sdiag_cnt = (int)P.sdiag_tasks.size() - ps.sdiag_off;
-      ps.col_cnt = (int)P.col_tasks.size() - ps.col_off - ps.fcol_cnt;
-      P.col_tasks.insert(P.col_tasks.end(), prep.begin(), prep.end());
-      ps.prep_cnt = (int)prep.size();
-      long long cnt128 = 0;
-      for (const int4& u : plain)
-        for (int c0 = u.y; c0 < u.z; c0 += kBigTile) cnt128 += (P.m[u.x] - c0 + kBigTile - 1) / kBigTile;
-      // (distributed top: 64-wide tiles, split where the column owner changes;
-      // a tile's elements are computed alike in either kernel, so this is
-      // bitwise the 128-tile update)
-      ps.syrk_tile = cnt128 >= 4096 && !dist ? kBigTile : kTile;
-      for (const int4& u : plain)
-        for (int c0 = u.y; c0 < u.z; c0 += ps.syrk_tile) {
-          if (!dist) {
-            for (int r0 = c0; r0 < P.m[u.x]; r0 += ps.syrk_tile) P.syrk_tasks.push_back(make_int4(u.x, r0, c0, u.w));
-            continue;
-          }
-          const int ce = std::min(c0 + kTile, u.z);
-          for (int a = c0; a < ce;) {   // runs of one column owner: (a, b)
-            int b = a + 1;
-            while (b < ce && cowner(u.x, b) == cowner(u.x, a)) b++;
-            if (mine(u.x, a)) {
-              const int clip = (a == c0 && b == ce) ? 0 : b - a;
-              for (int r0 = c0; r0 < P.m[u.x]; r0 += kTile)
-                P.syrk_tasks.push_back(make_int4(u.x, r0 | (clip << kClipShift), a, u.w));
-            }
-            a = b;
-          }
-        }
-      {   // XCD-aware order of this step's Schur-update tiles
-        std::vector<int4> mine(P.syrk_tasks.begin() + ps.syrk_off, P.syrk_tasks.end());
-        xcd_order(mine, ps.syrk_tile);
-        std::copy(mine.begin(), mine.end(), P.syrk_tasks.begin() + ps.syrk_off);
-      }
-      ps.syrk_cnt = (int)P.syrk_tasks.size() - ps.syrk_off;
-      ps.syrk_inline = !apart && ps.syrk_tile == kTile && ps.syrk_cnt <= kInlineTiles;
-      // an apart launch no front's next step reads is joined before the step after next
-      ps.plain_lag = ps.syrk_cnt > 0 && !ps.syrk_inline ? (conflict ? 1 : 2) : 0;
-      // (an inline plain after a lag-2 apart one could touch its tiles at once)
-      apart_chain = apart_chain || (ps.plain_lag == 2);
-      if (ps.syrk_inline) ps.step_flops += ps.plain_flops;
-      P.syrk_flops += ps.plain_flops;
-      ps.xstep = add_exchange(xstep);
-      lv.panels.push_back(ps);
-    }
-    if (dist) {   // update columns past a front's last whole panel, factored with it: to every rank
-      std::vector<int4> tails;
-      for (int s : big) {
-        const int w = P.w[s], wr = std::min(P.m[s], (w + kNB - 1) / kNB * kNB);
-        if (wr > w) tails.push_back(make_int4(s, w, (wr - w) | (1 << 16), cowner(s, w)));
-      }
-      lv.xtail = add_exchange(tails);
-    }
-    // every column has its updates: pivot columns up to their panel, the
-    // trailing ones from every panel
-    for (size_t i = 0; i < big.size(); i++) {
-      const int s = big[i], w = P.w[s];
-      for (int j = 0; j < P.m[s]; j++)
-        if (applied[i][j] != (j < w ? (j / kNB) * kNB : w)) {
-          if (getenv("PGO_SCHED_DEBUG") && !P.schedule_error)
-            fprintf(stderr, "sched: end front %d w %d m %d col %d applied %d\n", s, w, P.m[s], j, applied[i][j]);
-          P.schedule_error = true;
-        }
-    }
-  }
-  phase("schedule");
-  chol_assembly(P, row_ptr, slot_col);
-  phase("assembly");
+  P.n_analyzed = n;
+  P.flops_analyzed = P.flops;
+  chol_schedule(P, row_ptr, slot_col);
 }
 
 // Assembly of H into the plan's fronts (k_assemble_tile's H entries): the
@@ -1001,104 +1138,154 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
 // incremental path re-runs it alone when appended factors fit the fronts.
 void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
   const int n = P.n, ns = P.ns;
+  const int nth = plan_threads();
   P.nslots = (long long)slot_col.size();
   // entries (j, i, k) of the permuted lower triangle (new indices i > j, slot
-  // k), ordered by (j, i, k): a counting sort by j (slot order within a
-  // bucket), then each bucket -- a column's few blocks -- by (i, k)
-  std::vector<int> jcnt(n + 1, 0);
-  for (int r = 0; r < n; r++) {
-    const int i = P.iperm[r];
-    for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) {
-      const int j = P.iperm[slot_col[k]];
-      if (i > j) jcnt[j + 1]++;
+  // k), ordered by (j, i, k): a counting sort by j (rows in chunks, one count
+  // array per chunk: slot order within a bucket), then each bucket -- a
+  // column's few blocks -- by (i, k)
+  std::vector<std::vector<int>> ccnt(nth);
+  parallel_chunks(n, nth, [&](int t, int r0, int r1) {
+    ccnt[t].assign(n + 1, 0);
+    for (int r = r0; r < r1; r++) {
+      const int i = P.iperm[r];
+      for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) {
+        const int j = P.iperm[slot_col[k]];
+        if (i > j) ccnt[t][j]++;
+      }
     }
+  });
+  std::vector<int> jcnt(n + 1, 0);
+  {   // bucket j: chunk 0's entries, then chunk 1's, ...; ccnt[t][j] := chunk t's first position
+    int pos = 0;
+    for (int j = 0; j < n; j++) {
+      jcnt[j] = pos;
+      for (int t = 0; t < nth; t++) {
+        const int c = ccnt[t][j];
+        ccnt[t][j] = pos;
+        pos += c;
+      }
+    }
+    jcnt[n] = pos;
   }
-  for (int j = 0; j < n; j++) jcnt[j + 1] += jcnt[j];
   std::vector<int2> eik(jcnt[n]);   // (i, k) per entry, bucketed by j
-  {
-    std::vector<int> fill(jcnt.begin(), jcnt.end() - 1);
-    for (int r = 0; r < n; r++) {
+  parallel_chunks(n, nth, [&](int t, int r0, int r1) {
+    std::vector<int>& fill = ccnt[t];
+    for (int r = r0; r < r1; r++) {
       const int i = P.iperm[r];
       for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) {
         const int j = P.iperm[slot_col[k]];
         if (i > j) eik[fill[j]++] = make_int2(i, k);
       }
     }
-  }
-  for (int j = 0; j < n; j++)
-    std::sort(eik.begin() + jcnt[j], eik.begin() + jcnt[j + 1],
-              [](const int2& a, const int2& b) { return a.x != b.x ? a.x < b.x : a.y < b.y; });
-  P.asm_front.clear();
-  P.asm_li.clear();
-  P.asm_lj.clear();
-  P.asm_ptr.assign(1, 0);
-  P.asm_src.clear();
-  P.asm_src.reserve(eik.size());
-  for (int j = 0; j < n; j++) {
-    const int s = P.dg_front[j], f = P.sfirst[s], l = P.sfirst[s + 1];
-    const int* b0 = P.rows.data() + P.rptr[s] + (l - f);
-    const int* b1 = P.rows.data() + P.rptr[s + 1];
-    const int* cur = b0;   // the bucket's rows come in increasing order: a forward scan finds them
-    for (int q = jcnt[j]; q < jcnt[j + 1]; q++) {
-      const int i = eik[q].x;
-      if (q == jcnt[j] || i != eik[q - 1].x) {
-        if (!P.asm_front.empty()) P.asm_ptr.push_back((int)P.asm_src.size());
-        P.asm_front.push_back(s);
-        P.asm_lj.push_back(j - f);
-        int li;
-        if (i < l) {
-          li = i - f;
-        } else {
-          cur = std::lower_bound(cur, b1, i);
-          li = (l - f) + (int)(cur - b0);
-        }
-        P.asm_li.push_back(li);
-      }
-      P.asm_src.push_back(eik[q].y);
+  });
+  ccnt.clear();
+  // targets: one per distinct (j, i) -- per column chunk counted, then written
+  std::vector<int> tstart(nth + 1, 0);
+  parallel_chunks(n, nth, [&](int t, int j0, int j1) {
+    int cnt = 0;
+    for (int j = j0; j < j1; j++) {
+      std::sort(eik.begin() + jcnt[j], eik.begin() + jcnt[j + 1],
+                [](const int2& x, const int2& y) { return x.x != y.x ? x.x < y.x : x.y < y.y; });
+      for (int q = jcnt[j]; q < jcnt[j + 1]; q++) cnt += (q == jcnt[j] || eik[q].x != eik[q - 1].x);
     }
-  }
-  P.asm_ptr.push_back((int)P.asm_src.size());
-  if (P.asm_front.empty()) P.asm_ptr.assign(1, 0);
+    tstart[t + 1] = cnt;
+  });
+  for (int t = 0; t < nth; t++) tstart[t + 1] += tstart[t];
+  const int ntg = tstart[nth];
+  P.asm_front.resize(ntg);
+  P.asm_li.resize(ntg);
+  P.asm_lj.resize(ntg);
+  P.asm_ptr.resize(ntg + 1);
+  P.asm_src.resize(eik.size());
+  parallel_chunks(n, nth, [&](int t, int j0, int j1) {
+    int g = tstart[t];
+    for (int j = j0; j < j1; j++) {
+      const int s = P.dg_front[j], f = P.sfirst[s], l = P.sfirst[s + 1];
+      const int* b0 = P.rows.data() + P.rptr[s] + (l - f);
+      const int* b1 = P.rows.data() + P.rptr[s + 1];
+      const int* cur = b0;   // the bucket's rows come in increasing order: a forward scan finds them
+      for (int q = jcnt[j]; q < jcnt[j + 1]; q++) {
+        const int i = eik[q].x;
+        if (q == jcnt[j] || i != eik[q - 1].x) {
+          P.asm_ptr[g] = q;
+          P.asm_front[g] = s;
+          P.asm_lj[g] = j - f;
+          int li;
+          if (i < l) {
+            li = i - f;
+          } else {
+            cur = std::lower_bound(cur, b1, i);
+            li = (l - f) + (int)(cur - b0);
+          }
+          P.asm_li[g++] = li;
+        }
+        P.asm_src[q] = eik[q].y;
+      }
+    }
+  });
+  P.asm_ptr[ntg] = (int)eik.size();
+  if (ntg == 0) P.asm_ptr.assign(1, 0);
   // H entries by front tile: every 64x64 lower tile of a front lists the 3x3
   // blocks of H (off-diagonal targets t >= 0, diagonal blocks ~pose) with an
   // element in it (a block can straddle tile boundaries); items of a tile in
-  // the order they are added (off-diagonal targets, then diagonal blocks) --
-  // a counting sort by (front, tile key)
-  std::vector<long long> tbase(ns + 1, 0);   // first tile key slot of each front
-  for (int s2 = 0; s2 < ns; s2++) {
-    const long long nt = (P.m[s2] + 63) / 64;
-    tbase[s2 + 1] = tbase[s2] + nt * (nt + 1) / 2;
-  }
-  std::vector<int> tcnt(tbase[ns] + 1, 0);
-  auto for_item = [&](int sf, int r0, int c0, auto&& fn) {
+  // the order they are added (off-diagonal targets, then diagonal blocks).
+  // Per front (its targets are contiguous: columns sorted), tiles in key order
+  // ti (ti + 1) / 2 + tj -- the order of the front's tile tasks in ea_tasks.
+  std::vector<int> fg(ns + 1, 0);   // targets of front s: [fg[s], fg[s + 1])
+  for (int g = 0; g < ntg; g++) fg[P.asm_front[g] + 1]++;
+  for (int s = 0; s < ns; s++) fg[s + 1] += fg[s];
+  auto for_item = [](int r0, int c0, auto&& fn) {
     for (int ti = r0 / 64; ti <= (r0 + 2) / 64; ti++)
       for (int tj = c0 / 64; tj <= (c0 + 2) / 64; tj++)
-        if (ti >= tj) fn(tbase[sf] + ti * (ti + 1) / 2 + tj);
+        if (ti >= tj) fn(ti * (ti + 1) / 2 + tj);
   };
-  for (size_t t = 0; t < P.asm_front.size(); t++)
-    for_item(P.asm_front[t], 3 * P.asm_li[t], 3 * P.asm_lj[t], [&](long long key) { tcnt[key + 1]++; });
-  for (int j = 0; j < n; j++)
-    for_item(P.dg_front[j], 3 * P.dg_loc[j], 3 * P.dg_loc[j], [&](long long key) { tcnt[key + 1]++; });
-  for (size_t q = 0; q + 1 < tcnt.size(); q++) tcnt[q + 1] += tcnt[q];
-  std::vector<int> titems(tcnt.back());
+  std::vector<long long> fitems(ns + 1, 0);   // items of front s (counted, then its offset)
+  std::vector<std::vector<int>> fcnt(ns);   // per front: item count per tile key, then start
+  parallel_chunks(ns, nth, [&](int, int s0, int s1) {
+    for (int s = s0; s < s1; s++) {
+      const long long nt = (P.m[s] + 63) / 64;
+      std::vector<int>& c = fcnt[s];
+      c.assign(nt * (nt + 1) / 2 + 1, 0);
+      for (int g = fg[s]; g < fg[s + 1]; g++) for_item(3 * P.asm_li[g], 3 * P.asm_lj[g], [&](int key) { c[key + 1]++; });
+      for (int j = P.sfirst[s]; j < P.sfirst[s + 1]; j++)
+        for_item(3 * P.dg_loc[j], 3 * P.dg_loc[j], [&](int key) { c[key + 1]++; });
+      for (size_t k = 0; k + 1 < c.size(); k++) c[k + 1] += c[k];
+      fitems[s + 1] = c.back();
+    }
+  });
+  // front blocks of at_items in the order of the fronts' tile tasks (level order)
+  std::vector<long long> fbase(ns, 0);
   {
-    std::vector<int> fill(tcnt.begin(), tcnt.end() - 1);
-    for (size_t t = 0; t < P.asm_front.size(); t++)
-      for_item(P.asm_front[t], 3 * P.asm_li[t], 3 * P.asm_lj[t], [&](long long key) { titems[fill[key]++] = (int)t; });
-    for (int j = 0; j < n; j++)
-      for_item(P.dg_front[j], 3 * P.dg_loc[j], 3 * P.dg_loc[j], [&](long long key) { titems[fill[key]++] = ~j; });
+    long long pos = 0;
+    for (size_t q = 0; q < P.ea_tasks.size(); q++) {
+      const int s = P.ea_tasks[q].x;
+      if (P.ea_tasks[q].y == 0) {   // the front's first tile (0, 0)
+        fbase[s] = pos;
+        pos += fitems[s + 1];
+      }
+    }
+    P.at_items.resize(pos);
   }
-  P.at_items.clear();
-  P.at_items.reserve(titems.size());
-  P.at_iptr.assign(P.ea_tasks.size(), make_int2(0, 0));
-  for (size_t q = 0; q < P.ea_tasks.size(); q++) {
-    const int4 t = P.ea_tasks[q];
-    const int ti = t.y >> 16, tj = t.y & 0xffff;
-    const long long key = tbase[t.x] + ti * (ti + 1) / 2 + tj;
-    const int i0 = (int)P.at_items.size();
-    P.at_items.insert(P.at_items.end(), titems.begin() + tcnt[key], titems.begin() + tcnt[key + 1]);
-    P.at_iptr[q] = make_int2(i0, (int)P.at_items.size() - i0);
-  }
+  parallel_chunks(ns, nth, [&](int, int s0, int s1) {
+    for (int s = s0; s < s1; s++) {
+      std::vector<int> fill(fcnt[s].begin(), fcnt[s].end() - 1);
+      int* out = P.at_items.data() + fbase[s];
+      for (int g = fg[s]; g < fg[s + 1]; g++)
+        for_item(3 * P.asm_li[g], 3 * P.asm_lj[g], [&](int key) { out[fill[key]++] = g; });
+      for (int j = P.sfirst[s]; j < P.sfirst[s + 1]; j++)
+        for_item(3 * P.dg_loc[j], 3 * P.dg_loc[j], [&](int key) { out[fill[key]++] = ~j; });
+    }
+  });
+  P.at_iptr.resize(P.ea_tasks.size());
+  parallel_chunks((int)P.ea_tasks.size(), nth, [&](int, int q0, int q1) {
+    for (int q = q0; q < q1; q++) {
+      const int4 t = P.ea_tasks[q];
+      const int ti = t.y >> 16, tj = t.y & 0xffff, key = ti * (ti + 1) / 2 + tj;
+      const std::vector<int>& c = fcnt[t.x];
+      P.at_iptr[q] = make_int2((int)(fbase[t.x] + c[key]), c[key + 1] - c[key]);
+    }
+  });
   static const bool timing = getenv("PGO_PLAN_TIMING") != nullptr;
   const auto ta = std::chrono::steady_clock::now();
   // sum_{t=A..B} clamp(t, 0, c) in closed form (G(x) = sum_{t=1..x} min(t, c))
@@ -1106,7 +1293,9 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
     if (x <= 0) return 0;
     return x <= c ? x * (x + 1) / 2 : c * (c + 1) / 2 + (x - c) * c;
   };
-  for (CholLevel& lv : P.levels) {   // algorithmic bytes of the levels' k_assemble_tile (profiles)
+  parallel_chunks((int)P.levels.size(), nth, [&](int, int l0, int l1) {
+  for (int L = l0; L < l1; L++) {   // algorithmic bytes of the levels' k_assemble_tile (profiles)
+    CholLevel& lv = P.levels[L];
     lv.at_bytes = 0;
     for (int q = lv.ea_off[0]; q < lv.ea_off[0] + lv.ea_cnt[0]; q++) {
       const int4 t = P.ea_tasks[q];
@@ -1130,6 +1319,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
       lv.at_bytes += 8.0 * e + h;
     }
   }
+  });
   if (timing) {
     double tot = 0;
     for (const CholLevel& lv : P.levels) tot += lv.at_bytes;
@@ -1143,6 +1333,136 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
 // Does the plan's factor structure hold every block of the pattern (old pose
 // indices)?  Block (r, c) with new indices i < j must have row j in the front of
 // column i (its own poses or its below rows).
+// Is block (a, b) (old pose indices < P.n) inside the plan's factor structure?
+static bool covered(const CholPlan& P, int a, int b) {
+  int i = P.iperm[a], j = P.iperm[b];
+  if (i == j) return true;
+  if (i > j) std::swap(i, j);
+  const int s = P.dg_front[i];
+  if (j < P.sfirst[s + 1]) return true;
+  const int* b0 = P.rows.data() + P.rptr[s] + (P.sfirst[s + 1] - P.sfirst[s]);
+  const int* b1 = P.rows.data() + P.rptr[s + 1];
+  return std::binary_search(b0, b1, j);
+}
+
+bool chol_covers(const CholPlan& P, const std::vector<int2>& pairs) {
+  for (const int2& e : pairs)
+    if (e.x >= P.n || e.y >= P.n || !covered(P, e.x, e.y)) return false;
+  return true;
+}
+
+// Incremental symbolic update for appended poses (the live re-solve,
+// graph.cpp:180-200): poses P.n .. n-1 are eliminated last, as extra pivot
+// columns of the root front (the last supernode), so no existing row moves.
+// A new pose v coupled to an old pose a fills L(v, .) along the elimination
+// tree path from a's front to the root: every front on it gains row v at the
+// end of its row list (old rows keep their local indices, so the children's
+// extend-add maps stay valid; v's own map entry points at the parent's new last
+// rows); a root other than the last supernode reached this way becomes its
+// child.  Only the fronts on these paths change size.  The schedules and
+// assembly lists are then rebuilt from the fronts (chol_schedule).
+// new_pairs: every factor added since the plan (old pose indices); factors
+// between old poses must lie in the existing structure.  Returns false (plan
+// untouched) when the update does not apply: a partitioned plan, an old-old
+// factor outside the fill, a tail past max_tail poses since the last full
+// analysis, or a factor past max_growth x the analysed one's flops.
+bool chol_append(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col,
+                 const std::vector<int2>& new_pairs, int max_tail, double max_growth) {
+  const int n0 = P.n, ns = P.ns;
+  if (n <= n0 || ns == 0 || P.part_size > 1 || P.parent[ns - 1] != -1 || n - P.n_analyzed > max_tail ||
+      P.flops > max_growth * P.flops_analyzed)
+    return false;
+  for (const int2& e : new_pairs)
+    if (e.x < n0 && e.y < n0 && !covered(P, e.x, e.y)) return false;
+  const int T = ns - 1;
+  // 1. the fill paths: (front, new pose) in increasing pose order per front
+  std::vector<int> stamp(ns, -1), added(ns, 0), reparent;
+  std::vector<int2> adds;
+  for (int v = n0; v < n; v++)
+    for (int q = row_ptr[v]; q < row_ptr[v + 1]; q++) {
+      const int a = slot_col[q];
+      if (a >= n0) continue;
+      int s = P.dg_front[P.iperm[a]];
+      while (s != T && stamp[s] != v) {
+        stamp[s] = v;
+        adds.push_back(make_int2(s, v));
+        added[s]++;
+        if (P.parent[s] < 0) {
+          reparent.push_back(s);
+          break;
+        }
+        s = P.parent[s];
+      }
+    }
+  // 2. row lists: old segment, then the new rows; the root front's own poses extended
+  std::vector<int> rptr(ns + 1, 0);
+  for (int s = 0; s < ns; s++) rptr[s + 1] = rptr[s] + (P.rptr[s + 1] - P.rptr[s]) + added[s] + (s == T ? n - n0 : 0);
+  std::vector<int> rows(rptr[ns]);
+  std::vector<int> fillp(ns);
+  for (int s = 0; s < ns; s++) {
+    std::copy(P.rows.begin() + P.rptr[s], P.rows.begin() + P.rptr[s + 1], rows.begin() + rptr[s]);
+    fillp[s] = rptr[s] + (P.rptr[s + 1] - P.rptr[s]);
+  }
+  for (int v = n0; v < n; v++) rows[fillp[T]++] = v;
+  std::stable_sort(adds.begin(), adds.end(), [](const int2& x, const int2& y) { return x.x < y.x; });
+  for (const int2& t : adds) rows[fillp[t.x]++] = t.y;
+  // 3. extend-add maps: old entries kept, the new rows' local index in the parent
+  for (int s : reparent) P.parent[s] = T;
+  std::vector<int> ea_ptr(ns + 1, 0);
+  for (int s = 0; s < ns; s++) ea_ptr[s + 1] = ea_ptr[s] + (P.ea_ptr[s + 1] - P.ea_ptr[s]) + added[s];
+  std::vector<int> ea_rel(ea_ptr[ns]);
+  P.sfirst[ns] = n;
+  for (int s = 0; s < ns; s++) {
+    const int old = P.ea_ptr[s + 1] - P.ea_ptr[s];
+    std::copy(P.ea_rel.begin() + P.ea_ptr[s], P.ea_rel.begin() + P.ea_ptr[s + 1], ea_rel.begin() + ea_ptr[s]);
+    if (!added[s]) continue;
+    const int p = P.parent[s];
+    const int* b0 = rows.data() + rptr[p];
+    const int* b1 = rows.data() + rptr[p + 1];
+    const int* nr = rows.data() + rptr[s + 1] - added[s];
+    for (int t = 0; t < added[s]; t++) {
+      const int v = nr[t];
+      // in the root front v is an own pose; elsewhere one of the parent's new rows
+      const int li = p == T ? v - P.sfirst[T] : (int)(std::lower_bound(b1 - added[p], b1, v) - b0);
+      ea_rel[ea_ptr[s] + old + t] = li;
+    }
+  }
+  // 4. the rest of the plan's per-front / per-pose arrays
+  P.rows.swap(rows);
+  P.rptr.swap(rptr);
+  P.ea_rel.swap(ea_rel);
+  P.ea_ptr.swap(ea_ptr);
+  for (int s = 0; s < ns; s++) P.m[s] += 3 * added[s];
+  P.w[T] = 3 * (n - P.sfirst[T]);
+  P.m[T] = P.w[T];
+  P.perm.resize(n);
+  P.iperm.resize(n);
+  P.dg_front.resize(n);
+  P.dg_loc.resize(n);
+  for (int v = n0; v < n; v++) {
+    P.perm[v] = P.iperm[v] = v;
+    P.dg_front[v] = T;
+    P.dg_loc[v] = v - P.sfirst[T];
+  }
+  if (!reparent.empty()) {
+    P.cptr.assign(ns + 1, 0);
+    for (int s = 0; s < ns; s++)
+      if (P.parent[s] >= 0) P.cptr[P.parent[s] + 1]++;
+    for (int s = 0; s < ns; s++) P.cptr[s + 1] += P.cptr[s];
+    P.children.assign(P.cptr[ns], 0);
+    std::vector<int> f(P.cptr.begin(), P.cptr.end() - 1);
+    for (int s = 0; s < ns; s++)
+      if (P.parent[s] >= 0) P.children[f[P.parent[s]]++] = s;
+    P.height.assign(ns, 0);
+    for (int s = 0; s < ns; s++)
+      if (P.parent[s] >= 0) P.height[P.parent[s]] = std::max(P.height[P.parent[s]], P.height[s] + 1);
+  }
+  P.n = n;
+  size_fronts(P);
+  chol_schedule(P, row_ptr, slot_col);
+  return true;
+}
+
 bool chol_covers(const CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
   if (n != P.n) return false;
   for (int r = 0; r < n; r++)

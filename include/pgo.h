@@ -168,7 +168,10 @@ typedef struct {
   /* the solver's plan on this call (the per-registration re-solve): 0 reused,
      1 same fronts / new H assembly (appended factors inside the existing fill),
      2 re-planned on the previous ordering with the appended poses inserted,
-     3 full analysis (first call, or too much appended); ms_plan its host+upload ms */
+     3 full analysis (first call, or too much appended), 4 appended poses
+     added to the plan incrementally (eliminated last, rows added along their
+     fill paths to the root; PGO_NO_PLAN_APPEND=1 disables); ms_plan its
+     host+upload ms */
   int plan_update;
   double ms_plan;
   /* how the device graph was brought up to date on this call: 0 resident, 1
