@@ -138,6 +138,30 @@ int check_distributed(const Pattern& G, int ordering, int size) {
   return 0;
 }
 
+// The tile lists of the H assembly (at_iptr / at_items): every tile task of
+// every front this rank assembles lists exactly the front's off-diagonal
+// targets, then its diagonal blocks, with an element in the tile, in order.
+int check_assembly(const pgo::CholPlan& P) {
+  std::vector<std::vector<int>> tg(P.ns);
+  for (size_t g = 0; g < P.asm_front.size(); g++) tg[P.asm_front[g]].push_back((int)g);
+  auto touches = [](int r0, int c0, int ti, int tj) {
+    return r0 / 64 <= ti && ti <= (r0 + 2) / 64 && c0 / 64 <= tj && tj <= (c0 + 2) / 64;
+  };
+  for (size_t q = 0; q < P.ea_tasks.size(); q++) {
+    const int4 t = P.ea_tasks[q];
+    const int s = t.x, ti = t.y >> 16, tj = t.y & 0xffff;
+    std::vector<int> want;
+    for (int g : tg[s])
+      if (touches(3 * P.asm_li[g], 3 * P.asm_lj[g], ti, tj)) want.push_back(g);
+    for (int j = P.sfirst[s]; j < P.sfirst[s + 1]; j++)
+      if (touches(3 * P.dg_loc[j], 3 * P.dg_loc[j], ti, tj)) want.push_back(~j);
+    const int2 it = P.at_iptr[q];
+    if (it.y != (int)want.size() || !std::equal(want.begin(), want.end(), P.at_items.begin() + it.x))
+      return fail("assembly: a tile's H entries");
+  }
+  return 0;
+}
+
 // the pattern restricted to poses [0, n)
 Pattern restrict_pattern(const Pattern& G, int n) {
   Pattern R;
@@ -167,6 +191,7 @@ int check_append(const Pattern& G, int n0, int ordering) {
     for (int k = Gn.row_ptr[n - 1]; k < Gn.row_ptr[n]; k++) pairs.push_back(make_int2(n - 1, Gn.col[k]));
     if (!pgo::chol_append(P, n, Gn.row_ptr, Gn.col, pairs, 1 << 30, 1e30)) return fail("append: refused");
     if (P.schedule_error) return fail("append: panel schedule bookkeeping");
+    if (check_assembly(P)) return 1;
     if (P.n != n || !pgo::chol_covers(P, n, Gn.row_ptr, Gn.col)) return fail("append: pattern not covered");
     for (int s = 0; s < P.ns; s++) {
       const int wp = P.sfirst[s + 1] - P.sfirst[s], nr = P.rptr[s + 1] - P.rptr[s];
@@ -199,6 +224,12 @@ int check_append(const Pattern& G, int n0, int ordering) {
 }  // namespace
 
 int main() {
+  for (int n : {1, 2, 5}) {   // graphs smaller than the planner's thread count
+    const Pattern G = restrict_pattern(make_pattern(40, 0, 3), n);
+    pgo::CholPlan P;
+    pgo::chol_analyze(P, G.n, G.row_ptr, G.col);
+    if (P.schedule_error || !pgo::chol_covers(P, G.n, G.row_ptr, G.col)) return fail("tiny graph");
+  }
   // every front a look-ahead front (the skip and prep bookkeeping on small ones too), then the default
   for (const char* la : {"64", "1000000000", ""}) {
   if (*la) setenv("PGO_LOOKAHEAD_M", la, 1);
@@ -211,6 +242,7 @@ int main() {
     if (P.ns <= 0 || P.flops <= 0) return fail("analysis");
     if (P.schedule_error) return fail("panel schedule bookkeeping");
     if (!pgo::chol_covers(P, G.n, G.row_ptr, G.col)) return fail("plan does not cover its own pattern");
+    if (check_assembly(P)) return 1;
     for (int size : {2, 4}) {
       std::vector<double> rf;
       double top = 0;
@@ -223,6 +255,7 @@ int main() {
         Q.part_rank = r;
         pgo::chol_analyze(Q, G.n, G.row_ptr, G.col);
         if (Q.ns != P.ns || Q.schedule_error) return fail("partitioned plan");
+        if (check_assembly(Q)) return 1;
       }
     }
     // a loop closure inside the existing fill: same fronts, new assembly lists

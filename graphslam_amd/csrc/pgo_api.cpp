@@ -41,6 +41,11 @@ struct Lane {
   double* scal = nullptr;
 };
 
+struct Staging {
+  char* buf = nullptr;
+  size_t cap = 0, used = 0;
+};
+
 struct HostStructure {
   std::vector<int2> eij;           // device order
   std::vector<int> dorder;         // device factor -> user factor index
@@ -100,7 +105,9 @@ struct pgo_graph {
   long long factorizations = 0;
   hipGraphExec_t fac_exec[9] = {};          // captured factorisation, per lane count (1: d.x path)
   hipGraphExec_t sol_exec[9] = {};          // captured triangular solves, per lane count
+  int graph_eager[9] = {};                  // eager factorisations of this plan before the capture
   double* h_lam = nullptr;                  // pinned lambda staging
+  Staging stage;                            // pinned upload staging (append_structure)
   // ---- multi-GPU speculative lambda search (pgo_comm_*) ----
   pgo::Comm comm;
   std::vector<Lane> lanes;                  // lanes 1..L-1 (speculative tries on this GPU)
@@ -196,11 +203,13 @@ int information(const double* q, double* om6) {
 
 // every captured factor / solve graph (they hold the plan's workspace pointers)
 void drop_graphs(pgo_graph* g) {
-  for (int l = 0; l < 9; l++)
+  for (int l = 0; l < 9; l++) {
     for (hipGraphExec_t* e : {&g->fac_exec[l], &g->sol_exec[l]}) {
       if (*e) (void)hipGraphExecDestroy(*e);
       *e = nullptr;
     }
+    g->graph_eager[l] = 0;
+  }
 }
 
 void free_lanes(pgo_graph* g) {
@@ -280,6 +289,20 @@ template <class T>
 int h2d(pgo_graph* g, T* dst, const T* src, size_t count) {
   if (count == 0) return PGO_OK;
   HIP_TRY(g, hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, g->d.stream));
+  return PGO_OK;
+}
+
+// Host -> device through the handle's pinned staging buffer (a bump region per
+// batch of copies; stage_reset after the stream has drained): the live
+// re-solve's per-registration uploads at pinned speed
+template <class T>
+int staged_h2d(pgo_graph* g, Staging& st, T* dst, const T* src, size_t count) {
+  if (count == 0) return PGO_OK;
+  const size_t bytes = count * sizeof(T), off = (st.used + 255) / 256 * 256;
+  if (off + bytes > st.cap) return h2d(g, dst, src, count);   // (full: a pageable copy)
+  std::memcpy(st.buf + off, src, bytes);
+  st.used = off + bytes;
+  HIP_TRY(g, hipMemcpyAsync(dst, st.buf + off, bytes, hipMemcpyHostToDevice, g->d.stream));
   return PGO_OK;
 }
 
@@ -790,10 +813,13 @@ int append_structure(pgo_graph* g) {
   phase("per-row");
   // the device: new factors, per-row arrays, slots
   HIP_TRY(g, hipStreamSynchronize(d.stream));
+  phase("sync");
   if (g->xb && (size_t)n > g->xb_n) free_lanes(g);   // (else the lanes hold the grown graph too)
   drop_graphs(g);
+  phase("drop graphs");
   if (d.pose_saved) (void)hipFree(d.pose_saved);   // (a snapshot of the old structure's values)
   d.pose_saved = nullptr;
+  phase("free");
   std::vector<double4> hz(nij.size());
   std::vector<double2> hom(3 * nij.size());
   for (size_t q = 0; q < nij.size(); q++) {
@@ -805,18 +831,43 @@ int append_structure(pgo_graph* g) {
     hom[3 * q + 1] = make_double2(o[2], o[3]);
     hom[3 * q + 2] = make_double2(o[4], o[5]);
   }
-  RC_TRY(h2d(g, d.eij + ne_old, nij.data(), nij.size()));
-  RC_TRY(h2d(g, d.ez + ne_old, hz.data(), hz.size()));
-  RC_TRY(h2d(g, d.eom + 3 * (size_t)ne_old, hom.data(), hom.size()));
-  RC_TRY(h2d(g, d.prior_ptr, H.prior_ptr.data(), n + 1));
-  RC_TRY(h2d(g, d.row_ptr, H.row_ptr.data(), n + 1));
-  RC_TRY(h2d(g, d.slot_edge, H.slot_edge.data(), ns));
-  RC_TRY(h2d(g, d.slot_col, H.slot_col.data(), ns));
-  RC_TRY(h2d(g, d.erow, erow.data(), n + 1));
-  RC_TRY(h2d(g, d.s1_ptr, s1_ptr.data(), n + 1));
-  RC_TRY(h2d(g, d.s1pos, s1pos.data(), ne));
-  RC_TRY(h2d(g, d.Dc, g->h_Dc.data(), 6 * (size_t)n));
-  RC_TRY(h2d(g, d.brow, brow.data(), brow.size()));
+  // only what changed: the new factors; the row / slot arrays from the first
+  // row with a new slot (earlier rows and their slots are unchanged); the
+  // side-1 sums of the rows that gained side-1 terms; whole for the rest
+  if (g->stage.cap < ((size_t)64 << 20)) {
+    if (g->stage.buf) (void)hipHostFree(g->stage.buf);
+    g->stage = Staging();
+    HIP_TRY(g, hipHostMalloc((void**)&g->stage.buf, (size_t)64 << 20, hipHostMallocDefault));
+    g->stage.cap = (size_t)64 << 20;
+  }
+  Staging& sg = g->stage;
+  sg.used = 0;
+  const int r0 = extra.empty() ? n_old : std::min(extra.front().x, n_old);   // first row with a new slot
+  int x0 = n_old, y0 = n_old;   // (the new rows always)
+  for (const int2& ij : nij) {
+    x0 = std::min(x0, ij.x);
+    y0 = std::min(y0, ij.y);
+  }
+  RC_TRY(staged_h2d(g, sg, d.eij + ne_old, nij.data(), nij.size()));
+  RC_TRY(staged_h2d(g, sg, d.ez + ne_old, hz.data(), hz.size()));
+  RC_TRY(staged_h2d(g, sg, d.eom + 3 * (size_t)ne_old, hom.data(), hom.size()));
+  RC_TRY(staged_h2d(g, sg, d.prior_ptr + n_old + 1, H.prior_ptr.data() + n_old + 1, n - n_old));
+  RC_TRY(staged_h2d(g, sg, d.row_ptr + r0 + 1, H.row_ptr.data() + r0 + 1, n - r0));
+  RC_TRY(staged_h2d(g, sg, d.slot_edge + H.row_ptr[r0], H.slot_edge.data() + H.row_ptr[r0], ns - H.row_ptr[r0]));
+  RC_TRY(staged_h2d(g, sg, d.slot_col + H.row_ptr[r0], H.slot_col.data() + H.row_ptr[r0], ns - H.row_ptr[r0]));
+  RC_TRY(staged_h2d(g, sg, d.erow + x0 + 1, erow.data() + x0 + 1, n - x0));
+  RC_TRY(staged_h2d(g, sg, d.s1_ptr + y0 + 1, s1_ptr.data() + y0 + 1, n - y0));
+  RC_TRY(staged_h2d(g, sg, d.s1pos, s1pos.data(), ne));
+  {
+    std::vector<int> ys;
+    for (const int2& ij : nij)
+      if (ij.y < n_old) ys.push_back(ij.y);
+    std::sort(ys.begin(), ys.end());
+    ys.erase(std::unique(ys.begin(), ys.end()), ys.end());
+    for (int y : ys) RC_TRY(staged_h2d(g, sg, d.Dc + 6 * (size_t)y, g->h_Dc.data() + 6 * (size_t)y, 6));
+    RC_TRY(staged_h2d(g, sg, d.Dc + 6 * (size_t)n_old, g->h_Dc.data() + 6 * (size_t)n_old, 6 * (size_t)(n - n_old)));
+  }
+  RC_TRY(staged_h2d(g, sg, d.brow, brow.data(), brow.size()));
   d.n = n;
   d.ne = ne;
   d.nslots = ns;
@@ -934,7 +985,9 @@ int ensure_chol(pgo_graph* g) {
     // appended poses: into the plan incrementally while the tail is short and
     // the factor has not grown much (then a re-plan below)
     constexpr int kMaxTail = 64;
+    PhaseTimer phase("ensure_chol");
     if (!getenv("PGO_NO_PLAN_APPEND") && pgo::chol_append(P, n, g->h_row_ptr, g->h_slot_col, pairs, kMaxTail, 1.05)) {
+      phase("chol_append");
       if (P.schedule_error) return fail(g, PGO_E_HIP, "internal: inconsistent panel schedule");
       drop_graphs(g);
       RC_TRY(bind_plan(g, true));
@@ -1027,11 +1080,16 @@ int bind_plan(pgo_graph* g, bool full) {
     }
     phase("chol_upload");
     if (!g->d.eside) RC_TRY(dev_alloc(g, &g->d.eside, std::max<size_t>(g->cap_ne, g->d.ne)));
-    RC_TRY(h2d(g, g->d.eside, eside.data(), eside.size()));
-    if (!slot_edge.empty())
-      HIP_TRY(g, hipMemcpyAsync(g->d.slot_edge, slot_edge.data(), slot_edge.size() * sizeof(int),
-                                hipMemcpyHostToDevice, g->d.stream));
-    HIP_TRY(g, hipStreamSynchronize(g->d.stream));
+    if (g->stage.buf) {   // pinned staging (the live re-solve: idle since append_structure drained
+                          // the stream; the copies and the fronts' zeroing run on unsynchronised)
+      g->stage.used = 0;
+      RC_TRY(staged_h2d(g, g->stage, g->d.eside, eside.data(), eside.size()));
+      RC_TRY(staged_h2d(g, g->stage, g->d.slot_edge, slot_edge.data(), slot_edge.size()));
+    } else {
+      RC_TRY(h2d(g, g->d.eside, eside.data(), eside.size()));
+      RC_TRY(h2d(g, g->d.slot_edge, slot_edge.data(), slot_edge.size()));
+      HIP_TRY(g, hipStreamSynchronize(g->d.stream));
+    }
     phase("slots");
   }
   return PGO_OK;
@@ -1089,8 +1147,20 @@ struct SolveState {
 // Replay of the captured factorisation and solve graphs for nb lanes (captured
 // on first use; one graph launch each instead of ~1e3 kernel launches), with
 // ev[5] recorded between them: the factorisation's device time is ev[2]..ev[5].
-int graph_factor_solve(pgo_graph* g, int nb, double* x, long long xstride) {
+int graph_factor_solve(pgo_graph* g, int nb, double* x, long long xstride, bool capture_now) {
   DevGraph& d = g->d;
+  // a plan's first factorisations per lane count run eagerly: capturing ~1e3
+  // launches costs ~14 ms on C3 and destroying the graphs ~10 ms, more than a
+  // few replays gain -- the live re-solve refreshes the plan every
+  // registration and factors it ~4 times; a full optimize captures early on
+  constexpr int kEagerFirst = 8;
+  if (!capture_now && !g->fac_exec[nb] && g->graph_eager[nb] < kEagerFirst) {
+    g->graph_eager[nb]++;
+    HIP_TRY(g, pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr, nb));
+    HIP_TRY(g, hipEventRecord(g->ev[5], d.stream));
+    HIP_TRY(g, pgo::chol_solve(g->chol, x, d.stream, nb, xstride));
+    return PGO_OK;
+  }
   auto capture = [&](hipGraphExec_t* exec, bool factor) -> int {
     if (*exec) return PGO_OK;
     PhaseTimer phase("graph_capture");
@@ -1155,7 +1225,7 @@ int linear_solve(pgo_graph* g, const pgo_params& p, double lam, pgo_stats* st, S
     HIP_TRY(g, es);
     if (prof) HIP_TRY(g, hipEventRecord(g->fev[2], d.stream));
   } else {
-    RC_TRY(graph_factor_solve(g, 1, d.x, 0));
+    RC_TRY(graph_factor_solve(g, 1, d.x, 0, false));
     ss->graph = true;
   }
   ss->known = false;
@@ -1303,7 +1373,7 @@ int run_lanes(pgo_graph* g, const pgo_params& p, int nb, const double* lams, dou
     if (g->hook.failed) return fail(g, PGO_E_COMM, g->last_error);
     HIP_TRY(g, es);
   } else {
-    RC_TRY(graph_factor_solve(g, nb, g->xb, 3LL * d.n));
+    RC_TRY(graph_factor_solve(g, nb, g->xb, 3LL * d.n, false));
   }
   HIP_TRY(g, hipEventRecord(ev[3], d.stream));
   for (int l = 0; l < nb; l++) {
@@ -1447,6 +1517,7 @@ void pgo_destroy(pgo_graph* g) {
     if (g->h_scal) (void)hipHostFree(g->h_scal);
     if (g->h_ctrl) (void)hipHostFree(g->h_ctrl);
     if (g->h_lam) (void)hipHostFree(g->h_lam);
+    if (g->stage.buf) (void)hipHostFree(g->stage.buf);
     if (g->h_lanes) (void)hipHostFree(g->h_lanes);
     for (auto& e : g->pev)
       if (e) (void)hipEventDestroy(e);
@@ -2358,7 +2429,7 @@ int pgo_debug_factor_time(pgo_graph* g, int lanes, int reps, double* ms) {
   for (int l = 0; l < L; l++) g->h_lanes[4 * 8 + l] = 1e-5 * std::pow(10.0, l);
   HIP_TRY(g, hipMemcpyAsync(g->chol.d_lambda, g->h_lanes + 4 * 8, L * sizeof(double), hipMemcpyHostToDevice,
                             d.stream));
-  RC_TRY(graph_factor_solve(g, L, L > 1 ? g->xb : d.x, L > 1 ? 3LL * d.n : 0));   // capture + warm
+  RC_TRY(graph_factor_solve(g, L, L > 1 ? g->xb : d.x, L > 1 ? 3LL * d.n : 0, true));   // capture + warm
   HIP_TRY(g, hipEventRecord(g->ev[0], d.stream));
   for (int r = 0; r < reps; r++) HIP_TRY(g, hipGraphLaunch(g->fac_exec[L], d.stream));
   HIP_TRY(g, hipEventRecord(g->ev[1], d.stream));

@@ -2234,7 +2234,7 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
     CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));
     for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
-  return hipStreamSynchronize(s);
+  return hipSuccess;   // (the fronts' zeroing runs on, stream-ordered before any use)
 }
 
 void chol_free(CholPlan& P) {

@@ -1138,7 +1138,15 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
 // incremental path re-runs it alone when appended factors fit the fronts.
 void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
   const int n = P.n, ns = P.ns;
-  const int nth = plan_threads();
+  const int nth = std::max(1, std::min(plan_threads(), n));   // (the chunks over the n poses: one per thread)
+  static const bool timing = getenv("PGO_PLAN_TIMING") != nullptr;
+  auto tl = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!timing) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "chol_assembly %-12s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - tl).count());
+    tl = t;
+  };
   P.nslots = (long long)slot_col.size();
   // entries (j, i, k) of the permuted lower triangle (new indices i > j, slot
   // k), ordered by (j, i, k): a counting sort by j (rows in chunks, one count
@@ -1155,18 +1163,27 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
       }
     }
   });
+  lap("count");
   std::vector<int> jcnt(n + 1, 0);
   {   // bucket j: chunk 0's entries, then chunk 1's, ...; ccnt[t][j] := chunk t's first position
-    int pos = 0;
-    for (int j = 0; j < n; j++) {
-      jcnt[j] = pos;
-      for (int t = 0; t < nth; t++) {
-        const int c = ccnt[t][j];
-        ccnt[t][j] = pos;
-        pos += c;
+    parallel_chunks(n, nth, [&](int, int j0, int j1) {
+      for (int j = j0; j < j1; j++) {
+        int c = 0;
+        for (int t = 0; t < nth; t++) c += ccnt[t][j];
+        jcnt[j + 1] = c;
       }
-    }
-    jcnt[n] = pos;
+    });
+    for (int j = 0; j < n; j++) jcnt[j + 1] += jcnt[j];
+    parallel_chunks(n, nth, [&](int, int j0, int j1) {
+      for (int j = j0; j < j1; j++) {
+        int pos = jcnt[j];
+        for (int t = 0; t < nth; t++) {
+          const int c = ccnt[t][j];
+          ccnt[t][j] = pos;
+          pos += c;
+        }
+      }
+    });
   }
   std::vector<int2> eik(jcnt[n]);   // (i, k) per entry, bucketed by j
   parallel_chunks(n, nth, [&](int t, int r0, int r1) {
@@ -1179,6 +1196,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
       }
     }
   });
+  lap("bucket");
   ccnt.clear();
   // targets: one per distinct (j, i) -- per column chunk counted, then written
   std::vector<int> tstart(nth + 1, 0);
@@ -1191,6 +1209,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
     }
     tstart[t + 1] = cnt;
   });
+  lap("sort");
   for (int t = 0; t < nth; t++) tstart[t + 1] += tstart[t];
   const int ntg = tstart[nth];
   P.asm_front.resize(ntg);
@@ -1224,6 +1243,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
       }
     }
   });
+  lap("targets");
   P.asm_ptr[ntg] = (int)eik.size();
   if (ntg == 0) P.asm_ptr.assign(1, 0);
   // H entries by front tile: every 64x64 lower tile of a front lists the 3x3
@@ -1254,8 +1274,9 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
       fitems[s + 1] = c.back();
     }
   });
+  lap("tile count");
   // front blocks of at_items in the order of the fronts' tile tasks (level order)
-  std::vector<long long> fbase(ns, 0);
+  std::vector<long long> fbase(ns, -1);   // (-1: a front this rank does not assemble)
   {
     long long pos = 0;
     for (size_t q = 0; q < P.ea_tasks.size(); q++) {
@@ -1269,6 +1290,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
   }
   parallel_chunks(ns, nth, [&](int, int s0, int s1) {
     for (int s = s0; s < s1; s++) {
+      if (fbase[s] < 0) continue;
       std::vector<int> fill(fcnt[s].begin(), fcnt[s].end() - 1);
       int* out = P.at_items.data() + fbase[s];
       for (int g = fg[s]; g < fg[s + 1]; g++)
@@ -1277,6 +1299,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
         for_item(3 * P.dg_loc[j], 3 * P.dg_loc[j], [&](int key) { out[fill[key]++] = ~j; });
     }
   });
+  lap("tile items");
   P.at_iptr.resize(P.ea_tasks.size());
   parallel_chunks((int)P.ea_tasks.size(), nth, [&](int, int q0, int q1) {
     for (int q = q0; q < q1; q++) {
@@ -1286,7 +1309,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
       P.at_iptr[q] = make_int2((int)(fbase[t.x] + c[key]), c[key + 1] - c[key]);
     }
   });
-  static const bool timing = getenv("PGO_PLAN_TIMING") != nullptr;
+  lap("tile ptrs");
   const auto ta = std::chrono::steady_clock::now();
   // sum_{t=A..B} clamp(t, 0, c) in closed form (G(x) = sum_{t=1..x} min(t, c))
   auto G = [](long long x, long long c) -> long long {

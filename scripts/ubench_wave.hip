@@ -67,8 +67,17 @@ int main(int argc, char** argv) {
   for (int r = 0; r < 5; r++) {
     hipMemcpyAsync(F, F0, bytes, hipMemcpyDeviceToDevice, st);
     hipEventRecord(a, st);
-    if (M > 64) k_front_wave<true><<<N, 64, (size_t)(M * (kWaveW + 1) + 130 + kWaveW) * 8, st>>>(c, dl);
-    else k_front_wave<false><<<N, 64, (size_t)(M * (kWaveW + 1) + 130 + kWaveW) * 8, st>>>(c, dl);
+    const int WC = W <= 8 ? 8 : W <= 16 ? 16 : kWaveW;   // the plan's panel-width classes
+    const size_t lds = (size_t)(M * (WC + 1) + 130 + WC) * 8;
+    if (M > 64) {
+      if (WC == 8) k_front_wave<8, true><<<N, 64, lds, st>>>(c, dl);
+      else if (WC == 16) k_front_wave<16, true><<<N, 64, lds, st>>>(c, dl);
+      else k_front_wave<kWaveW, true><<<N, 64, lds, st>>>(c, dl);
+    } else {
+      if (WC == 8) k_front_wave<8, false><<<N, 64, lds, st>>>(c, dl);
+      else if (WC == 16) k_front_wave<16, false><<<N, 64, lds, st>>>(c, dl);
+      else k_front_wave<kWaveW, false><<<N, 64, lds, st>>>(c, dl);
+    }
     hipEventRecord(b, st);
     hipEventSynchronize(b);
     float ms;
