@@ -106,6 +106,7 @@ struct pgo_graph {
   hipGraphExec_t fac_exec[9] = {};          // captured factorisation, per lane count (1: d.x path)
   hipGraphExec_t sol_exec[9] = {};          // captured triangular solves, per lane count
   int graph_eager[9] = {};                  // eager factorisations of this plan before the capture
+  int eager_first = 0;                      // ... how many (8 after an incremental plan update, else 0)
   double* h_lam = nullptr;                  // pinned lambda staging
   Staging stage;                            // pinned upload staging (append_structure)
   // ---- multi-GPU speculative lambda search (pgo_comm_*) ----
@@ -979,6 +980,7 @@ int ensure_chol(pgo_graph* g) {
       RC_TRY(bind_plan(g, false));
       g->plan_stale = false;
       g->plan_edges = g->ek1.size();
+      g->eager_first = 8;
       timed(1);
       return PGO_OK;
     }
@@ -993,6 +995,7 @@ int ensure_chol(pgo_graph* g) {
       RC_TRY(bind_plan(g, true));
       g->plan_stale = false;
       g->plan_edges = g->ek1.size();
+      g->eager_first = 8;
       timed(4);
       return PGO_OK;
     }
@@ -1042,6 +1045,7 @@ int ensure_chol(pgo_graph* g) {
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count());
   g->chol_ready = true;
   g->plan_edges = g->ek1.size();
+  g->eager_first = 0;
   timed(order_in.empty() ? 3 : 2);
   return PGO_OK;
 }
@@ -1149,12 +1153,11 @@ struct SolveState {
 // ev[5] recorded between them: the factorisation's device time is ev[2]..ev[5].
 int graph_factor_solve(pgo_graph* g, int nb, double* x, long long xstride, bool capture_now) {
   DevGraph& d = g->d;
-  // a plan's first factorisations per lane count run eagerly: capturing ~1e3
-  // launches costs ~14 ms on C3 and destroying the graphs ~10 ms, more than a
-  // few replays gain -- the live re-solve refreshes the plan every
-  // registration and factors it ~4 times; a full optimize captures early on
-  constexpr int kEagerFirst = 8;
-  if (!capture_now && !g->fac_exec[nb] && g->graph_eager[nb] < kEagerFirst) {
+  // after an incremental plan update the first factorisations per lane count
+  // run eagerly: capturing ~1e3 launches costs ~14 ms on C3 and destroying the
+  // graphs ~10 ms, more than a few replays gain -- the live re-solve refreshes
+  // the plan every registration and factors it ~4 times (eager_first)
+  if (!capture_now && !g->fac_exec[nb] && g->graph_eager[nb] < g->eager_first) {
     g->graph_eager[nb]++;
     HIP_TRY(g, pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr, nb));
     HIP_TRY(g, hipEventRecord(g->ev[5], d.stream));

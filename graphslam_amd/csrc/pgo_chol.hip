@@ -347,15 +347,13 @@ __device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double*
   double va = ra ? fv[l] : 0.0, vb = rb ? fv[lb] : 0.0;
   bool bad = false;
   DIAG_CLK(24);
+  // pivot k: column k of the panel is lane j's pa[k] (rows j < W <= 64), read
+  // with v_readlane (no LDS round trip on the pivot chain)
 #pragma unroll
   for (int k = 0; k < W; k++) {
     if (k < w) {                              // uniform
-      cb[l] = pa[k];
-      cb[64 + l] = pb[k];
-      if (l == k) cb[128] = va;
-      __builtin_amdgcn_wave_barrier();
-      double d = cb[k];
-      const double vk = cb[128];
+      double d = readlane_f64(pa[k], k);
+      const double vk = readlane_f64(va, k);
       if (!(d > 0.0) || !isfinite(d)) {
         bad = true;
         d = 1.0;
@@ -365,19 +363,21 @@ __device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double*
       const double la = l > k ? pa[k] * r : (l == k ? d * r : pa[k]);
       const double lbv = pb[k] * r;
 #pragma unroll
-      for (int j = k + 1; j < W; j++) {   // branch-free: the LDS reads issue together
-        const double lj = j < w ? cb[j] * r : 0.0;
-        pa[j] = fma(l >= j ? -la : 0.0, lj, pa[j]);
-        pb[j] = fma(-lbv, lj, pb[j]);
+      for (int j = k + 1; j < W; j++) {
+        if (j < w) {                          // uniform
+          const double lj = readlane_f64(pa[k], j) * r;
+          pa[j] = fma(l >= j ? -la : 0.0, lj, pa[j]);
+          pb[j] = fma(-lbv, lj, pb[j]);
+        }
       }
       pa[k] = la;
       pb[k] = lbv;
       va = l == k ? yk : (l > k ? fma(-la, yk, va) : va);
       vb = fma(-lbv, yk, vb);
       if (l == 0) invs[k] = r;
-      __builtin_amdgcn_wave_barrier();
     }
   }
+  __builtin_amdgcn_wave_barrier();
   if (bad && l == 0) *c.flag = 1;
   DIAG_CLK(25);
   // L back to the front (and a row-major LDS copy), y to the frontal vector
@@ -394,30 +394,45 @@ __device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double*
   if (rb) fv[lb] = vb;
   __builtin_amdgcn_wave_barrier();
   DIAG_CLK(26);
-  // trailing update C[i][j] -= L[i,:] L[j,:]', w <= j <= i < m; lane rows l, l + 64;
-  // 16 columns per round so that their loads are in flight together
-  constexpr int JB = 16;
-  for (int j0 = w; j0 < m; j0 += JB) {
-    double ca[JB], cbv[JB];
+  // trailing update C[i][j] -= L[i,:] L[j,:]', w <= j <= i < m, on
+  // v_mfma_f64_16x16x4f64: per 16 x 16 lower tile D(jj, ii) = sum_k L[j0 + jj][k]
+  // L[i0 + ii][k] with both operands from the row-major LDS copy (zero beyond
+  // w); lane l holds rows i0 + (l & 15) of columns j0 + (l >> 4) + 4 r, so each
+  // column's 16 rows are one coalesced segment of the front.  A 16-column block
+  // at a time: all its tiles' loads in flight together (m <= 128: <= 8 tiles).
+  {
+    constexpr int NT = kTwoRows ? 8 : 4;   // tiles per column block (m <= 128 | 64)
+    const int u = m - w, nt = (u + 15) >> 4, li = l & 15, lk = l >> 4;
+    for (int tj = 0; tj < nt; tj++) {
+      const int j0 = w + 16 * tj;
+      const double* Aj = PR + min(j0 + li, m - 1) * LDP + lk;
+      double a[W / 4];
 #pragma unroll
-    for (int q = 0; q < JB; q++) {
-      const int j = j0 + q;
-      ca[q] = (ra && l >= w && j < m && j <= l) ? Fs[l + (size_t)j * m] : 0.0;
-      cbv[q] = (rb && j < m && j <= lb) ? Fs[lb + (size_t)j * m] : 0.0;
-    }
+      for (int kc = 0; kc < W / 4; kc++) a[kc] = Aj[4 * kc];
+      double cv[NT][4];
 #pragma unroll
-    for (int q = 0; q < JB; q++) {
-      const int j = min(j0 + q, m - 1);
-      double sa = 0.0, sb = 0.0;
+      for (int q = 0; q < NT; q++) {
+        const int i = w + 16 * (tj + q) + li;
 #pragma unroll
-      for (int k = 0; k < W; k++) {   // branch-free (pa, pb, PR are zero beyond w)
-        const double ljk = PR[j * LDP + k];
-        sa = fma(pa[k], ljk, sa);
-        if (kTwoRows) sb = fma(pb[k], ljk, sb);
+        for (int r = 0; r < 4; r++) {
+          const int j = j0 + lk + 4 * r;
+          cv[q][r] = (tj + q < nt && i < m && j <= i) ? Fs[i + (size_t)j * m] : 0.0;
+        }
       }
-      const int jj = j0 + q;
-      if (ra && l >= w && jj < m && jj <= l) Fs[l + (size_t)jj * m] = ca[q] - sa;
-      if (rb && jj < m && jj <= lb) Fs[lb + (size_t)jj * m] = cbv[q] - sb;
+#pragma unroll
+      for (int q = 0; q < NT; q++) {
+        if (tj + q >= nt) break;   // uniform
+        const int i = w + 16 * (tj + q) + li;
+        const double* Bi = PR + min(i, m - 1) * LDP + lk;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kc = 0; kc < W / 4; kc++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kc], Bi[4 * kc], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int j = j0 + lk + 4 * r;
+          if (i < m && j <= i) Fs[i + (size_t)j * m] = cv[q][r] - acc[r];
+        }
+      }
     }
   }
   DIAG_CLK(27);

@@ -6,6 +6,7 @@
 #include "../graphslam_amd/csrc/pgo_chol.hip"
 
 #include <cstdio>
+#include <cmath>
 #include <cstdlib>
 #include <vector>
 
@@ -84,6 +85,27 @@ int main(int argc, char** argv) {
     hipEventElapsedTime(&ms, a, b);
     best = ms < best ? ms : best;
   }
+  // check: the lower triangle of fronts 0, N/2, N-1 against a host partial
+  // Cholesky (w pivots, then the trailing update)
+  std::vector<double> out(h.size());
+  hipMemcpy(out.data(), F, bytes, hipMemcpyDeviceToHost);
+  double maxd = 0;
+  for (int s : {0, N / 2, N - 1}) {
+    std::vector<double> A(h.begin() + (size_t)s * M * M, h.begin() + (size_t)(s + 1) * M * M);
+    for (int k = 0; k < W; k++) {
+      const double p = std::sqrt(A[k + k * M]);
+      A[k + k * M] = p;
+      for (int i = k + 1; i < M; i++) A[i + k * M] /= p;
+      for (int j = k + 1; j < M; j++)
+        for (int i = j; i < M; i++) A[i + j * M] -= A[i + k * M] * A[j + k * M];
+    }
+    for (int j = 0; j < M; j++)
+      for (int i = j; i < M; i++) {
+        const double d = std::fabs(A[i + j * M] - out[(size_t)s * M * M + i + (size_t)j * M]);
+        maxd = d > maxd ? d : maxd;
+      }
+  }
+  printf("  max |F - host| over 3 fronts: %.3g\n", maxd);
   long long clk[32];
   hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_diag_clk), sizeof(clk));
   int fl = 0;
