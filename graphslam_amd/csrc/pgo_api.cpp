@@ -44,6 +44,7 @@ struct Lane {
 struct Staging {
   char* buf = nullptr;
   size_t cap = 0, used = 0;
+  hipEvent_t done = nullptr;                // recorded after a batch's copies (stage_end)
 };
 
 struct HostStructure {
@@ -296,6 +297,19 @@ int h2d(pgo_graph* g, T* dst, const T* src, size_t count) {
 // Host -> device through the handle's pinned staging buffer (a bump region per
 // batch of copies; stage_reset after the stream has drained): the live
 // re-solve's per-registration uploads at pinned speed
+// a batch of staged copies: wait until the previous batch's copies have read
+// the buffer, then refill it from the start; stage_end marks the batch
+int stage_begin(pgo_graph* g, Staging& st) {
+  if (st.done) HIP_TRY(g, hipEventSynchronize(st.done));
+  else HIP_TRY(g, hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
+  st.used = 0;
+  return PGO_OK;
+}
+int stage_end(pgo_graph* g, Staging& st) {
+  HIP_TRY(g, hipEventRecord(st.done, g->d.stream));
+  return PGO_OK;
+}
+
 template <class T>
 int staged_h2d(pgo_graph* g, Staging& st, T* dst, const T* src, size_t count) {
   if (count == 0) return PGO_OK;
@@ -526,6 +540,18 @@ int upload_structure(pgo_graph* g) {
   const size_t ce = (size_t)ne + std::max<size_t>(4096, ne / 8), cs = 2 * ce;
   g->cap_n = cn;
   g->cap_ne = ce;
+  {   // the appends' pinned staging (append_structure / bind_plan), sized for the
+      // largest per-registration upload of this graph, allocated with the graph
+    const size_t want = 8 * cs + 8 * ce + 80 * cn + ((size_t)1 << 20);
+    if (g->stage.cap < want) {
+      if (g->stage.done) HIP_TRY(g, hipEventSynchronize(g->stage.done));
+      if (g->stage.buf) (void)hipHostFree(g->stage.buf);
+      g->stage.buf = nullptr;
+      g->stage.cap = 0;
+      HIP_TRY(g, hipHostMalloc((void**)&g->stage.buf, want, hipHostMallocDefault));
+      g->stage.cap = want;
+    }
+  }
   // lanes per row: smallest power of two >= mean degree, in [4, 32]
   const double mean_deg = n ? (double)ns / n : 0.0;
   d.G = 4;
@@ -835,14 +861,8 @@ int append_structure(pgo_graph* g) {
   // only what changed: the new factors; the row / slot arrays from the first
   // row with a new slot (earlier rows and their slots are unchanged); the
   // side-1 sums of the rows that gained side-1 terms; whole for the rest
-  if (g->stage.cap < ((size_t)64 << 20)) {
-    if (g->stage.buf) (void)hipHostFree(g->stage.buf);
-    g->stage = Staging();
-    HIP_TRY(g, hipHostMalloc((void**)&g->stage.buf, (size_t)64 << 20, hipHostMallocDefault));
-    g->stage.cap = (size_t)64 << 20;
-  }
-  Staging& sg = g->stage;
-  sg.used = 0;
+  Staging& sg = g->stage;   // (allocated by upload_structure; staged_h2d falls back to pageable copies)
+  RC_TRY(stage_begin(g, sg));
   const int r0 = extra.empty() ? n_old : std::min(extra.front().x, n_old);   // first row with a new slot
   int x0 = n_old, y0 = n_old;   // (the new rows always)
   for (const int2& ij : nij) {
@@ -869,6 +889,7 @@ int append_structure(pgo_graph* g) {
     RC_TRY(staged_h2d(g, sg, d.Dc + 6 * (size_t)n_old, g->h_Dc.data() + 6 * (size_t)n_old, 6 * (size_t)(n - n_old)));
   }
   RC_TRY(staged_h2d(g, sg, d.brow, brow.data(), brow.size()));
+  RC_TRY(stage_end(g, sg));
   d.n = n;
   d.ne = ne;
   d.nslots = ns;
@@ -1084,11 +1105,11 @@ int bind_plan(pgo_graph* g, bool full) {
     }
     phase("chol_upload");
     if (!g->d.eside) RC_TRY(dev_alloc(g, &g->d.eside, std::max<size_t>(g->cap_ne, g->d.ne)));
-    if (g->stage.buf) {   // pinned staging (the live re-solve: idle since append_structure drained
-                          // the stream; the copies and the fronts' zeroing run on unsynchronised)
-      g->stage.used = 0;
+    if (g->stage.buf) {   // pinned staging: the copies (and the fronts' zeroing) run on unsynchronised
+      RC_TRY(stage_begin(g, g->stage));
       RC_TRY(staged_h2d(g, g->stage, g->d.eside, eside.data(), eside.size()));
       RC_TRY(staged_h2d(g, g->stage, g->d.slot_edge, slot_edge.data(), slot_edge.size()));
+      RC_TRY(stage_end(g, g->stage));
     } else {
       RC_TRY(h2d(g, g->d.eside, eside.data(), eside.size()));
       RC_TRY(h2d(g, g->d.slot_edge, slot_edge.data(), slot_edge.size()));
@@ -1521,6 +1542,7 @@ void pgo_destroy(pgo_graph* g) {
     if (g->h_ctrl) (void)hipHostFree(g->h_ctrl);
     if (g->h_lam) (void)hipHostFree(g->h_lam);
     if (g->stage.buf) (void)hipHostFree(g->stage.buf);
+    if (g->stage.done) (void)hipEventDestroy(g->stage.done);
     if (g->h_lanes) (void)hipHostFree(g->h_lanes);
     for (auto& e : g->pev)
       if (e) (void)hipEventDestroy(e);
