@@ -162,6 +162,22 @@ int check_assembly(const pgo::CholPlan& P) {
   return 0;
 }
 
+// Packed fronts: no Schur tile's columns straddle a 64-column block (the
+// kernels address a tile's columns from one block base).
+int check_tiles(const pgo::CholPlan& P) {
+  for (const auto& lv : P.levels)
+    for (const auto& ps : lv.panels)
+      for (int q = ps.syrk_off; q < ps.syrk_off + ps.syrk_cnt; q++) {
+        const int4 t = P.syrk_tasks[q];
+        const int clip = t.y >> pgo::kClipShift, c0 = t.z, T = ps.syrk_tile;
+        const int c1 = std::min(c0 + (clip ? clip : T), P.m[t.x]);
+        if (T == pgo::kTile && (c0 >> 6) != ((c1 - 1) >> 6)) return fail("a 64-tile straddles two column blocks");
+        if (T == pgo::kBigTile && (c0 & 63) && (c0 >> 6) != ((c1 - 1) >> 6))
+          return fail("an unaligned 128-tile straddles two column blocks");
+      }
+  return 0;
+}
+
 // the pattern restricted to poses [0, n)
 Pattern restrict_pattern(const Pattern& G, int n) {
   Pattern R;
@@ -242,7 +258,7 @@ int main() {
     if (P.ns <= 0 || P.flops <= 0) return fail("analysis");
     if (P.schedule_error) return fail("panel schedule bookkeeping");
     if (!pgo::chol_covers(P, G.n, G.row_ptr, G.col)) return fail("plan does not cover its own pattern");
-    if (check_assembly(P)) return 1;
+    if (check_assembly(P) || check_tiles(P)) return 1;
     for (int size : {2, 4}) {
       std::vector<double> rf;
       double top = 0;
@@ -255,7 +271,7 @@ int main() {
         Q.part_rank = r;
         pgo::chol_analyze(Q, G.n, G.row_ptr, G.col);
         if (Q.ns != P.ns || Q.schedule_error) return fail("partitioned plan");
-        if (check_assembly(Q)) return 1;
+        if (check_assembly(Q) || check_tiles(Q)) return 1;
       }
     }
     // a loop closure inside the existing fill: same fronts, new assembly lists
@@ -298,6 +314,7 @@ int main() {
     }
     pgo::CholPlan P;
     pgo::chol_analyze(P, G.n, G.row_ptr, G.col);
+    if (check_tiles(P)) return 1;
     for (int size : {2, 3, 4, 8})
       if (check_distributed(G, pgo::kOrderNd, size)) return 1;
     int maxw = 0;

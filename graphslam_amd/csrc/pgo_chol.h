@@ -9,8 +9,9 @@
 // (leaves first), every front of a level in flight at once.
 //
 // Fronts: supernode s has w_s = 3 * (its poses) pivot columns and
-// m_s = w_s + 3 * (its below-diagonal pose rows) rows; its m_s x m_s frontal
-// matrix lives column-major at F + foff[s] for the whole factorisation, so the
+// m_s = w_s + 3 * (its below-diagonal pose rows) rows; its frontal matrix (the
+// lower trapezoid by 64-column blocks, or m_s x m_s for a small front:
+// front_packed) lives at F + foff[s] for the whole factorisation, so the
 // L panel (first w_s columns) stays in place for the solves and the update
 // matrix (trailing block) stays in place until the parent pulls it.
 #pragma once
@@ -36,6 +37,21 @@ constexpr int kBwdRows = 512;      // rows per partial product of the backward s
 // tile split where the column owner changes)
 constexpr int kClipShift = 20;
 constexpr int kRowMask = (1 << kClipShift) - 1;
+
+// Front storage.  A front on the blocked path (front_packed: more than
+// kSmallFront rows or more than kWaveW pivot columns) keeps only its lower
+// trapezoid, in 64-column blocks: block b (columns [64 b, 64 b + 64)) holds
+// rows [64 b, m) column-major with leading dimension m - 64 b, the blocks back
+// to back from fblock_off(m, b) -- about half the m x m square.  The small
+// fronts (one wavefront / workgroup each, m <= kSmallFront) stay m x m
+// column-major.  front_elems: the doubles a front occupies.
+__host__ __device__ inline bool front_packed(int m, int w) { return m > kSmallFront || w > kWaveW; }
+__host__ __device__ inline long long fblock_off(int m, long long b) { return 64 * b * m - 2048 * b * (b - 1); }
+__host__ __device__ inline long long front_elems(int m, int w) {
+  if (!front_packed(m, w)) return (long long)m * m;
+  const long long nb = (m + 63) / 64, r = m - 64 * (nb - 1);
+  return fblock_off(m, nb - 1) + r * r;
+}
 
 struct PanelStep {                 // one 64-column panel kb of every big front of a level
   int kb;

@@ -88,6 +88,22 @@ static CholDev dev_view(const CholPlan& P) {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+// Front storage (pgo_chol.h front_packed / front_elems): element (i, j) of the
+// front at Fs is fcol(Fs, m, pk, j)[i] -- for a packed front (the blocked
+// path) column block b = j / 64 holds rows [64 b, m) with leading dimension
+// fld(m, pk, j) = m - 64 b, so i >= 64 b; an unpacked one is m x m.
+__device__ __forceinline__ long long fcol_off(int m, bool pk, int j) {
+  if (!pk) return (long long)j * m;
+  const long long b = j >> 6, c0 = b << 6;
+  return fblock_off(m, b) + (j - c0) * (long long)(m - c0) - c0;
+}
+template <class T>
+__device__ __forceinline__ T* fcol(T* Fs, int m, bool pk, int j) {
+  return Fs + fcol_off(m, pk, j);
+}
+__device__ __forceinline__ int fld(int m, bool pk, int j) { return pk ? m - (j & ~63) : m; }
+
+
 // Step timing stamps (diagnostics, PGO_STEP_STAMPS): k_step launches given a
 // slot >= 0 record wall-clock stamps of their first diagonal workgroup and first
 // waiting workgroup; read back with chol_step_stamps.  Written only here and
@@ -123,6 +139,7 @@ __global__ __launch_bounds__(256) void k_assemble_tile(CholDev c, const int4* __
   lane_offset(c);
   __shared__ double T[64 * 65];
   __shared__ int prow[64], pcol[64];
+  __shared__ long long ucol[64];   // the child's update-matrix columns: offset of (wc, wc + b0 + q) in its front
   const int4 t = tasks[blockIdx.x];
   const int p = t.x, mp = c.m[p];
   const int R0 = 64 * (t.y >> 16), C0 = 64 * (t.y & 0xffff);
@@ -172,17 +189,19 @@ __global__ __launch_bounds__(256) void k_assemble_tile(CholDev c, const int4* __
     } else if (tid >= 64 && tid - 64 < nc) {
       const int b = b0 + tid - 64;
       pcol[tid - 64] = (3 * rel[b / 3] + b % 3 - C0) * 65;
+    } else if (tid >= 128 && tid - 128 < nc) {
+      ucol[tid - 128] = fcol_off(mc, front_packed(mc, wc), wc + b0 + tid - 128) + wc;
     }
     __syncthreads();
     if (r >= nr) continue;
     const int a = a0 + r;
-    const double* __restrict__ U = c.F + c.foff[ch] + wc + (size_t)wc * mc + a;
+    const double* __restrict__ Fch = c.F + c.foff[ch] + a;
     constexpr int R = 16;
     double v[R];
 #pragma unroll
     for (int j = 0; j < R; j++) {
       const int bb = cg + 4 * j;
-      v[j] = (bb < nc && b0 + bb <= a) ? U[(size_t)(b0 + bb) * mc] : 0.0;
+      v[j] = (bb < nc && b0 + bb <= a) ? Fch[ucol[bb]] : 0.0;
     }
     const int pr = prow[r];
 #pragma unroll
@@ -192,11 +211,13 @@ __global__ __launch_bounds__(256) void k_assemble_tile(CholDev c, const int4* __
     }
   }
   __syncthreads();
-  double* __restrict__ Fp = c.F + c.foff[p];
+  const bool pkp = front_packed(mp, c.w[p]);
+  double* __restrict__ Fp = fcol(c.F + c.foff[p], mp, pkp, C0);   // the tile's columns: one column block
+  const int ldp = fld(mp, pkp, C0);
 #pragma unroll
   for (int u = 0; u < 16; u++) {
     const int i = tid & 63, j = (tid >> 6) + 4 * u, row = R0 + i, col = C0 + j;
-    if (row < mp && col < mp && row >= col) Fp[row + (size_t)col * mp] = T[i + j * 65];
+    if (row < mp && col < mp && row >= col) Fp[row + (size_t)j * ldp] = T[i + j * 65];
   }
 }
 
@@ -795,14 +816,14 @@ __device__ __forceinline__ void publish_inverse(double* __restrict__ Mf, const d
   }
 }
 
-// After the hand-off: L (LDS Ts, ld 65) back into the front, X row-major to M
-// (the backward solve's copy)
-__device__ __forceinline__ void store_factor(double* Fs, int m, double* __restrict__ M, const double* Ts,
+// After the hand-off: L (LDS Ts, ld 65) back into the front (Fs: the tile, ld
+// its column block's), X row-major to M (the backward solve's copy)
+__device__ __forceinline__ void store_factor(double* Fs, int ld, double* __restrict__ M, const double* Ts,
                                              const double* Ws, int nb) {
   const int tid = threadIdx.x;
   for (int idx = tid; idx < 4096; idx += 256) {
     const int i = idx & 63, j = idx >> 6;
-    if (i < nb && j < nb && i >= j) Fs[i + (size_t)j * m] = Ts[i + j * 65];
+    if (i < nb && j < nb && i >= j) Fs[i + (size_t)j * ld] = Ts[i + j * 65];
     const int a = idx >> 6, b = idx & 63;
     M[idx] = (a < nb && b < nb && a >= b) ? Ws[a + b * 65] : 0.0;
   }
@@ -813,7 +834,7 @@ __device__ __forceinline__ void store_factor(double* Fs, int m, double* __restri
 // columns < nb) while the block was factored; solved here: L = A X^T (X = Ws),
 // written to the front (columns < nb) and v -= L y for those rows (rows with
 // r0 + i >= m, i >= rrem, skipped).  Ts is scratch (the live block is stored).
-__device__ __forceinline__ void diag_own_rows(double* Fs, int m, int rrem, double* v, const double* keep, double* Ts,
+__device__ __forceinline__ void diag_own_rows(double* Fs, int ld, int rrem, double* v, const double* keep, double* Ts,
                                               const double* Ws, const double* ys, int nb) {
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
 #pragma unroll
@@ -848,7 +869,7 @@ __device__ __forceinline__ void diag_own_rows(double* Fs, int m, int rrem, doubl
     double t = 0.0;
     for (int j = 0; j < nb; j++) {
       const double lij = Ts[tid + j * 65];
-      Fs[tid + (size_t)j * m] = lij;
+      Fs[tid + (size_t)j * ld] = lij;
       t = fma(lij, ys[j], t);
     }
     v[tid] -= t;
@@ -893,7 +914,8 @@ __device__ __forceinline__ void trsm_rows(const CholDev& c, int s, int r0, int k
   }
   __syncthreads();
   if (rw >= m) return;                                // (no barriers below)
-  double* Fc = c.F + c.foff[s] + (size_t)kn * m;
+  double* Fc = fcol(c.F + c.foff[s], m, true, kn);   // the panel's column block (blocked fronts are packed)
+  const int ldc = m - kn;
   const int il = wv * 16 + (l & 15), arow = r0 + il;
   double a[16], tb[16][4];   // A fragments, inverse fragments
 #pragma unroll
@@ -924,7 +946,7 @@ __device__ __forceinline__ void trsm_rows(const CholDev& c, int s, int r0, int k
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int row = rw + kl + 4 * r;
-      if (row < m) Fc[row + (size_t)col * m] = v[r];
+      if (row < m) Fc[row + (size_t)col * ldc] = v[r];
     }
   }
 #pragma unroll
@@ -956,6 +978,8 @@ __device__ __forceinline__ void syrk_tile64(const CholDev& c, const int4 t, int 
   if (row0 == col0 && qi < qj) return;       // strictly upper quarter of a diagonal tile (caller syncs)
   const int li = l & 15, lk = l >> 4;
   double* Fs = c.F + c.foff[s];
+  double* Cb = fcol(Fs, m, true, col0);   // the tile's columns: one column block (col0 = kn)
+  const int ldc = m - (col0 & ~63);
   const int rA = row0 + qi + li, rB = rA + 16;          // C rows (B operand rows)
   const int cA = col0 + qj + li, cB = cA + 16;          // C columns (A operand rows)
   // C prefetch (output layout: lane l, reg r -> column col0+qj+16mj+lk+4r, row row0+qi+16mi+li)
@@ -967,18 +991,17 @@ __device__ __forceinline__ void syrk_tile64(const CholDev& c, const int4 t, int 
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int row = row0 + qi + 16 * mi + li, col = col0 + qj + 16 * mj + lk + 4 * r;
-        cold[mi][mj][r] = (row < m && col < colend && row >= col) ? Fs[row + (size_t)col * m] : 0.0;
+        cold[mi][mj][r] = (row < m && col < colend && row >= col) ? Cb[row + (size_t)(col - col0) * ldc] : 0.0;
       }
   const bool vrA = rA < m, vrB = rB < m, vcA = cA < m, vcB = cB < m;
-  const double* P = Fs + (size_t)(k0 + lk) * m;
   d4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc10 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
   const int K = kend - k0;
   for (int kk = 0; kk < K; kk += 16) {       // 16 operand loads in flight, then 16 MFMAs
     double ra[4], rb[4], ca[4], cb[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const bool kin = kk + 4 * u + lk < K;
-      const double* pk = P + (size_t)(kk + 4 * u) * m;
+      const bool kin = kk + 4 * u + lk < K;   // (16 panel columns from k0 + kk: one column block)
+      const double* pk = fcol(Fs, m, true, k0 + kk) + (size_t)(4 * u + lk) * (m - ((k0 + kk) & ~63));
       ra[u] = (kin && vrA) ? pk[rA] : 0.0;
       rb[u] = (kin && vrB) ? pk[rB] : 0.0;
       ca[u] = (kin && vcA) ? pk[cA] : 0.0;
@@ -1002,7 +1025,7 @@ __device__ __forceinline__ void syrk_tile64(const CholDev& c, const int4 t, int 
         const int row = row0 + qi + 16 * mi + li, col = col0 + qj + 16 * mj + lk + 4 * r;
         if (row < m && col < colend && row >= col) {
           const double v = cold[mi][mj][r] - a[r];
-          Fs[row + (size_t)col * m] = v;
+          Cb[row + (size_t)(col - col0) * ldc] = v;
           if (kToLds) Ts[(row - row0) + (col - col0) * 65] = v;
         }
       }
@@ -1034,7 +1057,6 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
   if (clip) colend = min(colend, col0 + clip);   // a split tile: its columns only
   const int K = kend - k0, nch = (K + 15) >> 4;
   double* Fs = c.F + c.foff[s];
-  const double* P = Fs + (size_t)k0 * m;
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   const int qi = 32 * (wv >> 1), qj = 32 * (wv & 1);
   const bool active = !(row0 == col0 && qi < qj);
@@ -1044,8 +1066,9 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
   auto load = [&](int ch) {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
+      // the chunk's 16 panel columns sit in one column block (k0: a panel start)
       const int idx = tid + 256 * q, k = 16 * ch + (idx >> 6), r = idx & 63;
-      const double* pk = P + (size_t)k * m;
+      const double* pk = fcol(Fs, m, true, k0 + 16 * ch) + (size_t)(idx >> 6) * (m - ((k0 + 16 * ch) & ~63));
       st[q] = (k < K && row0 + r < m) ? pk[row0 + r] : 0.0;
       st[4 + q] = (k < K && col0 + r < m) ? pk[col0 + r] : 0.0;
     }
@@ -1096,21 +1119,24 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
     __syncthreads();
   }
   if (!active) return;
-  // C read-modify-write: lane l holds (row row0 + qi + 16h + (l & 15), column col0 + qj + 4p + (l >> 4))
+  // C read-modify-write: lane l holds (row row0 + qi + 16h + (l & 15), column col0 + qj + 4p + (l >> 4));
+  // the tile's columns lie in col0's column block (the planner never lets a tile straddle two)
+  double* Cb = fcol(Fs, m, true, col0);
+  const int ldc = m - (col0 & ~63);
   double cold[8][2];
 #pragma unroll
   for (int p = 0; p < 8; p++)
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int row = row0 + qi + 16 * h + (l & 15), col = col0 + qj + 4 * p + lk;
-      cold[p][h] = (row < m && col < colend && row >= col) ? Fs[row + (size_t)col * m] : 0.0;
+      cold[p][h] = (row < m && col < colend && row >= col) ? Cb[row + (size_t)(col - col0) * ldc] : 0.0;
     }
 #pragma unroll
   for (int p = 0; p < 8; p++)
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int row = row0 + qi + 16 * h + (l & 15), col = col0 + qj + 4 * p + lk;
-      if (row < m && col < colend && row >= col) Fs[row + (size_t)col * m] = cold[p][h] - acc[p][h];
+      if (row < m && col < colend && row >= col) Cb[row + (size_t)(col - col0) * ldc] = cold[p][h] - acc[p][h];
     }
 }
 
@@ -1141,18 +1167,22 @@ __device__ __forceinline__ void diag_tile_update(const CholDev& c, const int4 t,
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   const int li = l & 15, lk = l >> 4;
   double st[16];
-  auto load = [&](int ch) {
+  auto load = [&](int ch) {   // chunk ch: panel columns k0 + 64 ch ..: one column block
+    const double* Pb = fcol(Fs, m, true, k0 + 64 * ch);
+    const int ldp = m - k0 - 64 * ch;
 #pragma unroll
     for (int q = 0; q < 16; q++) {
       const int idx = tid + 256 * q, i = idx & 63, k = 64 * ch + (idx >> 6);
-      st[q] = (k < K && r0 + i < m) ? Fs[(r0 + i) + (size_t)(k0 + k) * m] : 0.0;
+      st[q] = (k < K && r0 + i < m) ? Pb[(r0 + i) + (size_t)(idx >> 6) * ldp] : 0.0;
     }
   };
+  double* Db = fcol(Fs, m, true, r0) + r0;   // the diagonal tile, ld m - r0
+  const int ldd = m - r0;
   double cv[16];   // C, lower part of the updated region: its loads and the first chunk's in flight together
 #pragma unroll
   for (int q = 0; q < 16; q++) {
     const int idx = tid + 256 * q, i = idx & 63, j = idx >> 6;
-    cv[q] = (i >= j && r0 + i < m && r0 + j < colend) ? Fs[(r0 + i) + (size_t)(r0 + j) * m] : 0.0;
+    cv[q] = (i >= j && r0 + i < m && r0 + j < colend) ? Db[i + (size_t)j * ldd] : 0.0;
   }
   load(0);
 #pragma unroll
@@ -1195,7 +1225,7 @@ __device__ __forceinline__ void diag_tile_update(const CholDev& c, const int4 t,
       if (i >= j && r0 + i < m && r0 + j < colend) {
         const double v = Ts[i + j * 65] - a[r];
         Ts[i + j * 65] = v;
-        if (!(i < nb && j < nb)) Fs[(r0 + i) + (size_t)(r0 + j) * m] = v;
+        if (!(i < nb && j < nb)) Db[i + (size_t)j * ldd] = v;
       }
     }
   }
@@ -1233,7 +1263,7 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
   __syncthreads();
   if (diag_factor_invert(Ts, Ws, bc)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   STAMP(slot, 2);
-  double* Fs = c.F + c.foff[s] + kn + (size_t)kn * m;
+  double* Fs = fcol(c.F + c.foff[s], m, true, kn) + kn;   // the diagonal tile, ld m - kn
   double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;   // row-major L^-1 of the tile
   double* v = c.fv + c.voff[s] + kn;
   publish_inverse(M + c.tfo, Ws, nb);
@@ -1241,10 +1271,10 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
   STAMP(slot, 3);
   publish_step(c.stepflag + s, kn / 64 + 1);
   STAMP(slot, 4);
-  store_factor(Fs, m, M, Ts, Ws, nb);
+  store_factor(Fs, m - kn, M, Ts, Ws, nb);
   if (nb < kNB) {
     __syncthreads();
-    diag_own_rows(Fs, m, m - kn, v, keep, Ts, Ws, ys, nb);
+    diag_own_rows(Fs, m - kn, m - kn, v, keep, Ts, Ws, ys, nb);
   }
 }
 
@@ -1443,15 +1473,15 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
   __shared__ __attribute__((aligned(16))) double Sr[2][16 * LD];
   __shared__ __attribute__((aligned(16))) double Sc[2][16 * LD];
   const int4 t = tasks[blockIdx.x];
-  const int s = t.x, row0 = t.y, col0 = t.z;
+  const int s = t.x, row0 = t.y & kRowMask, col0 = t.z, clip = t.y >> kClipShift;
   const bool inner = t.w < 0;
   const int k0 = t.w & 0x7fffffff;
   const int m = c.m[s], w = c.w[s];
   const int kend = min(kb + kNB, w);
-  const int colend = inner ? min((kb & ~(kKB - 1)) + kKB, w) : m;
+  int colend = inner ? min((kb & ~(kKB - 1)) + kKB, w) : m;
+  if (clip) colend = min(colend, col0 + clip);   // a narrow tile (up to its column block's end)
   const int K = kend - k0, nchunk = (K + 15) >> 4;
   double* Fs = c.F + c.foff[s];
-  const double* P = Fs + (size_t)k0 * m;
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   const int wi = wv >> 1, wj = wv & 1;
   const bool active = !(row0 == col0 && wi < wj) && row0 + 64 * wi < m && col0 + 64 * wj < colend;
@@ -1462,7 +1492,7 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
     for (int q = 0; q < 8; q++) {
       const int idx = tid + 256 * q, k = 16 * ch + (idx >> 7), r = idx & 127;
       const bool kin = k < K;
-      const double* pk = P + (size_t)k * m;
+      const double* pk = fcol(Fs, m, true, k0 + 16 * ch) + (size_t)(idx >> 7) * (m - ((k0 + 16 * ch) & ~63));
       st[q] = (kin && row0 + r < m) ? pk[row0 + r] : 0.0;
       st[8 + q] = (kin && col0 + r < m) ? pk[col0 + r] : 0.0;
     }
@@ -1510,6 +1540,8 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
     __syncthreads();
   }
   if (!active) return;
+  double* Cb = fcol(Fs, m, true, col0 + 64 * wj);   // the wave's columns: one column block
+  const int ldc = m - ((col0 + 64 * wj) & ~63);
 #pragma unroll
   for (int p = 0; p < 16; p++) {
     double cold[4];
@@ -1517,12 +1549,12 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
 #pragma unroll
     for (int h = 0; h < 4; h++) {
       const int row = row0 + 64 * wi + 16 * h + (l & 15);
-      cold[h] = (row < m && col < colend && row >= col) ? Fs[row + (size_t)col * m] : 0.0;
+      cold[h] = (row < m && col < colend && row >= col) ? Cb[row + (size_t)(col - col0 - 64 * wj) * ldc] : 0.0;
     }
 #pragma unroll
     for (int h = 0; h < 4; h++) {
       const int row = row0 + 64 * wi + 16 * h + (l & 15);
-      if (row < m && col < colend && row >= col) Fs[row + (size_t)col * m] = cold[h] - acc[p][h];
+      if (row < m && col < colend && row >= col) Cb[row + (size_t)(col - col0 - 64 * wj) * ldc] = cold[h] - acc[p][h];
     }
   }
 }
@@ -1541,15 +1573,17 @@ __global__ __launch_bounds__(256) void k_xroots(CholDev c, const int4* __restric
   lane_offset(c);
   const int4 t = tasks[blockIdx.x];
   const int s = t.x, u = t.z, m = c.m[s], w = c.w[s];
-  double* U = c.F + c.foff[s] + w + (size_t)w * m;
+  double* Fs = c.F + c.foff[s];
+  const bool pk = front_packed(m, w);
   double* v = c.fv + c.voff[s] + w;
   double* b = buf + t.w * rstride + blockIdx.y * slot + t.y;
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
   for (int j = wv; j < u; j += 4) {
     double* col = b + (size_t)j * u - (size_t)j * (j - 1) / 2;
+    double* U = fcol(Fs, m, pk, w + j) + w;   // U(i, j) = U[i]
     for (int i = j + l; i < u; i += 64) {
-      if (kPack) col[i - j] = U[i + (size_t)j * m];
-      else U[i + (size_t)j * m] = col[i - j];
+      if (kPack) col[i - j] = U[i];
+      else U[i] = col[i - j];
     }
   }
   double* bv = b + (size_t)u * (u + 1) / 2;
@@ -1609,10 +1643,10 @@ __global__ __launch_bounds__(256) void k_xpanel(CholDev c, const int4* __restric
   if (kPack != (t.w == me)) return;
   const int s = t.x, kn = t.y, nb = t.z & 0xffff, kind = t.z >> 16, m = c.m[s];
   double* b = buf + t.w * rstride + blockIdx.y * offs[2 * blockIdx.x + 1] + offs[2 * blockIdx.x];
-  double* F = c.F + c.foff[s] + kn + (size_t)kn * m;
+  double* Fs = c.F + c.foff[s];
   const int rows = m - kn, tid = threadIdx.x;
   for (int cc = 0; cc < nb; cc++) {
-    double* col = F + (size_t)cc * m;
+    double* col = fcol(Fs, m, true, kn + cc) + kn;   // (a top front on the blocked path)
     double* bc = b + (size_t)cc * rows;
     for (int r = tid; r < rows; r += 256) {
       if (kPack) bc[r] = col[r];
@@ -1723,7 +1757,7 @@ __device__ __forceinline__ void halve(double* acc, int lane) {
 // memory latencies.  NC = 16 serves the narrow fronts near the leaves with a
 // quarter of the reduction.
 template <int NC>
-__device__ __forceinline__ double bwd_part_wave(const CholDev& c, const double* L, const int* rows, int m,
+__device__ __forceinline__ double bwd_part_wave(const CholDev& c, const double* L, const int* rows, int ld,
                                                 int ncol, int rbeg, int r1, int lane) {
   double acc[NC];
 #pragma unroll
@@ -1733,7 +1767,7 @@ __device__ __forceinline__ double bwd_part_wave(const CholDev& c, const double* 
     const double* Lr = L + r;
     double lv[NC];
 #pragma unroll
-    for (int q = 0; q < NC; q++) lv[q] = Lr[(size_t)min(q, ncol - 1) * m];
+    for (int q = 0; q < NC; q++) lv[q] = Lr[(size_t)min(q, ncol - 1) * ld];
 #pragma unroll
     for (int q = 0; q < NC; q++)
       if (q < ncol) acc[q] += lv[q] * xr;
@@ -1766,15 +1800,17 @@ __global__ __launch_bounds__(256) void k_bwd_part(CholDev c, const int4* __restr
   const int s = t.x, c0 = t.y, r0 = t.z, slot = t.w;
   const int m = c.m[s], w = c.w[s];
   const int ncol = min(64, w - c0), r1 = min(r0 + kBwdRows, m);
-  const double* L = c.F + c.foff[s] + (size_t)c0 * m;
+  const bool pk = front_packed(m, w);
+  const double* L = fcol(c.F + c.foff[s], m, pk, c0);   // columns c0 .. c0 + 63: one column block
+  const int ld = fld(m, pk, c0);
   const int* rows = c.rows + c.rptr[s];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (r0 + 64 * wv >= r1)
     red[wv][lane] = 0.0;   // no rows for this wave (small fronts): skip the reduction
   else if (ncol <= 16)
-    red[wv][lane] = bwd_part_wave<16>(c, L, rows, m, ncol, r0 + tid, r1, lane);
+    red[wv][lane] = bwd_part_wave<16>(c, L, rows, ld, ncol, r0 + tid, r1, lane);
   else
-    red[wv][lane] = bwd_part_wave<64>(c, L, rows, m, ncol, r0 + tid, r1, lane);
+    red[wv][lane] = bwd_part_wave<64>(c, L, rows, ld, ncol, r0 + tid, r1, lane);
   __syncthreads();
   if (tid < 64) part[(size_t)slot * 64 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
 }
@@ -1834,9 +1870,11 @@ __global__ __launch_bounds__(256) void k_bwd_step(CholDev c, const int4* __restr
   // wave wv: columns c0 + 16 wv + q (q < 16), lane = row jb + lane of block b
   double acc[16];
   const bool rin = lane < nbk;
-  const double* Lr = L + (jb + lane) + (size_t)(c0 + 16 * wv) * m;
+  const bool pk = front_packed(m, w);
+  const double* Lr = fcol(L, m, pk, c0 + 16 * wv) + (jb + lane);   // (c0: a column block's start)
+  const int ld = fld(m, pk, c0);
 #pragma unroll
-  for (int q = 0; q < 16; q++) acc[q] = (rin && c0 + 16 * wv + q < c1) ? Lr[(size_t)q * m] : 0.0;
+  for (int q = 0; q < 16; q++) acc[q] = (rin && c0 + 16 * wv + q < c1) ? Lr[(size_t)q * ld] : 0.0;
   if (tid < 64) xbk[tid] = tid < nbk ? fv[jb + tid] : 0.0;
   __syncthreads();
   const double xl = xbk[lane];
@@ -1895,9 +1933,11 @@ __global__ __launch_bounds__(256) void k_bwd_chain(CholDev c, const int4* __rest
     const int jb = b * 64, nbk = min(64, w - jb);
     double acc[16];
     const bool rin = lane < nbk;
-    const double* Lr = L + (jb + lane) + (size_t)(c0 + 16 * wv) * m;
+    const bool pk = front_packed(m, w);
+    const double* Lr = fcol(L, m, pk, c0 + 16 * wv) + (jb + lane);   // (c0: a column block's start)
+    const int ld = fld(m, pk, c0);
 #pragma unroll
-    for (int q = 0; q < 16; q++) acc[q] = (rin && c0 + 16 * wv + q < c1) ? Lr[(size_t)q * m] : 0.0;
+    for (int q = 0; q < 16; q++) acc[q] = (rin && c0 + 16 * wv + q < c1) ? Lr[(size_t)q * ld] : 0.0;
     if (b < nblk - 1) wait_step(c, c.stepflag + s, nblk - 1 - b);   // x_b from its chain workgroup
     if (tid < 64) xbk[tid] = tid < nbk ? ld_sc1(fv + jb + tid) : 0.0;
     __syncthreads();
@@ -1977,10 +2017,13 @@ __global__ __launch_bounds__(256) void k_marginals(CholDev c, const int2* __rest
         g[5] += y2 * y2;
       }
       __syncthreads();
+      const bool pk = front_packed(m, w);
+      const double* Lb = fcol(L, m, pk, c0);   // columns c0 .. c0 + n2: one column block
+      const int ld = fld(m, pk, c0);
       for (int r = c0 + n2 + tid; r < m; r += 256) {
         double a0 = 0, a1 = 0, a2 = 0;
         for (int k = 0; k < n2; k++) {
-          const double l = L[r + (size_t)(c0 + k) * m];
+          const double l = Lb[r + (size_t)k * ld];
           a0 = fma(l, ys[0][k], a0);
           a1 = fma(l, ys[1][k], a1);
           a2 = fma(l, ys[2][k], a2);

@@ -157,9 +157,7 @@ static double front_flops(int m, int w) {
 }
 
 // blocked path (64-column panels) vs one workgroup / wavefront per front
-static bool is_blocked(const CholPlan& P, int s) {
-  return P.m[s] > kSmallFront || (P.w[s] > kWaveW && !getenv("PGO_SMALL_LDS"));
-}
+static bool is_blocked(const CholPlan& P, int s) { return front_packed(P.m[s], P.w[s]); }
 
 // Column owners of the distributed top (see chol_analyze): per top front s
 // (owner[s] < 0) its m columns at cown[off[s] ..]: rank, or -1 (every rank).
@@ -221,8 +219,7 @@ static void size_fronts(CholPlan& P) {
   P.flops = 0;
   P.nnzl = 0;
   for (int s = 0; s < ns; s++) {
-    const long long mm = P.m[s];
-    P.foff[s + 1] = P.foff[s] + ((mm * mm + 7) / 8) * 8;   // 64-byte aligned fronts
+    P.foff[s + 1] = P.foff[s] + ((front_elems(P.m[s], P.w[s]) + 7) / 8) * 8;   // 64-byte aligned fronts
     P.voff[s + 1] = P.voff[s] + ((P.m[s] + 7) / 8) * 8;
     P.toff[s + 1] = P.toff[s] + (long long)((P.w[s] + 63) / 64) * 4096;
     for (int k = 0; k < P.w[s]; k++) {
@@ -309,8 +306,7 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
   }
   if (psz > 1) {   // offsets over the needed fronts only
     for (int s = 0; s < ns; s++) {
-      const long long mm = need[s] ? P.m[s] : 0;
-      P.foff[s + 1] = P.foff[s] + ((mm * mm + 7) / 8) * 8;
+      P.foff[s + 1] = P.foff[s] + (need[s] ? ((front_elems(P.m[s], P.w[s]) + 7) / 8) * 8 : 0);
       P.voff[s + 1] = P.voff[s] + (need[s] ? ((P.m[s] + 7) / 8) * 8 : 0);
       P.toff[s + 1] = P.toff[s] + (need[s] ? (long long)((P.w[s] + 63) / 64) * 4096 : 0);
     }
@@ -762,23 +758,31 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       // a tile's elements are computed alike in either kernel, so this is
       // bitwise the 128-tile update)
       ps.syrk_tile = cnt128 >= 4096 && !dist ? kBigTile : kTile;
+      // A tile's columns stay inside one 64-column block of the packed front
+      // (pgo_chol.h front_packed): a range starting inside a block (the update
+      // matrix starts at w) opens with a narrow tile up to the block's end,
+      // clipped; a tile's elements are computed alike whatever its shape
       for (const int4& u : plain)
-        for (int c0 = u.y; c0 < u.z; c0 += ps.syrk_tile) {
+        for (int c0 = u.y; c0 < u.z;) {
+          const int T = ps.syrk_tile;
+          const int ce = (c0 & 63) ? std::min(u.z, (c0 + 63) & ~63) : std::min(u.z, c0 + T);
+          const bool narrow = ce - c0 < T && ce < u.z;   // (a range's last tile is clipped by the range end)
           if (!dist) {
-            for (int r0 = c0; r0 < P.m[u.x]; r0 += ps.syrk_tile) S.syrk_tasks.push_back(make_int4(u.x, r0, c0, u.w));
-            continue;
-          }
-          const int ce = std::min(c0 + kTile, u.z);
-          for (int a = c0; a < ce;) {   // runs of one column owner: (a, b)
-            int b = a + 1;
-            while (b < ce && cowner(u.x, b) == cowner(u.x, a)) b++;
-            if (mine(u.x, a)) {
-              const int clip = (a == c0 && b == ce) ? 0 : b - a;
-              for (int r0 = c0; r0 < P.m[u.x]; r0 += kTile)
-                S.syrk_tasks.push_back(make_int4(u.x, r0 | (clip << kClipShift), a, u.w));
+            const int clip = narrow ? ce - c0 : 0;
+            for (int r0 = c0; r0 < P.m[u.x]; r0 += T) S.syrk_tasks.push_back(make_int4(u.x, r0 | (clip << kClipShift), c0, u.w));
+          } else {
+            for (int a = c0; a < ce;) {   // runs of one column owner: (a, b)
+              int b = a + 1;
+              while (b < ce && cowner(u.x, b) == cowner(u.x, a)) b++;
+              if (mine(u.x, a)) {
+                const int clip = (a == c0 && b == ce && !narrow) ? 0 : b - a;
+                for (int r0 = c0; r0 < P.m[u.x]; r0 += kTile)
+                  S.syrk_tasks.push_back(make_int4(u.x, r0 | (clip << kClipShift), a, u.w));
+              }
+              a = b;
             }
-            a = b;
           }
+          c0 = ce;
         }
       {   // XCD-aware order of this step's Schur-update tiles
         std::vector<int4> mine(S.syrk_tasks.begin() + ps.syrk_off, S.syrk_tasks.end());
@@ -1261,17 +1265,22 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
         if (ti >= tj) fn(ti * (ti + 1) / 2 + tj);
   };
   std::vector<long long> fitems(ns + 1, 0);   // items of front s (counted, then its offset)
-  std::vector<std::vector<int>> fcnt(ns);   // per front: item count per tile key, then start
+  // per front: item count per tile key, then its start (flat: front s at kbase[s], nt (nt + 1) / 2 + 1 keys)
+  std::vector<long long> kbase(ns + 1, 0);
+  for (int s = 0; s < ns; s++) {
+    const long long nt = (P.m[s] + 63) / 64;
+    kbase[s + 1] = kbase[s] + nt * (nt + 1) / 2 + 1;
+  }
+  std::vector<int> fcnt(kbase[ns], 0);
   parallel_chunks(ns, nth, [&](int, int s0, int s1) {
     for (int s = s0; s < s1; s++) {
-      const long long nt = (P.m[s] + 63) / 64;
-      std::vector<int>& c = fcnt[s];
-      c.assign(nt * (nt + 1) / 2 + 1, 0);
+      int* c = fcnt.data() + kbase[s];
+      const long long nk = kbase[s + 1] - kbase[s];
       for (int g = fg[s]; g < fg[s + 1]; g++) for_item(3 * P.asm_li[g], 3 * P.asm_lj[g], [&](int key) { c[key + 1]++; });
       for (int j = P.sfirst[s]; j < P.sfirst[s + 1]; j++)
         for_item(3 * P.dg_loc[j], 3 * P.dg_loc[j], [&](int key) { c[key + 1]++; });
-      for (size_t k = 0; k + 1 < c.size(); k++) c[k + 1] += c[k];
-      fitems[s + 1] = c.back();
+      for (long long k = 0; k + 1 < nk; k++) c[k + 1] += c[k];
+      fitems[s + 1] = c[nk - 1];
     }
   });
   lap("tile count");
@@ -1289,9 +1298,10 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
     P.at_items.resize(pos);
   }
   parallel_chunks(ns, nth, [&](int, int s0, int s1) {
+    std::vector<int> fill;   // (reused across the chunk's fronts)
     for (int s = s0; s < s1; s++) {
       if (fbase[s] < 0) continue;
-      std::vector<int> fill(fcnt[s].begin(), fcnt[s].end() - 1);
+      fill.assign(fcnt.begin() + kbase[s], fcnt.begin() + kbase[s + 1] - 1);
       int* out = P.at_items.data() + fbase[s];
       for (int g = fg[s]; g < fg[s + 1]; g++)
         for_item(3 * P.asm_li[g], 3 * P.asm_lj[g], [&](int key) { out[fill[key]++] = g; });
@@ -1305,7 +1315,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
     for (int q = q0; q < q1; q++) {
       const int4 t = P.ea_tasks[q];
       const int ti = t.y >> 16, tj = t.y & 0xffff, key = ti * (ti + 1) / 2 + tj;
-      const std::vector<int>& c = fcnt[t.x];
+      const int* c = fcnt.data() + kbase[t.x];
       P.at_iptr[q] = make_int2((int)(fbase[t.x] + c[key]), c[key + 1] - c[key]);
     }
   });

@@ -44,7 +44,7 @@ int main(int argc, char** argv) {
   double tri = 0, ftot = 0;
   for (int s = 0; s < P.ns; s++) {
     tri += 0.5 * P.m[s] * (P.m[s] + 1.0);
-    ftot += (double)P.m[s] * P.m[s];
+    ftot += (double)pgo::front_elems(P.m[s], P.w[s]);
   }
   printf("fronts %d, F %.0fM doubles, lower triangles %.0fM, flops %.3g, syrk_flops %.3g\n", P.ns, ftot / 1e6, tri / 1e6,
          P.flops, P.syrk_flops);
