@@ -660,17 +660,13 @@ int upload_structure(pgo_graph* g) {
 // structure is updated in step (block-CSR rows merged, side-1 lists, row
 // blocks); only the new factors, the per-row arrays and the slot arrays are
 // uploaded.  Returns 1 when the full upload must run instead.
-// fn(begin, end) over contiguous chunks of [0, n) on up to 16 host threads
+// fn(begin, end) over contiguous chunks of [0, n) on the planner's host threads
 // (the live re-solve's per-registration host work; chunk results independent)
 template <class F>
 void host_parallel(int n, F&& fn) {
   static const int hw = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
   const int nth = std::max(1, std::min(hw, n / 16384));
-  std::vector<std::thread> pool;
-  for (int t = 1; t < nth; t++)
-    pool.emplace_back([&fn, t, n, nth] { fn((int)((long long)n * t / nth), (int)((long long)n * (t + 1) / nth)); });
-  fn(0, (int)((long long)n / nth));
-  for (auto& th : pool) th.join();
+  pgo::plan_parallel(nth, [&](int t) { fn((int)((long long)n * t / nth), (int)((long long)n * (t + 1) / nth)); });
 }
 
 // PGO_PLAN_TIMING: phase times of the plan / append paths on stderr

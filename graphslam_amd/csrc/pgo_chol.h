@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 namespace pgo {
@@ -236,6 +237,10 @@ std::vector<int> partition_subtrees(const CholPlan& P, int size, std::vector<dou
 // top (subtrees + the rank's top columns + the top work every rank repeats,
 // returned in *replicated)
 std::vector<double> distributed_rank_flops(const CholPlan& P, int size, double* replicated = nullptr);
+
+// host: fn(t) for t in [0, ntask) on the planner's thread pool (the caller
+// takes part; PGO_PLAN_THREADS threads, default the hardware's, at most 16)
+void plan_parallel(int ntask, const std::function<void(int)>& fn);
 
 // host: symbolic analysis from the block-CSR pattern (old pose indices)
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);

@@ -2,6 +2,9 @@
 // Runs once per graph structure (GTSAM recomputes COLAMD every solve).
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <chrono>
 #include <thread>
 #include <tuple>
@@ -234,8 +237,8 @@ static void size_fronts(CholPlan& P) {
 }
 
 // Threads of the host planning (PGO_PLAN_THREADS, default: the hardware's, at
-// most 16); parallel_chunks runs fn(t, begin, end) on nth contiguous chunks of
-// [0, n), chunk t on thread t (the results are independent of nth).
+// most 16), kept in a pool for the process (a plan refresh runs ~10 parallel
+// passes: spawning threads per pass cost more than some passes).
 static int plan_threads() {
   static const int t = [] {
     if (const char* e = getenv("PGO_PLAN_THREADS")) return std::max(1, atoi(e));
@@ -244,14 +247,81 @@ static int plan_threads() {
   return t;
 }
 
+namespace {
+class PlanPool {
+ public:
+  explicit PlanPool(int workers) {
+    for (int i = 0; i < workers; i++) th_.emplace_back([this] { work(); });
+  }
+  ~PlanPool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // fn(t) for t in [0, ntask), on the workers and the caller; one job at a time
+  void run(int ntask, const std::function<void(int)>& fn) {
+    if (ntask <= 1 || th_.empty()) {
+      for (int t = 0; t < ntask; t++) fn(t);
+      return;
+    }
+    std::lock_guard<std::mutex> job(job_m_);
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      fn_ = &fn;
+      ntask_ = ntask;
+      next_ = 0;
+      busy_ = (int)th_.size();
+      gen_++;
+    }
+    cv_.notify_all();
+    for (int t; (t = next_.fetch_add(1)) < ntask;) fn(t);
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return busy_ == 0; });
+  }
+
+ private:
+  void work() {
+    unsigned long seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(m_);
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      const std::function<void(int)>* fn = fn_;
+      const int n = ntask_;
+      lk.unlock();
+      for (int t; (t = next_.fetch_add(1)) < n;) (*fn)(t);
+      lk.lock();
+      if (--busy_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_, job_m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int ntask_ = 0, busy_ = 0;
+  std::atomic<int> next_{0};
+  unsigned long gen_ = 0;
+  bool stop_ = false;
+};
+
+PlanPool& plan_pool() {
+  static PlanPool pool(plan_threads() - 1);
+  return pool;
+}
+}  // namespace
+
+void plan_parallel(int ntask, const std::function<void(int)>& fn) { plan_pool().run(ntask, fn); }
+
+// fn(t, begin, end) on nth contiguous chunks of [0, n), chunk t by index (the
+// results are independent of which thread runs it and of nth)
 template <class F>
 static void parallel_chunks(int n, int nth, F&& fn) {
   nth = std::max(1, std::min(nth, n));
-  std::vector<std::thread> pool;
-  for (int t = 1; t < nth; t++)
-    pool.emplace_back([&fn, t, n, nth] { fn(t, (int)((long long)n * t / nth), (int)((long long)n * (t + 1) / nth)); });
-  fn(0, 0, (int)((long long)n / nth));
-  for (auto& th : pool) th.join();
+  plan_parallel(nth, [&](int t) { fn(t, (int)((long long)n * t / nth), (int)((long long)n * (t + 1) / nth)); });
 }
 
 // One level's share of the schedule lists (chol_schedule builds the levels
@@ -820,17 +890,7 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
     }
   };
   std::vector<LevelLists> out(nl);
-  {
-    const int nth = std::min(plan_threads(), nl);
-    std::atomic<int> next(0);
-    auto work = [&] {
-      for (int L; (L = next.fetch_add(1)) < nl;) schedule_level(L, out[L]);
-    };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < nth; t++) pool.emplace_back(work);
-    work();
-    for (auto& t : pool) t.join();
-  }
+  plan_parallel(nl, [&](int L) { schedule_level(L, out[L]); });
   P.small_list.clear();
   P.level_fronts.clear();
   P.syrk_tasks.clear();
