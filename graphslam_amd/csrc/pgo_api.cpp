@@ -108,6 +108,7 @@ struct pgo_graph {
   hipGraphExec_t sol_exec[9] = {};          // captured triangular solves, per lane count
   int graph_eager[9] = {};                  // eager factorisations of this plan before the capture
   int eager_first = 0;                      // ... how many (8 after an incremental plan update, else 0)
+  std::thread reaper;                       // destroys dropped graphs (drop_graphs)
   double* h_lam = nullptr;                  // pinned lambda staging
   Staging stage;                            // pinned upload staging (append_structure)
   // ---- multi-GPU speculative lambda search (pgo_comm_*) ----
@@ -124,6 +125,7 @@ struct pgo_graph {
   size_t cap_n = 0, cap_ne = 0;             // device capacities in vertices / factors
   bool dev_complete = false;                // the device holds hs exactly (appendable)
   int last_upload = 0;                      // 1 full upload, 2 append (diagnostics)
+  bool saved_valid = false;                 // d.pose_saved holds a snapshot of this structure (pgo_save_values)
   // ---- closest-keyframe search scratch ----
   double* s_d = nullptr;                    // [kMaxBlocks + 1] partial / final distances
   int* s_i = nullptr;                       // [kMaxBlocks + 1] partial / final indices
@@ -204,14 +206,29 @@ int information(const double* q, double* om6) {
 }
 
 // every captured factor / solve graph (they hold the plan's workspace pointers)
+void join_reaper(pgo_graph* g) {
+  if (g->reaper.joinable()) g->reaper.join();
+}
+
+// The captured graphs are destroyed on a helper thread (hipGraphExecDestroy of
+// a factorisation's ~1e3 nodes takes ~10 ms each; the callers have drained the
+// stream, so nothing still runs them)
 void drop_graphs(pgo_graph* g) {
+  std::vector<hipGraphExec_t> dead;
   for (int l = 0; l < 9; l++) {
     for (hipGraphExec_t* e : {&g->fac_exec[l], &g->sol_exec[l]}) {
-      if (*e) (void)hipGraphExecDestroy(*e);
+      if (*e) dead.push_back(*e);
       *e = nullptr;
     }
     g->graph_eager[l] = 0;
   }
+  if (dead.empty()) return;
+  join_reaper(g);
+  const int dev = g->device;
+  g->reaper = std::thread([dead, dev] {
+    (void)hipSetDevice(dev);
+    for (hipGraphExec_t e : dead) (void)hipGraphExecDestroy(e);
+  });
 }
 
 void free_lanes(pgo_graph* g) {
@@ -840,8 +857,8 @@ int append_structure(pgo_graph* g) {
   if (g->xb && (size_t)n > g->xb_n) free_lanes(g);   // (else the lanes hold the grown graph too)
   drop_graphs(g);
   phase("drop graphs");
-  if (d.pose_saved) (void)hipFree(d.pose_saved);   // (a snapshot of the old structure's values)
-  d.pose_saved = nullptr;
+  g->saved_valid = false;   // (the snapshot holds the old structure's values; its buffer, sized
+                            // for the capacity, is kept: a hipFree would wait for the device)
   phase("free");
   std::vector<double4> hz(nij.size());
   std::vector<double2> hom(3 * nij.size());
@@ -1532,6 +1549,7 @@ void pgo_destroy(pgo_graph* g) {
     (void)hipSetDevice(g->device);
     (void)hipStreamSynchronize(g->d.stream);
     free_device(g);
+    join_reaper(g);
     for (auto& e : g->ev)
       if (e) (void)hipEventDestroy(e);
     if (g->h_scal) (void)hipHostFree(g->h_scal);
@@ -1554,6 +1572,7 @@ void pgo_destroy(pgo_graph* g) {
       if (e) (void)hipEventDestroy(e);
     if (g->d.stream) (void)hipStreamDestroy(g->d.stream);
   }
+  join_reaper(g);
   delete g;
 }
 
@@ -1675,13 +1694,15 @@ int pgo_save_values(pgo_graph* g) {
   if (d.n)
     HIP_TRY(g, hipMemcpyAsync(d.pose_saved, d.pose, d.n * sizeof(double4), hipMemcpyDeviceToDevice, d.stream));
   HIP_TRY(g, hipStreamSynchronize(d.stream));
+  g->saved_valid = true;
   return PGO_OK;
 }
 
 int pgo_restore_values(pgo_graph* g) {
   if (!g) return PGO_E_ARG;
   DevGraph& d = g->d;
-  if (!g->dev_structure || !d.pose_saved) return fail(g, PGO_E_ARG, "no saved values (graph changed or never saved)");
+  if (!g->dev_structure || !d.pose_saved || !g->saved_valid)
+    return fail(g, PGO_E_ARG, "no saved values (graph changed or never saved)");
   if (d.n)
     HIP_TRY(g, hipMemcpyAsync(d.pose, d.pose_saved, d.n * sizeof(double4), hipMemcpyDeviceToDevice, d.stream));
   g->dev_values = true;
