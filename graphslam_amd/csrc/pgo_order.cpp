@@ -17,6 +17,7 @@
 // of at most kLeaf (64) vertices are ordered by exact minimum degree.  Deterministic
 // (fixed-seed generator), so the plan and the results are reproducible.
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <numeric>
 #include <queue>
@@ -33,6 +34,8 @@ constexpr int kLeaf = 64;         // subgraphs this small: minimum degree
 constexpr int kCoarsest = 96;     // stop coarsening below this many vertices
 constexpr int kInitTries = 8;     // region-growing seeds on the coarsest graph
 constexpr double kMaxSide = 0.55; // heaviest side <= this fraction of the weight
+constexpr int kTopTries = 24;      // bisection tries at the root of the dissection (half that below it)
+constexpr int kTriedDepth = 8;    // ... down to this depth
 
 struct Graph {
   int n = 0;
@@ -437,9 +440,37 @@ std::vector<int> nd(const Graph& g, const std::vector<int>& gid, uint64_t seed, 
     leaf_order(g, gid, order);
     return order;
   }
-  Rng rng(seed);
-  const std::vector<char> part = bisect(g, rng);
-  const std::vector<char> sep = cut_cover(g, part);
+  // near the root of the dissection the separators become the largest fronts
+  // and the longest panel chains: there the bisection is tried from several
+  // seeds (concurrently) and the smallest separator kept (ties: the first try)
+  static const int top = getenv("PGO_ND_TRIES") ? std::max(1, atoi(getenv("PGO_ND_TRIES"))) : kTopTries;   // (A/B knob)
+  const int tries = depth == 0 ? top : depth < kTriedDepth ? std::max(1, top / 2) : 1;
+  std::vector<std::vector<char>> parts(tries), seps(tries);
+  auto attempt = [&](int t) {
+    Rng rng(seed + 0x632be59bd9b4e019ULL * (uint64_t)t);
+    parts[t] = bisect(g, rng);
+    seps[t] = cut_cover(g, parts[t]);
+  };
+  if (tries > 1 && g.n > 4096) {
+    std::vector<std::thread> th;
+    for (int t = 1; t < tries; t++) th.emplace_back(attempt, t);
+    attempt(0);
+    for (auto& x : th) x.join();
+  } else {
+    for (int t = 0; t < tries; t++) attempt(t);
+  }
+  int pick = 0;
+  long long best = -1;
+  for (int t = 0; t < tries; t++) {
+    long long ns = 0;
+    for (char v : seps[t]) ns += v;
+    if (best < 0 || ns < best) {
+      best = ns;
+      pick = t;
+    }
+  }
+  const std::vector<char>& part = parts[pick];
+  const std::vector<char>& sep = seps[pick];
   std::vector<int> side[2], sv;
   for (int v = 0; v < g.n; v++) (sep[v] ? sv : side[(int)part[v]]).push_back(v);
   if (side[0].empty() || side[1].empty()) {   // no useful split
@@ -488,7 +519,9 @@ std::vector<int> order_nd(int n, const std::vector<int>& xadj, const std::vector
   g.tw = n;
   std::vector<int> gid(n);
   std::iota(gid.begin(), gid.end(), 0);
-  return nd(g, gid, 0x2545f4914f6cdd1dULL, 0);
+  uint64_t seed = 0x2545f4914f6cdd1dULL;
+  if (const char* e = getenv("PGO_ND_SEED")) seed += strtoull(e, nullptr, 10);
+  return nd(g, gid, seed, 0);
 }
 
 }  // namespace pgo

@@ -1,0 +1,33 @@
+"""Per-level split of one factorisation replay (diagnostics): segments a
+rocprofv3 kernel trace of scripts/replay_trace.py at the levels' tile-assembly
+launches (one per level, on the library stream) and prints, per level, its
+span, the launches of each family in it and the k_step cadence (span / steps).
+
+    python scripts/level_summary.py OUT/.../t_kernel_trace.csv
+"""
+import csv
+import sys
+from collections import Counter
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+ev = []
+for r in rows:
+    name = r.get("Kernel_Name") or r.get("KernelName") or r.get("Name")
+    fam = name.split("(")[0].split("<")[0].replace("void ", "").replace("pgo::", "").strip()
+    ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), fam))
+ev.sort()
+starts = [i for i, x in enumerate(ev) if x[2] == "k_perm_in"]
+ev = ev[starts[-1] if starts else 0:]
+end = max(e for _, e, _ in ev)
+cuts = [i for i, x in enumerate(ev) if x[2] == "k_assemble_tile"] + [len(ev)]
+print(f"replay span {(end - ev[0][0]) / 1e6:.3f} ms")
+for li in range(len(cuts) - 1):
+    seg = ev[cuts[li]:cuts[li + 1]]
+    t0 = seg[0][0]
+    t1 = ev[cuts[li + 1]][0] if cuts[li + 1] < len(ev) else end
+    n = Counter(f for _, _, f in seg)
+    steps = n.get("k_step", 0)
+    busy = sum(e - s for s, e, f in seg if f == "k_step")
+    cad = f" step cadence {(t1 - t0) / 1e3 / steps:6.1f} us (busy {busy / 1e3 / steps:5.1f})" if steps else ""
+    fams = " ".join(f"{k}:{v}" for k, v in sorted(n.items()))
+    print(f"level {li:2d} span {(t1 - t0) / 1e3:8.1f} us{cad}  {fams}")
