@@ -34,7 +34,7 @@ constexpr int kLeaf = 64;         // subgraphs this small: minimum degree
 constexpr int kCoarsest = 96;     // stop coarsening below this many vertices
 constexpr int kInitTries = 8;     // region-growing seeds on the coarsest graph
 constexpr double kMaxSide = 0.55; // heaviest side <= this fraction of the weight
-constexpr int kTopTries = 24;      // bisection tries at the root of the dissection (half that below it)
+constexpr int kTopTries = 24;     // bisection tries at the root of the dissection (half that below it)
 constexpr int kTriedDepth = 8;    // ... down to this depth
 
 struct Graph {
