@@ -743,7 +743,9 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       // wins, scripts/ubench_syrk.hip), else 64x64; few 64-tiles ride in k_step,
       // many go to a concurrent launch (k_step's LDS request, sized for the
       // diagonal workgroups, halves their occupancy)
-      const int tile0 = ntiles(kBigTile) >= 4096 ? kBigTile : kTile;
+      // (PGO_BIGTILE_MIN: the 128-tile threshold, a tuning knob)
+      static const long long big_min = getenv("PGO_BIGTILE_MIN") ? atoll(getenv("PGO_BIGTILE_MIN")) : 4096;
+      const int tile0 = ntiles(kBigTile) >= big_min ? kBigTile : kTile;
       const bool apart = apart_chain || !(tile0 == kTile && ntiles(kTile) <= kInlineTiles);
       std::vector<int4> plain;   // (front, first column, end column, k0): rows from the column down
       std::vector<int4> prep;    // prep tiles (front, r0, c0, k0), whole 64x64 tiles
@@ -827,7 +829,7 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       // (distributed top: 64-wide tiles, split where the column owner changes;
       // a tile's elements are computed alike in either kernel, so this is
       // bitwise the 128-tile update)
-      ps.syrk_tile = cnt128 >= 4096 && !dist ? kBigTile : kTile;
+      ps.syrk_tile = cnt128 >= big_min && !dist ? kBigTile : kTile;
       // A tile's columns stay inside one 64-column block of the packed front
       // (pgo_chol.h front_packed): a range starting inside a block (the update
       // matrix starts at w) opens with a narrow tile up to the block's end,
