@@ -1886,12 +1886,18 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   std::vector<double> lam_k(T), fac_k(T), outs(4 * T);
   int last_outcome = PGO_STOP_CONVERGED;     // how the last linearisation's tries ended
   std::vector<char> valid(T);
-  // Lanes sized to the tries expected: a linearisation is taken to need as
-  // many tries as the previous one walked, so the round that should reach the
+  // Lanes sized to the tries expected, so the round that should reach the
   // accepted try runs only the lanes up to it (a one-lane round is cheaper than
-  // a batched one); more lanes again if that try fails.  The tries and their
-  // order are unchanged (PGO_LANES_ADAPT=0: every round runs all lanes).
-  static const bool adapt_lanes = !(getenv("PGO_LANES_ADAPT") && atoi(getenv("PGO_LANES_ADAPT")) == 0);
+  // a batched one); all lanes again if that try fails.  The expectation follows
+  // GTSAM's lambda dynamics: after a first-try acceptance lambda keeps falling
+  // and the next linearisation is expected to accept at once (1 try); after an
+  // acceptance that needed k >= 2 tries the next linearisation starts one decade
+  // below the accepted lambda, which just failed, so 2 tries are expected
+  // rather than k (C3: 13 rounds either way, two of them 2-lane instead of
+  // 3-lane).  The tries and their order are unchanged (PGO_LANES_ADAPT=0: every
+  // round runs all lanes; PGO_LANES_ADAPT=2: the previous linearisation's count).
+  static const int adapt_mode = getenv("PGO_LANES_ADAPT") ? atoi(getenv("PGO_LANES_ADAPT")) : 1;
+  static const bool adapt_lanes = adapt_mode != 0;
   int prev_walked = 0;   // tries the previous linearisation walked (0: none yet)
   if (!(err <= p.error_tol) && iters < p.max_iterations && d.n > 0) {
     double new_err = err;
@@ -1935,7 +1941,8 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
           // a profiled factorisation (lane 0, eager, timed launches) runs alone
           const bool prof_next = p.profile_every > 0 && (g->factorizations % p.profile_every) == 0;
           int Lr = prof_next ? 1 : L;
-          if (adapt_lanes && !exchange && prev_walked > walked) Lr = std::min(Lr, prev_walked - walked);
+          const int expect = adapt_mode == 2 ? prev_walked : std::min(prev_walked, 2);
+          if (adapt_lanes && !exchange && expect > walked) Lr = std::min(Lr, expect - walked);
           std::vector<double> mine(4 * L, 0.0);
           for (int l = 0; l < L; l++) mine[4 * l] = -1.0;  // -1: no try (past the bound / lane idle)
           int nb = 0;   // this rank's valid tries (a prefix of its lanes)
