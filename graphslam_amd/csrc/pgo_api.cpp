@@ -1894,8 +1894,11 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   // acceptance that needed k >= 2 tries the next linearisation starts one decade
   // below the accepted lambda, which just failed, so 2 tries are expected
   // rather than k (C3: 13 rounds either way, two of them 2-lane instead of
-  // 3-lane).  The tries and their order are unchanged (PGO_LANES_ADAPT=0: every
-  // round runs all lanes; PGO_LANES_ADAPT=2: the previous linearisation's count).
+  // 3-lane).  The first linearisation of an optimize() expects 1: GTSAM starts
+  // at lambda = 1e-5, a nearly undamped step, which from odometry-initialised
+  // or warm-started values is accepted.  The tries and their order are
+  // unchanged (PGO_LANES_ADAPT=0: every round runs all lanes; 2: the previous
+  // linearisation's count, all lanes first; 3: this rule, all lanes first).
   static const int adapt_mode = getenv("PGO_LANES_ADAPT") ? atoi(getenv("PGO_LANES_ADAPT")) : 1;
   static const bool adapt_lanes = adapt_mode != 0;
   int prev_walked = 0;   // tries the previous linearisation walked (0: none yet)
@@ -1941,7 +1944,8 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
           // a profiled factorisation (lane 0, eager, timed launches) runs alone
           const bool prof_next = p.profile_every > 0 && (g->factorizations % p.profile_every) == 0;
           int Lr = prof_next ? 1 : L;
-          const int expect = adapt_mode == 2 ? prev_walked : std::min(prev_walked, 2);
+          const int expect = adapt_mode == 2 ? prev_walked : prev_walked == 0 ? (adapt_mode == 3 ? 0 : 1)
+                                                                              : std::min(prev_walked, 2);
           if (adapt_lanes && !exchange && expect > walked) Lr = std::min(Lr, expect - walked);
           std::vector<double> mine(4 * L, 0.0);
           for (int l = 0; l < L; l++) mine[4 * l] = -1.0;  // -1: no try (past the bound / lane idle)
