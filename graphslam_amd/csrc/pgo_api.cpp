@@ -108,7 +108,6 @@ struct pgo_graph {
   hipGraphExec_t sol_exec[9] = {};          // captured triangular solves, per lane count
   int graph_eager[9] = {};                  // eager factorisations of this plan before the capture
   int eager_first = 0;                      // ... how many (8 after an incremental plan update, else 0)
-  std::thread reaper;                       // destroys dropped graphs (drop_graphs)
   double* h_lam = nullptr;                  // pinned lambda staging
   Staging stage;                            // pinned upload staging (append_structure)
   // ---- multi-GPU speculative lambda search (pgo_comm_*) ----
@@ -205,30 +204,19 @@ int information(const double* q, double* om6) {
   return PGO_OK;
 }
 
-// every captured factor / solve graph (they hold the plan's workspace pointers)
-void join_reaper(pgo_graph* g) {
-  if (g->reaper.joinable()) g->reaper.join();
-}
 
-// The captured graphs are destroyed on a helper thread (hipGraphExecDestroy of
-// a factorisation's ~1e3 nodes takes ~10 ms each; the callers have drained the
-// stream, so nothing still runs them)
+// The captured graphs are destroyed here, before the caller frees or
+// re-allocates the memory they point to (destroying them on a helper thread
+// while the workspaces were freed and re-allocated raced: an intermittent host
+// segfault on rapid lane-count changes).  The callers have drained the stream.
 void drop_graphs(pgo_graph* g) {
-  std::vector<hipGraphExec_t> dead;
   for (int l = 0; l < 9; l++) {
     for (hipGraphExec_t* e : {&g->fac_exec[l], &g->sol_exec[l]}) {
-      if (*e) dead.push_back(*e);
+      if (*e) (void)hipGraphExecDestroy(*e);
       *e = nullptr;
     }
     g->graph_eager[l] = 0;
   }
-  if (dead.empty()) return;
-  join_reaper(g);
-  const int dev = g->device;
-  g->reaper = std::thread([dead, dev] {
-    (void)hipSetDevice(dev);
-    for (hipGraphExec_t e : dead) (void)hipGraphExecDestroy(e);
-  });
 }
 
 void free_lanes(pgo_graph* g) {
@@ -1549,7 +1537,6 @@ void pgo_destroy(pgo_graph* g) {
     (void)hipSetDevice(g->device);
     (void)hipStreamSynchronize(g->d.stream);
     free_device(g);
-    join_reaper(g);
     for (auto& e : g->ev)
       if (e) (void)hipEventDestroy(e);
     if (g->h_scal) (void)hipHostFree(g->h_scal);
@@ -1572,7 +1559,6 @@ void pgo_destroy(pgo_graph* g) {
       if (e) (void)hipEventDestroy(e);
     if (g->d.stream) (void)hipStreamDestroy(g->d.stream);
   }
-  join_reaper(g);
   delete g;
 }
 

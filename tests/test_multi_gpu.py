@@ -210,14 +210,15 @@ def _same(st, x, st1, x1):
 ])
 def test_lanes_match_sequential(case, lanes, kw):
     """Concurrent lambda tries on one GPU (pgo_params.lambda_lanes) reproduce
-    the sequential search bit for bit, in fewer rounds."""
+    the sequential search bit for bit, in no more rounds.  (Rounds are sized to
+    the tries expected -- one after a first-try acceptance, two after a
+    multi-try one -- so a trajectory whose multi-try linearisations all follow
+    first-try ones takes as many rounds as the sequential search, each of them
+    a one-lane round.)"""
     st1, x1 = _single(case, kw, lanes=1)
     st, x = _single(case, kw, lanes=lanes)
     _same(st, x, st1, x1)
-    if st1["inner_iterations"] > st1["linearizations"]:
-        # profiled factorisations run alone: their rounds need not shrink
-        assert st["lambda_rounds"] <= st1["lambda_rounds"] if kw.get("profile_every") else \
-            st["lambda_rounds"] < st1["lambda_rounds"]
+    assert st["lambda_rounds"] <= st1["lambda_rounds"]
     assert st["solves"] >= st1["solves"]
 
 
@@ -298,8 +299,8 @@ def test_partitioned_factorisation_matches_one_rank(case, world, lanes, kw):
         assert st["linearizations"] == st1["linearizations"]
         assert st["final_error"] == st1["final_error"]
         np.testing.assert_array_equal(x, x1)
-        if lanes > 1 and st1["inner_iterations"] > st1["linearizations"]:
-            assert st["lambda_rounds"] < st1["lambda_rounds"]
+        if lanes > 1:   # (rounds sized to the tries expected: no more than one lane's)
+            assert st["lambda_rounds"] <= st1["lambda_rounds"]
 
 
 @pytest.mark.gpu
