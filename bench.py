@@ -505,7 +505,12 @@ def main():
     elif args.multi == "auto":
         args.multi = "spec"
     if args.lanes is None:
-        args.lanes = 2 if world > 1 and args.multi == "spec" else 3
+        # speculative search: one lane per rank -- a round's time is its
+        # slowest rank's replay, and a one-lane replay costs half a three-lane
+        # one, while P ranks already cover P tries (C3 trajectory: 1-4 tries per
+        # linearisation but one of 10: 8 ranks x 1 lane = 9 one-lane rounds
+        # against 8 two-lane ones)
+        args.lanes = 1 if world > 1 and args.multi == "spec" else 3
     spec = world > 1 and args.multi in ("spec", "partition")   # one job over all ranks
     part = world > 1 and args.multi == "partition"
     hc = None
