@@ -383,13 +383,17 @@ __device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double*
       const double yk = vk * r;
       const double la = l > k ? pa[k] * r : (l == k ? d * r : pa[k]);
       const double lbv = pb[k] * r;
+      // columns j >= w (the class width W past the front's w) are updated
+      // with a zero multiplier -- fma(x, 0, y) == y exactly, so they stay zero
+      // -- instead of a branch per column: the per-(k, j) branches compiled to
+      // ~500 out-of-line blocks, a 16k-line kernel thrashing the instruction
+      // cache on the pivot chain
+      const double rj = r;
 #pragma unroll
       for (int j = k + 1; j < W; j++) {
-        if (j < w) {                          // uniform
-          const double lj = readlane_f64(pa[k], j) * r;
-          pa[j] = fma(l >= j ? -la : 0.0, lj, pa[j]);
-          pb[j] = fma(-lbv, lj, pb[j]);
-        }
+        const double lj = readlane_f64(pa[k], j) * (j < w ? rj : 0.0);
+        pa[j] = fma(l >= j ? -la : 0.0, lj, pa[j]);
+        pb[j] = fma(-lbv, lj, pb[j]);
       }
       pa[k] = la;
       pb[k] = lbv;
