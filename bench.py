@@ -36,6 +36,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_MFMA_PEAK_TFS = 78.6  # MI355X datasheet: FP64 matrix (and vector) 78.6 TFLOP/s dense
+# kernel families bound by HBM bytes even where they report flops (factor_roofline)
+HBM_FAMILIES = ("k_bwd_part",)
 # measured on the box (scripts/ubench_syrk.hip): a bare v_mfma_f64_16x16x4_f64 loop,
 # 8 independent chains per wave, 8-32 waves per CU, sustains 45-49 TFLOP/s
 FP64_MFMA_LOOP_TFS = 49.0
@@ -200,7 +202,9 @@ def factor_roofline(kprof, totals, factor_flops):
     for k, v in kprof.items():
         if v["launches"] == 0:
             continue
-        mfma = v["flops"] > 0
+        # the backward solve's partial products stream L once (2 flops per 8 B):
+        # priced on HBM bytes like the other families without MFMA work
+        mfma = v["flops"] > 0 and k not in HBM_FAMILIES
         per = (v["flops"] if mfma else v["bytes"]) / v["launches"]
         avg = v["ms"] / v["launches"]
         ach = per / (avg * 1e-3) / (1e12 if mfma else 1e9) if avg > 0 else None

@@ -75,7 +75,14 @@ struct pgo_graph {
   DevGraph d;
   std::vector<int> edge_slot0;              // side-0 slot of every between factor (user order)
   std::vector<int> h_slot_edge;             // host copy of slot_edge (owner bits)
-  bool gauge_free = false;                  // some connected component has no prior
+  // the device slot_edge carries the Cholesky plan's owner bits (bind_plan);
+  // after an in-place append its rows from the first changed one carry the
+  // pre-plan codes instead (side 0 owns), so the two halves disagree until the
+  // next bind_plan -- the PCG path (k_model_decrease counts `se & 2` slots)
+  // re-uploads the whole array first (slot_codes_mixed)
+  bool slot_codes_plan = false;
+  bool slot_codes_mixed = false;
+  bool gauge_free = false;                 // some connected component has no prior
   double* h_scal = nullptr;                 // pinned
   int* h_ctrl = nullptr;                    // pinned
   hipEvent_t ev[6] = {};
@@ -642,6 +649,7 @@ int upload_structure(pgo_graph* g) {
   RC_TRY(h2d(g, d.pom, hpom.data(), 3 * (size_t)np));
   RC_TRY(h2d(g, d.row_ptr, row_ptr.data(), n + 1));
   RC_TRY(h2d(g, d.slot_edge, slot_edge.data(), ns));
+  g->slot_codes_plan = g->slot_codes_mixed = false;   // pre-plan codes throughout
   RC_TRY(h2d(g, d.slot_col, slot_col.data(), ns));
   HIP_TRY(g, hipMemsetAsync(d.part, 0, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices, d.stream));
   HIP_TRY(g, hipStreamSynchronize(d.stream));
@@ -903,6 +911,7 @@ int append_structure(pgo_graph* g) {
   HIP_TRY(g, hipStreamSynchronize(d.stream));
   g->dev_structure = true;
   g->last_upload = 2;
+  if (g->slot_codes_plan && H.row_ptr[r0] > 0) g->slot_codes_mixed = true;   // rows < r0 keep the plan's bits
   if (g->chol_ready) g->plan_stale = true;   // ensure_chol decides what to keep
   phase("upload");
   // the new vertices' values (the resident ones stay bit for bit, unless the
@@ -965,6 +974,17 @@ int exchange_group(void* ctx, int begin) {
 }
 
 int bind_plan(pgo_graph* g, bool full);
+
+// Before a PCG linearisation: an in-place append after a Cholesky plan left
+// the device owner bits half the plan's, half pre-plan; upload the host's
+// pre-plan codes whole so every factor has exactly one `se & 2` slot.
+int unmix_slot_codes(pgo_graph* g) {
+  if (!g->slot_codes_mixed) return PGO_OK;
+  RC_TRY(h2d(g, g->d.slot_edge, g->h_slot_edge.data(), g->h_slot_edge.size()));
+  HIP_TRY(g, hipStreamSynchronize(g->d.stream));
+  g->slot_codes_plan = g->slot_codes_mixed = false;
+  return PGO_OK;
+}
 
 int ensure_chol(pgo_graph* g) {
   const int psz = g->part_size > 1 ? g->comm.size : 1, prk = psz > 1 ? g->comm.rank : 0;
@@ -1116,6 +1136,8 @@ int bind_plan(pgo_graph* g, bool full) {
       RC_TRY(h2d(g, g->d.slot_edge, slot_edge.data(), slot_edge.size()));
       HIP_TRY(g, hipStreamSynchronize(g->d.stream));
     }
+    g->slot_codes_plan = true;
+    g->slot_codes_mixed = false;
     phase("slots");
   }
   return PGO_OK;
@@ -1796,6 +1818,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
     st.plan_update = g->plan_update;
     st.ms_plan = g->plan_ms;
   }
+  if (p.linear_solver == PGO_SOLVER_PCG) RC_TRY(unmix_slot_codes(g));
   d.write_all = p.linear_solver == PGO_SOLVER_PCG ? 1 : 0;
   // One lambda try (GTSAM tryLambda): solve (H + lam I) delta = -g, retract into
   // pose_cand, error there and the linear model decrease; one read-back.
@@ -2487,6 +2510,7 @@ int pgo_debug_solve(pgo_graph* g, double lambda, const pgo_params* params, doubl
   // the Cholesky assembly reads the owner blocks in factor order (k_linearize_own)
   g->part_size = 1;
   if (p.linear_solver != PGO_SOLVER_PCG && d.n > 0) RC_TRY(ensure_chol(g));
+  if (p.linear_solver == PGO_SOLVER_PCG) RC_TRY(unmix_slot_codes(g));
   d.write_all = p.linear_solver == PGO_SOLVER_PCG ? 1 : 0;
   HIP_TRY(g, pgo::launch_linearize(d));
   pgo_stats st;

@@ -105,6 +105,9 @@ struct CholLevel {
   int xtail = -1;                  // distributed top: the fronts' tail columns to every rank at the level's end
   double at_bytes = 0;             // algorithmic HBM bytes of the level's k_assemble_tile
   double bwd_part_flops = 0;       // ... flops of its k_bwd_part
+  // algorithmic HBM bytes of the level's k_vec_assemble, k_bwd_part,
+  // k_bwd_init and k_bwd_chain (k_bwd_step: the same reads, split by step)
+  double vec_bytes = 0, bwd_part_bytes = 0, bwd_init_bytes = 0, bwd_chain_bytes = 0;
 };
 
 enum { kOrderNd = 0, kOrderAmd = 1 };

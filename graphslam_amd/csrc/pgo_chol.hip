@@ -2403,7 +2403,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
     if (vec) {
       CH_TRY(hipEventRecord(P.evs[0], s));
       CH_TRY(hipStreamWaitEvent(P.side2, P.evs[0], 0));
-      launch(prof, kFamVecAssemble, [&] { return make_double2(0, 0); }, k_vec_assemble, dim3(lv.front_cnt, nb), B256,
+      launch(prof, kFamVecAssemble, [&] { return make_double2(0, lv.vec_bytes * nb); }, k_vec_assemble, dim3(lv.front_cnt, nb), B256,
              (size_t)lv.maxm * sizeof(double), P.side2, c, (const int*)(P.d_level_fronts + lv.front_off));
       CH_TRY(hipEventRecord(P.evs[1], P.side2));
     }
@@ -2586,15 +2586,15 @@ hipError_t chol_solve(const CholPlan& P, double* x, hipStream_t s, int nb, long 
     const CholLevel& lv = *it;
     if (prof) prof->cur_tag = (int)(&lv - P.levels.data()) << 16;
     if (lv.bwd_part.cnt)
-      launch(prof, kFamBwdPart, [&] { return make_double2(lv.bwd_part_flops * nb, 0); },
+      launch(prof, kFamBwdPart, [&] { return make_double2(lv.bwd_part_flops * nb, lv.bwd_part_bytes * nb); },
              k_bwd_part, dim3(lv.bwd_part.cnt, nb), B256, 0, s, c, (const int4*)(P.d_bwd_part + lv.bwd_part.off),
              P.d_partial);
-    launch(prof, kFamBwdInit, [&] { return make_double2(0, 0); }, k_bwd_init, dim3(lv.bwd[0].cnt, nb), B256, 0, s, c,
+    launch(prof, kFamBwdInit, [&] { return make_double2(0, lv.bwd_init_bytes * nb); }, k_bwd_init, dim3(lv.bwd[0].cnt, nb), B256, 0, s, c,
            (const int4*)(P.d_bwd + lv.bwd[0].off), (const int2*)(P.d_bwd_pref + lv.bwd[0].off),
            (const double*)P.d_partial);
     if (chain) {
       if (lv.bwdc.cnt)
-        launch(prof, kFamBwdStep, [&] { return make_double2(0, 0); }, k_bwd_chain, dim3(lv.bwdc.cnt, nb), B256, 0,
+        launch(prof, kFamBwdStep, [&] { return make_double2(0, lv.bwd_chain_bytes * nb); }, k_bwd_chain, dim3(lv.bwdc.cnt, nb), B256, 0,
                s, c, (const int4*)(P.d_bwdc + lv.bwdc.off));
     } else {
       for (size_t q = 1; q < lv.bwd.size(); q++) {

@@ -511,9 +511,23 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       sp.cnt = (int)S.bwd_part_tasks.size() - sp.off;
       for (int q = sp.off; q < sp.off + sp.cnt; q++) {
         const int4 t = S.bwd_part_tasks[q];
-        lv.bwd_part_flops += 2.0 * std::min(64, P.w[t.x] - t.y) * std::min(kBwdRows, P.m[t.x] - t.z);
+        const double ncol = std::min(64, P.w[t.x] - t.y), rows = std::min(kBwdRows, P.m[t.x] - t.z);
+        lv.bwd_part_flops += 2.0 * ncol * rows;
+        // L rows x columns, x gathered per row (+ its pose index per 3 rows), the 64 partial sums out
+        lv.bwd_part_bytes += 8.0 * ncol * rows + rows * (8.0 + 4.0 / 3.0) + 8.0 * 64;
       }
       st.cnt = (int)S.bwd_tasks.size() - st.off;
+      for (int q = st.off; q < st.off + st.cnt; q++) {   // init: partials + y in, X_jj' z for the last block, x out
+        const int4 t = S.bwd_tasks[q];
+        const double n2 = t.z - t.y, np = S.bwd_pref[q].y;
+        lv.bwd_init_bytes += 8.0 * n2 * (np + 2.0) + (t.w >= 0 ? 8.0 * n2 * (64.0 + 1.0) + 4.0 * n2 / 3.0 : 0.0);
+      }
+      // frontal vectors: own rows gathered from the permuted rhs, the children's
+      // update vectors with their row maps, the vector written
+      for (int s : bylevel[L]) {
+        lv.vec_bytes += 8.0 * P.m[s] + (8.0 + 4.0 / 3.0) * P.w[s];
+        for (int q = P.cptr[s]; q < P.cptr[s + 1]; q++) lv.vec_bytes += (8.0 + 4.0 / 3.0) * (P.m[P.children[q]] - P.w[P.children[q]]);
+      }
       lv.bwd_part = sp;
       lv.bwd.push_back(st);
     }
@@ -527,6 +541,9 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
           if (d >= nblk) continue;
           const int j = nblk - 1 - d;
           S.bwdc_tasks.push_back(make_int4(s, j * 64, j * 64 + 64, j));
+          // L[block b, block j] for every block b below j and its x_b, X_jj, z in, x out
+          const double n2 = std::min(64, w - 64 * j);
+          lv.bwd_chain_bytes += 8.0 * (w - 64.0 * (j + 1)) * (n2 + 1.0) + 8.0 * n2 * (64.0 + 3.0) + 4.0 * n2 / 3.0;
         }
       lv.bwdc.cnt = (int)S.bwdc_tasks.size() - lv.bwdc.off;
     }

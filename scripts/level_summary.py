@@ -31,3 +31,20 @@ for li in range(len(cuts) - 1):
     cad = f" step cadence {(t1 - t0) / 1e3 / steps:6.1f} us (busy {busy / 1e3 / steps:5.1f})" if steps else ""
     fams = " ".join(f"{k}:{v}" for k, v in sorted(n.items()))
     print(f"level {li:2d} span {(t1 - t0) / 1e3:8.1f} us{cad}  {fams}")
+
+# the top level's panel steps: k_step duration, the gap to the previous
+# launch that ended before it (launch latency or a join), and the plain-tile
+# launches (k_panel_syrk*) that were still running when it started
+seg = ev[cuts[-2]:]
+steps = [x for x in seg if x[2] == "k_step"]
+gaps, durs = [], []
+for i, (s, e, _) in enumerate(steps):
+    prev_end = max((e2 for s2, e2, f2 in seg if e2 <= s), default=s)
+    plain_busy = sum(1 for s2, e2, f2 in seg if f2.startswith("k_panel_syrk") and s2 < s < e2)
+    gaps.append((s - prev_end) / 1e3)
+    durs.append((e - s) / 1e3)
+    if i < 12 or i == len(steps) - 1:
+        print(f"  top step {i:3d}: k_step {durs[-1]:6.1f} us, gap {gaps[-1]:5.1f} us, plain running {plain_busy}")
+if steps:
+    print(f"top level: {len(steps)} steps, k_step mean {sum(durs) / len(durs):.1f} us, gap mean {sum(gaps) / len(gaps):.1f} us, "
+          f"cadence {(steps[-1][1] - steps[0][0]) / 1e3 / len(steps):.1f} us")

@@ -220,6 +220,36 @@ def test_lanes_match_sequential(case, lanes, kw):
     _same(st, x, st1, x1)
     assert st["lambda_rounds"] <= st1["lambda_rounds"]
     assert st["solves"] >= st1["solves"]
+    if st1["inner_iterations"] > st1["linearizations"]:
+        # a multi-try linearisation: the round after it is sized to two tries,
+        # so some round ran more than one lane (a regression to one-lane
+        # rounds throughout would keep solves == lambda_rounds)
+        assert st["solves"] > st["lambda_rounds"], (st["solves"], st["lambda_rounds"])
+
+
+def _single_worker(rank, world, port, q, case, kw, lanes, env):
+    """_single in a fresh process (PGO_LANES_ADAPT is read once per process)."""
+    try:
+        os.environ.update(env)
+        st, x = _single(case, kw, lanes)
+        q.put((rank, st, x, None))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, None, repr(e)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,lanes", [("C2p", 3), ("C3", 3)])
+def test_full_lane_rounds_save_rounds(case, lanes):
+    """With every round running all its lanes (PGO_LANES_ADAPT=0) consecutive
+    tries of a multi-try linearisation share a round: strictly fewer rounds
+    than the sequential search's tries, and the same trajectory bit for bit."""
+    st1, x1 = _single(case, {}, lanes=1)
+    assert st1["inner_iterations"] > st1["linearizations"]   # some linearisation walked several tries
+    (_, st, x, err), = _run(1, _single_worker, (case, {}, lanes, {"PGO_LANES_ADAPT": "0"}), timeout=600)
+    assert err is None, err
+    _same(st, x, st1, x1)
+    assert st["lambda_rounds"] < st1["lambda_rounds"], (st["lambda_rounds"], st1["lambda_rounds"])
+    assert st["solves"] > st["lambda_rounds"]
 
 
 @pytest.mark.gpu
@@ -301,6 +331,26 @@ def test_partitioned_factorisation_matches_one_rank(case, world, lanes, kw):
         np.testing.assert_array_equal(x, x1)
         if lanes > 1:   # (rounds sized to the tries expected: no more than one lane's)
             assert st["lambda_rounds"] <= st1["lambda_rounds"]
+            if st1["inner_iterations"] > st1["linearizations"]:
+                assert st["solves"] > st["lambda_rounds"]   # some round batched tries
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["partition", "spec"])
+def test_c5_two_ranks_match_one_rank(mode):
+    """BASELINE config C5 (1M poses / 5M edges) with two ranks sharing cuda:0
+    over the host transport, first linearisation (max_outer 1): the
+    partitioned factorisation (subtrees per rank, distributed top, 2.3 TFLOP
+    per factorisation) and the speculative lambda search each reproduce the
+    one-rank trajectory and values bit for bit."""
+    kw = {"max_outer": 1}
+    st1, x1 = _single("C5", kw)
+    mkw = dict(kw, multi_gpu=1, lambda_lanes=1) if mode == "partition" else dict(kw, lambda_lanes=1)
+    out = _run(2, _opt_worker, ("C5", mkw), timeout=1200)
+    for rank, st, x, err in out:
+        assert err is None, err
+        assert st["ranks"] == 2
+        _same(st, x, st1, x1)
 
 
 @pytest.mark.gpu
