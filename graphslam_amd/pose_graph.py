@@ -357,6 +357,15 @@ class PoseGraph:
                                                      lv.ctypes.data_as(ip), ns)))
         return w, m, lv
 
+    def debug_parents(self):
+        """Host-only: the parent supernode of every supernode (-1: a root)."""
+        ns = self._L.pgo_debug_fronts(self._h, None, None, None, 0)
+        if ns < 0:
+            self._check(ns)
+        par = np.zeros(ns, np.int32)
+        self._check(min(0, self._L.pgo_debug_parents(self._h, par.ctypes.data_as(C.POINTER(C.c_int)), ns)))
+        return par
+
     def debug_solve(self, lam, params=None, **kw):
         p = params if params is not None else default_params(**kw)
         d = np.zeros((self.num_vertices, 3))

@@ -3,12 +3,13 @@
 For each config and rank count P: the per-rank flops of one factorisation with
 the distributed top (subtrees + the rank's top columns + the top work every
 rank repeats), the flop bound on the speed-up (total / busiest rank), the same
-bound with the top replicated on every rank (round-2 scheme), and the
-distributed top's exchanges per factorisation (broadcast rounds, bytes every
-rank receives).  Also a latency/bandwidth estimate with stated constants
-(bench.py's --multi auto uses the same model).  Writes profiles/<out>.json.
+bound with the top replicated on every rank, and the distributed top's
+exchanges per factorisation (broadcast rounds, bytes every rank receives).
+Also graphslam_amd/multi_model.py's level-by-level time estimates of both tops
+and of the speculative search (bench.py's --multi auto uses the same model).
+Writes profiles/<out>.json.
 
-    python scripts/partition_bounds.py [--configs C3 C5] [--out r03_partition_bounds]
+    python scripts/partition_bounds.py [--configs C3 C5] [--out r04_partition_bounds]
 """
 from __future__ import annotations
 
@@ -20,14 +21,14 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from graphslam_amd.multi_model import partition_estimate  # noqa: E402
+from graphslam_amd.multi_model import estimate  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", nargs="+", default=["C3", "C5"])
     ap.add_argument("--ranks", nargs="+", type=int, default=[2, 4, 8])
-    ap.add_argument("--out", default="r03_partition_bounds")
+    ap.add_argument("--out", default="r04_partition_bounds")
     args = ap.parse_args()
     from graphslam_amd import datasets
     from graphslam_amd.pose_graph import PoseGraph
@@ -39,7 +40,7 @@ def main():
         for P in args.ranks:
             b = pg.debug_partition_bound(P)
             b["rank_flops"] = [float(v) for v in b["rank_flops"]]
-            b.update(partition_estimate(b))
+            b.update(estimate(pg, P, c, bound=b))
             res[c][str(P)] = b
             print(c, P, json.dumps({k: v for k, v in b.items() if k != "rank_flops"}))
         pg.close()
