@@ -499,13 +499,16 @@ def main():
         if rank == 0:
             b = pg.debug_partition_bound(world)
             b["rank_flops"] = [float(v) for v in b["rank_flops"]]
-            b.update(multi_model.partition_estimate(b))
-            obj = [(multi_model.choose_mode(b), b)]
+            b.update(multi_model.estimate(pg, world, args.config, bound=b))
+            obj = [(multi_model.choose_mode(b), multi_model.dist_top(b), b)]
         r.dist.broadcast_object_list(obj, src=0)
-        args.multi, b = obj[0]
+        args.multi, dist_top, b = obj[0]
+        if args.multi == "partition" and not dist_top:
+            os.environ["PGO_DIST_TOP"] = "0"   # the replicated top (read when the plan is built)
         bounds[str(world)] = b
-        mode_why = (f"auto: partition est {b['est_speedup']:.2f}x vs speculative bound {multi_model.SPEC_GAIN}x "
-                    f"({b['model']})")
+        mode_why = (f"auto: partition est {b['est_speedup_replicated_top']:.2f}x (replicated top) / "
+                    f"{b['est_speedup_distributed_top']:.2f}x (distributed top) vs speculative "
+                    f"{b['est_speedup_spec']:.2f}x ({b['model']}; level times: {b['level_times']})")
     elif args.multi == "auto":
         args.multi = "spec"
     if args.lanes is None:
