@@ -113,6 +113,11 @@ struct pgo_graph {
   long long factorizations = 0;
   hipGraphExec_t fac_exec[9] = {};          // captured factorisation, per lane count (1: d.x path)
   hipGraphExec_t sol_exec[9] = {};          // captured triangular solves, per lane count
+  // graphs of a plan an incremental update replaced: destroyed only at the next
+  // capture or with the device state (a destruction costs ~10 ms, on the first
+  // live registration after a full optimize otherwise; on this thread only --
+  // destroying them on a helper thread raced with the workspace re-allocation)
+  std::vector<hipGraphExec_t> stale_exec;
   int graph_eager[9] = {};                  // eager factorisations of this plan before the capture
   int eager_first = 0;                      // ... how many (8 after an incremental plan update, else 0)
   double* h_lam = nullptr;                  // pinned lambda staging
@@ -216,14 +221,24 @@ int information(const double* q, double* om6) {
 // re-allocates the memory they point to (destroying them on a helper thread
 // while the workspaces were freed and re-allocated raced: an intermittent host
 // segfault on rapid lane-count changes).  The callers have drained the stream.
-void drop_graphs(pgo_graph* g) {
+void destroy_stale_graphs(pgo_graph* g) {
+  for (hipGraphExec_t e : g->stale_exec) (void)hipGraphExecDestroy(e);
+  g->stale_exec.clear();
+}
+
+// defer: keep the execs for destroy_stale_graphs (they are never launched again)
+void drop_graphs(pgo_graph* g, bool defer = false) {
   for (int l = 0; l < 9; l++) {
     for (hipGraphExec_t* e : {&g->fac_exec[l], &g->sol_exec[l]}) {
-      if (*e) (void)hipGraphExecDestroy(*e);
+      if (*e) {
+        if (defer) g->stale_exec.push_back(*e);
+        else (void)hipGraphExecDestroy(*e);
+      }
       *e = nullptr;
     }
     g->graph_eager[l] = 0;
   }
+  if (!defer) destroy_stale_graphs(g);
 }
 
 void free_lanes(pgo_graph* g) {
@@ -851,7 +866,7 @@ int append_structure(pgo_graph* g) {
   HIP_TRY(g, hipStreamSynchronize(d.stream));
   phase("sync");
   if (g->xb && (size_t)n > g->xb_n) free_lanes(g);   // (else the lanes hold the grown graph too)
-  drop_graphs(g);
+  drop_graphs(g, true);
   phase("drop graphs");
   g->saved_valid = false;   // (the snapshot holds the old structure's values; its buffer, sized
                             // for the capacity, is kept: a hipFree would wait for the device)
@@ -1033,7 +1048,7 @@ int ensure_chol(pgo_graph* g) {
     if (!getenv("PGO_NO_PLAN_APPEND") && pgo::chol_append(P, n, g->h_row_ptr, g->h_slot_col, pairs, kMaxTail, 1.05)) {
       phase("chol_append");
       if (P.schedule_error) return fail(g, PGO_E_HIP, "internal: inconsistent panel schedule");
-      drop_graphs(g);
+      drop_graphs(g, true);
       RC_TRY(bind_plan(g, true));
       g->plan_stale = false;
       g->plan_edges = g->ek1.size();
@@ -1211,6 +1226,7 @@ int graph_factor_solve(pgo_graph* g, int nb, double* x, long long xstride, bool 
   auto capture = [&](hipGraphExec_t* exec, bool factor) -> int {
     if (*exec) return PGO_OK;
     PhaseTimer phase("graph_capture");
+    destroy_stale_graphs(g);
     hipGraph_t graph = nullptr;
     HIP_TRY(g, hipStreamBeginCapture(d.stream, hipStreamCaptureModeThreadLocal));
     const hipError_t e1 = factor ? pgo::chol_factor(g->chol, d.D, d.V, d.g, -1.0, d.stream, nullptr, nb)
@@ -2357,7 +2373,7 @@ int pgo_debug_plan(pgo_graph* g, double* out, int cap) {
     lf += (long long)lv.ea_off.size() + 1 + lv.small.size();
     for (const auto& ps : lv.panels)
       lf += (ps.potrf_cnt > 0) + (ps.sdiag_cnt + ps.col_cnt + ps.prep_cnt + (ps.syrk_inline ? ps.syrk_cnt : 0) > 0) +
-            (ps.syrk_cnt > 0 && !ps.syrk_inline);
+            (ps.syrk_cnt > 0 && !ps.syrk_inline) + (ps.far_cnt > 0);
     ls += (lv.bwd_part.cnt > 0) + (long long)lv.bwd.size();
     for (const auto& ps : lv.panels) {
       trsm += ps.fcol_cnt + ps.col_cnt;

@@ -72,6 +72,14 @@ struct PanelStep {                 // one 64-column panel kb of every big front 
   double step_flops;               // ... of k_step (updates, factor, inverse, trsm, inline tiles)
   int plain_lag = 0;               // apart plain tiles: joined before step +1 or (look-ahead skip) +2
   int xfirst = -1, xstep = -1;     // distributed top: exchanges after k_panel_first / k_step (index in xchg)
+  // deferred far updates: the last far_cnt of the syrk tiles (an apart step at a
+  // kKB block end: the columns past the next block) go to their own launch on a
+  // fourth stream, joined before step far_join of the level (-1: its end)
+  int far_cnt = 0, far_join = -1;
+  double far_flops = 0;            // ... their share of plain_flops
+  // k_step's flops by role (sdiag; col + prep updates; col solves): a step with
+  // many diagonal tiles runs them as three launches instead (chol_factor)
+  double diag_flops = 0, colupd_flops = 0, trsm_flops = 0;
 };
 
 // Distributed top (part_size > 1): one exchange point -- the panels (or tails)
@@ -210,6 +218,9 @@ struct CholPlan {
   hipStream_t side = nullptr;      // look-ahead diagonal tiles
   hipStream_t side2 = nullptr;     // small fronts beside the blocked path
   hipStream_t side3 = nullptr;     // the second wavefront class of small fronts, beside side2
+  hipStream_t side4 = nullptr;     // deferred far Schur updates (PanelStep::far_cnt)
+  hipStream_t side5 = nullptr;     // a split step's column-block updates beside its diagonal tiles
+  hipEvent_t fev[4] = {nullptr, nullptr, nullptr, nullptr};   // their join events (ring)
   hipEvent_t evs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int4 *d_bwd = nullptr, *d_bwd_part = nullptr, *d_bwdc = nullptr;
   int2* d_bwd_pref = nullptr;
@@ -290,7 +301,7 @@ struct ExchangeHook {
 enum KernelFamily {
   kFamAssemble = 0, kFamUnused1, kFamPerm, kFamUnused3, kFamVecAssemble, kFamFrontWave, kFamFrontSmall,
   kFamPanelFirst, kFamStep, kFamPanelSyrk, kFamPanelSyrk128,
-  kFamBwdPart, kFamBwdInit, kFamBwdStep, kFamCount
+  kFamBwdPart, kFamBwdInit, kFamBwdStep, kFamStepDiag, kFamColTrsm, kFamCount
 };
 const char* kernel_family_name(int f);
 struct LaunchProfile {

@@ -124,14 +124,155 @@ __device__ long long g_diag_clk[32];
 
 // ------------------------------------------------------------ assembly
 // One 64x64 lower tile (ti, tj) of a front per workgroup, written whole (so no
-// front is ever zeroed): in LDS, the tile's H entries -- off-diagonal blocks
-// H_{i,j} (i > j) summed over their slots (V, structure of arrays), diagonal
-// blocks H_jj + lambda I (lower part) -- then the front's children's
-// update-matrix elements in child order (fixed summation order, bitwise
-// reproducible, no atomics), then the lower part of the tile to the front.
-// Lane r <-> child row a0 + r (column-major: a column's loads are coalesced),
-// the 4 waves take every 4th column; loads first.
-__global__ __launch_bounds__(256) void k_assemble_tile(CholDev c, const int4* __restrict__ tasks,
+// front is ever zeroed), gathered element by element: thread (i = tid & 63,
+// columns j = tid / 64 + 4u) owns 16 elements of the tile and forms each as
+// its H entry -- an off-diagonal block H_{a,b} summed over its slots (V,
+// structure of arrays) or a diagonal block H_jj + lambda I, lower part -- plus
+// the front's children's update-matrix elements that land on it, in child
+// order (fixed summation order, bitwise reproducible, no atomics, no LDS
+// read-modify-write).  What an element needs is looked up in LDS maps built
+// once per tile: the H item of each 3x3 pose block the tile spans, and per
+// child rectangle the child row of each tile row and the child column (and
+// its column offset) of each tile column.  Two barriers per tile (per 16 child
+// rectangles), and every element's loads are in flight together.
+constexpr int kAsmPairs = 16;
+constexpr int kAsmNone = (int)0x80000000;
+__global__ __launch_bounds__(256, 4) void k_assemble_tile(CholDev c, const int4* __restrict__ tasks,
+                                                       const int2* __restrict__ iptr, const int* __restrict__ items,
+                                                       const int4* __restrict__ pairs, const double* __restrict__ V,
+                                                       long long S, const double* __restrict__ D,
+                                                       const double* __restrict__ lam_p) {
+  lane_offset(c);
+  __shared__ int bcode[22 * 22];   // H item of pose block (bi, bj): asm target >= 0, ~pose (diagonal), or none
+  __shared__ int bsrc[22 * 22];    // ... its first slot's factor (off-diagonal) or its pose's old index (diagonal)
+  __shared__ int bcnt[22 * 22];    // ... its slot count
+  __shared__ int rmap[kAsmPairs][64];            // child row landing on tile row i (-1: none)
+  __shared__ int cmap[kAsmPairs][64];            // child column landing on tile column j (-1: none)
+  __shared__ long long coff[kAsmPairs][64];      // ... its offset in the child front (row wc)
+  __shared__ long long pbase[kAsmPairs];         // the child front's base
+  const int4 t = tasks[blockIdx.x];
+  const int p = t.x, mp = c.m[p];
+  const int R0 = 64 * (t.y >> 16), C0 = 64 * (t.y & 0xffff);
+  const int P0 = R0 / 3, Q0 = C0 / 3;   // first pose block row / column the tile touches
+  const int tid = threadIdx.x, i = tid & 63, cg = tid >> 6;
+  const double lam = lam_p[blockIdx.y];
+  const int2 it = iptr[blockIdx.x];
+  for (int q = tid; q < 22 * 22; q += 256) bcode[q] = kAsmNone;
+  for (int q = tid; q < kAsmPairs * 64; q += 256) {
+    rmap[q >> 6][q & 63] = -1;
+    cmap[q >> 6][q & 63] = -1;
+  }
+  __syncthreads();
+  for (int q = tid; q < it.y; q += 256) {   // H items -> their pose blocks
+    const int code = items[it.x + q];
+    int li, lj, src, cnt;
+    if (code >= 0) {
+      li = c.asm_li[code];
+      lj = c.asm_lj[code];
+      const int k0 = c.asm_ptr[code];
+      cnt = c.asm_ptr[code + 1] - k0;
+      src = c.asm_src[k0];
+    } else {
+      li = lj = c.dg_loc[~code];
+      src = c.perm[~code];
+      cnt = 0;
+    }
+    const int bq = (li - P0) * 22 + (lj - Q0);
+    bcode[bq] = code;
+    bsrc[bq] = src;
+    bcnt[bq] = cnt;
+  }
+  // this thread's 16 elements: (R0 + i, C0 + cg + 4u), in two groups of 8
+  const int row = R0 + i;
+  const int a3 = row - 3 * (row / 3), bi = row / 3 - P0;
+  const bool pkp = front_packed(mp, c.w[p]);
+  double* __restrict__ Fp = fcol(c.F + c.foff[p], mp, pkp, C0);   // the tile's columns: one column block
+  const int ldp = fld(mp, pkp, C0);
+  for (int pass = 0; pass * kAsmPairs < t.w || pass == 0; pass++) {
+    const int k0 = pass * kAsmPairs, np = min(kAsmPairs, t.w - k0);
+    if (pass > 0) {   // the previous pass's maps are read: reset them
+      __syncthreads();
+      for (int q = tid; q < kAsmPairs * 64; q += 256) {
+        rmap[q >> 6][q & 63] = -1;
+        cmap[q >> 6][q & 63] = -1;
+      }
+      __syncthreads();
+    }
+    for (int q = tid; q < np * 128; q += 256) {   // child rectangles -> row / column maps
+      const int kk = q >> 7, h = q & 127;
+      const int4 pr = pairs[t.z + k0 + kk];
+      const int ch = pr.x, nr = pr.w & 0xff, nc = pr.w >> 8;
+      const int* __restrict__ rel = c.ea_rel + c.ea_ptr[ch];
+      if (h < 64) {
+        if (h < nr) {
+          const int a = pr.y + h;
+          rmap[kk][3 * rel[a / 3] + a % 3 - R0] = a;
+        }
+        if (h == 0) pbase[kk] = c.foff[ch];
+      } else if (h - 64 < nc) {
+        const int b = pr.z + h - 64, mc = c.m[ch], wc = c.w[ch];
+        const int pc = 3 * rel[b / 3] + b % 3 - C0;
+        cmap[kk][pc] = b;
+        coff[kk][pc] = fcol_off(mc, front_packed(mc, wc), wc + b) + wc;
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int g = 0; g < 2; g++) {
+      double val[8];
+      if (pass == 0) {   // the H entries
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int col = C0 + cg + 4 * (8 * g + u);
+          const int bq = bi * 22 + (col / 3 - Q0), b3 = col - 3 * (col / 3);
+          const int code = bcode[bq];
+          double v = 0.0;
+          if (code >= 0) {
+            const int e = 3 * a3 + b3;
+            v += V[bsrc[bq] + e * S];   // (0 + first slot: the sum's order and zero signs as before)
+            for (int k = 1; k < bcnt[bq]; k++) v += V[c.asm_src[c.asm_ptr[code] + k] + e * S];   // (repeated factors)
+          } else if (code != kAsmNone && a3 >= b3) {
+            const double* d = D + 6 * (size_t)bsrc[bq];
+            const int e = a3 == 0 ? 0 : (a3 == 1 ? (b3 == 0 ? 1 : 3) : (b3 == 0 ? 2 : (b3 == 1 ? 4 : 5)));
+            v = d[e] + (a3 == b3 ? lam : 0.0);
+          }
+          val[u] = v;
+        }
+      } else {           // a later pass (more than 16 child rectangles): this thread's partial sums so far
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int j = cg + 4 * (8 * g + u), col = C0 + j;
+          val[u] = (row < mp && col < mp && row >= col) ? Fp[row + (size_t)j * ldp] : 0.0;
+        }
+      }
+      for (int kk = 0; kk < np; kk++) {   // the children's elements, in child order
+        const int a = rmap[kk][i];
+        if (a < 0) continue;
+        const double* __restrict__ Fch = c.F + pbase[kk] + a;
+        double add[8];
+        bool in[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int b = cmap[kk][cg + 4 * (8 * g + u)];
+          in[u] = b >= 0 && b <= a;
+          add[u] = in[u] ? Fch[coff[kk][cg + 4 * (8 * g + u)]] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+          if (in[u]) val[u] += add[u];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int j = cg + 4 * (8 * g + u), col = C0 + j;
+        if (row < mp && col < mp && row >= col) Fp[row + (size_t)j * ldp] = val[u];
+      }
+    }
+  }
+}
+
+// The previous form of the same assembly (scatter into an LDS tile, two barriers
+// per child rectangle), bitwise the same tile: PGO_ASM_PUSH=1 selects it (A/B)
+__global__ __launch_bounds__(256) void k_assemble_tile_push(CholDev c, const int4* __restrict__ tasks,
                                                        const int2* __restrict__ iptr, const int* __restrict__ items,
                                                        const int4* __restrict__ pairs, const double* __restrict__ V,
                                                        long long S, const double* __restrict__ D,
@@ -286,6 +427,34 @@ __device__ __forceinline__ void copy_in(double* __restrict__ dst, const double* 
   }
 }
 
+// 8x8 lower triangle packed row by row
+#define P8(i, j) ((i) * ((i) + 1) / 2 + (j))
+
+// Cholesky factor of an 8x8 SPD block held whole, the same values, in every
+// lane: the pivot chain (rsqrt, scale, rank-1 update of the next diagonal) runs
+// in registers with no cross-lane traffic.  a: lower, packed; iv[j] = 1 / L_jj.
+__device__ __forceinline__ bool chol8_lane(double (&a)[36], double (&iv)[8]) {
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    double d = a[P8(j, j)];
+    if (!(d > 0.0) || !isfinite(d)) {
+      bad = true;
+      d = 1.0;
+    }
+    const double inv = rsqrt_nr(d);
+    iv[j] = inv;
+    a[P8(j, j)] = d * inv;
+#pragma unroll
+    for (int i = j + 1; i < 8; i++) a[P8(i, j)] *= inv;
+#pragma unroll
+    for (int i = j + 1; i < 8; i++)
+#pragma unroll
+      for (int k = j + 1; k <= i; k++) a[P8(i, k)] = fma(-a[P8(i, j)], a[P8(k, j)], a[P8(i, k)]);
+  }
+  return bad;
+}
+
 // ------------------------------------------------------------ small fronts (LDS)
 // m <= 128: the whole front in LDS; right-looking, two threads per row (the
 // row's columns split even/odd) so LDS accesses of a wave are consecutive rows.
@@ -368,38 +537,133 @@ __device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double*
   double va = ra ? fv[l] : 0.0, vb = rb ? fv[lb] : 0.0;
   bool bad = false;
   DIAG_CLK(24);
-  // pivot k: column k of the panel is lane j's pa[k] (rows j < W <= 64), read
-  // with v_readlane (no LDS round trip on the pivot chain)
-#pragma unroll
-  for (int k = 0; k < W; k++) {
-    if (k < w) {                              // uniform
-      double d = readlane_f64(pa[k], k);
-      const double vk = readlane_f64(va, k);
-      if (!(d > 0.0) || !isfinite(d)) {
-        bad = true;
-        d = 1.0;
+  if constexpr (W == 8) {
+    // (the narrowest class, most leaves: one pivot at a time, its 8 pivots
+    // cost little next to the blocked form's registers)
+    // pivot k: column k of the panel is lane j's pa[k] (rows j < W <= 64), read
+    // with v_readlane (no LDS round trip on the pivot chain)
+  #pragma unroll
+    for (int k = 0; k < W; k++) {
+      if (k < w) {                              // uniform
+        double d = readlane_f64(pa[k], k);
+        const double vk = readlane_f64(va, k);
+        if (!(d > 0.0) || !isfinite(d)) {
+          bad = true;
+          d = 1.0;
+        }
+        const double r = rsqrt_nr(d);
+        const double yk = vk * r;
+        const double la = l > k ? pa[k] * r : (l == k ? d * r : pa[k]);
+        const double lbv = pb[k] * r;
+        // columns j >= w (the class width W past the front's w) are updated
+        // with a zero multiplier -- fma(x, 0, y) == y exactly, so they stay zero
+        // -- instead of a branch per column: the per-(k, j) branches compiled to
+        // ~500 out-of-line blocks, a 16k-line kernel thrashing the instruction
+        // cache on the pivot chain
+        const double rj = r;
+  #pragma unroll
+        for (int j = k + 1; j < W; j++) {
+          const double lj = readlane_f64(pa[k], j) * (j < w ? rj : 0.0);
+          pa[j] = fma(l >= j ? -la : 0.0, lj, pa[j]);
+          pb[j] = fma(-lbv, lj, pb[j]);
+        }
+        pa[k] = la;
+        pb[k] = lbv;
+        va = l == k ? yk : (l > k ? fma(-la, yk, va) : va);
+        vb = fma(-lbv, yk, vb);
+        if (l == 0) invs[k] = r;
       }
-      const double r = rsqrt_nr(d);
-      const double yk = vk * r;
-      const double la = l > k ? pa[k] * r : (l == k ? d * r : pa[k]);
-      const double lbv = pb[k] * r;
-      // columns j >= w (the class width W past the front's w) are updated
-      // with a zero multiplier -- fma(x, 0, y) == y exactly, so they stay zero
-      // -- instead of a branch per column: the per-(k, j) branches compiled to
-      // ~500 out-of-line blocks, a 16k-line kernel thrashing the instruction
-      // cache on the pivot chain
-      const double rj = r;
-#pragma unroll
-      for (int j = k + 1; j < W; j++) {
-        const double lj = readlane_f64(pa[k], j) * (j < w ? rj : 0.0);
-        pa[j] = fma(l >= j ? -la : 0.0, lj, pa[j]);
-        pb[j] = fma(-lbv, lj, pb[j]);
+    }
+  } else {
+    // pivots in blocks of 8 columns kb .. kb + 7 (right-looking): the block's
+    // diagonal 8x8 (rows kb .. kb + 7, lanes kb ..) and their v go through LDS
+    // once, every lane factors it in registers (chol8_lane: no cross-lane
+    // traffic on the pivot chain) and forms y; each lane then solves its own
+    // rows' L(row, kb ..) against it; the panel columns right of the block get
+    // the block's rank-8 update with the block's L rows read back from LDS as
+    // broadcasts.  Every element sees the same fma's in the same order as the
+    // one-pivot-at-a-time sweep (fma(-L(row, k), L(col, k), a) per pivot k in
+    // increasing k; L(row, k) = a * 1/L(k, k); y likewise): bitwise its result.
+    double* db = cb;                // 8 x 9: the diagonal block's rows and their v
+    double* lrb = PR;               // (W - 8) x 8: L rows of the columns right of the block
+    // (no data-dependent loop exits: pivots past w are identity pivots on zero
+    // columns -- fma(-0, x, a) == a, the zero columns stay zero -- so every loop
+    // unrolls with static register indices; only whole 8-blocks past w are skipped)
+  #pragma unroll
+    for (int kb = 0; kb < W; kb += 8) {
+      if (kb < w) {                 // uniform
+        const int nb8 = min(8, w - kb);
+        if (l >= kb && l < kb + nb8) {
+  #pragma unroll
+          for (int q = 0; q < 8; q++) db[(l - kb) * 9 + q] = pa[kb + q];
+          db[(l - kb) * 9 + 8] = va;
+        }
+        __builtin_amdgcn_wave_barrier();
+        double a[36], iv[8], y[8];
+  #pragma unroll
+        for (int i = 0; i < 8; i++) {
+  #pragma unroll
+          for (int j = 0; j <= i; j++) a[P8(i, j)] = i < nb8 ? db[i * 9 + j] : (i == j ? 1.0 : 0.0);
+          y[i] = i < nb8 ? db[i * 9 + 8] : 0.0;
+        }
+        __builtin_amdgcn_wave_barrier();   // (db is rewritten by the next block)
+        bad = chol8_lane(a, iv) || bad;    // (padded pivots: 1, so L = I there)
+  #pragma unroll
+        for (int q = 0; q < 8; q++) {
+          y[q] *= iv[q];
+  #pragma unroll
+          for (int i = q + 1; i < 8; i++) y[i] = fma(-a[P8(i, q)], y[q], y[i]);
+        }
+        if (l == 0)
+  #pragma unroll
+          for (int q = 0; q < 8; q++) invs[kb + q] = iv[q];   // (past w: never read)
+        const bool own = l >= kb && l < kb + nb8, below = l >= kb + nb8;
+        if (own) {                       // the block's own rows: L and y (static register indices)
+  #pragma unroll
+          for (int i = 0; i < 8; i++)
+            if (i == l - kb) {
+  #pragma unroll
+              for (int q = 0; q <= i; q++) pa[kb + q] = a[P8(i, q)];
+              va = y[i];
+            }
+        }
+  #pragma unroll
+        for (int q = 0; q < 8; q++) {    // rows below: L(row, kb + q) against the block, then v
+  #pragma unroll
+          for (int t = 0; t < q; t++) {
+            if (below) pa[kb + q] = fma(-pa[kb + t], a[P8(q, t)], pa[kb + q]);
+            pb[kb + q] = fma(-pb[kb + t], a[P8(q, t)], pb[kb + q]);   // (rows l + 64: always below)
+          }
+          if (below) pa[kb + q] *= iv[q];
+          pb[kb + q] *= iv[q];
+        }
+  #pragma unroll
+        for (int q = 0; q < 8; q++) {
+          if (below) va = fma(-pa[kb + q], y[q], va);
+          vb = fma(-pb[kb + q], y[q], vb);
+        }
+        // columns right of the block: rank-8 update with L(col, kb ..) from the
+        // lanes holding those rows (rows past w: zero)
+        if (kb + 8 < W && kb + 8 < w) {  // uniform
+          if (l >= kb + 8 && l < W)
+  #pragma unroll
+            for (int q = 0; q < 8; q++) lrb[(l - kb - 8) * 8 + q] = l < w ? pa[kb + q] : 0.0;
+          __builtin_amdgcn_wave_barrier();
+  #pragma unroll
+          for (int j = kb + 8; j < W; j++) {
+            const double2* lj2 = reinterpret_cast<const double2*>(lrb + (j - kb - 8) * 8);
+  #pragma unroll
+            for (int q2 = 0; q2 < 4; q2++) {
+              const double2 t2 = lj2[q2];
+              pa[j] = fma(l >= j ? -pa[kb + 2 * q2] : 0.0, t2.x, pa[j]);
+              pb[j] = fma(-pb[kb + 2 * q2], t2.x, pb[j]);
+              pa[j] = fma(l >= j ? -pa[kb + 2 * q2 + 1] : 0.0, t2.y, pa[j]);
+              pb[j] = fma(-pb[kb + 2 * q2 + 1], t2.y, pb[j]);
+            }
+          }
+          __builtin_amdgcn_wave_barrier();   // (lrb is rewritten by the next block)
+        }
       }
-      pa[k] = la;
-      pb[k] = lbv;
-      va = l == k ? yk : (l > k ? fma(-la, yk, va) : va);
-      vb = fma(-lbv, yk, vb);
-      if (l == 0) invs[k] = r;
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -514,34 +778,6 @@ __device__ __forceinline__ void st16(double* C, d4 v, bool sub) {
     double* p = C + ((l >> 4) + 4 * r) + (l & 15) * 65;
     *p = sub ? *p - v[r] : v[r];
   }
-}
-
-// 8x8 lower triangle packed row by row
-#define P8(i, j) ((i) * ((i) + 1) / 2 + (j))
-
-// Cholesky factor of an 8x8 SPD block held whole, the same values, in every
-// lane: the pivot chain (rsqrt, scale, rank-1 update of the next diagonal) runs
-// in registers with no cross-lane traffic.  a: lower, packed; iv[j] = 1 / L_jj.
-__device__ __forceinline__ bool chol8_lane(double (&a)[36], double (&iv)[8]) {
-  bool bad = false;
-#pragma unroll
-  for (int j = 0; j < 8; j++) {
-    double d = a[P8(j, j)];
-    if (!(d > 0.0) || !isfinite(d)) {
-      bad = true;
-      d = 1.0;
-    }
-    const double inv = rsqrt_nr(d);
-    iv[j] = inv;
-    a[P8(j, j)] = d * inv;
-#pragma unroll
-    for (int i = j + 1; i < 8; i++) a[P8(i, j)] *= inv;
-#pragma unroll
-    for (int i = j + 1; i < 8; i++)
-#pragma unroll
-      for (int k = j + 1; k <= i; k++) a[P8(i, k)] = fma(-a[P8(i, j)], a[P8(k, j)], a[P8(i, k)]);
-  }
-  return bad;
 }
 
 // In place L -> L^-1 (8x8 lower, packed), columns right to left:
@@ -1352,14 +1588,18 @@ __global__ __launch_bounds__(256, 2) void k_first_diag(CholDev c, const int* __r
   first_diag_body(c, list[blockIdx.x], smem);
 }
 
+// (k_col_trsm: the same for the tiles below panel kn = task.z of a split step
+// (k_step's column workgroups, after k_step_diag published the inverse and
+// k_panel_syrk_lds updated the tiles): same arithmetic as trsm_rows)
 __global__ __launch_bounds__(256) void k_first_trsm(CholDev c, const int4* __restrict__ col) {
   lane_offset(c);
   __shared__ __attribute__((aligned(16))) double xs[4096];
   const int4 t = col[blockIdx.x];
-  const int s = t.x, m = c.m[s], nb = min(kNB, c.w[s]), r0 = t.y;
-  const double* Mf = c.Tinv + c.tfo + c.toff[s];
+  const int s = t.x, m = c.m[s], r0 = t.y, kn = max(t.z, 0), nb = min(kNB, c.w[s] - kn);
+  const int ld = m - kn;                                      // (blocked fronts are packed)
+  const double* Mf = c.Tinv + c.tfo + c.toff[s] + (kn / 64) * 4096;
   double* fv = c.fv + c.voff[s];
-  const double* A = c.F + c.foff[s] + r0;   // A(i, k) = A[i + k m]
+  const double* A = fcol(c.F + c.foff[s], m, true, kn) + r0;  // A(i, k) = A[i + k ld]
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   {
     double2 tq[8];
@@ -1376,7 +1616,7 @@ __global__ __launch_bounds__(256) void k_first_trsm(CholDev c, const int4* __res
 #pragma unroll
   for (int ct = 0; ct < 4; ct++) {
     const int col = 16 * ct + (l & 15);
-    yc[ct] = col < nb ? fv[col] : 0.0;
+    yc[ct] = col < nb ? fv[kn + col] : 0.0;
   }
 #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -1388,11 +1628,11 @@ __global__ __launch_bounds__(256) void k_first_trsm(CholDev c, const int4* __res
 #pragma unroll
   for (int ks = 0; ks < 16; ks++) {
     const int k = 4 * ks + kl;
-    a[ks] = (arow < m && k < nb) ? A[il + (size_t)k * m] : 0.0;
+    a[ks] = (arow < m && k < nb) ? A[il + (size_t)k * ld] : 0.0;
   }
   __syncthreads();
   if (rw >= m) return;
-  double* Fc = c.F + c.foff[s];
+  double* Fc = fcol(c.F + c.foff[s], m, true, kn);
   d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0}, acc3 = {0, 0, 0, 0};
 #pragma unroll
   for (int ks = 0; ks < 16; ks++) {
@@ -1413,7 +1653,7 @@ __global__ __launch_bounds__(256) void k_first_trsm(CholDev c, const int4* __res
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int row = rw + kl + 4 * r;
-      if (row < m) Fc[row + (size_t)col * m] = v[r];
+      if (row < m) Fc[row + (size_t)col * ld] = v[r];
     }
   }
 #pragma unroll
@@ -1464,6 +1704,15 @@ __global__ __launch_bounds__(256, 2) void k_step(CholDev c, const int4* __restri
     return;
   }
   syrk_lds_body(c, tiles[b - nsd - ncol - nprep], kb, smem);
+}
+
+// A split step's diagonal tiles (k_step's [0, nsd) role alone): updated,
+// factored, inverted, stored; the tiles below them are updated by a concurrent
+// k_panel_syrk_lds and solved by k_first_trsm after both (chol_factor)
+__global__ __launch_bounds__(256, 2) void k_step_diag(CholDev c, const int4* __restrict__ sdiag, int kb) {
+  lane_offset(c);
+  __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
+  syrk_diag_body(c, sdiag[blockIdx.x], kb, smem);
 }
 
 // Schur update of one 128x128 lower tile (same task format and semantics as
@@ -1760,13 +2009,13 @@ __device__ __forceinline__ void halve(double* acc, int lane) {
 // column made the compiler branch around each one and wait on it, NC serial
 // memory latencies.  NC = 16 serves the narrow fronts near the leaves with a
 // quarter of the reduction.
-template <int NC>
+template <int NC, int STRIDE = 256>
 __device__ __forceinline__ double bwd_part_wave(const CholDev& c, const double* L, const int* rows, int ld,
                                                 int ncol, int rbeg, int r1, int lane) {
   double acc[NC];
 #pragma unroll
   for (int q = 0; q < NC; q++) acc[q] = 0.0;
-  for (int r = rbeg; r < r1; r += 256) {
+  for (int r = rbeg; r < r1; r += STRIDE) {
     const double xr = c.xv[3 * rows[r / 3] + r % 3];
     const double* Lr = L + r;
     double lv[NC];
@@ -1809,12 +2058,23 @@ __global__ __launch_bounds__(256) void k_bwd_part(CholDev c, const int4* __restr
   const int ld = fld(m, pk, c0);
   const int* rows = c.rows + c.rptr[s];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (ncol > 16) {
+    // wave wv: columns [16 wv, 16 wv + 16) over all the task's rows (lane =
+    // row, stride 64): 16 accumulators per lane reduced over the wave -- a
+    // quarter of the shuffles of 64 per lane, and no cross-wave sum
+    const int nw = min(16, ncol - 16 * wv);
+    if (nw <= 0) {
+      if (lane < 16) part[(size_t)slot * 64 + 16 * wv + lane] = 0.0;
+      return;
+    }
+    const double v = bwd_part_wave<16, 64>(c, L + (size_t)(16 * wv) * ld, rows, ld, nw, r0 + lane, r1, lane);
+    if (lane < 16) part[(size_t)slot * 64 + 16 * wv + lane] = v;
+    return;
+  }
   if (r0 + 64 * wv >= r1)
     red[wv][lane] = 0.0;   // no rows for this wave (small fronts): skip the reduction
-  else if (ncol <= 16)
-    red[wv][lane] = bwd_part_wave<16>(c, L, rows, ld, ncol, r0 + tid, r1, lane);
   else
-    red[wv][lane] = bwd_part_wave<64>(c, L, rows, ld, ncol, r0 + tid, r1, lane);
+    red[wv][lane] = bwd_part_wave<16>(c, L, rows, ld, ncol, r0 + tid, r1, lane);
   __syncthreads();
   if (tid < 64) part[(size_t)slot * 64 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
 }
@@ -2294,7 +2554,16 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
       CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
     CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
     CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));
+    CH_TRY(hipStreamCreateWithFlags(&P.side5, hipStreamNonBlocking));
+    // the deferred far updates fill the CUs the panel chain leaves idle: their
+    // stream at the lowest dispatch priority (PGO_FAR_PRIORITY=0: default)
+    const char* fp = getenv("PGO_FAR_PRIORITY");
+    if (!(fp && fp[0] == '0') && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      CH_TRY(hipStreamCreateWithPriority(&P.side4, hipStreamNonBlocking, least));
+    else
+      CH_TRY(hipStreamCreateWithFlags(&P.side4, hipStreamNonBlocking));
     for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : P.fev) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   return hipSuccess;   // (the fronts' zeroing runs on, stream-ordered before any use)
 }
@@ -2305,9 +2574,13 @@ void chol_free(CholPlan& P) {
   if (P.h_blob) (void)hipHostFree(P.h_blob);
   for (hipEvent_t e : P.evs)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : P.fev)
+    if (e) (void)hipEventDestroy(e);
   if (P.side) (void)hipStreamDestroy(P.side);
   if (P.side2) (void)hipStreamDestroy(P.side2);
   if (P.side3) (void)hipStreamDestroy(P.side3);
+  if (P.side4) (void)hipStreamDestroy(P.side4);
+  if (P.side5) (void)hipStreamDestroy(P.side5);
   P = CholPlan();
 }
 
@@ -2315,7 +2588,7 @@ const char* kernel_family_name(int f) {
   static const char* const names[kFamCount] = {
       "k_assemble_tile", "(unused)", "k_perm_in+k_perm_out", "(unused)", "k_vec_assemble",
       "k_front_wave", "k_front_small", "k_panel_first", "k_step", "k_panel_syrk_lds", "k_panel_syrk128",
-      "k_bwd_part", "k_bwd_init", "k_bwd_step"};
+      "k_bwd_part", "k_bwd_init", "k_bwd_step", "k_step_diag", "k_col_trsm"};
   return f >= 0 && f < kFamCount ? names[f] : "?";
 }
 
@@ -2407,11 +2680,13 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
              (size_t)lv.maxm * sizeof(double), P.side2, c, (const int*)(P.d_level_fronts + lv.front_off));
       CH_TRY(hipEventRecord(P.evs[1], P.side2));
     }
+    static const bool asm_push = getenv("PGO_ASM_PUSH") && atoi(getenv("PGO_ASM_PUSH")) == 1;
     if (lv.ea_cnt[0] && !off("assemble"))
       launch(prof, kFamAssemble, [&] { return make_double2(0, lv.at_bytes * nb); },
-             k_assemble_tile, dim3(lv.ea_cnt[0], nb), B256, 0, s, c, (const int4*)(P.d_ea_tasks + lv.ea_off[0]),
-             (const int2*)(P.d_at_iptr + lv.ea_off[0]), (const int*)P.d_at_items, (const int4*)P.d_ea_pairs, V,
-             (long long)P.nslots, D, (const double*)P.d_lambda);
+             asm_push ? k_assemble_tile_push : k_assemble_tile, dim3(lv.ea_cnt[0], nb), B256, 0, s, c,
+             (const int4*)(P.d_ea_tasks + lv.ea_off[0]), (const int2*)(P.d_at_iptr + lv.ea_off[0]),
+             (const int*)P.d_at_items, (const int4*)P.d_ea_pairs, V, (long long)P.nslots, D,
+             (const double*)P.d_lambda);
     if (vec) CH_TRY(hipStreamWaitEvent(s, P.evs[1], 0));
     // small fronts on the second side stream, beside the blocked path of the
     // same level (disjoint fronts); joined before the next level
@@ -2459,8 +2734,23 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
     // level's end.  Ring of two join events (evs[3], evs[5]).
     bool side_pending = false;
     std::vector<char> on_side(lv.panels.size(), 0);   // plain(j) went to P.side and recorded its event
+    // deferred far updates on P.side4: (join step, event slot) of the pending ones
+    std::vector<int2> far_pending;
+    int fslot = 0;
+    auto join_far = [&](int step) -> hipError_t {   // step -1: all of them
+      for (size_t q = 0; q < far_pending.size();) {
+        if (step < 0 || far_pending[q].x == step) {
+          CH_TRY(hipStreamWaitEvent(s, P.fev[far_pending[q].y], 0));
+          far_pending.erase(far_pending.begin() + q);
+        } else {
+          q++;
+        }
+      }
+      return hipSuccess;
+    };
     for (size_t j = 0; j < lv.panels.size(); j++) {
       const PanelStep& ps = lv.panels[j];
+      CH_TRY(join_far((int)j));
       for (size_t back = 1; back <= 2 && back <= j; back++) {
         const PanelStep& pp = lv.panels[j - back];
         if (on_side[j - back] && pp.plain_lag == (int)back)
@@ -2489,26 +2779,62 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       const int nin = ps.syrk_inline && !off("plain") ? ps.syrk_cnt : 0;
       const bool apart = ps.syrk_cnt > 0 && !ps.syrk_inline && !off("plain");   // plain tiles in their own launch
       const bool step = ps.sdiag_cnt + ps.col_cnt + ps.prep_cnt + nin > 0 && !off("step");
-      auto plain = [&](hipStream_t st) {
+      auto plain = [&](hipStream_t st, int first, int cnt, double flops) {
         const bool big = ps.syrk_tile == kBigTile;
-        launch(prof, big ? kFamPanelSyrk128 : kFamPanelSyrk, [&] { return make_double2(ps.plain_flops * nb, 0); },
-               big ? k_panel_syrk128 : k_panel_syrk_lds, dim3(ps.syrk_cnt, nb), B256, 0, st, c, tiles, ps.kb);
+        launch(prof, big ? kFamPanelSyrk128 : kFamPanelSyrk, [&] { return make_double2(flops * nb, 0); },
+               big ? k_panel_syrk128 : k_panel_syrk_lds, dim3(cnt, nb), B256, 0, st, c, tiles + first, ps.kb);
       };
       if (apart) {   // on the side stream (beside k_step, behind the earlier plains)
         CH_TRY(hipEventRecord(P.evs[2], s));
         CH_TRY(hipStreamWaitEvent(P.side, P.evs[2], 0));
       }
-      if (step)
+      // many diagonal tiles (x lanes): the step as three launches -- the
+      // diagonal tiles (k_step_diag: 2 workgroups per CU) beside the column
+      // block's, prep and inline tile updates (k_panel_syrk_lds on P.side5:
+      // 4 per CU), then the column block's solves (k_first_trsm) -- instead of
+      // one k_step whose column workgroups hold a diagonal workgroup's LDS and
+      // registers while they wait; same arithmetic (the tile kernels compute a
+      // tile's elements alike), bitwise k_step's factor
+      static const int step_split = getenv("PGO_STEP_SPLIT") ? atoi(getenv("PGO_STEP_SPLIT")) : 64;
+      const bool split = step && step_split > 0 && ps.sdiag_cnt * nb >= step_split && ps.col_cnt > 0;
+      if (split) {
+        const int4* cupd = cols + ps.fcol_cnt;   // col then prep tasks: 64x64 tile updates
+        CH_TRY(hipEventRecord(P.evs[0], s));
+        CH_TRY(hipStreamWaitEvent(P.side5, P.evs[0], 0));
+        launch(prof, kFamPanelSyrk, [&] { return make_double2(ps.colupd_flops * nb, 0); }, k_panel_syrk_lds,
+               dim3(ps.col_cnt + ps.prep_cnt, nb), B256, 0, P.side5, c, cupd, ps.kb);
+        if (nin)
+          launch(prof, kFamPanelSyrk, [&] { return make_double2(ps.plain_flops * nb, 0); }, k_panel_syrk_lds,
+                 dim3(nin, nb), B256, 0, P.side5, c, tiles, ps.kb);
+        CH_TRY(hipEventRecord(P.evs[1], P.side5));
+        launch(prof, kFamStepDiag, [&] { return make_double2(ps.diag_flops * nb, 0); }, k_step_diag,
+               dim3(ps.sdiag_cnt, nb), B256, 0, s, c, (const int4*)(P.d_sdiag + ps.sdiag_off), ps.kb);
+        CH_TRY(hipStreamWaitEvent(s, P.evs[1], 0));
+        launch(prof, kFamColTrsm, [&] { return make_double2(ps.trsm_flops * nb, 0); }, k_first_trsm,
+               dim3(ps.col_cnt, nb), B256, 0, s, c, cupd);
+      } else if (step)
         launch(prof, kFamStep, [&] { return make_double2(ps.step_flops * nb, 0); }, k_step,
                dim3(ps.sdiag_cnt + ps.col_cnt + ps.prep_cnt + nin, nb), B256, 0, s, c,
                (const int4*)(P.d_sdiag + ps.sdiag_off), ps.sdiag_cnt, cols + ps.fcol_cnt, ps.col_cnt, ps.prep_cnt,
                tiles, ps.kb,
                stamps && li + 1 == P.levels.size() && ps.kb / kNB < kMaxStampSlots ? ps.kb / kNB : -1);
       if (apart) {   // (never on the main stream: an earlier plain may still run on P.side)
-        plain(P.side);
+        const int nnear = ps.syrk_cnt - ps.far_cnt;
+        plain(P.side, 0, nnear, ps.plain_flops - ps.far_flops);
         CH_TRY(hipEventRecord(P.evs[j & 1 ? 5 : 3], P.side));
         side_pending = true;
         on_side[j] = 1;
+        if (ps.far_cnt > 0) {   // the far columns: on P.side4 (behind the earlier far launches), joined late
+          int busy = -2;   // (a ring slot still pending: joined now)
+          for (const int2& fp : far_pending)
+            if (fp.y == fslot) busy = fp.x;
+          if (busy != -2) CH_TRY(join_far(busy));
+          CH_TRY(hipStreamWaitEvent(P.side4, P.evs[2], 0));
+          plain(P.side4, nnear, ps.far_cnt, ps.far_flops);
+          CH_TRY(hipEventRecord(P.fev[fslot], P.side4));
+          far_pending.push_back(make_int2(ps.far_join, fslot));
+          fslot = (fslot + 1) % 4;
+        }
       }
       // the panel this step factored, to every rank (the apart plain tiles
       // beside it neither read nor write its columns)
@@ -2518,6 +2844,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       CH_TRY(hipEventRecord(P.evs[2], P.side));
       CH_TRY(hipStreamWaitEvent(s, P.evs[2], 0));
     }
+    CH_TRY(join_far(-1));
     if (fork_small || fork_wave) {
       CH_TRY(hipEventRecord(P.evs[1], P.side2));
       CH_TRY(hipStreamWaitEvent(s, P.evs[1], 0));

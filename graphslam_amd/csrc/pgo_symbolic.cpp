@@ -683,7 +683,14 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       return true;
     };
     bool apart_chain = false;   // once a step's plain tiles go to their own launch, the later ones do too
+    // deferred far updates (apart steps at a kKB block end): per step and big
+    // front, the largest column its k_step tasks and near plain tiles touch
+    // (touch), and the first column of its far plain tiles (far0, m = none)
+    std::vector<std::vector<int>> touch, far0;
     for (int kb = 0; kb < maxw; kb += kNB) {
+      touch.emplace_back(big.size(), 0);
+      far0.emplace_back(big.size(), 0);
+      for (size_t i = 0; i < big.size(); i++) far0.back()[i] = P.m[big[i]];
       PanelStep ps;
       ps.kb = kb;
       ps.syrk_flops = ps.plain_flops = ps.step_flops = ps.first_flops = 0;
@@ -721,6 +728,7 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       // front is the same in every plan (the partitioned plans' fronts are bit
       // for bit the one-rank plan's).
       const bool lookahead = !getenv("PGO_NO_LOOKAHEAD");
+      const bool far_on = getenv("PGO_FAR") && atoi(getenv("PGO_FAR")) == 1;
       // (PGO_LOOKAHEAD_M: the front height threshold, a test knob)
       const int la_m = getenv("PGO_LOOKAHEAD_M") ? atoi(getenv("PGO_LOOKAHEAD_M")) : kLookaheadM;
       auto front_skip = [&](int s) { return lookahead && P.m[s] >= la_m; };
@@ -765,6 +773,11 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       const int tile0 = ntiles(kBigTile) >= big_min ? kBigTile : kTile;
       const bool apart = apart_chain || !(tile0 == kTile && ntiles(kTile) <= kInlineTiles);
       std::vector<int4> plain;   // (front, first column, end column, k0): rows from the column down
+      // ... the far part of an apart step's plain range (a kKB block end: the
+      // columns past the next block, [be + kKB, m)): its own launch on a fourth
+      // stream, joined only before the first later step that touches them
+      std::vector<int4> plain_far;
+      std::vector<int> far_front;   // big-front index of each plain_far range
       std::vector<int4> prep;    // prep tiles (front, r0, c0, k0), whole 64x64 tiles
       bool conflict = false;   // a front's next step reads this step's plain tiles
       for (size_t i = 0; i < big.size(); i++) {
@@ -784,16 +797,21 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
             S.schedule_error = true;
           }
           for (int j = kn; j < c1; j++) applied[i][j] = kn;
+          touch.back()[i] = std::max(touch.back()[i], c1);
           const int depth = kn - k0, kw = inner ? (k0 | (int)0x80000000) : k0;
           if (dist) xstep.push_back(make_int4(s, kn, nb2, cowner(s, kn)));
           const bool own = mine(s, kn);
           if (own) S.sdiag_tasks.push_back(make_int4(s, kn, kn, kw));
-          ps.step_flops += (double)depth * kNB * (kNB + 1) + 2.0 * nb2 * nb2 * (double)nb2 / 3.0 +
-                           (double)std::min(kNB - nb2, m - kn - nb2) * nb2 * nb2;
+          const double fd = (double)depth * kNB * (kNB + 1) + 2.0 * nb2 * nb2 * (double)nb2 / 3.0 +
+                            (double)std::min(kNB - nb2, m - kn - nb2) * nb2 * nb2;
+          ps.step_flops += fd;
+          ps.diag_flops += fd;
           for (int r0 = kn + kNB; r0 < m; r0 += kNB) {
             if (own) S.col_tasks.push_back(make_int4(s, r0, kn, kw));
             const int rows = std::min(kNB, m - r0);
             ps.step_flops += 2.0 * depth * rows * (c1 - kn) + (double)rows * nb2 * nb2;
+            ps.colupd_flops += 2.0 * depth * rows * (c1 - kn);
+            ps.trsm_flops += (double)rows * nb2 * nb2;
           }
           ps.syrk_flops += (double)depth * (c1 - kn) * (2.0 * m - kn - c1 + 1.0);
         }
@@ -805,18 +823,27 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
             S.schedule_error = true;
           }
           for (int j = b0; j < b1; j++) applied[i][j] = kn;
+          touch.back()[i] = std::max(touch.back()[i], b1);
           if (mine(s, b0))
             for (int r0 = b0; r0 < m; r0 += kNB) prep.push_back(make_int4(s, r0, b0, k0));
           const double f = (double)(kn - k0) * kNB * (2.0 * m - b0 - b1 + 1.0);
           ps.step_flops += f;
+          ps.colupd_flops += f;
           ps.syrk_flops += f;
         }
         int cstart, cend;
         plain_range(s, front_skip(s), cstart, cend);
-        if (kn + kNB < w && cstart < cend) {   // the next step prepares [kn2, c2) of this front
+        // far split at a block end: columns past the next kKB block (the next
+        // steps touch none of them until that block ends)
+        // (PGO_FAR=1: measured within the replay noise on C3 -- 8.70 / 17.50 ms
+        // at 1 / 3 lanes with and without, profiles/r04c_ab_far.txt -- while
+        // the concurrent far tiles slow the k_step launches they overlap; off)
+        const int nend = (!inner && cstart < cend && far_on) ? std::max(cstart, std::min(cend, std::min(be + kKB, w)))
+                                                             : cend;
+        if (kn + kNB < w && cstart < nend) {   // the next step prepares [kn2, c2) of this front
           const int kn2 = kn + kNB, bs2 = kn & ~(kKB - 1), be2 = std::min(bs2 + kKB, w);
           const int c2 = std::min(kn2 + kNB, kn2 < be2 ? be2 : m);
-          if (cstart < c2 && kn2 < cend) conflict = true;   // this step's plain tiles feed it: lag 1
+          if (cstart < c2 && kn2 < nend) conflict = true;   // this step's plain tiles feed it: lag 1
         }
         if (cstart < cend) {
           int k0 = applied[i][cstart];
@@ -830,9 +857,16 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
             k0 = kb;
           }
           for (int j = cstart; j < cend; j++) applied[i][j] = kn;
-          const int depth = kn - k0;
+          const int depth = kn - k0, kw = inner ? (k0 | (int)0x80000000) : k0;
           for (int cc = cstart; cc < cend; cc++) ps.plain_flops += 2.0 * depth * (m - cc);
-          plain.push_back(make_int4(s, cstart, cend, inner ? (k0 | (int)0x80000000) : k0));
+          for (int cc = nend; cc < cend; cc++) ps.far_flops += 2.0 * depth * (m - cc);
+          if (cstart < nend) plain.push_back(make_int4(s, cstart, nend, kw));
+          touch.back()[i] = std::max(touch.back()[i], nend);
+          if (nend < cend) {
+            plain_far.push_back(make_int4(s, nend, cend, kw));
+            far_front.push_back((int)i);
+            far0.back()[i] = nend;
+          }
         }
       }
       ps.syrk_flops += ps.plain_flops;
@@ -841,8 +875,9 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       S.col_tasks.insert(S.col_tasks.end(), prep.begin(), prep.end());
       ps.prep_cnt = (int)prep.size();
       long long cnt128 = 0;
-      for (const int4& u : plain)
-        for (int c0 = u.y; c0 < u.z; c0 += kBigTile) cnt128 += (P.m[u.x] - c0 + kBigTile - 1) / kBigTile;
+      for (const std::vector<int4>* pl : {&plain, &plain_far})
+        for (const int4& u : *pl)
+          for (int c0 = u.y; c0 < u.z; c0 += kBigTile) cnt128 += (P.m[u.x] - c0 + kBigTile - 1) / kBigTile;
       // (distributed top: 64-wide tiles, split where the column owner changes;
       // a tile's elements are computed alike in either kernel, so this is
       // bitwise the 128-tile update)
@@ -851,11 +886,16 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       // (pgo_chol.h front_packed): a range starting inside a block (the update
       // matrix starts at w) opens with a narrow tile up to the block's end,
       // clipped; a tile's elements are computed alike whatever its shape
-      for (const int4& u : plain)
+      auto gen_tiles = [&](const std::vector<int4>& ranges) {
+      for (const int4& u : ranges)
         for (int c0 = u.y; c0 < u.z;) {
           const int T = ps.syrk_tile;
           const int ce = (c0 & 63) ? std::min(u.z, (c0 + 63) & ~63) : std::min(u.z, c0 + T);
-          const bool narrow = ce - c0 < T && ce < u.z;   // (a range's last tile is clipped by the range end)
+          // a tile narrower than T carries its width (the kernels clip its columns
+          // there): a block's end inside the range, or the range's end -- which
+          // is not the kernels' own column end where a step's range is split
+          // into near and far parts
+          const bool narrow = ce - c0 < T;
           if (!dist) {
             const int clip = narrow ? ce - c0 : 0;
             for (int r0 = c0; r0 < P.m[u.x]; r0 += T) S.syrk_tasks.push_back(make_int4(u.x, r0 | (clip << kClipShift), c0, u.w));
@@ -873,13 +913,27 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
           }
           c0 = ce;
         }
-      {   // XCD-aware order of this step's Schur-update tiles
-        std::vector<int4> mine(S.syrk_tasks.begin() + ps.syrk_off, S.syrk_tasks.end());
-        xcd_order(mine, ps.syrk_tile);
-        std::copy(mine.begin(), mine.end(), S.syrk_tasks.begin() + ps.syrk_off);
-      }
+      };
+      gen_tiles(plain);
+      const int near_end = (int)S.syrk_tasks.size();
+      gen_tiles(plain_far);
       ps.syrk_cnt = (int)S.syrk_tasks.size() - ps.syrk_off;
       ps.syrk_inline = !apart && ps.syrk_tile == kTile && ps.syrk_cnt <= kInlineTiles;
+      ps.far_cnt = ps.syrk_inline ? 0 : (int)S.syrk_tasks.size() - near_end;
+      if (ps.far_cnt == 0) {   // (inline, or nothing far: the far ranges' columns are this step's)
+        for (size_t q = 0; q < plain_far.size(); q++) {
+          touch.back()[far_front[q]] = std::max(touch.back()[far_front[q]], plain_far[q].z);
+          far0.back()[far_front[q]] = P.m[big[far_front[q]]];
+        }
+        ps.far_flops = 0;
+      }
+      auto xcd = [&](int b, int e) {   // XCD-aware order of a launch's Schur-update tiles
+        std::vector<int4> mine(S.syrk_tasks.begin() + b, S.syrk_tasks.begin() + e);
+        xcd_order(mine, ps.syrk_tile);
+        std::copy(mine.begin(), mine.end(), S.syrk_tasks.begin() + b);
+      };
+      xcd(ps.syrk_off, ps.syrk_off + ps.syrk_cnt - ps.far_cnt);
+      xcd(ps.syrk_off + ps.syrk_cnt - ps.far_cnt, ps.syrk_off + ps.syrk_cnt);
       // an apart launch no front's next step reads is joined before the step after next
       ps.plain_lag = ps.syrk_cnt > 0 && !ps.syrk_inline ? (conflict ? 1 : 2) : 0;
       // (an inline plain after a lag-2 apart one could touch its tiles at once)
@@ -887,6 +941,19 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       if (ps.syrk_inline) ps.step_flops += ps.plain_flops;
       ps.xstep = add_exchange(S, xstep);
       lv.panels.push_back(ps);
+    }
+    // a far launch is joined before the first later step whose k_step tasks or
+    // near plain tiles touch one of its columns (-1: at the level's end)
+    for (size_t j = 0; j < lv.panels.size(); j++) {
+      PanelStep& ps = lv.panels[j];
+      ps.far_join = -1;
+      if (ps.far_cnt == 0) continue;
+      for (size_t j2 = j + 1; j2 < lv.panels.size() && ps.far_join < 0; j2++)
+        for (size_t i = 0; i < big.size(); i++)
+          if (touch[j2][i] > far0[j][i]) {
+            ps.far_join = (int)j2;
+            break;
+          }
     }
     if (dist) {   // update columns past a front's last whole panel, factored with it: to every rank
       std::vector<int4> tails;

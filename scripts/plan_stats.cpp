@@ -68,8 +68,11 @@ int main(int argc, char** argv) {
         ea += (pr.w & 0xff) * (pr.w >> 8);
       }
     }
-    int nfused = 0, ntr = 0, nsy = 0, npotrf = 0;
+    int nfused = 0, ntr = 0, nsy = 0, npotrf = 0, nfar = 0;
+    std::string joins;
     for (const auto& ps : lv.panels) {
+      if (ps.far_cnt) joins += " " + std::to_string(&ps - lv.panels.data()) + "->" + std::to_string(ps.far_join);
+      nfar += ps.far_cnt;
       nfused += ps.syrk_inline;
       ntr += ps.fcol_cnt + ps.col_cnt;
       nsy += ps.syrk_cnt;
@@ -77,6 +80,18 @@ int main(int argc, char** argv) {
     }
     printf("level %2d: fronts %6d (small %6d) maxm %5d tiles %6d ea %6.1fM dbl, steps %3zu (inline %3d) potrf %5d trsm %6d syrk %7d\n",
            li++, lv.front_cnt, nsmall, lv.maxm, lv.ea_cnt[0], ea / 1e6, lv.panels.size(), nfused, npotrf, ntr, nsy);
+    if (nfar) printf("          far tiles %d, far launches (step->join):%s\n", nfar, joins.c_str());
+    {   // assembly: pairs (child rectangles) and H items per tile task
+      int hist[6] = {0, 0, 0, 0, 0, 0};
+      double items = 0;
+      for (int q = 0; q < lv.ea_cnt[0]; q++) {
+        const int4 t = P.ea_tasks[lv.ea_off[0] + q];
+        hist[std::min(t.w, 5)]++;
+        items += P.at_iptr[lv.ea_off[0] + q].y;
+      }
+      printf("          assembly tiles by child pairs 0/1/2/3/4/5+: %d %d %d %d %d %d, H items per tile %.1f\n", hist[0],
+             hist[1], hist[2], hist[3], hist[4], hist[5], lv.ea_cnt[0] ? items / lv.ea_cnt[0] : 0.0);
+    }
   }
   for (int size : {2, 4, 8}) {
     std::vector<double> rf;

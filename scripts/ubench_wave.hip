@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 using namespace pgo;
@@ -31,7 +32,12 @@ int main(int argc, char** argv) {
   hipMalloc(&F0, bytes);
   hipMalloc(&T, (size_t)N * 4096 * 8);
   hipMalloc(&fv, (size_t)N * M * 8);
-  hipMemset(fv, 0, (size_t)N * M * 8);
+  {
+    std::vector<double> hv((size_t)N * M);
+    for (size_t q = 0; q < hv.size(); q++) hv[q] = ((int)(q * 2654435761u % 2001) - 1000) / 1000.0;
+    hipMemcpy(fv, hv.data(), hv.size() * 8, hipMemcpyHostToDevice);
+  }
+  hipMemset(T, 0, (size_t)N * 4096 * 8);
   hipMemcpy(F0, h.data(), bytes, hipMemcpyHostToDevice);
   std::vector<int> hm(N, M), hw(N, W), list(N), voff(N + 1);
   std::vector<long long> foff(N + 1), toff(N + 1);
@@ -106,6 +112,23 @@ int main(int argc, char** argv) {
       }
   }
   printf("  max |F - host| over 3 fronts: %.3g\n", maxd);
+  {   // bitwise fingerprint of every output (F, frontal vectors, inverses): old / new builds compare equal
+    std::vector<double> vv((size_t)N * M), tt((size_t)N * 4096);
+    hipMemcpy(vv.data(), fv, vv.size() * 8, hipMemcpyDeviceToHost);
+    hipMemcpy(tt.data(), T, tt.size() * 8, hipMemcpyDeviceToHost);
+    unsigned long long hsh = 1469598103934665603ULL;
+    auto mix = [&](const std::vector<double>& a) {
+      for (double x : a) {
+        unsigned long long u;
+        memcpy(&u, &x, 8);
+        hsh = (hsh ^ u) * 1099511628211ULL;
+      }
+    };
+    mix(out);
+    mix(vv);
+    mix(tt);
+    printf("  output fingerprint %016llx\n", hsh);
+  }
   long long clk[32];
   hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_diag_clk), sizeof(clk));
   int fl = 0;
