@@ -271,7 +271,9 @@ def live_resolve_bench(pg, g, k=5, params=None):
         st = pg.optimize(params)
         rows.append({"ms": 1e3 * (time.perf_counter() - t0), "plan_update": st["plan_update"],
                      "upload_kind": st["upload_kind"],
-                     "ms_plan": st["ms_plan"], "ms_upload": st["ms_upload"], "linearizations": st["linearizations"],
+                     "ms_plan": st["ms_plan"], "ms_upload": st["ms_upload"], "ms_optimize": st["ms_total"],
+                     "ms_linearize": st["ms_linearize"], "ms_solve": st["ms_solve"], "ms_update": st["ms_update"],
+                     "linearizations": st["linearizations"],
                      "lm_tries": st["inner_iterations"], "initial_error": st["initial_error"],
                      "final_error": st["final_error"],
                      "stop_reason": _lib.STOP_REASONS.get(st["stop_reason"], str(st["stop_reason"]))})

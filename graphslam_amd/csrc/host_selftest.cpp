@@ -162,6 +162,32 @@ int check_assembly(const pgo::CholPlan& P) {
   return 0;
 }
 
+// The assembly's targets and sources against the pattern: every target (j, i)
+// of the permuted lower triangle (i > j) lists exactly the slots of one end of
+// the block -- as many as row perm[i] holds to column perm[j] -- and every
+// slot of the lower triangle is listed once.
+int check_sources(const pgo::CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& col) {
+  long long total = 0, want = 0;
+  for (size_t g = 0; g < P.asm_front.size(); g++) {
+    const int s = P.asm_front[g], j = P.sfirst[s] + P.asm_lj[g], i = P.rows[P.rptr[s] + P.asm_li[g]];
+    if (i <= j) return fail("assembly: a target above the diagonal");
+    const int a = P.perm[i], b = P.perm[j];
+    int cnt = 0;
+    for (int k = row_ptr[a]; k < row_ptr[a + 1]; k++) cnt += col[k] == b;
+    if (P.asm_ptr[g + 1] - P.asm_ptr[g] != cnt) return fail("assembly: a target's source count");
+    for (int q = P.asm_ptr[g]; q < P.asm_ptr[g + 1]; q++) {
+      const int k = P.asm_src[q];
+      const int r = (int)(std::upper_bound(row_ptr.begin(), row_ptr.end(), k) - row_ptr.begin()) - 1;
+      if (!((r == a && col[k] == b) || (r == b && col[k] == a))) return fail("assembly: a source off its block");
+    }
+    total += cnt;
+  }
+  for (int r = 0; r + 1 < (int)row_ptr.size(); r++)
+    for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) want += P.iperm[r] > P.iperm[col[k]];
+  if (total != want || P.asm_ptr.back() != want) return fail("assembly: sources of the lower triangle");
+  return 0;
+}
+
 // Packed fronts: no Schur tile's columns straddle a 64-column block (the
 // kernels address a tile's columns from one block base).
 int check_tiles(const pgo::CholPlan& P) {
@@ -207,7 +233,7 @@ int check_append(const Pattern& G, int n0, int ordering) {
     for (int k = Gn.row_ptr[n - 1]; k < Gn.row_ptr[n]; k++) pairs.push_back(make_int2(n - 1, Gn.col[k]));
     if (!pgo::chol_append(P, n, Gn.row_ptr, Gn.col, pairs, 1 << 30, 1e30)) return fail("append: refused");
     if (P.schedule_error) return fail("append: panel schedule bookkeeping");
-    if (check_assembly(P)) return 1;
+    if (check_assembly(P) || check_sources(P, Gn.row_ptr, Gn.col)) return 1;
     if (P.n != n || !pgo::chol_covers(P, n, Gn.row_ptr, Gn.col)) return fail("append: pattern not covered");
     for (int s = 0; s < P.ns; s++) {
       const int wp = P.sfirst[s + 1] - P.sfirst[s], nr = P.rptr[s + 1] - P.rptr[s];
@@ -258,7 +284,7 @@ int main() {
     if (P.ns <= 0 || P.flops <= 0) return fail("analysis");
     if (P.schedule_error) return fail("panel schedule bookkeeping");
     if (!pgo::chol_covers(P, G.n, G.row_ptr, G.col)) return fail("plan does not cover its own pattern");
-    if (check_assembly(P) || check_tiles(P)) return 1;
+    if (check_assembly(P) || check_tiles(P) || check_sources(P, G.row_ptr, G.col)) return 1;
     for (int size : {2, 4}) {
       std::vector<double> rf;
       double top = 0;

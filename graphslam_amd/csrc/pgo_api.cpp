@@ -52,6 +52,7 @@ struct HostStructure {
   std::vector<int> dorder;         // device factor -> user factor index
   std::vector<int> pv, row_ptr, slot_edge, slot_col, prior_ptr, porder;
   std::vector<int> uf;             // union-find parents over the vertices (gauge check)
+  std::vector<int> erow, s1_ptr, s1pos;   // the Cholesky-mode sweep structure (upload_structure)
   bool gauge_free = false;
 };
 
@@ -82,6 +83,12 @@ struct pgo_graph {
   // re-uploads the whole array first (slot_codes_mixed)
   bool slot_codes_plan = false;
   bool slot_codes_mixed = false;
+  // rows from bind_row0 on need their owner bits (re)computed by the next
+  // bind_plan (in-place appends: the plan keeps the old poses' order, so the
+  // earlier rows' bits and their factors' owner sides stand); h_eside the
+  // owner side of every factor, as uploaded
+  int bind_row0 = 0;
+  std::vector<unsigned char> h_eside;
   bool gauge_free = false;                 // some connected component has no prior
   double* h_scal = nullptr;                 // pinned
   int* h_ctrl = nullptr;                    // pinned
@@ -665,11 +672,15 @@ int upload_structure(pgo_graph* g) {
   RC_TRY(h2d(g, d.row_ptr, row_ptr.data(), n + 1));
   RC_TRY(h2d(g, d.slot_edge, slot_edge.data(), ns));
   g->slot_codes_plan = g->slot_codes_mixed = false;   // pre-plan codes throughout
+  g->bind_row0 = 0;
   RC_TRY(h2d(g, d.slot_col, slot_col.data(), ns));
   HIP_TRY(g, hipMemsetAsync(d.part, 0, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices, d.stream));
   HIP_TRY(g, hipStreamSynchronize(d.stream));
   g->dev_structure = true;
   g->h_Dc = std::move(Dc);
+  H.erow = std::move(erow);
+  H.s1_ptr = std::move(s1_ptr);
+  H.s1pos = std::move(s1pos);
   g->hs = std::move(H);
   g->dev_complete = true;
   g->last_upload = 1;
@@ -718,7 +729,8 @@ int append_structure(pgo_graph* g) {
   const int n_old = d.n, ne_old = d.ne;
   const int n = (int)g->keys.size(), ne = (int)g->ek1.size(), np = (int)g->pk.size();
   if (!g->dev_complete || !g->hip_ready || np != d.np || n < n_old || ne < ne_old || (n == n_old && ne == ne_old) ||
-      (size_t)n > g->cap_n || (size_t)ne > g->cap_ne || (int)H.eij.size() != ne_old || getenv("PGO_NO_APPEND"))
+      (size_t)n > g->cap_n || (size_t)ne > g->cap_ne || (int)H.eij.size() != ne_old ||
+      (int)H.erow.size() != n_old + 1 || (int)H.s1pos.size() != ne_old || getenv("PGO_NO_APPEND"))
     return 1;
   // the new factors, resolved and in device order
   std::vector<int> nd(ne - ne_old);
@@ -829,25 +841,56 @@ int append_structure(pgo_graph* g) {
   }
   H.prior_ptr.resize(n + 1, H.prior_ptr.empty() ? 0 : H.prior_ptr.back());
   phase("rows");
-  g->h_row_ptr = H.row_ptr;
-  g->h_slot_col = H.slot_col;
-  g->h_slot_edge = H.slot_edge;
-  g->edge_slot0.assign(ne, -1);
-  for (int k = 0; k < ns; k++)
+  // rows before r0 (the first with a new slot) and their slots are unchanged:
+  // the host mirrors, the factor -> side-0 slot map and the sweep structure
+  // are updated from there on (h_slot_edge keeps the plan's bits before r0,
+  // as the device copy does)
+  const int r0 = extra.empty() ? n_old : std::min(extra.front().x, n_old);
+  const int k0 = H.row_ptr[r0];
+  g->h_row_ptr.resize(n + 1);
+  std::copy(H.row_ptr.begin() + r0, H.row_ptr.end(), g->h_row_ptr.begin() + r0);
+  g->h_slot_col.resize(ns);
+  std::copy(H.slot_col.begin() + k0, H.slot_col.end(), g->h_slot_col.begin() + k0);
+  g->h_slot_edge.resize(ns);
+  std::copy(H.slot_edge.begin() + k0, H.slot_edge.end(), g->h_slot_edge.begin() + k0);
+  g->edge_slot0.resize(ne, -1);
+  for (int k = k0; k < ns; k++)
     if ((H.slot_edge[k] & 1) == 0) g->edge_slot0[H.dorder[H.slot_edge[k] >> 2]] = k;
-  // Cholesky-mode sweep structure (see upload_structure)
-  std::vector<int> erow(n + 1, 0), s1_ptr(n + 1, 0), s1pos(ne);
-  for (int e = 0; e < ne; e++) {
-    erow[H.eij[e].x + 1]++;
-    s1_ptr[H.eij[e].y + 1]++;
+  // Cholesky-mode sweep structure (see upload_structure): the new factors come
+  // last in device order, so an old factor keeps its rank among its row's
+  // side-1 factors and moves by its row's shift of s1_ptr
+  int x0 = n_old, y0 = n_old;   // first rows of erow / s1_ptr that change (the new rows always)
+  for (const int2& ij : nij) {
+    x0 = std::min(x0, ij.x);
+    y0 = std::min(y0, ij.y);
   }
-  for (int i = 0; i < n; i++) {
-    erow[i + 1] += erow[i];
-    s1_ptr[i + 1] += s1_ptr[i];
-  }
+  std::vector<int>& erow = H.erow;
+  std::vector<int>& s1_ptr = H.s1_ptr;
+  std::vector<int>& s1pos = H.s1pos;
   {
-    std::vector<int> f(s1_ptr.begin(), s1_ptr.end() - 1);
-    for (int e = 0; e < ne; e++) s1pos[e] = f[H.eij[e].y]++;
+    std::vector<int> ecnt(n, 0), scnt(n, 0);   // new factors per row, by side
+    for (const int2& ij : nij) {
+      ecnt[ij.x]++;
+      scnt[ij.y]++;
+    }
+    erow.resize(n + 1, erow.back());
+    s1_ptr.resize(n + 1, s1_ptr.back());
+    for (int i = x0, c = 0; i < n; i++) erow[i + 1] += (c += ecnt[i]);
+    std::vector<int> dy(n + 1, 0);   // new side-1 factors in rows < j
+    for (int j = y0, c = 0; j < n; j++) {
+      dy[j] = c;
+      s1_ptr[j + 1] += (c += scnt[j]);
+    }
+    for (int e = 0; e < ne_old; e++) {
+      const int y = H.eij[e].y;
+      if (y > y0) s1pos[e] += dy[y];
+    }
+    s1pos.resize(ne);
+    std::vector<int> f(n, 0);   // the new factors after the old ones of their row
+    for (size_t q = 0; q < nij.size(); q++) {
+      const int y = nij[q].y;
+      s1pos[ne_old + q] = s1_ptr[y + 1] - scnt[y] + f[y]++;
+    }
   }
   g->h_Dc.resize(6 * (size_t)n, 0.0);
   for (size_t q = 0; q < nij.size(); q++) {   // new side-1 terms, in device order after the old ones
@@ -887,12 +930,6 @@ int append_structure(pgo_graph* g) {
   // side-1 sums of the rows that gained side-1 terms; whole for the rest
   Staging& sg = g->stage;   // (allocated by upload_structure; staged_h2d falls back to pageable copies)
   RC_TRY(stage_begin(g, sg));
-  const int r0 = extra.empty() ? n_old : std::min(extra.front().x, n_old);   // first row with a new slot
-  int x0 = n_old, y0 = n_old;   // (the new rows always)
-  for (const int2& ij : nij) {
-    x0 = std::min(x0, ij.x);
-    y0 = std::min(y0, ij.y);
-  }
   RC_TRY(staged_h2d(g, sg, d.eij + ne_old, nij.data(), nij.size()));
   RC_TRY(staged_h2d(g, sg, d.ez + ne_old, hz.data(), hz.size()));
   RC_TRY(staged_h2d(g, sg, d.eom + 3 * (size_t)ne_old, hom.data(), hom.size()));
@@ -927,6 +964,7 @@ int append_structure(pgo_graph* g) {
   g->dev_structure = true;
   g->last_upload = 2;
   if (g->slot_codes_plan && H.row_ptr[r0] > 0) g->slot_codes_mixed = true;   // rows < r0 keep the plan's bits
+  g->bind_row0 = std::min(g->bind_row0, r0);
   if (g->chol_ready) g->plan_stale = true;   // ensure_chol decides what to keep
   phase("upload");
   // the new vertices' values (the resident ones stay bit for bit, unless the
@@ -991,13 +1029,16 @@ int exchange_group(void* ctx, int begin) {
 int bind_plan(pgo_graph* g, bool full);
 
 // Before a PCG linearisation: an in-place append after a Cholesky plan left
-// the device owner bits half the plan's, half pre-plan; upload the host's
-// pre-plan codes whole so every factor has exactly one `se & 2` slot.
+// the device owner bits (and the host mirror h_slot_edge) half the plan's, half
+// pre-plan; upload the pre-plan codes whole so every factor has exactly one
+// `se & 2` slot.
 int unmix_slot_codes(pgo_graph* g) {
   if (!g->slot_codes_mixed) return PGO_OK;
+  g->h_slot_edge = g->hs.slot_edge;
   RC_TRY(h2d(g, g->d.slot_edge, g->h_slot_edge.data(), g->h_slot_edge.size()));
   HIP_TRY(g, hipStreamSynchronize(g->d.stream));
   g->slot_codes_plan = g->slot_codes_mixed = false;
+  g->bind_row0 = 0;
   return PGO_OK;
 }
 
@@ -1094,6 +1135,7 @@ int ensure_chol(pgo_graph* g) {
   g->hook.broadcast = exchange_broadcast;
   g->hook.group = exchange_group;
   pgo::chol_analyze(g->chol, g->d.n, g->h_row_ptr, g->h_slot_col);
+  g->bind_row0 = 0;   // (a new order: every owner bit)
   if (g->chol.schedule_error) return fail(g, PGO_E_HIP, "internal: inconsistent panel schedule");
   const auto tb = std::chrono::steady_clock::now();
   RC_TRY(bind_plan(g, true));
@@ -1115,13 +1157,15 @@ int ensure_chol(pgo_graph* g) {
 int bind_plan(pgo_graph* g, bool full) {
   PhaseTimer phase("bind_plan");
   {
-    const int n = g->d.n;
+    const int n = g->d.n, ne = g->d.ne;
+    const int r0 = std::min(std::max(g->bind_row0, 0), n), k0 = g->h_row_ptr[r0];
     std::vector<int>& slot_edge = g->h_slot_edge;
-    std::vector<unsigned char> eside(g->d.ne, 0);
+    std::vector<unsigned char>& eside = g->h_eside;
+    eside.resize(ne, 0);
     // Cholesky-mode linearisation writes each factor's owner block at its
     // device factor index (coalesced), so the assembly reads V[q*S + e]
-    host_parallel(n, [&](int r0, int r1) {
-      for (int r = r0; r < r1; r++)
+    host_parallel(n - r0, [&](int a, int b) {
+      for (int r = r0 + a; r < r0 + b; r++)
         for (int k = g->h_row_ptr[r]; k < g->h_row_ptr[r + 1]; k++) {
           const bool own = g->chol.iperm[r] > g->chol.iperm[g->h_slot_col[k]];
           slot_edge[k] = (slot_edge[k] & ~2) | (own ? 2 : 0);
@@ -1144,15 +1188,16 @@ int bind_plan(pgo_graph* g, bool full) {
     if (g->stage.buf) {   // pinned staging: the copies (and the fronts' zeroing) run on unsynchronised
       RC_TRY(stage_begin(g, g->stage));
       RC_TRY(staged_h2d(g, g->stage, g->d.eside, eside.data(), eside.size()));
-      RC_TRY(staged_h2d(g, g->stage, g->d.slot_edge, slot_edge.data(), slot_edge.size()));
+      RC_TRY(staged_h2d(g, g->stage, g->d.slot_edge + k0, slot_edge.data() + k0, slot_edge.size() - k0));
       RC_TRY(stage_end(g, g->stage));
     } else {
       RC_TRY(h2d(g, g->d.eside, eside.data(), eside.size()));
-      RC_TRY(h2d(g, g->d.slot_edge, slot_edge.data(), slot_edge.size()));
+      RC_TRY(h2d(g, g->d.slot_edge + k0, slot_edge.data() + k0, slot_edge.size() - k0));
       HIP_TRY(g, hipStreamSynchronize(g->d.stream));
     }
     g->slot_codes_plan = true;
     g->slot_codes_mixed = false;
+    g->bind_row0 = n;
     phase("slots");
   }
   return PGO_OK;

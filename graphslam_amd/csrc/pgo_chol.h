@@ -73,9 +73,11 @@ struct PanelStep {                 // one 64-column panel kb of every big front 
   int plain_lag = 0;               // apart plain tiles: joined before step +1 or (look-ahead skip) +2
   int xfirst = -1, xstep = -1;     // distributed top: exchanges after k_panel_first / k_step (index in xchg)
   // deferred far updates: the last far_cnt of the syrk tiles (an apart step at a
-  // kKB block end: the columns past the next block) go to their own launch on a
-  // fourth stream, joined before step far_join of the level (-1: its end)
-  int far_cnt = 0, far_join = -1;
+  // kKB block end: the columns past the next block) go to launches of their own
+  // on a fourth stream, one per piece (a kKB column block of every front, the
+  // update-matrix columns one piece: CholLevel::far_pieces [far_p0, +far_np)),
+  // each joined before the first step that touches it
+  int far_cnt = 0, far_p0 = 0, far_np = 0;
   double far_flops = 0;            // ... their share of plain_flops
   // k_step's flops by role (sdiag; col + prep updates; col solves): a step with
   // many diagonal tiles runs them as three launches instead (chol_factor)
@@ -111,11 +113,15 @@ struct CholLevel {
   SolveStep bwd_part{0, 0};        // partial products feeding the init tasks
   SolveStep bwdc{0, 0};            // the backward steps as one chained launch (k_bwd_chain)
   int xtail = -1;                  // distributed top: the fronts' tail columns to every rank at the level's end
-  double at_bytes = 0;             // algorithmic HBM bytes of the level's k_assemble_tile
+  mutable double at_bytes = -1;    // algorithmic HBM bytes of the level's k_assemble_tile (-1: not yet, level_at_bytes)
   double bwd_part_flops = 0;       // ... flops of its k_bwd_part
   // algorithmic HBM bytes of the level's k_vec_assemble, k_bwd_part,
   // k_bwd_init and k_bwd_chain (k_bwd_step: the same reads, split by step)
   double vec_bytes = 0, bwd_part_bytes = 0, bwd_init_bytes = 0, bwd_chain_bytes = 0;
+  // far pieces (PanelStep::far_*): (step, first tile relative to its syrk_off,
+  // tiles, join step or -1 = the level's end) and their flops
+  std::vector<int4> far_pieces;
+  std::vector<double> far_piece_flops;
 };
 
 enum { kOrderNd = 0, kOrderAmd = 1 };
@@ -220,7 +226,7 @@ struct CholPlan {
   hipStream_t side3 = nullptr;     // the second wavefront class of small fronts, beside side2
   hipStream_t side4 = nullptr;     // deferred far Schur updates (PanelStep::far_cnt)
   hipStream_t side5 = nullptr;     // a split step's column-block updates beside its diagonal tiles
-  hipEvent_t fev[4] = {nullptr, nullptr, nullptr, nullptr};   // their join events (ring)
+  hipEvent_t fev[8] = {};          // their join events (ring)
   hipEvent_t evs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int4 *d_bwd = nullptr, *d_bwd_part = nullptr, *d_bwdc = nullptr;
   int2* d_bwd_pref = nullptr;
@@ -260,6 +266,7 @@ void plan_parallel(int ntask, const std::function<void(int)>& fn);
 void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
 // host: (re)build the plan's H assembly lists for a pattern its fronts hold
 void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
+double level_at_bytes(const CholPlan& P, int L);
 // host: does the plan's factor structure hold every block of this pattern?
 bool chol_covers(const CholPlan& P, int n, const std::vector<int>& row_ptr, const std::vector<int>& slot_col);
 // ... every given block (old pose index pairs)?

@@ -743,6 +743,171 @@ __device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double*
   DIAG_CLK(28);
 }
 
+// Small front with 64 < m <= 128 rows and w <= W (16 or 32) pivot columns, by
+// two wavefronts: wave q holds rows [64 q, 64 q + 64) of the m x w panel in
+// registers (thread t: row t) -- half the registers of one wave holding two
+// rows per lane -- and the trailing update's 16-column blocks are dealt to the
+// two waves.  The pivot steps are front_wave_body's blocked form, with
+// workgroup barriers where its LDS hand-offs cross the waves; every element
+// sees the same fma's in the same order: bitwise front_wave_body's front.
+template <int W>
+__device__ __forceinline__ void front_wave2_body(const CholDev& c, int s, double* S) {
+  constexpr int LDP = W + 1;
+  const int m = c.m[s], w = c.w[s];
+  double* PR = S;                 // m x W row-major copy of L (after the factorisation)
+  double* cb = S + m * LDP;       // the diagonal block's rows and v (8 x 9)
+  double* invs = cb + 130;        // [W] 1 / L(k,k)
+  double* Fs = c.F + c.foff[s];
+  double* fv = c.fv + c.voff[s];
+  const int row = threadIdx.x, l = row & 63, wq = row >> 6;
+  const bool ra = row < m;
+  DIAG_CLK(23);
+  double pa[W];
+#pragma unroll
+  for (int k = 0; k < W; k++) pa[k] = (ra && k < w && k <= row) ? Fs[row + (size_t)k * m] : 0.0;
+  double va = ra ? fv[row] : 0.0;
+  bool bad = false;
+  DIAG_CLK(24);
+  double* db = cb;
+  double* lrb = PR;               // (W - 8) x 8: L rows of the columns right of the block
+#pragma unroll
+  for (int kb = 0; kb < W; kb += 8) {
+    if (kb < w) {                 // uniform
+      const int nb8 = min(8, w - kb);
+      if (row >= kb && row < kb + nb8) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) db[(row - kb) * 9 + q] = pa[kb + q];
+        db[(row - kb) * 9 + 8] = va;
+      }
+      __syncthreads();
+      double a[36], iv[8], y[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+#pragma unroll
+        for (int j = 0; j <= i; j++) a[P8(i, j)] = i < nb8 ? db[i * 9 + j] : (i == j ? 1.0 : 0.0);
+        y[i] = i < nb8 ? db[i * 9 + 8] : 0.0;
+      }
+      bad = chol8_lane(a, iv) || bad;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        y[q] *= iv[q];
+#pragma unroll
+        for (int i = q + 1; i < 8; i++) y[i] = fma(-a[P8(i, q)], y[q], y[i]);
+      }
+      if (row == 0)
+#pragma unroll
+        for (int q = 0; q < 8; q++) invs[kb + q] = iv[q];
+      const bool own = row >= kb && row < kb + nb8, below = row >= kb + nb8;
+      if (own) {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+          if (i == row - kb) {
+#pragma unroll
+            for (int q = 0; q <= i; q++) pa[kb + q] = a[P8(i, q)];
+            va = y[i];
+          }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+#pragma unroll
+        for (int t = 0; t < q; t++)
+          if (below) pa[kb + q] = fma(-pa[kb + t], a[P8(q, t)], pa[kb + q]);
+        if (below) pa[kb + q] *= iv[q];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; q++)
+        if (below) va = fma(-pa[kb + q], y[q], va);
+      const bool right = kb + 8 < W && kb + 8 < w;   // uniform
+      if (right && row >= kb + 8 && row < W)
+#pragma unroll
+        for (int q = 0; q < 8; q++) lrb[(row - kb - 8) * 8 + q] = row < w ? pa[kb + q] : 0.0;
+      __syncthreads();            // lrb written; every db read done before the next block's
+      if (right) {
+#pragma unroll
+        for (int j = kb + 8; j < W; j++) {
+          const double2* lj2 = reinterpret_cast<const double2*>(lrb + (j - kb - 8) * 8);
+#pragma unroll
+          for (int q2 = 0; q2 < 4; q2++) {
+            const double2 t2 = lj2[q2];
+            pa[j] = fma(row >= j ? -pa[kb + 2 * q2] : 0.0, t2.x, pa[j]);
+            pa[j] = fma(row >= j ? -pa[kb + 2 * q2 + 1] : 0.0, t2.y, pa[j]);
+          }
+        }
+      }
+      __syncthreads();            // lrb read before the next block rewrites it (or PR below)
+    }
+  }
+  if (bad && row == 0) *c.flag = 1;
+  DIAG_CLK(25);
+  // L back to the front (and the row-major LDS copy), y to the frontal vector
+#pragma unroll
+  for (int k = 0; k < W; k++) {
+    if (ra && k < w && k <= row) Fs[row + (size_t)k * m] = pa[k];
+    if (ra) PR[row * LDP + k] = k <= row ? pa[k] : 0.0;
+  }
+  if (ra) fv[row] = va;
+  __syncthreads();
+  DIAG_CLK(26);
+  {   // trailing update C[i][j] -= L[i,:] L[j,:]' as front_wave_body's, 16-column blocks dealt to the waves
+    const int u = m - w, nt = (u + 15) >> 4, li = l & 15, lk = l >> 4;
+    for (int tj = wq; tj < nt; tj += 2) {
+      const int j0 = w + 16 * tj;
+      const double* Aj = PR + min(j0 + li, m - 1) * LDP + lk;
+      double a[W / 4];
+#pragma unroll
+      for (int kc = 0; kc < W / 4; kc++) a[kc] = Aj[4 * kc];
+      double cv[8][4];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const int i = w + 16 * (tj + q) + li;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int j = j0 + lk + 4 * r;
+          cv[q][r] = (tj + q < nt && i < m && j <= i) ? Fs[i + (size_t)j * m] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        if (tj + q >= nt) break;   // uniform
+        const int i = w + 16 * (tj + q) + li;
+        const double* Bi = PR + min(i, m - 1) * LDP + lk;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kc = 0; kc < W / 4; kc++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kc], Bi[4 * kc], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int j = j0 + lk + 4 * r;
+          if (i < m && j <= i) Fs[i + (size_t)j * m] = cv[q][r] - acc[r];
+        }
+      }
+    }
+  }
+  DIAG_CLK(27);
+  // X = L11^-1 (w x w), thread = column (wave 0)
+  if (row < w) {
+    double x[W];
+#pragma unroll
+    for (int r = 0; r < W; r++) {
+      double acc = r == row ? 1.0 : 0.0;
+#pragma unroll
+      for (int t = 0; t < r; t++) acc = fma(-PR[min(r, m - 1) * LDP + t], x[t], acc);
+      x[r] = r < w ? acc * invs[r] : 0.0;
+    }
+    double* M = c.Tinv + c.toff[s];   // row-major, live w x w
+#pragma unroll
+    for (int r = 0; r < W; r++)
+      if (r < w) M[r * 64 + row] = r >= row ? x[r] : 0.0;
+  }
+  DIAG_CLK(28);
+}
+
+template <int W>
+__global__ __launch_bounds__(128) void k_front_wave2(CholDev c, const int* __restrict__ list) {
+  lane_offset(c);
+  extern __shared__ __attribute__((aligned(16))) double S[];
+  front_wave2_body<W>(c, list[blockIdx.x], S);
+}
+
 template <int W, bool kTwoRows>
 __global__ __launch_bounds__(64) void k_front_wave(CholDev c, const int* __restrict__ list) {
   lane_offset(c);
@@ -2613,6 +2778,42 @@ static void launch(LaunchProfile* prof, int fam, Cost cost, K kern, dim3 grid, d
   }
 }
 
+// Algorithmic HBM bytes of level L's k_assemble_tile (the profiles' family
+// table): children's elements read + tile elements written, 8 B each, plus the
+// H slots read.  Computed on first use (profiled runs only), cached in the level.
+double level_at_bytes(const CholPlan& P, int L) {
+  const CholLevel& lv = P.levels[L];
+  if (lv.at_bytes >= 0) return lv.at_bytes;
+  // sum_{t=A..B} clamp(t, 0, c) in closed form (G(x) = sum_{t=1..x} min(t, c))
+  auto G = [](long long x, long long c) -> long long {
+    if (x <= 0) return 0;
+    return x <= c ? x * (x + 1) / 2 : c * (c + 1) / 2 + (x - c) * c;
+  };
+  double bytes = 0;
+  for (int q = lv.ea_off[0]; q < lv.ea_off[0] + lv.ea_cnt[0]; q++) {
+    const int4 t = P.ea_tasks[q];
+    double e = 0, h = 0;   // children's elements read + tile elements written; H slots read
+    for (int k = 0; k < t.w; k++) {   // rows r < nr of a child rectangle: min(max(a0 + r - b0 + 1, 0), nc) columns
+      const int4 pr = P.ea_pairs[t.z + k];
+      const long long nr = pr.w & 0xff, ncl = pr.w >> 8, d = pr.y - pr.z + 1;
+      e += (double)(G(d + nr - 1, ncl) - G(d - 1, ncl));
+    }
+    const int2 it = P.at_iptr[q];
+    for (int k = 0; k < it.y; k++) {
+      const int code = P.at_items[it.x + k];
+      h += code >= 0 ? 72.0 * (P.asm_ptr[code + 1] - P.asm_ptr[code]) : 48.0;
+    }
+    const long long mp = P.m[t.x], R0 = 64 * (t.y >> 16), C0 = 64 * (t.y & 0xffff);
+    const long long R1 = std::min(R0 + 64, mp), C1 = std::min(C0 + 64, mp);
+    // tile elements: columns j in [C0, C1), rows [max(R0, j), R1)
+    const long long jd = std::min(std::max(R0, C0), C1);   // columns below jd see all R1 - R0 rows
+    e += (double)((jd - C0) * std::max(0LL, R1 - R0));
+    for (long long a = std::max(jd, C0); a < C1; a++) e += (double)std::max(0LL, R1 - a);
+    bytes += 8.0 * e + h;
+  }
+  return lv.at_bytes = bytes;
+}
+
 hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, const double* b, double scale_b,
                        hipStream_t s, LaunchProfile* prof, int nb, ExchangeHook* hook) {
   if (P.n == 0) return hipSuccess;
@@ -2682,7 +2883,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
     }
     static const bool asm_push = getenv("PGO_ASM_PUSH") && atoi(getenv("PGO_ASM_PUSH")) == 1;
     if (lv.ea_cnt[0] && !off("assemble"))
-      launch(prof, kFamAssemble, [&] { return make_double2(0, lv.at_bytes * nb); },
+      launch(prof, kFamAssemble, [&] { return make_double2(0, level_at_bytes(P, (int)li) * nb); },
              asm_push ? k_assemble_tile_push : k_assemble_tile, dim3(lv.ea_cnt[0], nb), B256, 0, s, c,
              (const int4*)(P.d_ea_tasks + lv.ea_off[0]), (const int2*)(P.d_at_iptr + lv.ea_off[0]),
              (const int*)P.d_at_items, (const int4*)P.d_ea_pairs, V, (long long)P.nslots, D,
@@ -2714,9 +2915,15 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
         const hipStream_t st = fork_wave && sc.mmax > 64 ? P.side3 : ss;
         const size_t lds = (size_t)(sc.mmax * (sc.wave + 1) + 130 + sc.wave) * sizeof(double);
         const dim3 g(sc.cnt, nb), b(64);
+        // (m > 64 with W 16 / 32: two waves per front, k_front_wave2; PGO_WAVE2=0:
+        // one wave holding two rows per lane -- bitwise the same fronts)
+        static const bool wave2 = !(getenv("PGO_WAVE2") && atoi(getenv("PGO_WAVE2")) == 0);
+        const dim3 b2(128);
         if (sc.mmax > 64) {
           if (sc.wave == 8) launch(prof, kFamFrontWave, small_cost, k_front_wave<8, true>, g, b, lds, st, c, list);
+          else if (sc.wave == 16 && wave2) launch(prof, kFamFrontWave, small_cost, k_front_wave2<16>, g, b2, lds, st, c, list);
           else if (sc.wave == 16) launch(prof, kFamFrontWave, small_cost, k_front_wave<16, true>, g, b, lds, st, c, list);
+          else if (wave2) launch(prof, kFamFrontWave, small_cost, k_front_wave2<kWaveW>, g, b2, lds, st, c, list);
           else launch(prof, kFamFrontWave, small_cost, k_front_wave<kWaveW, true>, g, b, lds, st, c, list);
         } else {
           if (sc.wave == 8) launch(prof, kFamFrontWave, small_cost, k_front_wave<8, false>, g, b, lds, st, c, list);
@@ -2824,16 +3031,20 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
         CH_TRY(hipEventRecord(P.evs[j & 1 ? 5 : 3], P.side));
         side_pending = true;
         on_side[j] = 1;
-        if (ps.far_cnt > 0) {   // the far columns: on P.side4 (behind the earlier far launches), joined late
-          int busy = -2;   // (a ring slot still pending: joined now)
-          for (const int2& fp : far_pending)
-            if (fp.y == fslot) busy = fp.x;
-          if (busy != -2) CH_TRY(join_far(busy));
+        if (ps.far_cnt > 0) {   // the far pieces: on P.side4 (behind the earlier far launches), each joined late
           CH_TRY(hipStreamWaitEvent(P.side4, P.evs[2], 0));
-          plain(P.side4, nnear, ps.far_cnt, ps.far_flops);
-          CH_TRY(hipEventRecord(P.fev[fslot], P.side4));
-          far_pending.push_back(make_int2(ps.far_join, fslot));
-          fslot = (fslot + 1) % 4;
+          for (int q = ps.far_p0; q < ps.far_p0 + ps.far_np; q++) {
+            const int4 fp = lv.far_pieces[q];
+            if (fp.z == 0) continue;
+            int busy = -2;   // (a ring slot still pending: joined now)
+            for (const int2& pend : far_pending)
+              if (pend.y == fslot) busy = pend.x;
+            if (busy != -2) CH_TRY(join_far(busy));
+            plain(P.side4, fp.y, fp.z, lv.far_piece_flops[q]);
+            CH_TRY(hipEventRecord(P.fev[fslot], P.side4));
+            far_pending.push_back(make_int2(fp.w, fslot));
+            fslot = (fslot + 1) % 8;
+          }
         }
       }
       // the panel this step factored, to every rank (the apart plain tiles

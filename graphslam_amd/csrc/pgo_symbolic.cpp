@@ -686,11 +686,13 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
     // deferred far updates (apart steps at a kKB block end): per step and big
     // front, the largest column its k_step tasks and near plain tiles touch
     // (touch), and the first column of its far plain tiles (far0, m = none)
-    std::vector<std::vector<int>> touch, far0;
+    // far0[step][piece][front]: the far pieces are the far range cut at the kKB
+    // blocks (the update-matrix columns past w one piece), each joined on its own
+    std::vector<std::vector<int>> touch;
+    std::vector<std::vector<std::vector<int>>> far0;
     for (int kb = 0; kb < maxw; kb += kNB) {
       touch.emplace_back(big.size(), 0);
-      far0.emplace_back(big.size(), 0);
-      for (size_t i = 0; i < big.size(); i++) far0.back()[i] = P.m[big[i]];
+      far0.emplace_back();
       PanelStep ps;
       ps.kb = kb;
       ps.syrk_flops = ps.plain_flops = ps.step_flops = ps.first_flops = 0;
@@ -776,8 +778,8 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       // ... the far part of an apart step's plain range (a kKB block end: the
       // columns past the next block, [be + kKB, m)): its own launch on a fourth
       // stream, joined only before the first later step that touches them
-      std::vector<int4> plain_far;
-      std::vector<int> far_front;   // big-front index of each plain_far range
+      std::vector<std::vector<int4>> plain_far;   // [piece]: the ranges of every front's piece g
+      std::vector<double> far_pflops;
       std::vector<int4> prep;    // prep tiles (front, r0, c0, k0), whole 64x64 tiles
       bool conflict = false;   // a front's next step reads this step's plain tiles
       for (size_t i = 0; i < big.size(); i++) {
@@ -859,13 +861,20 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
           for (int j = cstart; j < cend; j++) applied[i][j] = kn;
           const int depth = kn - k0, kw = inner ? (k0 | (int)0x80000000) : k0;
           for (int cc = cstart; cc < cend; cc++) ps.plain_flops += 2.0 * depth * (m - cc);
-          for (int cc = nend; cc < cend; cc++) ps.far_flops += 2.0 * depth * (m - cc);
           if (cstart < nend) plain.push_back(make_int4(s, cstart, nend, kw));
           touch.back()[i] = std::max(touch.back()[i], nend);
-          if (nend < cend) {
-            plain_far.push_back(make_int4(s, nend, cend, kw));
-            far_front.push_back((int)i);
-            far0.back()[i] = nend;
+          for (int c0 = nend, g = 0; c0 < cend; g++) {   // far pieces: a kKB block each, [w, m) one
+            const int c1 = c0 < w ? std::min(std::min(cend, w), (c0 / kKB + 1) * kKB) : cend;
+            if ((int)plain_far.size() <= g) {
+              plain_far.emplace_back();
+              far_pflops.push_back(0.0);
+              far0.back().emplace_back(big.size(), 0);
+              for (size_t i2 = 0; i2 < big.size(); i2++) far0.back()[g][i2] = P.m[big[i2]];
+            }
+            plain_far[g].push_back(make_int4(s, c0, c1, kw));
+            far0.back()[g][i] = c0;
+            for (int cc = c0; cc < c1; cc++) far_pflops[g] += 2.0 * depth * (m - cc);
+            c0 = c1;
           }
         }
       }
@@ -875,8 +884,10 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       S.col_tasks.insert(S.col_tasks.end(), prep.begin(), prep.end());
       ps.prep_cnt = (int)prep.size();
       long long cnt128 = 0;
-      for (const std::vector<int4>* pl : {&plain, &plain_far})
-        for (const int4& u : *pl)
+      for (const int4& u : plain)
+        for (int c0 = u.y; c0 < u.z; c0 += kBigTile) cnt128 += (P.m[u.x] - c0 + kBigTile - 1) / kBigTile;
+      for (const auto& pl : plain_far)
+        for (const int4& u : pl)
           for (int c0 = u.y; c0 < u.z; c0 += kBigTile) cnt128 += (P.m[u.x] - c0 + kBigTile - 1) / kBigTile;
       // (distributed top: 64-wide tiles, split where the column owner changes;
       // a tile's elements are computed alike in either kernel, so this is
@@ -916,24 +927,39 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       };
       gen_tiles(plain);
       const int near_end = (int)S.syrk_tasks.size();
-      gen_tiles(plain_far);
+      std::vector<int> piece_end;
+      for (const auto& pl : plain_far) {
+        gen_tiles(pl);
+        piece_end.push_back((int)S.syrk_tasks.size());
+      }
       ps.syrk_cnt = (int)S.syrk_tasks.size() - ps.syrk_off;
       ps.syrk_inline = !apart && ps.syrk_tile == kTile && ps.syrk_cnt <= kInlineTiles;
       ps.far_cnt = ps.syrk_inline ? 0 : (int)S.syrk_tasks.size() - near_end;
-      if (ps.far_cnt == 0) {   // (inline, or nothing far: the far ranges' columns are this step's)
-        for (size_t q = 0; q < plain_far.size(); q++) {
-          touch.back()[far_front[q]] = std::max(touch.back()[far_front[q]], plain_far[q].z);
-          far0.back()[far_front[q]] = P.m[big[far_front[q]]];
-        }
-        ps.far_flops = 0;
-      }
       auto xcd = [&](int b, int e) {   // XCD-aware order of a launch's Schur-update tiles
         std::vector<int4> mine(S.syrk_tasks.begin() + b, S.syrk_tasks.begin() + e);
         xcd_order(mine, ps.syrk_tile);
         std::copy(mine.begin(), mine.end(), S.syrk_tasks.begin() + b);
       };
-      xcd(ps.syrk_off, ps.syrk_off + ps.syrk_cnt - ps.far_cnt);
-      xcd(ps.syrk_off + ps.syrk_cnt - ps.far_cnt, ps.syrk_off + ps.syrk_cnt);
+      if (ps.far_cnt == 0) {   // (inline, or nothing far: the far ranges' columns are this step's)
+        for (const auto& pl : plain_far)
+          for (const int4& u : pl)
+            for (size_t i = 0; i < big.size(); i++)
+              if (big[i] == u.x) touch.back()[i] = std::max(touch.back()[i], u.z);
+        far0.back().clear();
+        xcd(ps.syrk_off, ps.syrk_off + ps.syrk_cnt);
+      } else {
+        xcd(ps.syrk_off, near_end);
+        ps.far_p0 = (int)lv.far_pieces.size();
+        int b = near_end;
+        for (size_t g = 0; g < plain_far.size(); g++) {   // (piece: first tile relative to syrk_off, count)
+          xcd(b, piece_end[g]);
+          lv.far_pieces.push_back(make_int4((int)lv.panels.size(), b - ps.syrk_off, piece_end[g] - b, -1));
+          lv.far_piece_flops.push_back(far_pflops[g]);   // (a piece may hold no tile of this rank)
+          ps.far_flops += far_pflops[g];
+          b = piece_end[g];
+        }
+        ps.far_np = (int)lv.far_pieces.size() - ps.far_p0;
+      }
       // an apart launch no front's next step reads is joined before the step after next
       ps.plain_lag = ps.syrk_cnt > 0 && !ps.syrk_inline ? (conflict ? 1 : 2) : 0;
       // (an inline plain after a lag-2 apart one could touch its tiles at once)
@@ -942,16 +968,17 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       ps.xstep = add_exchange(S, xstep);
       lv.panels.push_back(ps);
     }
-    // a far launch is joined before the first later step whose k_step tasks or
+    // a far piece is joined before the first later step whose k_step tasks or
     // near plain tiles touch one of its columns (-1: at the level's end)
-    for (size_t j = 0; j < lv.panels.size(); j++) {
-      PanelStep& ps = lv.panels[j];
-      ps.far_join = -1;
-      if (ps.far_cnt == 0) continue;
-      for (size_t j2 = j + 1; j2 < lv.panels.size() && ps.far_join < 0; j2++)
+    for (size_t q = 0; q < lv.far_pieces.size(); q++) {
+      int4& fp = lv.far_pieces[q];
+      const int j = fp.x, g = (int)q - lv.panels[j].far_p0;
+      const std::vector<int>& f0 = far0[j][g];
+      fp.w = -1;
+      for (size_t j2 = j + 1; j2 < lv.panels.size() && fp.w < 0; j2++)
         for (size_t i = 0; i < big.size(); i++)
-          if (touch[j2][i] > far0[j][i]) {
-            ps.far_join = (int)j2;
+          if (touch[j2][i] > f0[i]) {
+            fp.w = (int)j2;
             break;
           }
     }
@@ -976,7 +1003,16 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
     }
   };
   std::vector<LevelLists> out(nl);
-  plan_parallel(nl, [&](int L) { schedule_level(L, out[L]); });
+  std::vector<double> lms(nl, 0.0);
+  plan_parallel(nl, [&](int L) {
+    const auto t0 = std::chrono::steady_clock::now();
+    schedule_level(L, out[L]);
+    lms[L] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  });
+  if (timing) {
+    for (int L = 0; L < nl; L++) fprintf(stderr, "  level %d: %.2f ms (%zu fronts)\n", L, lms[L], bylevel[L].size());
+    phase("levels");
+  }
   P.small_list.clear();
   P.level_fronts.clear();
   P.syrk_tasks.clear();
@@ -1309,57 +1345,37 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
     tl = t;
   };
   P.nslots = (long long)slot_col.size();
-  // entries (j, i, k) of the permuted lower triangle (new indices i > j, slot
-  // k), ordered by (j, i, k): a counting sort by j (rows in chunks, one count
-  // array per chunk: slot order within a bucket), then each bucket -- a
-  // column's few blocks -- by (i, k)
-  std::vector<std::vector<int>> ccnt(nth);
-  parallel_chunks(n, nth, [&](int t, int r0, int r1) {
-    ccnt[t].assign(n + 1, 0);
+  // entries (j, i, k) of the permuted lower triangle (new indices i > j), by
+  // (j, i, k).  Column j's entries are read from row perm[j]: its slots whose
+  // column comes later, i.e. the mirror slot of each block (i, j).  Both slots
+  // of a factor carry its device index, the only thing bind_plan keeps of k,
+  // and a row's slots to one column are in the factors' device order whichever
+  // end the row is: the same sources in the same order as from row perm[i].
+  // Each column's few entries then sorted by (i, k) and its targets (distinct
+  // (j, i)) counted per chunk of columns, then written.
+  std::vector<int> jcnt(n + 1, 0);
+  parallel_chunks(n, nth, [&](int, int r0, int r1) {   // (rows in their order: streamed)
     for (int r = r0; r < r1; r++) {
-      const int i = P.iperm[r];
-      for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) {
-        const int j = P.iperm[slot_col[k]];
-        if (i > j) ccnt[t][j]++;
-      }
+      const int j = P.iperm[r];
+      int c = 0;
+      for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) c += P.iperm[slot_col[k]] > j;
+      jcnt[j + 1] = c;
     }
   });
+  for (int j = 0; j < n; j++) jcnt[j + 1] += jcnt[j];
   lap("count");
-  std::vector<int> jcnt(n + 1, 0);
-  {   // bucket j: chunk 0's entries, then chunk 1's, ...; ccnt[t][j] := chunk t's first position
-    parallel_chunks(n, nth, [&](int, int j0, int j1) {
-      for (int j = j0; j < j1; j++) {
-        int c = 0;
-        for (int t = 0; t < nth; t++) c += ccnt[t][j];
-        jcnt[j + 1] = c;
-      }
-    });
-    for (int j = 0; j < n; j++) jcnt[j + 1] += jcnt[j];
-    parallel_chunks(n, nth, [&](int, int j0, int j1) {
-      for (int j = j0; j < j1; j++) {
-        int pos = jcnt[j];
-        for (int t = 0; t < nth; t++) {
-          const int c = ccnt[t][j];
-          ccnt[t][j] = pos;
-          pos += c;
-        }
-      }
-    });
-  }
   std::vector<int2> eik(jcnt[n]);   // (i, k) per entry, bucketed by j
-  parallel_chunks(n, nth, [&](int t, int r0, int r1) {
-    std::vector<int>& fill = ccnt[t];
+  parallel_chunks(n, nth, [&](int, int r0, int r1) {
     for (int r = r0; r < r1; r++) {
-      const int i = P.iperm[r];
+      const int j = P.iperm[r];
+      int q = jcnt[j];
       for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) {
-        const int j = P.iperm[slot_col[k]];
-        if (i > j) eik[fill[j]++] = make_int2(i, k);
+        const int i = P.iperm[slot_col[k]];
+        if (i > j) eik[q++] = make_int2(i, k);
       }
     }
   });
   lap("bucket");
-  ccnt.clear();
-  // targets: one per distinct (j, i) -- per column chunk counted, then written
   std::vector<int> tstart(nth + 1, 0);
   parallel_chunks(n, nth, [&](int t, int j0, int j1) {
     int cnt = 0;
@@ -1477,47 +1493,8 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
     }
   });
   lap("tile ptrs");
-  const auto ta = std::chrono::steady_clock::now();
-  // sum_{t=A..B} clamp(t, 0, c) in closed form (G(x) = sum_{t=1..x} min(t, c))
-  auto G = [](long long x, long long c) -> long long {
-    if (x <= 0) return 0;
-    return x <= c ? x * (x + 1) / 2 : c * (c + 1) / 2 + (x - c) * c;
-  };
-  parallel_chunks((int)P.levels.size(), nth, [&](int, int l0, int l1) {
-  for (int L = l0; L < l1; L++) {   // algorithmic bytes of the levels' k_assemble_tile (profiles)
-    CholLevel& lv = P.levels[L];
-    lv.at_bytes = 0;
-    for (int q = lv.ea_off[0]; q < lv.ea_off[0] + lv.ea_cnt[0]; q++) {
-      const int4 t = P.ea_tasks[q];
-      double e = 0, h = 0;   // children's elements read + tile elements written; H slots read
-      for (int k = 0; k < t.w; k++) {   // rows r < nr of a child rectangle: min(max(a0 + r - b0 + 1, 0), nc) columns
-        const int4 pr = P.ea_pairs[t.z + k];
-        const long long nr = pr.w & 0xff, ncl = pr.w >> 8, d = pr.y - pr.z + 1;
-        e += (double)(G(d + nr - 1, ncl) - G(d - 1, ncl));
-      }
-      const int2 it = P.at_iptr[q];
-      for (int k = 0; k < it.y; k++) {
-        const int code = P.at_items[it.x + k];
-        h += code >= 0 ? 72.0 * (P.asm_ptr[code + 1] - P.asm_ptr[code]) : 48.0;
-      }
-      const long long mp = P.m[t.x], R0 = 64 * (t.y >> 16), C0 = 64 * (t.y & 0xffff);
-      const long long R1 = std::min(R0 + 64, mp), C1 = std::min(C0 + 64, mp);
-      // tile elements: columns j in [C0, C1), rows [max(R0, j), R1)
-      const long long jd = std::min(std::max(R0, C0), C1);   // columns below jd see all R1 - R0 rows
-      e += (double)((jd - C0) * std::max(0LL, R1 - R0));
-      for (long long a = std::max(jd, C0); a < C1; a++) e += (double)std::max(0LL, R1 - a);
-      lv.at_bytes += 8.0 * e + h;
-    }
-  }
-  });
-  if (timing) {
-    double tot = 0;
-    for (const CholLevel& lv : P.levels) tot += lv.at_bytes;
-    fprintf(stderr, "chol_assembly at_bytes total %.0f\n", tot);
-  }
-  if (timing)
-    fprintf(stderr, "chol_assembly at_bytes %8.2f ms\n",
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count());
+  // (the levels' k_assemble_tile bytes: on first use, level_at_bytes)
+  for (CholLevel& lv : P.levels) lv.at_bytes = -1.0;
 }
 
 // Does the plan's factor structure hold every block of the pattern (old pose

@@ -71,7 +71,9 @@ int main(int argc, char** argv) {
     int nfused = 0, ntr = 0, nsy = 0, npotrf = 0, nfar = 0;
     std::string joins;
     for (const auto& ps : lv.panels) {
-      if (ps.far_cnt) joins += " " + std::to_string(&ps - lv.panels.data()) + "->" + std::to_string(ps.far_join);
+      for (int q = ps.far_p0; q < ps.far_p0 + ps.far_np; q++)
+        joins += " " + std::to_string(&ps - lv.panels.data()) + "->" + std::to_string(lv.far_pieces[q].w) + "(" +
+                 std::to_string(lv.far_pieces[q].z) + ")";
       nfar += ps.far_cnt;
       nfused += ps.syrk_inline;
       ntr += ps.fcol_cnt + ps.col_cnt;

@@ -76,7 +76,11 @@ int main(int argc, char** argv) {
     hipEventRecord(a, st);
     const int WC = W <= 8 ? 8 : W <= 16 ? 16 : kWaveW;   // the plan's panel-width classes
     const size_t lds = (size_t)(M * (WC + 1) + 130 + WC) * 8;
-    if (M > 64) {
+    static const bool wave2 = getenv("UB_WAVE2") != nullptr;   // the two-wave kernel (m > 64, W 16 / 32)
+    if (M > 64 && WC >= 16 && wave2) {
+      if (WC == 16) k_front_wave2<16><<<N, 128, lds, st>>>(c, dl);
+      else k_front_wave2<kWaveW><<<N, 128, lds, st>>>(c, dl);
+    } else if (M > 64) {
       if (WC == 8) k_front_wave<8, true><<<N, 64, lds, st>>>(c, dl);
       else if (WC == 16) k_front_wave<16, true><<<N, 64, lds, st>>>(c, dl);
       else k_front_wave<kWaveW, true><<<N, 64, lds, st>>>(c, dl);
