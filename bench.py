@@ -427,16 +427,19 @@ def log(msg):
 
 def _partition_bounds(live):
     """{config: {P: {bound, bound_replicated_top, est_speedup, exchange_points,
-    exchange_bytes}}}: profiles/r03_partition_bounds.json (host-computed for C3
-    and C5), plus this run's own rank count when it was computed live."""
-    path = os.path.join(ROOT, "profiles", "r03_partition_bounds.json")
-    keep = ("bound", "bound_replicated_top", "est_speedup", "exchange_points", "exchange_bytes")
+    exchange_bytes, the model's per-mode estimates}}}:
+    profiles/r04_partition_bounds.json (host-computed for C3 and C5,
+    scripts/partition_bounds.py), plus this run's own rank count when it was
+    computed live."""
+    path = os.path.join(ROOT, "profiles", "r04_partition_bounds.json")
+    keep = ("bound", "bound_replicated_top", "est_speedup", "exchange_points", "exchange_bytes",
+            "est_speedup_distributed_top", "est_speedup_replicated_top", "est_speedup_spec")
     out = {}
     if os.path.exists(path):
         for c, per in json.load(open(path)).items():
             out[c] = {P: {k: v[k] for k in keep} for P, v in per.items()}
     if live:
-        out["this_run"] = {P: {k: v[k] for k in keep} for P, v in live.items()}
+        out["this_run"] = {P: {k: v[k] for k in keep if k in v} for P, v in live.items()}
     return out
 
 

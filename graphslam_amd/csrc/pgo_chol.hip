@@ -516,6 +516,9 @@ __global__ __launch_bounds__(256) void k_front_small(CholDev c, const int* __res
 // W: the compile-time panel width (8, 16 or kWaveW >= w): the pivot loop, the
 // per-pivot column updates and the trailing update's inner products run over W,
 // so narrow fronts (most leaves) do a quarter of the wide ones' work.
+#ifndef PGO_WAVE_PERPIVOT_W
+#define PGO_WAVE_PERPIVOT_W 16   // widest class factored one pivot at a time (scripts/ubench_wave.hip A/B)
+#endif
 template <int W, bool kTwoRows>   // m > 64: lane also owns row l + 64
 __device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double* S) {
   constexpr int LDP = W + 1;   // odd row stride: conflict-free per-lane rows
@@ -537,9 +540,12 @@ __device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double*
   double va = ra ? fv[l] : 0.0, vb = rb ? fv[lb] : 0.0;
   bool bad = false;
   DIAG_CLK(24);
-  if constexpr (W == 8) {
-    // (the narrowest class, most leaves: one pivot at a time, its 8 pivots
-    // cost little next to the blocked form's registers)
+  if constexpr (W <= PGO_WAVE_PERPIVOT_W) {
+    // (the narrow classes, most leaves: one pivot at a time.  The blocked form
+    // below needs ~210 VGPRs at W = 16 -- 2 waves per SIMD instead of 4 -- and
+    // measured 33-38 % slower on 4096 fronts of m = 64, w = 12 / 16, 9 % on
+    // m = 90, w = 12; it pays at W = 32: m = 100, w = 24 9 % faster;
+    // profiles/r04c_front_wave_ubench_blocked.txt)
     // pivot k: column k of the panel is lane j's pa[k] (rows j < W <= 64), read
     // with v_readlane (no LDS round trip on the pivot chain)
   #pragma unroll
@@ -2915,13 +2921,17 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
         const hipStream_t st = fork_wave && sc.mmax > 64 ? P.side3 : ss;
         const size_t lds = (size_t)(sc.mmax * (sc.wave + 1) + 130 + sc.wave) * sizeof(double);
         const dim3 g(sc.cnt, nb), b(64);
-        // (m > 64 with W 16 / 32: two waves per front, k_front_wave2; PGO_WAVE2=0:
-        // one wave holding two rows per lane -- bitwise the same fronts)
-        static const bool wave2 = !(getenv("PGO_WAVE2") && atoi(getenv("PGO_WAVE2")) == 0);
+        // (m > 64 with W = 32: two waves per front, k_front_wave2, 15-24 % faster
+        // per 4096 fronts (profiles/r04e_front_wave_ubench.txt); PGO_WAVE2=0: one
+        // wave holding two rows per lane -- bitwise the same fronts.  W = 16
+        // stays one wave of per-pivot steps: 102 us against 124 for the two-wave
+        // blocked form on m = 90, w = 12; PGO_WAVE2=2 forces the two waves there)
+        static const int wave2_mode = getenv("PGO_WAVE2") ? atoi(getenv("PGO_WAVE2")) : 1;
+        const bool wave2 = wave2_mode != 0;
         const dim3 b2(128);
         if (sc.mmax > 64) {
           if (sc.wave == 8) launch(prof, kFamFrontWave, small_cost, k_front_wave<8, true>, g, b, lds, st, c, list);
-          else if (sc.wave == 16 && wave2) launch(prof, kFamFrontWave, small_cost, k_front_wave2<16>, g, b2, lds, st, c, list);
+          else if (sc.wave == 16 && wave2_mode == 2) launch(prof, kFamFrontWave, small_cost, k_front_wave2<16>, g, b2, lds, st, c, list);
           else if (sc.wave == 16) launch(prof, kFamFrontWave, small_cost, k_front_wave<16, true>, g, b, lds, st, c, list);
           else if (wave2) launch(prof, kFamFrontWave, small_cost, k_front_wave2<kWaveW>, g, b2, lds, st, c, list);
           else launch(prof, kFamFrontWave, small_cost, k_front_wave<kWaveW, true>, g, b, lds, st, c, list);
