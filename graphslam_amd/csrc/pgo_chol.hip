@@ -1455,6 +1455,7 @@ __global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int4* __res
 // per chunk, issued one chunk ahead of the MFMAs).  Low register count, so
 // several workgroups per CU hide the load latency.
 // smem: 4 * 16 * 68 doubles (Sr[2], Sc[2])
+template <bool kPrefC = false>   // true: the C tile's loads issued before the k loop (latency under the MFMAs)
 __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, int kb, double* smem) {
   constexpr int LD = 64 + 4;
   double(*Sr)[16 * LD] = reinterpret_cast<double(*)[16 * LD]>(smem);
@@ -1504,6 +1505,21 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
   double acc[8][2];
 #pragma unroll
   for (int p = 0; p < 8; p++) acc[p][0] = acc[p][1] = 0.0;
+  // C read-modify-write: lane l holds (row row0 + qi + 16h + (l & 15), column col0 + qj + 4p + (l >> 4));
+  // the tile's columns lie in col0's column block (the planner never lets a tile straddle two)
+  double* Cb = fcol(Fs, m, true, col0);
+  const int ldc = m - (col0 & ~63);
+  double cold[8][2];
+  auto load_c = [&] {
+#pragma unroll
+    for (int p = 0; p < 8; p++)
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int row = row0 + qi + 16 * h + (l & 15), col = col0 + qj + 4 * p + lk;
+        cold[p][h] = (active && row < m && col < colend && row >= col) ? Cb[row + (size_t)(col - col0) * ldc] : 0.0;
+      }
+  };
+  if (kPrefC) load_c();
   load(0);
   stash(0);
   __syncthreads();
@@ -1530,18 +1546,7 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
     __syncthreads();
   }
   if (!active) return;
-  // C read-modify-write: lane l holds (row row0 + qi + 16h + (l & 15), column col0 + qj + 4p + (l >> 4));
-  // the tile's columns lie in col0's column block (the planner never lets a tile straddle two)
-  double* Cb = fcol(Fs, m, true, col0);
-  const int ldc = m - (col0 & ~63);
-  double cold[8][2];
-#pragma unroll
-  for (int p = 0; p < 8; p++)
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int row = row0 + qi + 16 * h + (l & 15), col = col0 + qj + 4 * p + lk;
-      cold[p][h] = (row < m && col < colend && row >= col) ? Cb[row + (size_t)(col - col0) * ldc] : 0.0;
-    }
+  if (!kPrefC) load_c();
 #pragma unroll
   for (int p = 0; p < 8; p++)
 #pragma unroll
@@ -1555,6 +1560,12 @@ __global__ __launch_bounds__(256) void k_panel_syrk_lds(CholDev c, const int4* _
   lane_offset(c);
   __shared__ __attribute__((aligned(16))) double smem[4 * 16 * 68];
   syrk_lds_body(c, tasks[blockIdx.x], kb, smem);
+}
+// (the C-prefetch form, for the microbenchmark A/B: scripts/ubench_syrk.hip)
+__global__ __launch_bounds__(256) void k_panel_syrk_lds_pc(CholDev c, const int4* __restrict__ tasks, int kb) {
+  lane_offset(c);
+  __shared__ __attribute__((aligned(16))) double smem[4 * 16 * 68];
+  syrk_lds_body<true>(c, tasks[blockIdx.x], kb, smem);
 }
 
 // Schur update of a diagonal 64x64 tile into LDS: Ts (ld 65, lower) = C - P P^T,

@@ -130,8 +130,8 @@ int main(int argc, char** argv) {
   // outer update after panel kb = 192 (block 0 = columns 0..255): trailing [256, M), k0 = 0
   const int kb = 192, be = 256;
   const double flops = 256.0 * (M - be) * (M - be + 1.0);
-  for (int T : {64, 65, 128}) {   // 65: the LDS-staged 64x64 kernel
-    const int TT = T == 65 ? 64 : T;
+  for (int T : {64, 65, 66, 128}) {   // 65: the LDS-staged 64x64 kernel; 66: the same with the C tile prefetched
+    const int TT = (T == 65 || T == 66) ? 64 : T;
     std::vector<int4> tasks;
     for (int c0 = be; c0 < M; c0 += TT)
       for (int r0 = c0; r0 < M; r0 += TT) tasks.push_back(make_int4(0, r0, c0, 0));
@@ -149,6 +149,7 @@ int main(int argc, char** argv) {
       hipEventRecord(a, st);
       if (T == 64) k_panel_syrk<<<(int)tasks.size(), 256, 0, st>>>(c, dt, kb);
       else if (T == 65) k_panel_syrk_lds<<<(int)tasks.size(), 256, 0, st>>>(c, dt, kb);
+      else if (T == 66) k_panel_syrk_lds_pc<<<(int)tasks.size(), 256, 0, st>>>(c, dt, kb);
       else k_panel_syrk128<<<(int)tasks.size(), 256, 0, st>>>(c, dt, kb);
       hipEventRecord(b, st);
       hipEventSynchronize(b);
