@@ -137,6 +137,7 @@ __device__ long long g_diag_clk[32];
 // rectangles), and every element's loads are in flight together.
 constexpr int kAsmPairs = 16;
 constexpr int kAsmNone = (int)0x80000000;
+template <int kUnroll>
 __global__ __launch_bounds__(256, 4) void k_assemble_tile(CholDev c, const int4* __restrict__ tasks,
                                                        const int2* __restrict__ iptr, const int* __restrict__ items,
                                                        const int4* __restrict__ pairs, const double* __restrict__ V,
@@ -245,21 +246,28 @@ __global__ __launch_bounds__(256, 4) void k_assemble_tile(CholDev c, const int4*
           val[u] = (row < mp && col < mp && row >= col) ? Fp[row + (size_t)j * ldp] : 0.0;
         }
       }
-      for (int kk = 0; kk < np; kk++) {   // the children's elements, in child order
-        const int a = rmap[kk][i];
-        if (a < 0) continue;
-        const double* __restrict__ Fch = c.F + pbase[kk] + a;
-        double add[8];
-        bool in[8];
+      // the children's elements, in child order; kUnroll children's loads in
+      // flight together (the adds stay in child order: the same sums)
+      for (int k1 = 0; k1 < np; k1 += kUnroll) {
+        double add[kUnroll][8];
+        bool in[kUnroll][8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const int b = cmap[kk][cg + 4 * (8 * g + u)];
-          in[u] = b >= 0 && b <= a;
-          add[u] = in[u] ? Fch[coff[kk][cg + 4 * (8 * g + u)]] : 0.0;
+        for (int x = 0; x < kUnroll; x++) {
+          const int kk = k1 + x;
+          const int a = kk < np ? rmap[kk][i] : -1;
+          const double* __restrict__ Fch = c.F + (kk < np ? pbase[kk] : 0) + a;
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const int b = a >= 0 ? cmap[kk][cg + 4 * (8 * g + u)] : -1;
+            in[x][u] = b >= 0 && b <= a;
+            add[x][u] = in[x][u] ? Fch[coff[kk][cg + 4 * (8 * g + u)]] : 0.0;
+          }
         }
 #pragma unroll
-        for (int u = 0; u < 8; u++)
-          if (in[u]) val[u] += add[u];
+        for (int x = 0; x < kUnroll; x++)
+#pragma unroll
+          for (int u = 0; u < 8; u++)
+            if (in[x][u]) val[u] += add[x][u];
       }
 #pragma unroll
       for (int u = 0; u < 8; u++) {
@@ -2899,9 +2907,12 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       CH_TRY(hipEventRecord(P.evs[1], P.side2));
     }
     static const bool asm_push = getenv("PGO_ASM_PUSH") && atoi(getenv("PGO_ASM_PUSH")) == 1;
+    // (PGO_ASM_UNROLL: children whose loads are in flight together, 1 or 2)
+    static const int asm_unroll = getenv("PGO_ASM_UNROLL") ? atoi(getenv("PGO_ASM_UNROLL")) : 1;
     if (lv.ea_cnt[0] && !off("assemble"))
       launch(prof, kFamAssemble, [&] { return make_double2(0, level_at_bytes(P, (int)li) * nb); },
-             asm_push ? k_assemble_tile_push : k_assemble_tile, dim3(lv.ea_cnt[0], nb), B256, 0, s, c,
+             asm_push ? k_assemble_tile_push : asm_unroll == 2 ? k_assemble_tile<2> : k_assemble_tile<1>,
+             dim3(lv.ea_cnt[0], nb), B256, 0, s, c,
              (const int4*)(P.d_ea_tasks + lv.ea_off[0]), (const int2*)(P.d_at_iptr + lv.ea_off[0]),
              (const int*)P.d_at_items, (const int4*)P.d_ea_pairs, V, (long long)P.nslots, D,
              (const double*)P.d_lambda);
