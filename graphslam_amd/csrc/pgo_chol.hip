@@ -2738,7 +2738,22 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
                    // the level ends back more than the panel chain gains -- so off)
     int least = 0, greatest = 0;
     const char* pr = getenv("PGO_SIDE_PRIORITY");
-    if (pr && pr[0] == '1' && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+    // PGO_SIDE_CUMASK=r (A/B): the plain Schur tiles' stream kept off r of every
+    // 32 CUs (PGO_SIDE_CUMASK_MODE=1: off CUs i with (i / 8) % 32 < r), so the
+    // panel chain's workgroups always find CUs free of them
+    const int cum = getenv("PGO_SIDE_CUMASK") ? atoi(getenv("PGO_SIDE_CUMASK")) : 0;
+    if (cum > 0) {
+      const int mode = getenv("PGO_SIDE_CUMASK_MODE") ? atoi(getenv("PGO_SIDE_CUMASK_MODE")) : 0;
+      int dev = 0, ncu = 0;
+      CH_TRY(hipGetDevice(&dev));
+      CH_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+      for (int i = 0; i < ncu; i++) {
+        const bool off_cu = mode == 1 ? (i / 8) % 32 < cum : i % 32 < cum;
+        if (!off_cu) mask[i / 32] |= 1u << (i % 32);
+      }
+      CH_TRY(hipExtStreamCreateWithCUMask(&P.side, (uint32_t)mask.size(), mask.data()));
+    } else if (pr && pr[0] == '1' && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
       CH_TRY(hipStreamCreateWithPriority(&P.side, hipStreamNonBlocking, least));
     else
       CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
