@@ -30,7 +30,9 @@ constexpr int kTile = 64;          // Schur-update output tile
 constexpr int kBigTile = 128;      // Schur-update output tile of the LDS-pipelined kernel
 constexpr int kKB = 256;         // Schur updates deferred per kKB-column block (inner steps update the block only)
 constexpr int kInlineTiles = 512;
-constexpr int kLookaheadM = 2048;  // fronts this tall skip the next step's column block in their plain tiles
+constexpr int kLookaheadM = 512;   // fronts this tall skip the next step's column block in their plain tiles
+                                   // (2048 until round 4: 512 measured 0.1 ms faster per replay at 1 and 3
+                                   // lanes, profiles/r04k_ab_lookahead_threshold.txt)
 constexpr int kMaxStampSlots = 256;  // PGO_STEP_STAMPS diagnostics // syrk tiles per step that ride inside k_step
 constexpr int kBwdRows = 512;      // rows per partial product of the backward solve
 // Schur-update tile tasks (front, row0 | clip << kClipShift, col0, k0): clip > 0

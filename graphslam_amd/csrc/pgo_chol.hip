@@ -757,17 +757,21 @@ __device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double*
   DIAG_CLK(28);
 }
 
-// Small front with 64 < m <= 128 rows and w <= W (16 or 32) pivot columns, by
-// two wavefronts: wave q holds rows [64 q, 64 q + 64) of the m x w panel in
+// Small front with 64 < m <= 64 NW rows and w <= W (16 or 32) pivot columns,
+// by NW wavefronts: wave q holds rows [64 q, 64 q + 64) of the m x w panel in
 // registers (thread t: row t) -- half the registers of one wave holding two
 // rows per lane -- and the trailing update's 16-column blocks are dealt to the
-// two waves.  The pivot steps are front_wave_body's blocked form, with
-// workgroup barriers where its LDS hand-offs cross the waves; every element
-// sees the same fma's in the same order: bitwise front_wave_body's front.
-template <int W>
+// waves.  The pivot steps are front_wave_body's blocked form, with workgroup
+// barriers where its LDS hand-offs cross the waves; every element sees the
+// same fma's in the same order: bitwise front_wave_body's front.  NW = 4
+// (round 4): 128 < m <= 256, fronts stored packed (pgo_chol.h front_packed:
+// the panel's columns lie in the first 64-column block, the trailing columns
+// are addressed by their block), which the blocked path took before.
+template <int W, int NW = 2>
 __device__ __forceinline__ void front_wave2_body(const CholDev& c, int s, double* S) {
   constexpr int LDP = W + 1;
   const int m = c.m[s], w = c.w[s];
+  const bool pk = front_packed(m, w);
   double* PR = S;                 // m x W row-major copy of L (after the factorisation)
   double* cb = S + m * LDP;       // the diagonal block's rows and v (8 x 9)
   double* invs = cb + 130;        // [W] 1 / L(k,k)
@@ -862,36 +866,42 @@ __device__ __forceinline__ void front_wave2_body(const CholDev& c, int s, double
   if (ra) fv[row] = va;
   __syncthreads();
   DIAG_CLK(26);
-  {   // trailing update C[i][j] -= L[i,:] L[j,:]' as front_wave_body's, 16-column blocks dealt to the waves
+  {   // trailing update C[i][j] -= L[i,:] L[j,:]' as front_wave_body's, 16-column blocks dealt to the
+      // waves, their row tiles 8 at a time
     const int u = m - w, nt = (u + 15) >> 4, li = l & 15, lk = l >> 4;
-    for (int tj = wq; tj < nt; tj += 2) {
+    for (int tj = wq; tj < nt; tj += NW) {
       const int j0 = w + 16 * tj;
       const double* Aj = PR + min(j0 + li, m - 1) * LDP + lk;
       double a[W / 4];
 #pragma unroll
       for (int kc = 0; kc < W / 4; kc++) a[kc] = Aj[4 * kc];
-      double cv[8][4];
+      double* colp[4];   // this lane's 4 columns (packed fronts: each in its own 64-column block)
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const int i = w + 16 * (tj + q) + li;
+      for (int r = 0; r < 4; r++) colp[r] = Fs + fcol_off(m, pk, min(j0 + lk + 4 * r, m - 1));
+      for (int qb = 0; tj + qb < nt; qb += 8) {
+        double cv[8][4];
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int j = j0 + lk + 4 * r;
-          cv[q][r] = (tj + q < nt && i < m && j <= i) ? Fs[i + (size_t)j * m] : 0.0;
+        for (int q = 0; q < 8; q++) {
+          const int i = w + 16 * (tj + qb + q) + li;
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int j = j0 + lk + 4 * r;
+            cv[q][r] = (tj + qb + q < nt && i < m && j <= i) ? colp[r][i] : 0.0;
+          }
         }
-      }
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
-        if (tj + q >= nt) break;   // uniform
-        const int i = w + 16 * (tj + q) + li;
-        const double* Bi = PR + min(i, m - 1) * LDP + lk;
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        for (int q = 0; q < 8; q++) {
+          if (tj + qb + q >= nt) break;   // uniform
+          const int i = w + 16 * (tj + qb + q) + li;
+          const double* Bi = PR + min(i, m - 1) * LDP + lk;
+          d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int kc = 0; kc < W / 4; kc++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kc], Bi[4 * kc], acc, 0, 0, 0);
+          for (int kc = 0; kc < W / 4; kc++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kc], Bi[4 * kc], acc, 0, 0, 0);
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int j = j0 + lk + 4 * r;
-          if (i < m && j <= i) Fs[i + (size_t)j * m] = cv[q][r] - acc[r];
+          for (int r = 0; r < 4; r++) {
+            const int j = j0 + lk + 4 * r;
+            if (i < m && j <= i) colp[r][i] = cv[q][r] - acc[r];
+          }
         }
       }
     }
@@ -919,7 +929,13 @@ template <int W>
 __global__ __launch_bounds__(128) void k_front_wave2(CholDev c, const int* __restrict__ list) {
   lane_offset(c);
   extern __shared__ __attribute__((aligned(16))) double S[];
-  front_wave2_body<W>(c, list[blockIdx.x], S);
+  front_wave2_body<W, 2>(c, list[blockIdx.x], S);
+}
+template <int W>
+__global__ __launch_bounds__(256) void k_front_wave4(CholDev c, const int* __restrict__ list) {
+  lane_offset(c);
+  extern __shared__ __attribute__((aligned(16))) double S[];
+  front_wave2_body<W, 4>(c, list[blockIdx.x], S);
 }
 
 template <int W, bool kTwoRows>
@@ -2740,7 +2756,9 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
     const char* pr = getenv("PGO_SIDE_PRIORITY");
     // PGO_SIDE_CUMASK=r (A/B): the plain Schur tiles' stream kept off r of every
     // 32 CUs (PGO_SIDE_CUMASK_MODE=1: off CUs i with (i / 8) % 32 < r), so the
-    // panel chain's workgroups always find CUs free of them
+    // panel chain's workgroups always find CUs free of them.  Measured on C3:
+    // 13.8 / 20.3 ms against 8.5 / 17.0 ms replays at 1 / 3 lanes
+    // (profiles/r04j_ab_queues_cumask_lookahead.txt), so off
     const int cum = getenv("PGO_SIDE_CUMASK") ? atoi(getenv("PGO_SIDE_CUMASK")) : 0;
     if (cum > 0) {
       const int mode = getenv("PGO_SIDE_CUMASK_MODE") ? atoi(getenv("PGO_SIDE_CUMASK_MODE")) : 0;
@@ -2769,6 +2787,10 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
       CH_TRY(hipStreamCreateWithFlags(&P.side4, hipStreamNonBlocking));
     for (auto& e : P.evs) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : P.fev) CH_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // the four-wave small fronts ask for up to 256 x 33 doubles of LDS (> 64 KiB;
+    // 160 KiB per CU on gfx950)
+    (void)hipFuncSetAttribute((const void*)k_front_wave4<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_front_wave4<kWaveW>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
   }
   return hipSuccess;   // (the fronts' zeroing runs on, stream-ordered before any use)
 }
@@ -2966,7 +2988,10 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
         static const int wave2_mode = getenv("PGO_WAVE2") ? atoi(getenv("PGO_WAVE2")) : 1;
         const bool wave2 = wave2_mode != 0;
         const dim3 b2(128);
-        if (sc.mmax > 64) {
+        if (sc.mmax > kSmallFront) {   // 128 < m <= 256: four waves (k_front_wave4), W 16 or 32
+          if (sc.wave == 16) launch(prof, kFamFrontWave, small_cost, k_front_wave4<16>, g, dim3(256), lds, st, c, list);
+          else launch(prof, kFamFrontWave, small_cost, k_front_wave4<kWaveW>, g, dim3(256), lds, st, c, list);
+        } else if (sc.mmax > 64) {
           if (sc.wave == 8) launch(prof, kFamFrontWave, small_cost, k_front_wave<8, true>, g, b, lds, st, c, list);
           else if (sc.wave == 16 && wave2_mode == 2) launch(prof, kFamFrontWave, small_cost, k_front_wave2<16>, g, b2, lds, st, c, list);
           else if (sc.wave == 16) launch(prof, kFamFrontWave, small_cost, k_front_wave<16, true>, g, b, lds, st, c, list);

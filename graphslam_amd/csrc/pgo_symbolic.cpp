@@ -160,7 +160,14 @@ static double front_flops(int m, int w) {
 }
 
 // blocked path (64-column panels) vs one workgroup / wavefront per front
-static bool is_blocked(const CholPlan& P, int s) { return front_packed(P.m[s], P.w[s]); }
+// Fronts of 128 < m <= 256 rows and w <= kWaveW pivots: one four-wave
+// workgroup each (k_front_wave4, round 4), not the blocked path, though stored
+// packed (PGO_WAVE4=0: the blocked path, as before)
+static bool wave4_front(int m, int w) {
+  static const bool on = !(getenv("PGO_WAVE4") && atoi(getenv("PGO_WAVE4")) == 0);
+  return on && m > kSmallFront && m <= 2 * kSmallFront && w <= kWaveW;
+}
+static bool is_blocked(const CholPlan& P, int s) { return front_packed(P.m[s], P.w[s]) && !wave4_front(P.m[s], P.w[s]); }
 
 // Column owners of the distributed top (see chol_analyze): per top front s
 // (owner[s] < 0) its m columns at cown[off[s] ..]: rank, or -1 (every rank).
@@ -629,11 +636,17 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
         while (P.m[s] > classes[q]) q++;
         bucket[q].push_back(s);
       }
-      for (int cls = 0; cls < 6; cls++) {   // m <= 64 (one row per lane) | m > 64  x  w <= 8 | 16 | 32
-        const int half = cls / 3, W = cls % 3 == 0 ? 8 : cls % 3 == 1 ? 16 : kWaveW, Wlo = cls % 3 == 0 ? 0 : W / 2;
+      // m <= 64 (one row per lane) | 64 < m <= 128 | 128 < m <= 256 (four waves)  x  w <= 8 | 16 | 32
+      // (the four-wave class has no W = 8 form: its w <= 8 fronts go with W = 16)
+      for (int cls = 0; cls < 9; cls++) {
+        const int rc = cls / 3, W = cls % 3 == 0 ? 8 : cls % 3 == 1 ? 16 : kWaveW;
+        const int Wlo = cls % 3 == 0 ? 0 : (rc == 2 && W == 16 ? 0 : W / 2);
+        if (rc == 2 && W == 8) continue;
         std::vector<int> part;
-        for (int s : wave)
-          if ((P.m[s] > 64) == (half == 1) && P.w[s] > Wlo && P.w[s] <= W) part.push_back(s);
+        for (int s : wave) {
+          const int mc = P.m[s] <= 64 ? 0 : P.m[s] <= kSmallFront ? 1 : 2;
+          if (mc == rc && P.w[s] > Wlo && P.w[s] <= W) part.push_back(s);
+        }
         if (part.empty()) continue;
         std::stable_sort(part.begin(), part.end(), [&](int a, int b) {
           const double wa = (double)P.m[a] * P.m[a] * P.w[a], wb = (double)P.m[b] * P.m[b] * P.w[b];
