@@ -48,6 +48,7 @@ struct CholDev {
   long long tfo;                   // Tinv + tfo: the inverses again, in the trsm's MFMA operand order
   int vst, xst, pst;               // fv, xv, backward partials per lane
   unsigned long long poll_ticks;   // in-launch hand-off: give up after this many 10 ns ticks
+  int diag_full;                   // PGO_DIAG_FULL=1 (A/B): diagonal tiles factored over all four 16-column blocks
 };
 
 // this workgroup's lane (blockIdx.y): every lane factors H + lambda_y I with
@@ -73,6 +74,8 @@ static CholDev dev_view(const CholPlan& P) {
   c.flag = P.d_flag;
   c.stepflag = P.d_stepflag;
   c.ns = P.ns;
+  static const int diag_full = getenv("PGO_DIAG_FULL") && atoi(getenv("PGO_DIAG_FULL")) == 1;
+  c.diag_full = diag_full;
   c.fst = P.ftotal;
   c.tst = 2 * P.ttotal;
   c.tfo = P.ttotal;
@@ -1086,12 +1089,17 @@ __device__ __forceinline__ bool diag16_lane(double* TJ, double* WJ, double* sc) 
 // trailing updates of step J, wave 0 takes only the next diagonal block's and
 // goes straight on to factor it while waves 1-3 finish the others (they touch
 // neither that block nor its W block).
+// nbl (round 4): the live size; the 16-column blocks past it (identity in T,
+// zeros in W) are skipped, which leaves them as they came in -- every live
+// element sees the same operations as with all four blocks, the callers read
+// only the live part of L and X.
 // Returns (wave 0) whether a pivot was not positive and finite.
-__device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double* bc) {
+__device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double* bc, int nbl = 64) {
   const int tid = threadIdx.x, wv = tid >> 6;
+  const int Jn = (nbl + 15) >> 4;   // live 16-column blocks (1..4)
   DIAG_CLK(0);
   bool bad = false;
-  for (int J = 0; J < 4; J++) {
+  for (int J = 0; J < Jn; J++) {
     const int o = 16 * J;
     double* TJ = T + o + o * 65;
     if (wv == 0) {
@@ -1104,19 +1112,19 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
     }
     __syncthreads();
     DIAG_CLK(1 + 3 * J);
-    // phase B: 3 independent products (3-J panel blocks, J blocks of X's row J)
-    if (wv < 3) {
-      if (wv < 3 - J) {
+    // phase B: Jn - 1 independent products (Jn-1-J panel blocks, J blocks of X's row J)
+    if (wv < Jn - 1) {
+      if (wv < Jn - 1 - J) {
         const int oi = o + 16 * (wv + 1);
         const d4 v = mm16(T + oi + o * 65, 1, 65, W + o + o * 65, 65, 1);
         st16(T + oi + o * 65, v, false);
       } else {
-        const int ok = 16 * (wv - (3 - J));
+        const int ok = 16 * (wv - (Jn - 1 - J));
         const d4 v = mm16(W + o + o * 65, 1, 65, W + o + ok * 65, 1, 65);
         st16(W + o + ok * 65, v, false);
       }
     }
-    if (J == 3) break;
+    if (J == Jn - 1) break;
     __syncthreads();
     DIAG_CLK(2 + 3 * J);
     // phase C on waves 1-3: trailing updates of T and W but the next diagonal
@@ -1124,7 +1132,7 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
     // J and write blocks outside it: all products' loads and MFMAs first, then
     // the read-modify-write stores, so their latencies overlap
     if (wv == 0) continue;
-    const int nA = (3 - J) * (4 - J) / 2, nW = (3 - J) * (J + 1);
+    const int nA = (Jn - 1 - J) * (Jn - J) / 2, nW = (Jn - 1 - J) * (J + 1);
     d4 acc[3];
     double* dst[3];
 #pragma unroll
@@ -1707,7 +1715,7 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
     Ws[i + j * 65] = 0.0;
   }
   __syncthreads();
-  if (diag_factor_invert(Ts, Ws, bc)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (diag_factor_invert(Ts, Ws, bc, c.diag_full ? 64 : nb)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   STAMP(slot, 2);
   double* Fs = fcol(c.F + c.foff[s], m, true, kn) + kn;   // the diagonal tile, ld m - kn
   double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;   // row-major L^-1 of the tile
@@ -1749,7 +1757,7 @@ __device__ __forceinline__ void first_diag_body(const CholDev& c, int s, double*
     Ws[i + j * 65] = 0.0;
   }
   __syncthreads();
-  if (diag_factor_invert(Ts, Ws, bc)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (diag_factor_invert(Ts, Ws, bc, c.diag_full ? 64 : nb)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   double* M = c.Tinv + c.toff[s];
   double* v = c.fv + c.voff[s];
   publish_inverse(M + c.tfo, Ws, nb);

@@ -161,10 +161,13 @@ static double front_flops(int m, int w) {
 
 // blocked path (64-column panels) vs one workgroup / wavefront per front
 // Fronts of 128 < m <= 256 rows and w <= kWaveW pivots: one four-wave
-// workgroup each (k_front_wave4, round 4), not the blocked path, though stored
-// packed (PGO_WAVE4=0: the blocked path, as before)
+// workgroup each (k_front_wave4) instead of the blocked path, though stored
+// packed -- opt-in, PGO_WAVE4=1: measured on C3 8.86 / 16.75 ms against 8.44 /
+// 16.92 ms replays at 1 / 3 lanes, 44.0 against 44.5 it/s
+// (profiles/r04m_ab_wave4.txt: one workgroup per front is a longer latency
+// than the blocked path's tiles spread over the chip)
 static bool wave4_front(int m, int w) {
-  static const bool on = !(getenv("PGO_WAVE4") && atoi(getenv("PGO_WAVE4")) == 0);
+  static const bool on = getenv("PGO_WAVE4") && atoi(getenv("PGO_WAVE4")) == 1;
   return on && m > kSmallFront && m <= 2 * kSmallFront && w <= kWaveW;
 }
 static bool is_blocked(const CholPlan& P, int s) { return front_packed(P.m[s], P.w[s]) && !wave4_front(P.m[s], P.w[s]); }
