@@ -1577,6 +1577,23 @@ bool chol_append(CholPlan& P, int n, const std::vector<int>& row_ptr, const std:
         s = P.parent[s];
       }
     }
+  // the growth limit on the plan after this append (the fronts on the fill
+  // paths gain 3 rows per new pose, the root its new poses), before anything
+  // of the plan is changed
+  {
+    auto pf = [](double m, double w) {   // size_fronts' flops of one front, closed form
+      // sum_{k<w} 1 + r + r (r + 1), r = m - 1 - k
+      const double s1 = w * (m - 1) - w * (w - 1) / 2;                       // sum r
+      auto sq = [](double a) { return a * (a + 1) * (2 * a + 1) / 6; };      // sum_{r=0..a} r^2
+      return w + 2 * s1 + (sq(m - 1) - sq(m - 1 - w));
+    };
+    double est = P.flops;
+    for (int s = 0; s < ns; s++)
+      if (added[s]) est += pf(P.m[s] + 3.0 * added[s], P.w[s]) - pf(P.m[s], P.w[s]);
+    const double wt = 3.0 * (n - P.sfirst[T]);
+    est += pf(wt, wt) - pf(P.m[T], P.w[T]);
+    if (est > max_growth * P.flops_analyzed) return false;
+  }
   // 2. row lists: old segment, then the new rows; the root front's own poses extended
   std::vector<int> rptr(ns + 1, 0);
   for (int s = 0; s < ns; s++) rptr[s + 1] = rptr[s] + (P.rptr[s + 1] - P.rptr[s]) + added[s] + (s == T ? n - n0 : 0);
