@@ -1016,7 +1016,9 @@ __device__ __forceinline__ bool diag16_lane(double* TJ, double* WJ, double* sc) 
     WJ[r + c * 65] = 0.0;
     WJ[(8 + r) + (8 + c) * 65] = 0.0;
   }
+  DIAG_CLK(13);
   bool bad = chol8_lane(a, iv);
+  DIAG_CLK(14);
   if (l == 0) {
 #pragma unroll
     for (int i = 0; i < 8; i++)
@@ -1024,6 +1026,7 @@ __device__ __forceinline__ bool diag16_lane(double* TJ, double* WJ, double* sc) 
       for (int j = 0; j <= i; j++) TJ[i + j * 65] = a[P8(i, j)];
   }
   inv8_lane(a, iv);
+  DIAG_CLK(15);
   if (l == 0) {
 #pragma unroll
     for (int i = 0; i < 8; i++)
@@ -1054,7 +1057,9 @@ __device__ __forceinline__ bool diag16_lane(double* TJ, double* WJ, double* sc) 
   for (int i = 0; i < 8; i++)
 #pragma unroll
     for (int j = 0; j <= i; j++) a[P8(i, j)] = TJ[(8 + i) + (8 + j) * 65];
+  DIAG_CLK(16);
   bad = chol8_lane(a, iv) || bad;
+  DIAG_CLK(17);
   if (l == 0) {
 #pragma unroll
     for (int i = 0; i < 8; i++)
@@ -1069,11 +1074,13 @@ __device__ __forceinline__ bool diag16_lane(double* TJ, double* WJ, double* sc) 
       for (int j = 0; j <= i; j++) WJ[(8 + i) + (8 + j) * 65] = a[P8(i, j)];
   }
   __builtin_amdgcn_wave_barrier();
+  DIAG_CLK(18);
   // X21 (r, c) = -sum_k X22 (r, k) Y (k, c)   (X22 upper is zero)
   double z = 0.0;
 #pragma unroll
   for (int k = 0; k < 8; k++) z = fma(WJ[(8 + r) + (8 + k) * 65], sc[k * 8 + c], z);
   WJ[(8 + r) + c * 65] = -z;
+  DIAG_CLK(19);
   return bad;
 }
 

@@ -72,6 +72,8 @@ int main() {
     printf("J%d A(+C) %lld  B %lld\n", J, clk[1 + 3 * J] - prev, b - clk[1 + 3 * J]);
     prev = b;
   }
+  printf("diag16_lane (last J), cycles: chol8 %lld, inv8 %lld, L21/A22/Y %lld, chol8 %lld, inv8 %lld, X21 %lld\n",
+         clk[14] - clk[13], clk[15] - clk[14], clk[16] - clk[15], clk[17] - clk[16], clk[18] - clk[17], clk[19] - clk[18]);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
