@@ -1029,64 +1029,104 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
     for (int L = 0; L < nl; L++) fprintf(stderr, "  level %d: %.2f ms (%zu fronts)\n", L, lms[L], bylevel[L].size());
     phase("levels");
   }
-  P.small_list.clear();
-  P.level_fronts.clear();
-  P.syrk_tasks.clear();
-  P.sdiag_tasks.clear();
-  P.potrf_list.clear();
-  P.col_tasks.clear();
-  P.bwd_tasks.clear();
-  P.bwdc_tasks.clear();
-  P.bwd_pref.clear();
-  P.bwd_part_tasks.clear();
-  P.npart = 0;
-  P.ea_tasks.clear();
-  P.ea_pairs.clear();
-  P.syrk_flops = 0;
-  for (int L = 0; L < nl; L++) {   // merge: level-relative offsets and indices made absolute
+  // merge: level-relative offsets and indices made absolute; the level lists
+  // copied into place level by level on the pool (offsets from a serial pass)
+  struct Base {
+    size_t small_list, level_fronts, potrf_list, syrk_tasks, sdiag_tasks, col_tasks, bwd_tasks, bwdc_tasks, bwd_pref,
+        bwd_part_tasks, ea_tasks, ea_pairs, xchg, xp_tasks, xp_loff, xp_lstride;
+    int npart;
+  };
+  std::vector<Base> base(nl + 1);
+  {
+    Base z{};
+    for (int L = 0; L < nl; L++) {
+      const LevelLists& S = out[L];
+      base[L] = z;
+      z.small_list += S.small_list.size();
+      z.level_fronts += S.level_fronts.size();
+      z.potrf_list += S.potrf_list.size();
+      z.syrk_tasks += S.syrk_tasks.size();
+      z.sdiag_tasks += S.sdiag_tasks.size();
+      z.col_tasks += S.col_tasks.size();
+      z.bwd_tasks += S.bwd_tasks.size();
+      z.bwdc_tasks += S.bwdc_tasks.size();
+      z.bwd_pref += S.bwd_pref.size();
+      z.bwd_part_tasks += S.bwd_part_tasks.size();
+      z.ea_tasks += S.ea_tasks.size();
+      z.ea_pairs += S.ea_pairs.size();
+      z.xchg += S.xchg.size();
+      z.xp_tasks += S.xp_tasks.size();
+      z.xp_loff += S.xp_loff.size();
+      z.xp_lstride += S.xp_lstride.size();
+      z.npart += S.npart;
+    }
+    base[nl] = z;
+  }
+  const Base& tot = base[nl];
+  P.small_list.resize(tot.small_list);
+  P.level_fronts.resize(tot.level_fronts);
+  P.potrf_list.resize(tot.potrf_list);
+  P.syrk_tasks.resize(tot.syrk_tasks);
+  P.sdiag_tasks.resize(tot.sdiag_tasks);
+  P.col_tasks.resize(tot.col_tasks);
+  P.bwd_tasks.resize(tot.bwd_tasks);
+  P.bwdc_tasks.resize(tot.bwdc_tasks);
+  P.bwd_pref.resize(tot.bwd_pref);
+  P.bwd_part_tasks.resize(tot.bwd_part_tasks);
+  P.ea_tasks.resize(tot.ea_tasks);
+  P.ea_pairs.resize(tot.ea_pairs);
+  P.xchg.resize(tot.xchg);
+  P.xp_tasks.resize(tot.xp_tasks);
+  P.xp_loff.resize(tot.xp_loff);
+  P.xp_lstride.resize(tot.xp_lstride);
+  P.npart = tot.npart;
+  plan_parallel(nl, [&](int L) {
     LevelLists& S = out[L];
     CholLevel& lv = P.levels[L];
-    const int bx = (int)P.xchg.size(), npart0 = P.npart;
-    lv.front_off += (int)P.level_fronts.size();
-    lv.bwd_part.off += (int)P.bwd_part_tasks.size();
+    const Base& b = base[L];
+    const int bx = (int)b.xchg, npart0 = b.npart;
+    lv.front_off += (int)b.level_fronts;
+    lv.bwd_part.off += (int)b.bwd_part_tasks;
     for (int4& t : S.bwd_part_tasks) t.w += npart0;
     for (int q = lv.bwd[0].off; q < lv.bwd[0].off + lv.bwd[0].cnt; q++) S.bwd_pref[q].x += npart0;   // init tasks
-    for (SolveStep& st : lv.bwd) st.off += (int)P.bwd_tasks.size();
-    lv.bwdc.off += (int)P.bwdc_tasks.size();
-    for (int& o : lv.ea_off) o += (int)P.ea_tasks.size();
-    for (int4& t : S.ea_tasks) t.z += (int)P.ea_pairs.size();
-    for (SmallClass& sc : lv.small) sc.off += (int)P.small_list.size();
+    for (SolveStep& st : lv.bwd) st.off += (int)b.bwd_tasks;
+    lv.bwdc.off += (int)b.bwdc_tasks;
+    for (int& o : lv.ea_off) o += (int)b.ea_tasks;
+    for (int4& t : S.ea_tasks) t.z += (int)b.ea_pairs;
+    for (SmallClass& sc : lv.small) sc.off += (int)b.small_list;
     for (PanelStep& ps : lv.panels) {
-      ps.potrf_off += (int)P.potrf_list.size();
-      ps.col_off += (int)P.col_tasks.size();
-      ps.syrk_off += (int)P.syrk_tasks.size();
-      ps.sdiag_off += (int)P.sdiag_tasks.size();
+      ps.potrf_off += (int)b.potrf_list;
+      ps.col_off += (int)b.col_tasks;
+      ps.syrk_off += (int)b.syrk_tasks;
+      ps.sdiag_off += (int)b.sdiag_tasks;
       if (ps.xfirst >= 0) ps.xfirst += bx;
       if (ps.xstep >= 0) ps.xstep += bx;
-      P.syrk_flops += ps.plain_flops;
     }
     if (lv.xtail >= 0) lv.xtail += bx;
-    for (XExchange& x : S.xchg) x.off += (int)P.xp_tasks.size();
-    auto cat = [](auto& dst, const auto& src) { dst.insert(dst.end(), src.begin(), src.end()); };
-    cat(P.small_list, S.small_list);
-    cat(P.level_fronts, S.level_fronts);
-    cat(P.potrf_list, S.potrf_list);
-    cat(P.syrk_tasks, S.syrk_tasks);
-    cat(P.sdiag_tasks, S.sdiag_tasks);
-    cat(P.col_tasks, S.col_tasks);
-    cat(P.bwd_tasks, S.bwd_tasks);
-    cat(P.bwdc_tasks, S.bwdc_tasks);
-    cat(P.bwd_pref, S.bwd_pref);
-    cat(P.bwd_part_tasks, S.bwd_part_tasks);
-    cat(P.ea_tasks, S.ea_tasks);
-    cat(P.ea_pairs, S.ea_pairs);
-    cat(P.xchg, S.xchg);
-    cat(P.xp_tasks, S.xp_tasks);
-    cat(P.xp_loff, S.xp_loff);
-    cat(P.xp_lstride, S.xp_lstride);
-    P.xp_rslot = std::max(P.xp_rslot, S.xp_rslot);
-    P.npart += S.npart;
-    P.schedule_error = P.schedule_error || S.schedule_error;
+    for (XExchange& x : S.xchg) x.off += (int)b.xp_tasks;
+    auto put = [](auto& dst, size_t at, const auto& src) { std::copy(src.begin(), src.end(), dst.begin() + at); };
+    put(P.small_list, b.small_list, S.small_list);
+    put(P.level_fronts, b.level_fronts, S.level_fronts);
+    put(P.potrf_list, b.potrf_list, S.potrf_list);
+    put(P.syrk_tasks, b.syrk_tasks, S.syrk_tasks);
+    put(P.sdiag_tasks, b.sdiag_tasks, S.sdiag_tasks);
+    put(P.col_tasks, b.col_tasks, S.col_tasks);
+    put(P.bwd_tasks, b.bwd_tasks, S.bwd_tasks);
+    put(P.bwdc_tasks, b.bwdc_tasks, S.bwdc_tasks);
+    put(P.bwd_pref, b.bwd_pref, S.bwd_pref);
+    put(P.bwd_part_tasks, b.bwd_part_tasks, S.bwd_part_tasks);
+    put(P.ea_tasks, b.ea_tasks, S.ea_tasks);
+    put(P.ea_pairs, b.ea_pairs, S.ea_pairs);
+    put(P.xchg, b.xchg, S.xchg);
+    put(P.xp_tasks, b.xp_tasks, S.xp_tasks);
+    put(P.xp_loff, b.xp_loff, S.xp_loff);
+    put(P.xp_lstride, b.xp_lstride, S.xp_lstride);
+  });
+  P.syrk_flops = 0;
+  for (int L = 0; L < nl; L++) {
+    for (const PanelStep& ps : P.levels[L].panels) P.syrk_flops += ps.plain_flops;
+    P.xp_rslot = std::max(P.xp_rslot, out[L].xp_rslot);
+    P.schedule_error = P.schedule_error || out[L].schedule_error;
   }
   phase("schedule");
   chol_assembly(P, row_ptr, slot_col);
@@ -1381,7 +1421,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
   for (int j = 0; j < n; j++) jcnt[j + 1] += jcnt[j];
   lap("count");
   std::vector<int2> eik(jcnt[n]);   // (i, k) per entry, bucketed by j
-  parallel_chunks(n, nth, [&](int, int r0, int r1) {
+  parallel_chunks(n, 8 * nth, [&](int, int r0, int r1) {
     for (int r = r0; r < r1; r++) {
       const int j = P.iperm[r];
       int q = jcnt[j];
@@ -1392,8 +1432,10 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
     }
   });
   lap("bucket");
-  std::vector<int> tstart(nth + 1, 0);
-  parallel_chunks(n, nth, [&](int t, int j0, int j1) {
+  // (column chunks: 8 per thread, dealt dynamically -- the columns' work varies)
+  const int nck = std::max(1, std::min(n, 8 * nth));
+  std::vector<int> tstart(nck + 1, 0);
+  parallel_chunks(n, nck, [&](int t, int j0, int j1) {
     int cnt = 0;
     for (int j = j0; j < j1; j++) {
       std::sort(eik.begin() + jcnt[j], eik.begin() + jcnt[j + 1],
@@ -1403,14 +1445,14 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
     tstart[t + 1] = cnt;
   });
   lap("sort");
-  for (int t = 0; t < nth; t++) tstart[t + 1] += tstart[t];
-  const int ntg = tstart[nth];
+  for (int t = 0; t < nck; t++) tstart[t + 1] += tstart[t];
+  const int ntg = tstart[nck];
   P.asm_front.resize(ntg);
   P.asm_li.resize(ntg);
   P.asm_lj.resize(ntg);
   P.asm_ptr.resize(ntg + 1);
   P.asm_src.resize(eik.size());
-  parallel_chunks(n, nth, [&](int t, int j0, int j1) {
+  parallel_chunks(n, nck, [&](int t, int j0, int j1) {
     int g = tstart[t];
     for (int j = j0; j < j1; j++) {
       const int s = P.dg_front[j], f = P.sfirst[s], l = P.sfirst[s + 1];
@@ -1445,9 +1487,13 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
   // the order they are added (off-diagonal targets, then diagonal blocks).
   // Per front (its targets are contiguous: columns sorted), tiles in key order
   // ti (ti + 1) / 2 + tj -- the order of the front's tile tasks in ea_tasks.
-  std::vector<int> fg(ns + 1, 0);   // targets of front s: [fg[s], fg[s + 1])
-  for (int g = 0; g < ntg; g++) fg[P.asm_front[g] + 1]++;
-  for (int s = 0; s < ns; s++) fg[s + 1] += fg[s];
+  // targets of front s: [fg[s], fg[s + 1]) -- asm_front is nondecreasing (targets
+  // by column, a front's columns contiguous and in front order): binary searches
+  std::vector<int> fg(ns + 1, 0);
+  parallel_chunks(ns + 1, nth, [&](int, int s0, int s1) {
+    for (int s = s0; s < s1; s++)
+      fg[s] = (int)(std::lower_bound(P.asm_front.begin(), P.asm_front.begin() + ntg, s) - P.asm_front.begin());
+  });
   auto for_item = [](int r0, int c0, auto&& fn) {
     for (int ti = r0 / 64; ti <= (r0 + 2) / 64; ti++)
       for (int tj = c0 / 64; tj <= (c0 + 2) / 64; tj++)
@@ -1461,7 +1507,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
     kbase[s + 1] = kbase[s] + nt * (nt + 1) / 2 + 1;
   }
   std::vector<int> fcnt(kbase[ns], 0);
-  parallel_chunks(ns, nth, [&](int, int s0, int s1) {
+  parallel_chunks(ns, 8 * nth, [&](int, int s0, int s1) {
     for (int s = s0; s < s1; s++) {
       int* c = fcnt.data() + kbase[s];
       const long long nk = kbase[s + 1] - kbase[s];
@@ -1486,7 +1532,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
     }
     P.at_items.resize(pos);
   }
-  parallel_chunks(ns, nth, [&](int, int s0, int s1) {
+  parallel_chunks(ns, 8 * nth, [&](int, int s0, int s1) {
     std::vector<int> fill;   // (reused across the chunk's fronts)
     for (int s = s0; s < s1; s++) {
       if (fbase[s] < 0) continue;
