@@ -227,6 +227,16 @@ int check_append(const Pattern& G, int n0, int ordering) {
   P.ordering = ordering;
   const Pattern B = restrict_pattern(G, n0);
   pgo::chol_analyze(P, n0, B.row_ptr, B.col);
+  {   // the growth limit applies to the plan after the append: no headroom refuses the first one
+    pgo::CholPlan Q;
+    Q.ordering = ordering;
+    pgo::chol_analyze(Q, n0, B.row_ptr, B.col);
+    const Pattern G1 = restrict_pattern(G, n0 + 1);
+    std::vector<int2> pairs;
+    for (int k = G1.row_ptr[n0]; k < G1.row_ptr[n0 + 1]; k++) pairs.push_back(make_int2(n0, G1.col[k]));
+    if (pgo::chol_append(Q, n0 + 1, G1.row_ptr, G1.col, pairs, 1 << 30, 1.0)) return fail("append: growth limit not applied");
+    if (Q.n != n0) return fail("append: a refused append changed the plan");
+  }
   for (int n = n0 + 1; n <= G.n; n++) {
     const Pattern Gn = restrict_pattern(G, n);
     std::vector<int2> pairs;

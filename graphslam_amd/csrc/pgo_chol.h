@@ -228,6 +228,8 @@ struct CholPlan {
   hipStream_t side3 = nullptr;     // the second wavefront class of small fronts, beside side2
   hipStream_t side4 = nullptr;     // deferred far Schur updates (PanelStep::far_cnt)
   hipStream_t side5 = nullptr;     // a split step's column-block updates beside its diagonal tiles
+  hipStream_t side6 = nullptr;     // the m > 64 small-front classes narrower than kWaveW (PGO_WAVE_STREAMS)
+  hipEvent_t ev6 = nullptr;        // ... joined at the level's end
   hipEvent_t fev[8] = {};          // their join events (ring)
   hipEvent_t evs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int4 *d_bwd = nullptr, *d_bwd_part = nullptr, *d_bwdc = nullptr;

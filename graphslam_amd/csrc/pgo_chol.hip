@@ -2793,6 +2793,8 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
     CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
     CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));
     CH_TRY(hipStreamCreateWithFlags(&P.side5, hipStreamNonBlocking));
+    CH_TRY(hipStreamCreateWithFlags(&P.side6, hipStreamNonBlocking));
+    CH_TRY(hipEventCreateWithFlags(&P.ev6, hipEventDisableTiming));
     // the deferred far updates fill the CUs the panel chain leaves idle: their
     // stream at the lowest dispatch priority (PGO_FAR_PRIORITY=0: default)
     const char* fp = getenv("PGO_FAR_PRIORITY");
@@ -2823,6 +2825,8 @@ void chol_free(CholPlan& P) {
   if (P.side3) (void)hipStreamDestroy(P.side3);
   if (P.side4) (void)hipStreamDestroy(P.side4);
   if (P.side5) (void)hipStreamDestroy(P.side5);
+  if (P.side6) (void)hipStreamDestroy(P.side6);
+  if (P.ev6) (void)hipEventDestroy(P.ev6);
   P = CholPlan();
 }
 
@@ -2978,11 +2982,16 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
     for (const SmallClass& sc : lv.small)
       if (sc.wave) (sc.mmax > 64 ? hi : lo) = true;
     const bool fork_wave = lo && hi;
+    // PGO_WAVE_STREAMS=1 (A/B): the m > 64 classes narrower than kWaveW (few
+    // fronts, latency-bound) on a fourth side stream instead of ahead of the
+    // kWaveW class on the third
+    static const bool wave_streams = getenv("PGO_WAVE_STREAMS") && atoi(getenv("PGO_WAVE_STREAMS")) == 1;
     hipStream_t ss = s;
     if (fork_small || fork_wave) {
       CH_TRY(hipEventRecord(P.evs[0], s));
       CH_TRY(hipStreamWaitEvent(P.side2, P.evs[0], 0));
       if (fork_wave) CH_TRY(hipStreamWaitEvent(P.side3, P.evs[0], 0));
+      if (fork_wave && wave_streams) CH_TRY(hipStreamWaitEvent(P.side6, P.evs[0], 0));
       ss = P.side2;
     }
     for (const SmallClass& sc : lv.small) {
@@ -2992,7 +3001,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       if (sc.wave) {
         // classes by (m <= 64 | m > 64) x panel width W in {8, 16, 32}; the
         // m > 64 ones on the third stream
-        const hipStream_t st = fork_wave && sc.mmax > 64 ? P.side3 : ss;
+        const hipStream_t st = fork_wave && sc.mmax > 64 ? (wave_streams && sc.wave < kWaveW ? P.side6 : P.side3) : ss;
         const size_t lds = (size_t)(sc.mmax * (sc.wave + 1) + 130 + sc.wave) * sizeof(double);
         const dim3 g(sc.cnt, nb), b(64);
         // (m > 64 with W = 32: two waves per front, k_front_wave2, 15-24 % faster
@@ -3149,6 +3158,10 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       if (fork_wave) {
         CH_TRY(hipEventRecord(P.evs[4], P.side3));
         CH_TRY(hipStreamWaitEvent(s, P.evs[4], 0));
+        if (wave_streams) {
+          CH_TRY(hipEventRecord(P.ev6, P.side6));
+          CH_TRY(hipStreamWaitEvent(s, P.ev6, 0));
+        }
       }
     }
     CH_TRY(xpanels(lv.xtail));
