@@ -166,7 +166,9 @@ int check_assembly(const pgo::CholPlan& P) {
 // of the permuted lower triangle (i > j) lists exactly the slots of one end of
 // the block -- as many as row perm[i] holds to column perm[j] -- and every
 // slot of the lower triangle is listed once.
-int check_sources(const pgo::CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& col) {
+// (sources: ~slot unbound; bound ones -- bind emulated by emulate_bind, ids
+// a * idn + b of the pose pair a < b -- checked against the block's poses)
+int check_sources(const pgo::CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& col, int idn = 0) {
   long long total = 0, want = 0;
   for (size_t g = 0; g < P.asm_front.size(); g++) {
     const int s = P.asm_front[g], j = P.sfirst[s] + P.asm_lj[g], i = P.rows[P.rptr[s] + P.asm_li[g]];
@@ -176,7 +178,11 @@ int check_sources(const pgo::CholPlan& P, const std::vector<int>& row_ptr, const
     for (int k = row_ptr[a]; k < row_ptr[a + 1]; k++) cnt += col[k] == b;
     if (P.asm_ptr[g + 1] - P.asm_ptr[g] != cnt) return fail("assembly: a target's source count");
     for (int q = P.asm_ptr[g]; q < P.asm_ptr[g + 1]; q++) {
-      const int k = P.asm_src[q];
+      if (P.asm_src[q] >= 0) {   // bound: the pair id
+        if (!idn || P.asm_src[q] != std::min(a, b) * idn + std::max(a, b)) return fail("assembly: a bound source off its block");
+        continue;
+      }
+      const int k = ~P.asm_src[q];
       const int r = (int)(std::upper_bound(row_ptr.begin(), row_ptr.end(), k) - row_ptr.begin()) - 1;
       if (!((r == a && col[k] == b) || (r == b && col[k] == a))) return fail("assembly: a source off its block");
     }
@@ -217,6 +223,36 @@ Pattern restrict_pattern(const Pattern& G, int n) {
   return R;
 }
 
+// The host's bind (pgo_api.cpp bind_plan) emulated: every unbound source ~k
+// becomes the id a * idn + b of its slot's pose pair (a < b) -- a factor index
+// in the library; equal for both slots of a pair, as the factor index is.
+void emulate_bind(pgo::CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& col, int idn) {
+  for (int& x : P.asm_src)
+    if (x < 0) {
+      const int k = ~x;
+      const int r = (int)(std::upper_bound(row_ptr.begin(), row_ptr.end(), k) - row_ptr.begin()) - 1;
+      x = std::min(r, col[k]) * idn + std::max(r, col[k]);
+    }
+  P.asm_bound = true;
+}
+
+// The spliced assembly targets of an append equal a rebuild of the same plan,
+// once both are bound.
+int check_splice(const pgo::CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& col, int idn) {
+  pgo::CholPlan R = P;
+  R.asm_splice = false;
+  pgo::chol_assembly(R, row_ptr, col);
+  emulate_bind(R, row_ptr, col, idn);
+  pgo::CholPlan Q = P;
+  emulate_bind(Q, row_ptr, col, idn);
+  if (Q.asm_front != R.asm_front || Q.asm_li != R.asm_li || Q.asm_lj != R.asm_lj || Q.asm_ptr != R.asm_ptr ||
+      Q.asm_src != R.asm_src || Q.at_items != R.at_items || Q.at_iptr.size() != R.at_iptr.size())
+    return fail("append: spliced assembly lists differ from a rebuild");
+  for (size_t q = 0; q < Q.at_iptr.size(); q++)
+    if (Q.at_iptr[q].x != R.at_iptr[q].x || Q.at_iptr[q].y != R.at_iptr[q].y) return fail("append: spliced tile items");
+  return 0;
+}
+
 // The incremental symbolic update (chol_append): poses appended one at a time
 // to a plan of the first n0 poses.  After each: the schedule is consistent,
 // every front's below rows sit in its parent at the extend-add map's index, the
@@ -227,6 +263,7 @@ int check_append(const Pattern& G, int n0, int ordering) {
   P.ordering = ordering;
   const Pattern B = restrict_pattern(G, n0);
   pgo::chol_analyze(P, n0, B.row_ptr, B.col);
+  emulate_bind(P, B.row_ptr, B.col, G.n);
   {   // the growth limit applies to the plan after the append: no headroom refuses the first one
     pgo::CholPlan Q;
     Q.ordering = ordering;
@@ -243,7 +280,8 @@ int check_append(const Pattern& G, int n0, int ordering) {
     for (int k = Gn.row_ptr[n - 1]; k < Gn.row_ptr[n]; k++) pairs.push_back(make_int2(n - 1, Gn.col[k]));
     if (!pgo::chol_append(P, n, Gn.row_ptr, Gn.col, pairs, 1 << 30, 1e30)) return fail("append: refused");
     if (P.schedule_error) return fail("append: panel schedule bookkeeping");
-    if (check_assembly(P) || check_sources(P, Gn.row_ptr, Gn.col)) return 1;
+    if (check_assembly(P) || check_sources(P, Gn.row_ptr, Gn.col, G.n) || check_splice(P, Gn.row_ptr, Gn.col, G.n)) return 1;
+    emulate_bind(P, Gn.row_ptr, Gn.col, G.n);   // (the next append splices)
     if (P.n != n || !pgo::chol_covers(P, n, Gn.row_ptr, Gn.col)) return fail("append: pattern not covered");
     for (int s = 0; s < P.ns; s++) {
       const int wp = P.sfirst[s + 1] - P.sfirst[s], nr = P.rptr[s + 1] - P.rptr[s];

@@ -1198,8 +1198,10 @@ int bind_plan(pgo_graph* g, bool full) {
     });
     std::vector<int>& src = g->chol.asm_src;
     host_parallel((int)src.size(), [&](int q0, int q1) {
-      for (int q = q0; q < q1; q++) src[q] = slot_edge[src[q]] >> 2;
+      for (int q = q0; q < q1; q++)   // (~slot: not yet bound; kept ones are factor indices already)
+        if (src[q] < 0) src[q] = slot_edge[~src[q]] >> 2;
     });
+    g->chol.asm_bound = true;
     phase("owners");
     const hipError_t e = full ? pgo::chol_upload(g->chol, g->d.stream) : pgo::chol_upload_assembly(g->chol, g->d.stream);
     if (e != hipSuccess) {

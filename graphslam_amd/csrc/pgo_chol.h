@@ -154,8 +154,15 @@ struct CholPlan {
   std::vector<int> cptr, children; // children of each supernode, increasing order
   std::vector<int> ea_rel;         // per supernode: local pose index in the parent of each below row
   std::vector<int> ea_ptr;         // [ns+1] into ea_rel
-  // assembly of H: target blocks (front, local row pose, local col pose) and their slots
+  // assembly of H: target blocks (front, local row pose, local col pose) and their
+  // sources: ~slot as chol_assembly writes them, the factor's device index once
+  // the host binds the plan (asm_bound: every source bound)
   std::vector<int> asm_front, asm_li, asm_lj, asm_ptr, asm_src;
+  bool asm_bound = false;
+  // chol_append -> chol_assembly: the columns whose entries the append changed
+  // (the rest of the bound lists are spliced, not rebuilt); asm_splice false: rebuild
+  std::vector<int> asm_dirty;
+  bool asm_splice = false;
   std::vector<int> dg_front, dg_loc;   // per new pose: front and local index (diagonal block)
   // schedules
   std::vector<CholLevel> levels;

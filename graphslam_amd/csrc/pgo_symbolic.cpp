@@ -1383,6 +1383,124 @@ void chol_analyze(CholPlan& P, int n, const std::vector<int>& row_ptr, const std
   chol_schedule(P, row_ptr, slot_col);
 }
 
+// The targets after an append (chol_append): the columns in P.asm_dirty (the
+// append's factors' columns and the new poses') get their entry lists rebuilt
+// from the pattern, as chol_assembly builds every column; the other columns'
+// targets and bound sources are kept (an append adds rows at the end of its
+// fronts' row lists, so their local indices stand) and moved past the rebuilt
+// ones.  Same lists as a rebuild once bound (host_selftest: check_append).
+static void assembly_splice(CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& slot_col) {
+  std::vector<int>& dc = P.asm_dirty;
+  std::sort(dc.begin(), dc.end());
+  dc.erase(std::unique(dc.begin(), dc.end()), dc.end());
+  const int ntg0 = (int)P.asm_front.size(), ne0 = P.asm_ptr[ntg0];
+  auto colof = [&](int g) { return P.sfirst[P.asm_front[g]] + P.asm_lj[g]; };
+  // old target range of each dirty column (targets are by column)
+  std::vector<int> glo(dc.size()), ghi(dc.size());
+  for (size_t d = 0; d < dc.size(); d++) {
+    int lo = 0, hi = ntg0;
+    while (lo < hi) {   // first g with colof(g) >= dc[d]
+      const int mid = (lo + hi) / 2;
+      if (colof(mid) < dc[d]) lo = mid + 1; else hi = mid;
+    }
+    glo[d] = lo;
+    int g = lo;
+    while (g < ntg0 && colof(g) == dc[d]) g++;
+    ghi[d] = g;
+  }
+  // the dirty columns' new lists
+  struct Col { std::vector<int> front, li, lj, cnt, src; };
+  std::vector<Col> nc(dc.size());
+  for (size_t d = 0; d < dc.size(); d++) {
+    const int j = dc[d], r = P.perm[j];
+    std::vector<int2> eik;
+    for (int k = row_ptr[r]; k < row_ptr[r + 1]; k++) {
+      const int i = P.iperm[slot_col[k]];
+      if (i > j) eik.push_back(make_int2(i, k));
+    }
+    std::sort(eik.begin(), eik.end(), [](const int2& x, const int2& y) { return x.x != y.x ? x.x < y.x : x.y < y.y; });
+    const int s = P.dg_front[j], f = P.sfirst[s], l = P.sfirst[s + 1];
+    const int* b0 = P.rows.data() + P.rptr[s] + (l - f);
+    const int* b1 = P.rows.data() + P.rptr[s + 1];
+    const int* cur = b0;
+    Col& c = nc[d];
+    for (size_t q = 0; q < eik.size(); q++) {
+      const int i = eik[q].x;
+      if (q == 0 || i != eik[q - 1].x) {
+        int li;
+        if (i < l) {
+          li = i - f;
+        } else {
+          cur = std::lower_bound(cur, b1, i);
+          li = (l - f) + (int)(cur - b0);
+        }
+        c.front.push_back(s);
+        c.li.push_back(li);
+        c.lj.push_back(j - f);
+        c.cnt.push_back(0);
+      }
+      c.cnt.back()++;
+      c.src.push_back(~eik[q].y);
+    }
+  }
+  // splice in place: the kept segments between the dirty columns' old ranges
+  // move up by the targets / entries the dirty columns before them gained (an
+  // append only adds to the pattern: shifts >= 0), last segment first, then the
+  // dirty columns' new lists are written into the gaps
+  const int D = (int)dc.size();
+  std::vector<long long> tshift(D + 1, 0), eshift(D + 1, 0);   // shift of kept segment d (after dirty d - 1)
+  std::vector<int> plo(D), phi(D);                             // old entry pointers at glo / ghi
+  for (int d = 0; d < D; d++) {
+    plo[d] = P.asm_ptr[glo[d]];
+    phi[d] = P.asm_ptr[ghi[d]];
+    tshift[d + 1] = tshift[d] + (long long)nc[d].front.size() - (ghi[d] - glo[d]);
+    eshift[d + 1] = eshift[d] + (long long)nc[d].src.size() - (phi[d] - plo[d]);
+  }
+  bool grows = true;
+  for (int d = 0; d <= D; d++) grows = grows && tshift[d] >= 0 && eshift[d] >= 0;
+  if (!grows) {   // (not an append: the caller's rebuild)
+    dc.clear();
+    P.asm_bound = false;
+    return;
+  }
+  const long long ntg = ntg0 + tshift[D], ne = ne0 + eshift[D];
+  auto grow = [](auto& v, long long n) {   // (room for the next appends too)
+    if ((long long)v.capacity() < n) v.reserve(n + n / 16 + 1024);
+    v.resize(n);
+  };
+  grow(P.asm_front, ntg);
+  grow(P.asm_li, ntg);
+  grow(P.asm_lj, ntg);
+  grow(P.asm_ptr, ntg + 1);
+  grow(P.asm_src, ne);
+  for (int d = D; d >= 1; d--) {   // kept segment d: old targets [ghi[d-1], glo[d] or ntg0)
+    const int a0 = ghi[d - 1], a1 = d < D ? glo[d] : ntg0;
+    const int e0 = phi[d - 1], e1 = d < D ? plo[d] : ne0;
+    const long long ts = tshift[d], es = eshift[d];
+    if (ts == 0 && es == 0) continue;
+    std::copy_backward(P.asm_src.begin() + e0, P.asm_src.begin() + e1, P.asm_src.begin() + e1 + es);
+    std::copy_backward(P.asm_front.begin() + a0, P.asm_front.begin() + a1, P.asm_front.begin() + a1 + ts);
+    std::copy_backward(P.asm_li.begin() + a0, P.asm_li.begin() + a1, P.asm_li.begin() + a1 + ts);
+    std::copy_backward(P.asm_lj.begin() + a0, P.asm_lj.begin() + a1, P.asm_lj.begin() + a1 + ts);
+    for (int g = a1 - 1; g >= a0; g--) P.asm_ptr[g + ts] = P.asm_ptr[g] + (int)es;
+  }
+  for (int d = 0; d < D; d++) {   // dirty column d's list: targets from glo[d] + tshift[d], entries from plo[d] + eshift[d]
+    const Col& c = nc[d];
+    const long long g0 = glo[d] + tshift[d];
+    long long e = plo[d] + eshift[d];
+    std::copy(c.src.begin(), c.src.end(), P.asm_src.begin() + e);
+    for (size_t t = 0; t < c.front.size(); t++) {
+      P.asm_front[g0 + t] = c.front[t];
+      P.asm_li[g0 + t] = c.li[t];
+      P.asm_lj[g0 + t] = c.lj[t];
+      P.asm_ptr[g0 + t] = (int)e;
+      e += c.cnt[t];
+    }
+  }
+  P.asm_ptr[ntg] = (int)ne;
+  dc.clear();
+}
+
 // Assembly of H into the plan's fronts (k_assemble_tile's H entries): the
 // targets (lower 3x3 blocks H_{i,j}, i > j, of the permuted pattern: front,
 // local row, local column, and their block-CSR slots -- parallel factors summed
@@ -1401,6 +1519,12 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
     tl = t;
   };
   P.nslots = (long long)slot_col.size();
+  const bool splice = P.asm_splice && P.asm_bound && !P.asm_ptr.empty();
+  P.asm_splice = false;
+  if (splice) {
+    assembly_splice(P, row_ptr, slot_col);
+    lap("splice");
+  } else {
   // entries (j, i, k) of the permuted lower triangle (new indices i > j), by
   // (j, i, k).  Column j's entries are read from row perm[j]: its slots whose
   // column comes later, i.e. the mirror slot of each block (i, j).  Both slots
@@ -1474,13 +1598,16 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
           }
           P.asm_li[g++] = li;
         }
-        P.asm_src[q] = eik[q].y;
+        P.asm_src[q] = ~eik[q].y;
       }
     }
   });
+  P.asm_bound = false;
   lap("targets");
   P.asm_ptr[ntg] = (int)eik.size();
   if (ntg == 0) P.asm_ptr.assign(1, 0);
+  }
+  const int ntg = (int)P.asm_front.size();
   // H entries by front tile: every 64x64 lower tile of a front lists the 3x3
   // blocks of H (off-diagonal targets t >= 0, diagonal blocks ~pose) with an
   // element in it (a block can straddle tile boundaries); items of a tile in
@@ -1705,6 +1832,11 @@ bool chol_append(CholPlan& P, int n, const std::vector<int>& row_ptr, const std:
   }
   P.n = n;
   size_fronts(P);
+  // the assembly targets: spliced (the columns of the new factors and poses rebuilt)
+  P.asm_dirty.clear();
+  for (const int2& e : new_pairs) P.asm_dirty.push_back(std::min(P.iperm[e.x], P.iperm[e.y]));
+  for (int v = n0; v < n; v++) P.asm_dirty.push_back(v);
+  P.asm_splice = !getenv("PGO_NO_ASM_SPLICE");
   chol_schedule(P, row_ptr, slot_col);
   return true;
 }
