@@ -674,6 +674,7 @@ int upload_structure(pgo_graph* g) {
   RC_TRY(h2d(g, d.slot_edge, slot_edge.data(), ns));
   g->slot_codes_plan = g->slot_codes_mixed = false;   // pre-plan codes throughout
   g->bind_row0 = 0;
+  g->chol.asm_bound = false;   // (a new device factor order: the plan's bound sources are void)
   RC_TRY(h2d(g, d.slot_col, slot_col.data(), ns));
   HIP_TRY(g, hipMemsetAsync(d.part, 0, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices, d.stream));
   HIP_TRY(g, hipStreamSynchronize(d.stream));
