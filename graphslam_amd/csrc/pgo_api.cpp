@@ -90,6 +90,11 @@ struct pgo_graph {
   // owner side of every factor, as uploaded
   int bind_row0 = 0;
   std::vector<unsigned char> h_eside;
+  // mirror_bound: h_slot_edge (and the device copy) carries the plan's owner
+  // bits on every slot but new_slots (an append's, pre-plan codes): the next
+  // bind_plan on the same order sets only those
+  bool mirror_bound = false;
+  std::vector<int> new_slots;
   bool gauge_free = false;                 // some connected component has no prior
   double* h_scal = nullptr;                 // pinned
   int* h_ctrl = nullptr;                    // pinned
@@ -674,6 +679,8 @@ int upload_structure(pgo_graph* g) {
   RC_TRY(h2d(g, d.slot_edge, slot_edge.data(), ns));
   g->slot_codes_plan = g->slot_codes_mixed = false;   // pre-plan codes throughout
   g->bind_row0 = 0;
+  g->mirror_bound = false;
+  g->new_slots.clear();
   g->chol.asm_bound = false;   // (a new device factor order: the plan's bound sources are void)
   RC_TRY(h2d(g, d.slot_col, slot_col.data(), ns));
   HIP_TRY(g, hipMemsetAsync(d.part, 0, sizeof(double) * pgo::kMaxBlocks * pgo::kPartSlices, d.stream));
@@ -876,8 +883,34 @@ int append_structure(pgo_graph* g) {
   std::copy(H.row_ptr.begin() + r0, H.row_ptr.end(), g->h_row_ptr.begin() + r0);
   g->h_slot_col.resize(ns);
   std::copy(H.slot_col.begin() + k0, H.slot_col.end(), g->h_slot_col.begin() + k0);
-  g->h_slot_edge.resize(ns);
-  std::copy(H.slot_edge.begin() + k0, H.slot_edge.end(), g->h_slot_edge.begin() + k0);
+  if (!g->new_slots.empty()) g->mirror_bound = false;   // (an earlier append not bound yet: its list is stale now)
+  if (g->mirror_bound && (int)g->h_slot_edge.size() >= k0) {
+    // the old slots keep their bound codes (the merge keeps their order), the
+    // new ones get pre-plan codes and are listed for bind_plan
+    std::vector<int> tail_old(g->h_slot_edge.begin() + k0, g->h_slot_edge.end());
+    g->h_slot_edge.resize(ns);
+    size_t kk = 0;
+    for (int o = k0; o < ns; o++) {
+      const int code = H.slot_edge[o];
+      if ((code >> 2) >= ne_old) {
+        g->h_slot_edge[o] = code;
+        g->new_slots.push_back(o);
+      } else {
+        g->h_slot_edge[o] = kk < tail_old.size() ? tail_old[kk] : code;
+        kk++;
+      }
+    }
+    if (kk != tail_old.size()) {   // (cannot happen: the merge keeps every old slot, in order)
+      std::copy(H.slot_edge.begin() + k0, H.slot_edge.end(), g->h_slot_edge.begin() + k0);
+      g->mirror_bound = false;
+      g->new_slots.clear();
+    }
+  } else {
+    g->h_slot_edge.resize(ns);
+    std::copy(H.slot_edge.begin() + k0, H.slot_edge.end(), g->h_slot_edge.begin() + k0);
+    g->mirror_bound = false;
+    g->new_slots.clear();
+  }
   g->edge_slot0.resize(ne, -1);
   for (int k = k0; k < ns; k++)
     if ((H.slot_edge[k] & 1) == 0) g->edge_slot0[H.dorder[H.slot_edge[k] >> 2]] = k;
@@ -960,7 +993,7 @@ int append_structure(pgo_graph* g) {
   RC_TRY(staged_h2d(g, sg, d.eom + 3 * (size_t)ne_old, hom.data(), hom.size()));
   RC_TRY(staged_h2d(g, sg, d.prior_ptr + n_old + 1, H.prior_ptr.data() + n_old + 1, n - n_old));
   RC_TRY(staged_h2d(g, sg, d.row_ptr + r0 + 1, H.row_ptr.data() + r0 + 1, n - r0));
-  RC_TRY(staged_h2d(g, sg, d.slot_edge + H.row_ptr[r0], H.slot_edge.data() + H.row_ptr[r0], ns - H.row_ptr[r0]));
+  RC_TRY(staged_h2d(g, sg, d.slot_edge + H.row_ptr[r0], g->h_slot_edge.data() + H.row_ptr[r0], ns - H.row_ptr[r0]));
   RC_TRY(staged_h2d(g, sg, d.slot_col + H.row_ptr[r0], H.slot_col.data() + H.row_ptr[r0], ns - H.row_ptr[r0]));
   RC_TRY(staged_h2d(g, sg, d.erow + x0 + 1, erow.data() + x0 + 1, n - x0));
   RC_TRY(staged_h2d(g, sg, d.s1_ptr + y0 + 1, s1_ptr.data() + y0 + 1, n - y0));
@@ -1060,6 +1093,8 @@ int bind_plan(pgo_graph* g, bool full);
 int unmix_slot_codes(pgo_graph* g) {
   if (!g->slot_codes_mixed) return PGO_OK;
   g->h_slot_edge = g->hs.slot_edge;
+  g->mirror_bound = false;
+  g->new_slots.clear();
   RC_TRY(h2d(g, g->d.slot_edge, g->h_slot_edge.data(), g->h_slot_edge.size()));
   HIP_TRY(g, hipStreamSynchronize(g->d.stream));
   g->slot_codes_plan = g->slot_codes_mixed = false;
@@ -1189,14 +1224,22 @@ int bind_plan(pgo_graph* g, bool full) {
     eside.resize(ne, 0);
     // Cholesky-mode linearisation writes each factor's owner block at its
     // device factor index (coalesced), so the assembly reads V[q*S + e]
-    host_parallel(n - r0, [&](int a, int b) {
-      for (int r = r0 + a; r < r0 + b; r++)
-        for (int k = g->h_row_ptr[r]; k < g->h_row_ptr[r + 1]; k++) {
-          const bool own = g->chol.iperm[r] > g->chol.iperm[g->h_slot_col[k]];
-          slot_edge[k] = (slot_edge[k] & ~2) | (own ? 2 : 0);
-          if (own) eside[slot_edge[k] >> 2] = (unsigned char)(slot_edge[k] & 1);   // one owner slot per factor
-        }
-    });
+    auto own_bit = [&](int r, int k) {
+      const bool own = g->chol.iperm[r] > g->chol.iperm[g->h_slot_col[k]];
+      slot_edge[k] = (slot_edge[k] & ~2) | (own ? 2 : 0);
+      if (own) eside[slot_edge[k] >> 2] = (unsigned char)(slot_edge[k] & 1);   // one owner slot per factor
+    };
+    if (r0 > 0 && g->mirror_bound) {   // the order kept and every other slot bound: the new slots only
+      for (int k : g->new_slots) {
+        const int r = (int)(std::upper_bound(g->h_row_ptr.begin(), g->h_row_ptr.begin() + n + 1, k) - g->h_row_ptr.begin()) - 1;
+        own_bit(r, k);
+      }
+    } else {
+      host_parallel(n - r0, [&](int a, int b) {
+        for (int r = r0 + a; r < r0 + b; r++)
+          for (int k = g->h_row_ptr[r]; k < g->h_row_ptr[r + 1]; k++) own_bit(r, k);
+      });
+    }
     std::vector<int>& src = g->chol.asm_src;
     host_parallel((int)src.size(), [&](int q0, int q1) {
       for (int q = q0; q < q1; q++)   // (~slot: not yet bound; kept ones are factor indices already)
@@ -1225,6 +1268,8 @@ int bind_plan(pgo_graph* g, bool full) {
     g->slot_codes_plan = true;
     g->slot_codes_mixed = false;
     g->bind_row0 = n;
+    g->mirror_bound = true;
+    g->new_slots.clear();
     phase("slots");
   }
   return PGO_OK;

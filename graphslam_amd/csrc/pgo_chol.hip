@@ -2663,6 +2663,12 @@ void blob_add(std::vector<BlobItem>& items, T** dptr, const std::vector<T>& h) {
 }
 }  // namespace
 
+// (pgo_symbolic.cpp's thread pool in the library; this serial stand-in only
+// for the microbenchmarks that compile this file alone)
+__attribute__((weak)) void plan_parallel(int ntask, const std::function<void(int)>& fn) {
+  for (int t = 0; t < ntask; t++) fn(t);
+}
+
 static hipError_t upload_index(CholPlan& P, hipStream_t s) {
   std::vector<int4> own, foreign, sown, sforeign;   // partition exchange lists (this rank's roots / the others')
   std::vector<long long> xo(2 * P.xp_tasks.size());
@@ -2748,10 +2754,18 @@ static hipError_t upload_index(CholPlan& P, hipStream_t s) {
   }
   char* h = static_cast<char*>(P.h_blob);
   char* d = static_cast<char*>(P.d_blob);
-  for (const BlobItem& b : it) {
-    if (b.bytes) memcpy(h + b.off, b.src, b.bytes);
-    *b.dptr = d + b.off;
+  // the host copies into the pinned staging on the plan's thread pool, in
+  // pieces of <= 1 MiB (the plan refresh of the live path uploads ~25 MB)
+  std::vector<std::pair<size_t, size_t>> piece;   // (item, byte offset)
+  for (size_t q = 0; q < it.size(); q++) {
+    *it[q].dptr = d + it[q].off;
+    for (size_t o = 0; o < it[q].bytes; o += (1u << 20)) piece.emplace_back(q, o);
   }
+  plan_parallel((int)piece.size(), [&](int t) {
+    const BlobItem& b = it[piece[t].first];
+    const size_t o = piece[t].second, n = std::min<size_t>(1u << 20, b.bytes - o);
+    memcpy(h + b.off + o, static_cast<const char*>(b.src) + o, n);
+  });
   CH_TRY(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, s));
   return hipSuccess;
 }
