@@ -1221,6 +1221,7 @@ int bind_plan(pgo_graph* g, bool full) {
     const int r0 = std::min(std::max(g->bind_row0, 0), n), k0 = g->h_row_ptr[r0];
     std::vector<int>& slot_edge = g->h_slot_edge;
     std::vector<unsigned char>& eside = g->h_eside;
+    if (eside.capacity() < (size_t)ne) eside.reserve(std::max<size_t>(g->cap_ne, ne));
     eside.resize(ne, 0);
     // Cholesky-mode linearisation writes each factor's owner block at its
     // device factor index (coalesced), so the assembly reads V[q*S + e]

@@ -326,6 +326,14 @@ PlanPool& plan_pool() {
 
 void plan_parallel(int ntask, const std::function<void(int)>& fn) { plan_pool().run(ntask, fn); }
 
+// v.resize(n) leaving room when it has to grow (the live path's plan refreshes
+// then resize within capacity: no reallocation and copy of the whole list)
+template <class V>
+static void resize_room(V& v, size_t n) {
+  if (v.capacity() < n) v.reserve(n + n / 16 + 1024);
+  v.resize(n);
+}
+
 // fn(t, begin, end) on nth contiguous chunks of [0, n), chunk t by index (the
 // results are independent of which thread runs it and of nth)
 template <class F>
@@ -1063,22 +1071,22 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
     base[nl] = z;
   }
   const Base& tot = base[nl];
-  P.small_list.resize(tot.small_list);
-  P.level_fronts.resize(tot.level_fronts);
-  P.potrf_list.resize(tot.potrf_list);
-  P.syrk_tasks.resize(tot.syrk_tasks);
-  P.sdiag_tasks.resize(tot.sdiag_tasks);
-  P.col_tasks.resize(tot.col_tasks);
-  P.bwd_tasks.resize(tot.bwd_tasks);
-  P.bwdc_tasks.resize(tot.bwdc_tasks);
-  P.bwd_pref.resize(tot.bwd_pref);
-  P.bwd_part_tasks.resize(tot.bwd_part_tasks);
-  P.ea_tasks.resize(tot.ea_tasks);
-  P.ea_pairs.resize(tot.ea_pairs);
+  resize_room(P.small_list, tot.small_list);
+  resize_room(P.level_fronts, tot.level_fronts);
+  resize_room(P.potrf_list, tot.potrf_list);
+  resize_room(P.syrk_tasks, tot.syrk_tasks);
+  resize_room(P.sdiag_tasks, tot.sdiag_tasks);
+  resize_room(P.col_tasks, tot.col_tasks);
+  resize_room(P.bwd_tasks, tot.bwd_tasks);
+  resize_room(P.bwdc_tasks, tot.bwdc_tasks);
+  resize_room(P.bwd_pref, tot.bwd_pref);
+  resize_room(P.bwd_part_tasks, tot.bwd_part_tasks);
+  resize_room(P.ea_tasks, tot.ea_tasks);
+  resize_room(P.ea_pairs, tot.ea_pairs);
   P.xchg.resize(tot.xchg);
-  P.xp_tasks.resize(tot.xp_tasks);
-  P.xp_loff.resize(tot.xp_loff);
-  P.xp_lstride.resize(tot.xp_lstride);
+  resize_room(P.xp_tasks, tot.xp_tasks);
+  resize_room(P.xp_loff, tot.xp_loff);
+  resize_room(P.xp_lstride, tot.xp_lstride);
   P.npart = tot.npart;
   plan_parallel(nl, [&](int L) {
     LevelLists& S = out[L];
@@ -1571,6 +1579,14 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
   lap("sort");
   for (int t = 0; t < nck; t++) tstart[t + 1] += tstart[t];
   const int ntg = tstart[nck];
+  {   // (room for the live path's spliced appends: no regrowth on the first one)
+    const size_t rt = ntg + ntg / 16 + 1024, re = eik.size() + eik.size() / 16 + 1024;
+    P.asm_front.reserve(rt);
+    P.asm_li.reserve(rt);
+    P.asm_lj.reserve(rt);
+    P.asm_ptr.reserve(rt + 1);
+    P.asm_src.reserve(re);
+  }
   P.asm_front.resize(ntg);
   P.asm_li.resize(ntg);
   P.asm_lj.resize(ntg);
@@ -1657,7 +1673,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
         pos += fitems[s + 1];
       }
     }
-    P.at_items.resize(pos);
+    resize_room(P.at_items, pos);
   }
   parallel_chunks(ns, 8 * nth, [&](int, int s0, int s1) {
     std::vector<int> fill;   // (reused across the chunk's fronts)
@@ -1672,7 +1688,7 @@ void chol_assembly(CholPlan& P, const std::vector<int>& row_ptr, const std::vect
     }
   });
   lap("tile items");
-  P.at_iptr.resize(P.ea_tasks.size());
+  resize_room(P.at_iptr, P.ea_tasks.size());
   parallel_chunks((int)P.ea_tasks.size(), nth, [&](int, int q0, int q1) {
     for (int q = q0; q < q1; q++) {
       const int4 t = P.ea_tasks[q];
