@@ -121,20 +121,28 @@ void xcd_order(std::vector<int4>& tasks, int tile) {
   constexpr int kXcd = 8, kBlk = 8;
   if ((int)tasks.size() < 4 * kXcd * kBlk) return;   // small launches: keep the natural order
   const int span = tile * kBlk;
-  std::vector<int> idx(tasks.size());
-  for (size_t i = 0; i < idx.size(); i++) idx[i] = (int)i;
-  auto key = [&](const int4& t) { return std::make_tuple(t.x, t.z / span, (t.y & kRowMask) / span); };
-  std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return key(tasks[a]) < key(tasks[b]); });
+  // (front, column block, row block) packed in the high bits, the task index in
+  // the low 32: a plain sort of the keys is the stable sort by block
+  // (block indices below 2^16: rows and columns below 2^20, span >= 512)
+  using u128 = unsigned __int128;
+  std::vector<u128> key(tasks.size());
+  for (size_t i = 0; i < tasks.size(); i++) {
+    const int4& t = tasks[i];
+    const unsigned long long blk = (unsigned long long)(unsigned)t.x << 32 | (unsigned long long)(t.z / span) << 16 |
+                                   (unsigned)((t.y & kRowMask) / span);
+    key[i] = (u128)blk << 32 | i;
+  }
+  std::sort(key.begin(), key.end());
   std::vector<std::vector<int4>> q(kXcd);
+  for (auto& v : q) v.reserve(tasks.size() / kXcd + 1);
   int blk = -1;
-  std::tuple<int, int, int> prev{-1, -1, -1};
-  for (int i : idx) {
-    const auto k = key(tasks[i]);
-    if (k != prev) {
+  unsigned long long prev = ~0ull;
+  for (const u128 k : key) {
+    if ((unsigned long long)(k >> 32) != prev) {
       blk++;
-      prev = k;
+      prev = (unsigned long long)(k >> 32);
     }
-    q[blk % kXcd].push_back(tasks[i]);
+    q[blk % kXcd].push_back(tasks[(size_t)(k & 0xffffffffu)]);
   }
   std::vector<int4> out;
   out.reserve(tasks.size());
@@ -354,6 +362,20 @@ struct LevelLists {
   long long xp_rslot = 0;
   int npart = 0;
   bool schedule_error = false;
+  // empty again, capacity kept
+  void reset() {
+    for (auto* v : {&small_list, &level_fronts, &potrf_list}) v->clear();
+    for (auto* v : {&syrk_tasks, &sdiag_tasks, &col_tasks, &bwd_tasks, &bwdc_tasks, &bwd_part_tasks, &ea_tasks, &ea_pairs,
+                    &xp_tasks})
+      v->clear();
+    bwd_pref.clear();
+    xchg.clear();
+    xp_loff.clear();
+    xp_lstride.clear();
+    xp_rslot = 0;
+    npart = 0;
+    schedule_error = false;
+  }
 };
 
 // The plan's schedules from its fronts (chol_analyze's second half; the
@@ -492,7 +514,7 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
   P.levels.assign(nl, CholLevel());
   // one level's schedule into its own lists (offsets level-relative; merged
   // below in level order, so the plan is the same for any thread count)
-  auto schedule_level = [&](int L, LevelLists& S) {
+  auto schedule_level = [&](int L, LevelLists& S, int part) {
     CholLevel& lv = P.levels[L];
     // distributed top level: this rank generates only the tasks of its columns
     const bool dist = dtop && L >= P.split;
@@ -502,127 +524,143 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       return o < 0 || o == prk;
     };
     auto cowner = [&](int s, int col) { return dist ? P.cown[P.cown_off[s] + col] : -1; };
-    lv.front_off = (int)S.level_fronts.size();
-    lv.front_cnt = (int)bylevel[L].size();
-    for (int s : bylevel[L]) {
-      S.level_fronts.push_back(s);
-      lv.maxm = std::max(lv.maxm, P.m[s]);
-      if (P.m[s] <= kSmallFront) lv.small_maxm = std::max(lv.small_maxm, P.m[s]);
-    }
-    // blocked backward solve (64-column blocks of each front's pivot columns);
-    // the forward substitution is carried by the factorisation
-    for (int s : bylevel[L]) lv.maxblk = std::max(lv.maxblk, (P.w[s] + 63) / 64);
-    {                                            // backward init: all columns vs the rows below w
-      // partial products L21[r0:r0+kBwdRows, block]' x_below, one task each,
-      // reduced in fixed order by the init task of the block
-      SolveStep sp{(int)S.bwd_part_tasks.size(), 0};
-      SolveStep st{(int)S.bwd_tasks.size(), 0};
+    // part 0: the front list, the backward-solve and assembly lists (members of
+    // S and lv disjoint from part 1's: the two parts of a level run concurrently)
+    if (part == 0) {
+      lv.front_off = (int)S.level_fronts.size();
+      lv.front_cnt = (int)bylevel[L].size();
       for (int s : bylevel[L]) {
-        const int w = P.w[s], m = P.m[s], nblk = (w + 63) / 64;
-        for (int b = 0; b < nblk; b++) {
-          const int p0 = S.npart;
-          for (int r0 = w; r0 < m; r0 += kBwdRows) S.bwd_part_tasks.push_back(make_int4(s, b * 64, r0, S.npart++));
-          S.bwd_tasks.push_back(make_int4(s, b * 64, std::min(b * 64 + 64, w), b == nblk - 1 ? b : -1));
-          S.bwd_pref.push_back(make_int2(p0, S.npart - p0));
+        S.level_fronts.push_back(s);
+        lv.maxm = std::max(lv.maxm, P.m[s]);
+        if (P.m[s] <= kSmallFront) lv.small_maxm = std::max(lv.small_maxm, P.m[s]);
+      }
+      // blocked backward solve (64-column blocks of each front's pivot columns);
+      // the forward substitution is carried by the factorisation
+      for (int s : bylevel[L]) lv.maxblk = std::max(lv.maxblk, (P.w[s] + 63) / 64);
+      {                                            // backward init: all columns vs the rows below w
+        // partial products L21[r0:r0+kBwdRows, block]' x_below, one task each,
+        // reduced in fixed order by the init task of the block
+        SolveStep sp{(int)S.bwd_part_tasks.size(), 0};
+        SolveStep st{(int)S.bwd_tasks.size(), 0};
+        for (int s : bylevel[L]) {
+          const int w = P.w[s], m = P.m[s], nblk = (w + 63) / 64;
+          for (int b = 0; b < nblk; b++) {
+            const int p0 = S.npart;
+            for (int r0 = w; r0 < m; r0 += kBwdRows) S.bwd_part_tasks.push_back(make_int4(s, b * 64, r0, S.npart++));
+            S.bwd_tasks.push_back(make_int4(s, b * 64, std::min(b * 64 + 64, w), b == nblk - 1 ? b : -1));
+            S.bwd_pref.push_back(make_int2(p0, S.npart - p0));
+          }
         }
+        sp.cnt = (int)S.bwd_part_tasks.size() - sp.off;
+        for (int q = sp.off; q < sp.off + sp.cnt; q++) {
+          const int4 t = S.bwd_part_tasks[q];
+          const double ncol = std::min(64, P.w[t.x] - t.y), rows = std::min(kBwdRows, P.m[t.x] - t.z);
+          lv.bwd_part_flops += 2.0 * ncol * rows;
+          // L rows x columns, x gathered per row (+ its pose index per 3 rows), the 64 partial sums out
+          lv.bwd_part_bytes += 8.0 * ncol * rows + rows * (8.0 + 4.0 / 3.0) + 8.0 * 64;
+        }
+        st.cnt = (int)S.bwd_tasks.size() - st.off;
+        for (int q = st.off; q < st.off + st.cnt; q++) {   // init: partials + y in, X_jj' z for the last block, x out
+          const int4 t = S.bwd_tasks[q];
+          const double n2 = t.z - t.y, np = S.bwd_pref[q].y;
+          lv.bwd_init_bytes += 8.0 * n2 * (np + 2.0) + (t.w >= 0 ? 8.0 * n2 * (64.0 + 1.0) + 4.0 * n2 / 3.0 : 0.0);
+        }
+        // frontal vectors: own rows gathered from the permuted rhs, the children's
+        // update vectors with their row maps, the vector written
+        for (int s : bylevel[L]) {
+          lv.vec_bytes += 8.0 * P.m[s] + (8.0 + 4.0 / 3.0) * P.w[s];
+          for (int q = P.cptr[s]; q < P.cptr[s + 1]; q++) lv.vec_bytes += (8.0 + 4.0 / 3.0) * (P.m[P.children[q]] - P.w[P.children[q]]);
+        }
+        lv.bwd_part = sp;
+        lv.bwd.push_back(st);
       }
-      sp.cnt = (int)S.bwd_part_tasks.size() - sp.off;
-      for (int q = sp.off; q < sp.off + sp.cnt; q++) {
-        const int4 t = S.bwd_part_tasks[q];
-        const double ncol = std::min(64, P.w[t.x] - t.y), rows = std::min(kBwdRows, P.m[t.x] - t.z);
-        lv.bwd_part_flops += 2.0 * ncol * rows;
-        // L rows x columns, x gathered per row (+ its pose index per 3 rows), the 64 partial sums out
-        lv.bwd_part_bytes += 8.0 * ncol * rows + rows * (8.0 + 4.0 / 3.0) + 8.0 * 64;
+      {   // the same steps as one chained launch (k_bwd_chain): block j of a front
+          // after the blocks above it, tasks ordered by distance from the last
+          // block so that every workgroup waits only on earlier-dispatched ones
+        lv.bwdc.off = (int)S.bwdc_tasks.size();
+        for (int d = 1; d < lv.maxblk; d++)
+          for (int s : bylevel[L]) {
+            const int w = P.w[s], nblk = (w + 63) / 64;
+            if (d >= nblk) continue;
+            const int j = nblk - 1 - d;
+            S.bwdc_tasks.push_back(make_int4(s, j * 64, j * 64 + 64, j));
+            // L[block b, block j] for every block b below j and its x_b, X_jj, z in, x out
+            const double n2 = std::min(64, w - 64 * j);
+            lv.bwd_chain_bytes += 8.0 * (w - 64.0 * (j + 1)) * (n2 + 1.0) + 8.0 * n2 * (64.0 + 3.0) + 4.0 * n2 / 3.0;
+          }
+        lv.bwdc.cnt = (int)S.bwdc_tasks.size() - lv.bwdc.off;
       }
-      st.cnt = (int)S.bwd_tasks.size() - st.off;
-      for (int q = st.off; q < st.off + st.cnt; q++) {   // init: partials + y in, X_jj' z for the last block, x out
-        const int4 t = S.bwd_tasks[q];
-        const double n2 = t.z - t.y, np = S.bwd_pref[q].y;
-        lv.bwd_init_bytes += 8.0 * n2 * (np + 2.0) + (t.w >= 0 ? 8.0 * n2 * (64.0 + 1.0) + 4.0 * n2 / 3.0 : 0.0);
-      }
-      // frontal vectors: own rows gathered from the permuted rhs, the children's
-      // update vectors with their row maps, the vector written
-      for (int s : bylevel[L]) {
-        lv.vec_bytes += 8.0 * P.m[s] + (8.0 + 4.0 / 3.0) * P.w[s];
-        for (int q = P.cptr[s]; q < P.cptr[s + 1]; q++) lv.vec_bytes += (8.0 + 4.0 / 3.0) * (P.m[P.children[q]] - P.w[P.children[q]]);
-      }
-      lv.bwd_part = sp;
-      lv.bwd.push_back(st);
-    }
-    {   // the same steps as one chained launch (k_bwd_chain): block j of a front
-        // after the blocks above it, tasks ordered by distance from the last
-        // block so that every workgroup waits only on earlier-dispatched ones
-      lv.bwdc.off = (int)S.bwdc_tasks.size();
-      for (int d = 1; d < lv.maxblk; d++)
+      for (int b = lv.maxblk - 1; b >= 1; b--) {   // backward step b: columns left of block b
+        SolveStep st{(int)S.bwd_tasks.size(), 0};
         for (int s : bylevel[L]) {
           const int w = P.w[s], nblk = (w + 63) / 64;
-          if (d >= nblk) continue;
-          const int j = nblk - 1 - d;
-          S.bwdc_tasks.push_back(make_int4(s, j * 64, j * 64 + 64, j));
-          // L[block b, block j] for every block b below j and its x_b, X_jj, z in, x out
-          const double n2 = std::min(64, w - 64 * j);
-          lv.bwd_chain_bytes += 8.0 * (w - 64.0 * (j + 1)) * (n2 + 1.0) + 8.0 * n2 * (64.0 + 3.0) + 4.0 * n2 / 3.0;
-        }
-      lv.bwdc.cnt = (int)S.bwdc_tasks.size() - lv.bwdc.off;
-    }
-    for (int b = lv.maxblk - 1; b >= 1; b--) {   // backward step b: columns left of block b
-      SolveStep st{(int)S.bwd_tasks.size(), 0};
-      for (int s : bylevel[L]) {
-        const int w = P.w[s], nblk = (w + 63) / 64;
-        if (b >= nblk) continue;
-        for (int c = 0; c < b; c++)
-        {
-          S.bwd_tasks.push_back(make_int4(s, c * 64, c * 64 + 64, c == b - 1 ? c : -1));
-          S.bwd_pref.push_back(make_int2(0, 0));
-        }
-      }
-      st.cnt = (int)S.bwd_tasks.size() - st.off;
-      lv.bwd.push_back(st);
-    }
-    // assembly: one task per 64x64 tile of every front's lower triangle, which
-    // it writes whole: its H entries (+ lambda on the diagonal), then the
-    // update-matrix elements of the front's children in order (fixed
-    // summation order, no atomics), each child contributing a rectangle of its
-    // update matrix (child rows [a0, a0+nr) x columns [b0, b0+nc), the rows /
-    // columns whose parent index falls in the tile).  No front is zeroed.
-    lv.ea_off.push_back((int)S.ea_tasks.size());
-    std::vector<int> tcnt, tpos;
-    std::vector<int4> runs;   // (child, tile, first child row, rows) of every child, children in order
-    for (int sp : bylevel[L]) {
-      const int nt = (P.m[sp] + 63) / 64;
-      tcnt.assign((size_t)nt * (nt + 1) / 2, 0);
-      runs.clear();
-      std::vector<int> cr(1, 0);   // runs of child q: [cr[q], cr[q + 1])
-      for (int q = P.cptr[sp]; q < P.cptr[sp + 1]; q++) {
-        const int c = P.children[q];
-        const int u = P.m[c] - P.w[c];
-        const size_t r0 = runs.size();
-        for (int a = 0; a < u; a++) {
-          const int t = (3 * P.ea_rel[P.ea_ptr[c] + a / 3] + a % 3) / 64;
-          if (runs.size() == r0 || runs.back().y != t) runs.push_back(make_int4(c, t, a, 0));
-          runs.back().w++;
-        }
-        for (size_t i = r0; i < runs.size(); i++)   // a child's runs are in increasing tiles: one pair per tile
-          for (size_t j = r0; j <= i; j++) tcnt[(size_t)runs[i].y * (runs[i].y + 1) / 2 + runs[j].y]++;
-        cr.push_back((int)runs.size());
-      }
-      const int base = (int)S.ea_pairs.size();
-      tpos.assign(tcnt.size(), 0);
-      for (size_t k = 1; k < tcnt.size(); k++) tpos[k] = tpos[k - 1] + tcnt[k - 1];
-      for (int ti = 0; ti < nt; ti++)
-        for (int tj = 0; tj <= ti; tj++) {
-          const size_t k = (size_t)ti * (ti + 1) / 2 + tj;
-          S.ea_tasks.push_back(make_int4(sp, (ti << 16) | tj, base + tpos[k], tcnt[k]));
-        }
-      S.ea_pairs.resize(base + (tcnt.empty() ? 0 : tpos.back() + tcnt.back()));
-      for (size_t q = 0; q + 1 < cr.size(); q++)   // children in order: their pairs in order within every tile
-        for (int i = cr[q]; i < cr[q + 1]; i++)
-          for (int j = cr[q]; j <= i; j++) {
-            const size_t k = (size_t)runs[i].y * (runs[i].y + 1) / 2 + runs[j].y;
-            S.ea_pairs[base + tpos[k]++] = make_int4(runs[i].x, runs[i].z, runs[j].z, runs[i].w | (runs[j].w << 8));
+          if (b >= nblk) continue;
+          for (int c = 0; c < b; c++)
+          {
+            S.bwd_tasks.push_back(make_int4(s, c * 64, c * 64 + 64, c == b - 1 ? c : -1));
+            S.bwd_pref.push_back(make_int2(0, 0));
           }
+        }
+        st.cnt = (int)S.bwd_tasks.size() - st.off;
+        lv.bwd.push_back(st);
+      }
+      // assembly: one task per 64x64 tile of every front's lower triangle, which
+      // it writes whole: its H entries (+ lambda on the diagonal), then the
+      // update-matrix elements of the front's children in order (fixed
+      // summation order, no atomics), each child contributing a rectangle of its
+      // update matrix (child rows [a0, a0+nr) x columns [b0, b0+nc), the rows /
+      // columns whose parent index falls in the tile).  No front is zeroed.
+      lv.ea_off.push_back((int)S.ea_tasks.size());
+      std::vector<int> tcnt, tpos;
+      std::vector<int4> runs;   // (child, tile, first child row, rows) of every child, children in order
+      for (int sp : bylevel[L]) {
+        const int nt = (P.m[sp] + 63) / 64;
+        tcnt.assign((size_t)nt * (nt + 1) / 2, 0);
+        runs.clear();
+        std::vector<int> cr(1, 0);   // runs of child q: [cr[q], cr[q + 1])
+        for (int q = P.cptr[sp]; q < P.cptr[sp + 1]; q++) {
+          const int c = P.children[q];
+          const int u = P.m[c] - P.w[c];
+          const size_t r0 = runs.size();
+          const int* rel = P.ea_rel.data() + P.ea_ptr[c];
+          auto add = [&](int t, int a, int nr) {
+            if (runs.size() == r0 || runs.back().y != t) runs.push_back(make_int4(c, t, a, 0));
+            runs.back().w += nr;
+          };
+          // (row a of the update matrix: parent row 3 rel[a / 3] + a % 3; a pose's
+          // three rows in one tile go as one)
+          for (int a = 0; a < u; a += 3) {
+            const int r = 3 * rel[a / 3];
+            if ((r >> 6) == ((r + 2) >> 6) && a + 3 <= u) {
+              add(r >> 6, a, 3);
+            } else {
+              for (int k = 0; k < 3 && a + k < u; k++) add((r + k) >> 6, a + k, 1);
+            }
+          }
+          for (size_t i = r0; i < runs.size(); i++)   // a child's runs are in increasing tiles: one pair per tile
+            for (size_t j = r0; j <= i; j++) tcnt[(size_t)runs[i].y * (runs[i].y + 1) / 2 + runs[j].y]++;
+          cr.push_back((int)runs.size());
+        }
+        const int base = (int)S.ea_pairs.size();
+        tpos.assign(tcnt.size(), 0);
+        for (size_t k = 1; k < tcnt.size(); k++) tpos[k] = tpos[k - 1] + tcnt[k - 1];
+        for (int ti = 0; ti < nt; ti++)
+          for (int tj = 0; tj <= ti; tj++) {
+            const size_t k = (size_t)ti * (ti + 1) / 2 + tj;
+            S.ea_tasks.push_back(make_int4(sp, (ti << 16) | tj, base + tpos[k], tcnt[k]));
+          }
+        S.ea_pairs.resize(base + (tcnt.empty() ? 0 : tpos.back() + tcnt.back()));
+        for (size_t q = 0; q + 1 < cr.size(); q++)   // children in order: their pairs in order within every tile
+          for (int i = cr[q]; i < cr[q + 1]; i++)
+            for (int j = cr[q]; j <= i; j++) {
+              const size_t k = (size_t)runs[i].y * (runs[i].y + 1) / 2 + runs[j].y;
+              S.ea_pairs[base + tpos[k]++] = make_int4(runs[i].x, runs[i].z, runs[j].z, runs[i].w | (runs[j].w << 8));
+            }
+      }
+      lv.ea_cnt.push_back((int)S.ea_tasks.size() - lv.ea_off.back());
+      return;
     }
-    lv.ea_cnt.push_back((int)S.ea_tasks.size() - lv.ea_off.back());
+    // part 1: the factorisation lists (small-front classes, blocked panel steps)
     // small fronts (m <= kSmallFront): with w <= kWaveW one wavefront each (the
     // m x w panel in LDS, the rank-w Schur update streamed), largest first;
     // else one workgroup each with the whole front in LDS, launched per size
@@ -1026,15 +1064,23 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
         }
     }
   };
-  std::vector<LevelLists> out(nl);
-  std::vector<double> lms(nl, 0.0);
-  plan_parallel(nl, [&](int L) {
+  // the level lists keep their storage from one schedule to the next on this
+  // thread (a live plan refresh rebuilds them all: fresh allocations cost it
+  // the page faults of ~tens of MB)
+  // (named through a reference: the pool's workers see the caller's lists)
+  static thread_local std::vector<LevelLists> tl_lists;
+  std::vector<LevelLists>& out = tl_lists;
+  if ((int)out.size() < nl) out.resize(nl);
+  for (int L = 0; L < nl; L++) out[L].reset();
+  std::vector<double> lms(2 * nl, 0.0);
+  plan_parallel(2 * nl, [&](int t) {
     const auto t0 = std::chrono::steady_clock::now();
-    schedule_level(L, out[L]);
-    lms[L] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    schedule_level(t >> 1, out[t >> 1], t & 1);
+    lms[t] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   });
   if (timing) {
-    for (int L = 0; L < nl; L++) fprintf(stderr, "  level %d: %.2f ms (%zu fronts)\n", L, lms[L], bylevel[L].size());
+    for (int L = 0; L < nl; L++)
+      fprintf(stderr, "  level %d: %.2f + %.2f ms (%zu fronts)\n", L, lms[2 * L], lms[2 * L + 1], bylevel[L].size());
     phase("levels");
   }
   // merge: level-relative offsets and indices made absolute; the level lists
