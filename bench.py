@@ -420,6 +420,47 @@ def scan_registration_bench(batch=1024, reps=3, cpu_sample=64):
     return res
 
 
+def c5_line(default_params, lanes=3, **common):
+    """BASELINE.json configs[4] (1M poses / 5M between factors, the city-scale
+    graph quoted on 8 GPUs) on this one GPU: one GTSAM-default LM optimize from
+    the dead-reckoned values after one warm-up optimize (the warm-up includes
+    the symbolic analysis, reported apart), 3 lambda lanes.  Reports GN
+    iterations/s, the tries / rounds / factorisations, and the factorisation
+    aggregate over the timed optimize's graph replays."""
+    from graphslam_amd import _lib, datasets
+    from graphslam_amd.pose_graph import PoseGraph
+    t0 = time.perf_counter()
+    g5 = datasets.make("C5")
+    t_gen = time.perf_counter() - t0
+    pg5 = PoseGraph.from_dataset(g5)
+    pg5.save_values()
+    p = default_params(lambda_lanes=lanes, **common)
+    t0 = time.perf_counter()
+    st0 = pg5.optimize(p)
+    t_first = time.perf_counter() - t0
+    pg5.restore_values()
+    t0 = time.perf_counter()
+    st = pg5.optimize(p)
+    dt = time.perf_counter() - t0
+    fl, fms = st["factor_graph_flops"], st["ms_factor_graph"]
+    tfs = fl / (fms * 1e-3) / 1e12 if fms > 0 else None
+    out = {"workload": f"C5: {g5.num_poses} poses / {g5.num_edges} between factors + 1 prior (seed "
+                       f"{g5.meta.get('seed')}), GTSAM-default LM from dead-reckoned values, one GPU",
+           "value": st["linearizations"] / dt, "unit": "GN iterations/s", "ms_per_optimize": 1e3 * dt,
+           "lambda_lanes": lanes, "linearizations": st["linearizations"], "lm_tries": st["inner_iterations"],
+           "accepted": st["iterations"], "lambda_rounds": st["lambda_rounds"], "factorizations": st["solves"],
+           "final_error": st["final_error"], "initial_error": st["initial_error"],
+           "stop_reason": _lib.STOP_REASONS.get(st["stop_reason"], str(st["stop_reason"])),
+           "factor_flops": st["factor_flops"],
+           "factorization": {"ms": fms, "flops": fl, "achieved": tfs, "unit": "TFLOP/s",
+                             "frac": tfs / FP64_MFMA_PEAK_TFS if tfs else None,
+                             "timing": "factorisation graph replays of the timed optimize"},
+           "ms_first_optimize_incl_analysis": 1e3 * t_first, "ms_plan_first": st0["ms_plan"],
+           "s_generate": t_gen}
+    pg5.close()
+    return out
+
+
 def log(msg):
     """Progress on stderr (the JSON line is stdout's only output)."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -480,6 +521,9 @@ def main():
     ap.add_argument("--gn", type=int, default=1, help="after the timed steps: the Gauss-Newton line (0: skip)")
     ap.add_argument("--converged", type=int, default=1,
                     help="after the timed steps: LM from the ground truth to convergence (0: skip)")
+    ap.add_argument("--c5", type=int, default=1,
+                    help="one GPU, C3 run: after the other lines, the 1M-pose C5 graph (BASELINE configs[4]): "
+                         "one warm-up + one timed optimize (0: skip)")
     ap.add_argument("--max-outer", type=int, default=0,
                     help="profiling runs only: stop each optimize after this many linearisations")
     args = ap.parse_args()
@@ -606,6 +650,11 @@ def main():
     if args.live and rank == 0 and not spec:
         log("live re-solve line")
         live = live_resolve_bench(pg, g, args.live, params)
+    c5 = None
+    if args.c5 and rank == 0 and world == 1 and args.config == "C3" and args.solver == "cholesky":
+        log("C5 line")
+        c5 = c5_line(default_params, lanes=args.lanes, **one)
+        log(f"C5 line done: {c5['value']:.2f} GN it/s")
     stats = [s for _, s in results]
     last = stats[-1]
     ps = prof_stats
@@ -696,6 +745,7 @@ def main():
             "closest_keyframe": search,
             "live_resolve": live,
             "scan_registration": scan,
+            "c5": c5,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(g, nd_order, out["per_step"], reps=args.cpu_reps)

@@ -147,6 +147,7 @@ def lib():
         "pgo_debug_spmv": (C.c_int, [vp, C.c_double, dp, dp]),
         "pgo_debug_solve": (C.c_int, [vp, C.c_double, C.POINTER(PgoParams), dp, C.POINTER(C.c_int)]),
         "pgo_debug_factor_time": (C.c_int, [vp, C.c_int, C.c_int, dp]),
+        "pgo_debug_poison_fronts": (C.c_int, [vp]),
         "pgo_debug_plan": (C.c_int, [vp, dp, C.c_int]),
         "pgo_marginal_covariances": (C.c_int, [vp, C.c_size_t, C.POINTER(C.c_uint64), dp]),
         "pgo_debug_fronts": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int]),

@@ -22,8 +22,11 @@ struct Pattern {
   std::vector<int> row_ptr, col;
 };
 
-// block pattern of H for a chain of n poses with `lc` random loop closures
-Pattern make_pattern(int n, int lc, unsigned seed, const std::vector<std::pair<int, int>>& extra = {}) {
+// block pattern of H for a chain of n poses with `lc` random loop closures;
+// `dups` of the loop closures (every lc / dups-th) repeated as a parallel
+// factor: the same block listed twice in both rows, as the library's block-CSR
+// lists parallel factors (one slot each, in device order)
+Pattern make_pattern(int n, int lc, unsigned seed, const std::vector<std::pair<int, int>>& extra = {}, int dups = 0) {
   std::mt19937 rng(seed);
   std::vector<std::pair<int, int>> e;
   for (int i = 0; i + 1 < n; i++) e.emplace_back(i, i + 1);
@@ -39,16 +42,27 @@ Pattern make_pattern(int n, int lc, unsigned seed, const std::vector<std::pair<i
     adj[a].push_back(b);
     adj[b].push_back(a);
   }
-  P.row_ptr.assign(1, 0);
   for (int i = 0; i < n; i++) {
     adj[i].push_back(i);
     std::sort(adj[i].begin(), adj[i].end());
     adj[i].erase(std::unique(adj[i].begin(), adj[i].end()), adj[i].end());
+  }
+  for (int q = 0; dups > 0 && q < lc; q += std::max(1, lc / dups)) {
+    const auto [a, b] = e[n - 1 + q];
+    if (a == b) continue;
+    adj[a].push_back(b);
+    adj[b].push_back(a);
+  }
+  P.row_ptr.assign(1, 0);
+  for (int i = 0; i < n; i++) {
+    std::sort(adj[i].begin(), adj[i].end());
     P.col.insert(P.col.end(), adj[i].begin(), adj[i].end());
     P.row_ptr.push_back((int)P.col.size());
   }
   return P;
 }
+
+constexpr int kDupIds = 8;   // parallel factors per pose pair the emulated bind tells apart
 
 int fail(const char* m) {
   std::fprintf(stderr, "host_selftest: %s\n", m);
@@ -167,7 +181,9 @@ int check_assembly(const pgo::CholPlan& P) {
 // the block -- as many as row perm[i] holds to column perm[j] -- and every
 // slot of the lower triangle is listed once.
 // (sources: ~slot unbound; bound ones -- bind emulated by emulate_bind, ids
-// a * idn + b of the pose pair a < b -- checked against the block's poses)
+// (a * idn + b) * kDupIds + k of the k-th parallel factor of the pose pair
+// a < b -- checked against the block's poses, and a target's parallel
+// factors in their slot order, the summation order)
 int check_sources(const pgo::CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& col, int idn = 0) {
   long long total = 0, want = 0;
   for (size_t g = 0; g < P.asm_front.size(); g++) {
@@ -178,8 +194,10 @@ int check_sources(const pgo::CholPlan& P, const std::vector<int>& row_ptr, const
     for (int k = row_ptr[a]; k < row_ptr[a + 1]; k++) cnt += col[k] == b;
     if (P.asm_ptr[g + 1] - P.asm_ptr[g] != cnt) return fail("assembly: a target's source count");
     for (int q = P.asm_ptr[g]; q < P.asm_ptr[g + 1]; q++) {
-      if (P.asm_src[q] >= 0) {   // bound: the pair id
-        if (!idn || P.asm_src[q] != std::min(a, b) * idn + std::max(a, b)) return fail("assembly: a bound source off its block");
+      if (P.asm_src[q] >= 0) {   // bound: the factor id
+        if (!idn || P.asm_src[q] / kDupIds != std::min(a, b) * idn + std::max(a, b))
+          return fail("assembly: a bound source off its block");
+        if (P.asm_src[q] % kDupIds != q - P.asm_ptr[g]) return fail("assembly: parallel factors out of slot order");
         continue;
       }
       const int k = ~P.asm_src[q];
@@ -224,14 +242,19 @@ Pattern restrict_pattern(const Pattern& G, int n) {
 }
 
 // The host's bind (pgo_api.cpp bind_plan) emulated: every unbound source ~k
-// becomes the id a * idn + b of its slot's pose pair (a < b) -- a factor index
-// in the library; equal for both slots of a pair, as the factor index is.
+// becomes a factor id, (a * idn + b) * kDupIds + j for the j-th slot of row r
+// to column c (pose pair a < b of {r, c}) -- a factor index in the library:
+// equal for both slots of a factor (a row lists a pair's parallel factors in
+// device order from either end), distinct between parallel factors, so a
+// splice that reorders them inside a target shows.
 void emulate_bind(pgo::CholPlan& P, const std::vector<int>& row_ptr, const std::vector<int>& col, int idn) {
   for (int& x : P.asm_src)
     if (x < 0) {
       const int k = ~x;
       const int r = (int)(std::upper_bound(row_ptr.begin(), row_ptr.end(), k) - row_ptr.begin()) - 1;
-      x = std::min(r, col[k]) * idn + std::max(r, col[k]);
+      int j = 0;
+      for (int q = row_ptr[r]; q < k; q++) j += col[q] == col[k];
+      x = (std::min(r, col[k]) * idn + std::max(r, col[k])) * kDupIds + j;
     }
   P.asm_bound = true;
 }
@@ -360,7 +383,7 @@ int main() {
     pgo::chol_analyze(R, G3.n, G3.row_ptr, G3.col);
     if (!pgo::chol_covers(R, G3.n, G3.row_ptr, G3.col) || R.schedule_error) return fail("given ordering");
     // appended poses: the incremental symbolic update
-    if (check_append(make_pattern(1500, 200, 9), 1490, ordering)) return 1;
+    if (check_append(make_pattern(1500, 200, 9, {}, 40), 1490, ordering)) return 1;
   }
   {   // a 2-D grid of poses: nested dissection gives big separator fronts (many
       // panels, kKB block boundaries, partial last panels) -- the look-ahead

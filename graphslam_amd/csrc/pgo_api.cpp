@@ -2648,6 +2648,14 @@ int pgo_debug_factor_time(pgo_graph* g, int lanes, int reps, double* ms) {
   return PGO_OK;
 }
 
+int pgo_debug_poison_fronts(pgo_graph* g) {
+  if (!g) return PGO_E_ARG;
+  if (!g->chol_ready || !g->chol.F) return fail(g, PGO_E_ARG, "no Cholesky workspace yet (optimize first)");
+  HIP_TRY(g, hipSetDevice(g->device));
+  HIP_TRY(g, pgo::chol_debug_poison(g->chol, g->d.stream));
+  return PGO_OK;
+}
+
 int pgo_debug_solve(pgo_graph* g, double lambda, const pgo_params* params, double* delta, int* pcg_iterations) {
   if (!g || !delta) return PGO_E_ARG;
   pgo_params p;

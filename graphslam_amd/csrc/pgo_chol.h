@@ -19,6 +19,7 @@
 
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <vector>
 
 namespace pgo {
@@ -202,6 +203,15 @@ struct CholPlan {
   double flops = 0, nnzl = 0, syrk_flops = 0;
   long long ftotal = 0, ttotal = 0;
   int vtotal = 0;
+  // chol_schedule's per-level scratch lists, kept with the plan from one
+  // schedule to the next (a live refresh reuses their storage) and released by
+  // chol_free; not copied with the plan (a copy starts without scratch)
+  struct Scratch {
+    std::shared_ptr<void> p;
+    Scratch() = default;
+    Scratch(const Scratch&) {}
+    Scratch& operator=(const Scratch&) { return *this; }
+  } sched_scratch;
 
   // ---- device copies ----
   void* d_blob = nullptr;          // every index array below (d_m ... d_ea_pairs) in one allocation
@@ -347,6 +357,9 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
 // diagnostics: the step stamps of the last factorisation run with PGO_STEP_STAMPS
 // set (top level's steps, 10 wall-clock ticks of 10 ns each per step)
 hipError_t chol_step_stamps(unsigned long long* out, int slots);
+// diagnostics (tests): NaN into everything a factorisation writes before it
+// reads it (fronts' lower trapezoids, frontal vectors, diagonal inverses), every lane
+hipError_t chol_debug_poison(const CholPlan& P, hipStream_t s);
 hipError_t chol_marginals(const CholPlan& P, const int* poses, int n, double* out, hipStream_t s);
 // after chol_factor: x = L^-T y = (L L^T)^{-1} scale_b b, indexed by old pose
 // lane y's solution to x + y * xstride

@@ -2775,6 +2775,24 @@ hipError_t chol_upload_assembly(CholPlan& P, hipStream_t s) {
   return hipStreamSynchronize(s);
 }
 
+// an opt-in environment knob set to 1
+static bool knob_on(const char* name) {
+  const char* v = getenv(name);
+  return v && atoi(v) == 1;
+}
+
+// PGO_STEP_SPLIT: diagonal tiles x lanes from which a panel step runs as three
+// launches (k_step_diag, k_panel_syrk_lds on P.side5, k_first_trsm) instead of
+// one k_step; 0 = never, the default since round 5: bitwise the same factor
+// (final error and pose hash equal at 0 / 64 / 1 on C2 and C3), and the
+// replays measured slower with it (C3 8.39 / 17.00 ms at 1 / 3 lanes against
+// 8.34 / 16.81 without, profiles/r05a_ab_split.txt; round 4's r04e A/B: within
+// noise)
+static int step_split_threshold() {
+  static const int v = getenv("PGO_STEP_SPLIT") ? atoi(getenv("PGO_STEP_SPLIT")) : 0;
+  return v;
+}
+
 hipError_t chol_upload(CholPlan& P, hipStream_t s) {
   CH_TRY(upload_index(P, s));
   CH_TRY(P.F ? refresh_numeric(P, std::max(P.batch, 1), s) : alloc_numeric(P, std::max(P.batch, 1), s));
@@ -2806,13 +2824,20 @@ hipError_t chol_upload(CholPlan& P, hipStream_t s) {
       CH_TRY(hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking));
     CH_TRY(hipStreamCreateWithFlags(&P.side2, hipStreamNonBlocking));
     CH_TRY(hipStreamCreateWithFlags(&P.side3, hipStreamNonBlocking));
-    CH_TRY(hipStreamCreateWithFlags(&P.side5, hipStreamNonBlocking));
-    CH_TRY(hipStreamCreateWithFlags(&P.side6, hipStreamNonBlocking));
-    CH_TRY(hipEventCreateWithFlags(&P.ev6, hipEventDisableTiming));
+    // the streams of opt-in knobs exist only with their knob (with
+    // GPU_MAX_HW_QUEUES=4 every idle stream still takes a slot in the
+    // round-robin mapping of streams to hardware queues)
+    if (step_split_threshold() > 0) CH_TRY(hipStreamCreateWithFlags(&P.side5, hipStreamNonBlocking));
+    if (knob_on("PGO_WAVE_STREAMS")) {
+      CH_TRY(hipStreamCreateWithFlags(&P.side6, hipStreamNonBlocking));
+      CH_TRY(hipEventCreateWithFlags(&P.ev6, hipEventDisableTiming));
+    }
     // the deferred far updates fill the CUs the panel chain leaves idle: their
     // stream at the lowest dispatch priority (PGO_FAR_PRIORITY=0: default)
     const char* fp = getenv("PGO_FAR_PRIORITY");
-    if (!(fp && fp[0] == '0') && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+    if (!knob_on("PGO_FAR"))
+      ;
+    else if (!(fp && fp[0] == '0') && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
       CH_TRY(hipStreamCreateWithPriority(&P.side4, hipStreamNonBlocking, least));
     else
       CH_TRY(hipStreamCreateWithFlags(&P.side4, hipStreamNonBlocking));
@@ -2841,6 +2866,7 @@ void chol_free(CholPlan& P) {
   if (P.side5) (void)hipStreamDestroy(P.side5);
   if (P.side6) (void)hipStreamDestroy(P.side6);
   if (P.ev6) (void)hipEventDestroy(P.ev6);
+  P.sched_scratch.p.reset();   // (not touched by the assignment below)
   P = CholPlan();
 }
 
@@ -2999,7 +3025,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
     // PGO_WAVE_STREAMS=1 (A/B): the m > 64 classes narrower than kWaveW (few
     // fronts, latency-bound) on a fourth side stream instead of ahead of the
     // kWaveW class on the third
-    static const bool wave_streams = getenv("PGO_WAVE_STREAMS") && atoi(getenv("PGO_WAVE_STREAMS")) == 1;
+    static const bool wave_streams = knob_on("PGO_WAVE_STREAMS");
     hipStream_t ss = s;
     if (fork_small || fork_wave) {
       CH_TRY(hipEventRecord(P.evs[0], s));
@@ -3112,7 +3138,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       // one k_step whose column workgroups hold a diagonal workgroup's LDS and
       // registers while they wait; same arithmetic (the tile kernels compute a
       // tile's elements alike), bitwise k_step's factor
-      static const int step_split = getenv("PGO_STEP_SPLIT") ? atoi(getenv("PGO_STEP_SPLIT")) : 64;
+      const int step_split = step_split_threshold();
       const bool split = step && step_split > 0 && ps.sdiag_cnt * nb >= step_split && ps.col_cnt > 0;
       if (split) {
         const int4* cupd = cols + ps.fcol_cnt;   // col then prep tasks: 64x64 tile updates
@@ -3191,6 +3217,39 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
     k_set_flag<<<1, nb, 0, s>>>(P.d_flag, 1);
   }
   return hipGetLastError();
+}
+
+// Diagnostics (tests): every element a factorisation must write before it
+// reads it -- the lower trapezoid of every front, the frontal vectors, the
+// diagonal inverses in both orders -- set to NaN in every lane's workspace.  A
+// factorisation that read one of them before writing it would carry the NaN
+// into its factor (the class of round 4's r04b failure: an element the tile
+// assembly did not write, read stale).  The small fronts' upper triangles stay
+// as allocated (zero): no kernel writes them.
+__global__ __launch_bounds__(256) void k_poison(CholDev c) {
+  lane_offset(c);
+  const int s = blockIdx.x;
+  const long long f0 = c.foff[s];
+  if (c.foff[s + 1] == f0) return;   // (a partitioned plan: no storage for another rank's front)
+  const int m = c.m[s];
+  const bool pk = front_packed(m, c.w[s]);
+  const double nan = __builtin_nan("");
+  for (int j = 0; j < m; j++) {
+    double* col = fcol(c.F + f0, m, pk, j);
+    for (int i = j + (int)threadIdx.x; i < m; i += 256) col[i] = nan;
+  }
+  for (int i = threadIdx.x; i < m; i += 256) c.fv[c.voff[s] + i] = nan;
+  for (long long q = c.toff[s] + threadIdx.x; q < c.toff[s + 1]; q += 256) {
+    c.Tinv[q] = nan;
+    c.Tinv[c.tfo + q] = nan;
+  }
+}
+
+hipError_t chol_debug_poison(const CholPlan& P, hipStream_t s) {
+  if (!P.F || P.ns == 0) return hipSuccess;
+  k_poison<<<dim3(P.ns, std::max(P.batch, 1)), 256, 0, s>>>(dev_view(P));
+  CH_TRY(hipGetLastError());
+  return hipStreamSynchronize(s);
 }
 
 hipError_t chol_step_stamps(unsigned long long* out, int slots) {

@@ -1064,12 +1064,11 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
         }
     }
   };
-  // the level lists keep their storage from one schedule to the next on this
-  // thread (a live plan refresh rebuilds them all: fresh allocations cost it
-  // the page faults of ~tens of MB)
-  // (named through a reference: the pool's workers see the caller's lists)
-  static thread_local std::vector<LevelLists> tl_lists;
-  std::vector<LevelLists>& out = tl_lists;
+  // the level lists keep their storage from one schedule to the next in the
+  // plan (a live plan refresh rebuilds them all: fresh allocations cost it the
+  // page faults of ~tens of MB); chol_free releases them with the plan
+  if (!P.sched_scratch.p) P.sched_scratch.p = std::make_shared<std::vector<LevelLists>>();
+  std::vector<LevelLists>& out = *static_cast<std::vector<LevelLists>*>(P.sched_scratch.p.get());
   if ((int)out.size() < nl) out.resize(nl);
   for (int L = 0; L < nl; L++) out[L].reset();
   std::vector<double> lms(2 * nl, 0.0);

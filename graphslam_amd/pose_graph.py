@@ -319,6 +319,10 @@ class PoseGraph:
         self._check(fn(self._h, L.dptr(hd), L.dptr(ho), L.dptr(g), C.byref(e)))
         return hd, ho, g, e.value
 
+    def debug_poison_fronts(self):
+        """NaN into the Cholesky workspace's written-before-read elements (tests)."""
+        self._check(self._L.pgo_debug_poison_fronts(self._h))
+
     def debug_factor_time(self, lanes=1, reps=10):
         """Device ms of one replay of the captured factorisation graph with
         `lanes` lambda lanes (diagnostics; PGO_ABLATE applies)."""

@@ -367,6 +367,12 @@ int pgo_debug_spmv(pgo_graph *g, double lambda, const double *x, double *y);
  * averaged over `reps` back-to-back replays (HIP events on the handle's
  * stream); PGO_ABLATE (families to leave out) applies at capture. */
 int pgo_debug_factor_time(pgo_graph *g, int lanes, int reps, double *ms);
+/* Diagnostics (tests): NaN into every element of the Cholesky workspace
+ * (all lambda lanes) that a factorisation must write before it reads it --
+ * the fronts' lower trapezoids, the frontal vectors, the diagonal inverses --
+ * so a later optimize equals a clean run bit for bit only if no stale element
+ * is ever read.  Needs the workspace (an optimize with the Cholesky solver). */
+int pgo_debug_poison_fronts(pgo_graph *g);
 /* delta = PCG solve of (H + lambda I) delta = -g at the current values */
 int pgo_debug_solve(pgo_graph *g, double lambda, const pgo_params *params, double *delta,
                     int *pcg_iterations);

@@ -285,6 +285,68 @@ def test_fronts_rezeroed_after_marginals(pg_cls):
         assert np.array_equal(pg.poses(), p0), graphs
 
 
+@pytest.mark.parametrize("name", ["C2", "C1-nn"])
+def test_poisoned_workspace_bitwise(pg_cls, name):
+    """Round 4's r04b failure (a first optimize off in the 12th digit, then a
+    non-positive pivot in the marginals) is the signature of an element read
+    before the factorisation wrote it.  Every element a factorisation must
+    write first -- the fronts' lower trapezoids, the frontal vectors, the
+    diagonal inverses, every lambda lane -- is set to NaN between two
+    optimizes: the second must equal a clean run bit for bit (a stale read
+    would carry the NaN into the factor), replayed graphs and eager launches."""
+    g = datasets.make(name)
+    ref = pg_cls.from_dataset(g)
+    ref.save_values()
+    st0 = ref.optimize(lambda_lanes=3)
+    p0 = ref.poses()
+    for graphs in (1, 0):
+        pg = pg_cls.from_dataset(g)
+        pg.save_values()
+        pg.optimize(use_graphs=graphs, lambda_lanes=3, max_outer=2)
+        pg.debug_poison_fronts()
+        pg.restore_values()
+        st = pg.optimize(use_graphs=graphs, lambda_lanes=3)
+        assert st["final_error"] == st0["final_error"], graphs
+        assert np.array_equal(pg.poses(), p0), graphs
+
+
+_KNOB_RUN = r"""
+import hashlib, json, sys
+sys.path.insert(0, {root!r})
+from graphslam_amd import datasets
+from graphslam_amd.pose_graph import PoseGraph, default_params
+pg = PoseGraph.from_dataset(datasets.make({name!r}))
+st = pg.optimize(default_params(lambda_lanes=3, profile_every=1))
+prof = pg.kernel_profile()
+print(json.dumps({{"final": st["final_error"].hex(), "poses": hashlib.sha256(pg.poses().tobytes()).hexdigest(),
+                   "split_launches": prof.get("k_step_diag", {{}}).get("launches", 0)}}))
+"""
+
+
+def test_step_split_bitwise_fresh_processes(pgo_lib):
+    """The split step (k_step_diag beside k_panel_syrk_lds on a fifth stream,
+    then k_first_trsm; PGO_STEP_SPLIT) and the deferred far updates (PGO_FAR)
+    reorder launches across streams, never the arithmetic: forced on C2 (every
+    step split), each in a fresh process, the trajectory must be bitwise the
+    default's, and the forced run must actually have taken the split path."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _KNOB_RUN.format(root=root, name="C2")
+    res = {}
+    for tag, env in (("default", {}), ("split", {"PGO_STEP_SPLIT": "1"}), ("nosplit", {"PGO_STEP_SPLIT": "0"}),
+                     ("split_far", {"PGO_STEP_SPLIT": "1", "PGO_FAR": "1"})):
+        r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[tag] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["split"]["split_launches"] > 0 and res["split_far"]["split_launches"] > 0
+    assert res["nosplit"]["split_launches"] == 0
+    for tag in ("split", "nosplit", "split_far"):
+        assert (res[tag]["final"], res[tag]["poses"]) == (res["default"]["final"], res["default"]["poses"]), tag
+
+
 # ------------------------------------------------------------ headline size
 @pytest.mark.parametrize("solver", [1, 0])
 def test_c3_full_size_against_golden(pg_cls, solver):
