@@ -420,6 +420,18 @@ def scan_registration_bench(batch=1024, reps=3, cpu_sample=64):
     return res
 
 
+def tries_per_linearization(pg):
+    """LM tries of each linearisation of the last optimize, from its trace
+    (column 0: accepted steps before the try -- constant within a
+    linearisation); the speculative multi-GPU model prices rounds with it."""
+    import numpy as np
+    tr = pg.trace()
+    if len(tr) == 0:
+        return []
+    _, idx, cnt = np.unique(tr[:, 0], return_index=True, return_counts=True)
+    return [int(c) for _, c in sorted(zip(idx, cnt))]
+
+
 def c5_line(default_params, lanes=3, **common):
     """BASELINE.json configs[4] (1M poses / 5M between factors, the city-scale
     graph quoted on 8 GPUs) on this one GPU: one GTSAM-default LM optimize from
@@ -455,6 +467,7 @@ def c5_line(default_params, lanes=3, **common):
            "factorization": {"ms": fms, "flops": fl, "achieved": tfs, "unit": "TFLOP/s",
                              "frac": tfs / FP64_MFMA_PEAK_TFS if tfs else None,
                              "timing": "factorisation graph replays of the timed optimize"},
+           "tries_per_linearization": tries_per_linearization(pg5),
            "ms_first_optimize_incl_analysis": 1e3 * t_first, "ms_plan_first": st0["ms_plan"],
            "s_generate": t_gen}
     pg5.close()
@@ -467,18 +480,18 @@ def log(msg):
 
 
 def _partition_bounds(live):
-    """{config: {P: {bound, bound_replicated_top, est_speedup, exchange_points,
-    exchange_bytes, the model's per-mode estimates}}}:
-    profiles/r04_partition_bounds.json (host-computed for C3 and C5,
-    scripts/partition_bounds.py), plus this run's own rank count when it was
-    computed live."""
-    path = os.path.join(ROOT, "profiles", "r04_partition_bounds.json")
-    keep = ("bound", "bound_replicated_top", "est_speedup", "exchange_points", "exchange_bytes",
-            "est_speedup_distributed_top", "est_speedup_replicated_top", "est_speedup_spec")
+    """{config: {P: {flop bounds, exchange points / bytes per rank, the model's
+    speed-up per mode at its central constants and its min-max range over the
+    swept ones, the auto choice}}}: profiles/r05_partition_bounds.json
+    (host-computed for C3 and C5, scripts/partition_bounds.py), plus this
+    run's own rank count when it was computed live.  All unmeasured on 8 GPUs."""
+    path = os.path.join(ROOT, "profiles", "r05_partition_bounds.json")
+    keep = ("bound", "bound_replicated_top", "exchange_points", "exchange_bytes", "est_speedup_distributed_top",
+            "est_speedup_replicated_top", "est_speedup_spec", "est_speedup_hybrid", "range_min", "range_max", "auto")
     out = {}
     if os.path.exists(path):
         for c, per in json.load(open(path)).items():
-            out[c] = {P: {k: v[k] for k in keep} for P, v in per.items()}
+            out[c] = {P: {k: v[k] for k in keep if k in v} for P, v in per.items()}
     if live:
         out["this_run"] = {P: {k: v[k] for k in keep if k in v} for P, v in live.items()}
     return out
@@ -503,11 +516,14 @@ def main():
                     help="consecutive lambda tries per batched factorisation (pgo_params.lambda_lanes; "
                          "default 3 on one GPU -- the rounds are sized to the tries expected -- and 2 per "
                          "rank in the speculative multi-GPU search, whose rounds run every lane)")
-    ap.add_argument("--multi", choices=["auto", "spec", "partition", "replicas"], default="auto",
+    ap.add_argument("--multi", choices=["auto", "spec", "partition", "hybrid", "replicas"], default="auto",
                     help="N>1: speculative lambda search over RCCL (one job), partitioned factorisation "
                          "(one job: subtrees per rank, Schur complements all-gathered, the top fronts' columns "
-                         "dealt to the ranks), independent replicas, or auto: the partitioned mode when the "
-                         "cost model (graphslam_amd/multi_model.py) puts it above the speculative search")
+                         "dealt to the ranks), hybrid (--groups G partition groups running the speculative "
+                         "search), independent replicas, or auto: the built mode whose worst case over the "
+                         "cost model's sensitivity range (graphslam_amd/multi_model.py) is best")
+    ap.add_argument("--groups", type=int, default=0,
+                    help="--multi hybrid: partition groups (N / groups ranks each); 0 = the model's choice")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a one-GPU box: every rank on device 0, host (gloo) transport")
     ap.add_argument("--ordering", choices=["nd", "amd"], default="nd",
@@ -542,38 +558,54 @@ def main():
     # anything is timed): the auto mode's choice, the line's config
     bounds = {}
     mode_why = None
-    if world > 1 and args.multi == "auto":
+    if world > 1 and (args.multi == "auto" or (args.multi == "hybrid" and args.groups <= 0)):
         from graphslam_amd import multi_model
         obj = [None]
         if rank == 0:
-            b = pg.debug_partition_bound(world)
+            pd = multi_model.PlanData(pg, args.config)
+            b = dict(pd.bound(world))
             b["rank_flops"] = [float(v) for v in b["rank_flops"]]
-            b.update(multi_model.estimate(pg, world, args.config, bound=b))
-            obj = [(multi_model.choose_mode(b), multi_model.dist_top(b), b)]
+            b.update(multi_model.estimate(pg, world, args.config, pd=pd))
+            obj = [(multi_model.choose(b), b)]
         r.dist.broadcast_object_list(obj, src=0)
-        args.multi, dist_top, b = obj[0]
-        if args.multi == "partition" and not dist_top:
-            os.environ["PGO_DIST_TOP"] = "0"   # the replicated top (read when the plan is built)
-        bounds[str(world)] = b
-        mode_why = (f"auto: partition est {b['est_speedup_replicated_top']:.2f}x (replicated top) / "
-                    f"{b['est_speedup_distributed_top']:.2f}x (distributed top) vs speculative "
-                    f"{b['est_speedup_spec']:.2f}x ({b['model']}; level times: {b['level_times']})")
+        (mode, groups, dist_top), b = obj[0]
+        if args.multi == "auto":
+            args.multi, args.groups = mode, groups
+            if args.multi in ("partition", "hybrid") and not dist_top:
+                os.environ["PGO_DIST_TOP"] = "0"   # the replicated top (read when the plan is built)
+        elif args.groups <= 0:   # hybrid, groups from the model
+            hy = b["range_min"]
+            args.groups = max((int(k[6:]) for k in hy if k.startswith("hybrid")), key=lambda G: hy[f"hybrid{G}"],
+                              default=world)
+        bounds[str(world)] = {k: v for k, v in b.items() if k != "sensitivity"}
+        lo, hi = b["range_min"], b["range_max"]
+        mode_why = (f"{'auto' if mode == args.multi else 'chosen'}: {args.multi}"
+                    f"{' x' + str(args.groups) + ' groups' if args.multi == 'hybrid' else ''}; model speed-up "
+                    "ranges (min-max over B, t_bcast): " +
+                    ", ".join(f"{k} {lo[k]:.2f}-{hi[k]:.2f}x" for k in lo) +
+                    f" ({b['model']}; level times: {b['level_times']}; unmeasured on 8 GPUs)")
     elif args.multi == "auto":
         args.multi = "spec"
+    if args.multi == "hybrid" and (args.groups < 2 or world % args.groups or args.groups >= world):
+        args.multi = "spec" if args.groups >= world else "partition"   # a degenerate hybrid
     if args.lanes is None:
         # speculative search: one lane per rank -- a round's time is its
         # slowest rank's replay, and a one-lane replay costs half a three-lane
         # one, while P ranks already cover P tries (C3 trajectory: 1-4 tries per
         # linearisation but one of 10: 8 ranks x 1 lane = 9 one-lane rounds
         # against 8 two-lane ones)
-        args.lanes = 1 if world > 1 and args.multi == "spec" else 3
-    spec = world > 1 and args.multi in ("spec", "partition")   # one job over all ranks
+        args.lanes = 1 if world > 1 and args.multi in ("spec", "hybrid") else 3
+    spec = world > 1 and args.multi in ("spec", "partition", "hybrid")   # one job over all ranks
     part = world > 1 and args.multi == "partition"
+    hybrid = world > 1 and args.multi == "hybrid"
     hc = None
     transport = "host" if args.same_device else "rccl"
     if spec:
         from graphslam_amd import multi_gpu
-        if args.same_device:
+        if hybrid:
+            hc = multi_gpu.attach_hybrid(pg, r.dist, rank, world, args.groups,
+                                         transport="host" if args.same_device else "rccl")
+        elif args.same_device:
             hc = multi_gpu.attach_host(pg, r.dist, rank, world)
         else:
             # RCCL over xGMI; should any rank fail to bring its communicator up,
@@ -600,7 +632,7 @@ def main():
     # factorisation run eagerly with per-launch events feeds the kernel tables
     common = dict(max_outer=args.max_outer, linear_solver=1 if args.solver == "cholesky" else 0,
                   use_graphs=0 if args.no_graphs else 1, lambda_lanes=args.lanes,
-                  multi_gpu=1 if part else 0)
+                  multi_gpu=2 if hybrid else 1 if part else 0)
     params = default_params(profile_every=0, **common)
     prof_params = default_params(profile_every=args.profile_every, **common)
 
@@ -621,6 +653,7 @@ def main():
     if spec:   # one job: every rank walked the same linearisations
         lin_total /= world
     prof_stats = [step(prof_params)[1]] if args.profile_every > 0 else []
+    tries_lin = tries_per_linearization(pg)   # (the timed steps' trajectory; before the side lines re-optimize)
     marg = None
     if args.marginals > 0 and rank == 0:
         import numpy as np
@@ -703,7 +736,8 @@ def main():
                 "workload": f"{args.config}: {n} poses / {ne} between factors + 1 prior, Manhattan walk "
                             f"(seed {g.meta.get('seed')}), GTSAM-default LM from dead-reckoned values",
                 "poses": n, "edges": ne,
-                "parallelism": ((f"partition{world}" if part else f"spec-lambda{world}") +
+                "parallelism": ((f"hybrid{args.groups}x{world // args.groups}" if hybrid else
+                                 f"partition{world}" if part else f"spec-lambda{world}") +
                                 "-" + transport) if spec else
                                (f"replicas{world}" if world > 1 else "single-gpu"),
                 "lambda_lanes": args.lanes,
@@ -725,6 +759,7 @@ def main():
                 "stop_reason": _lib.STOP_REASONS.get(last["stop_reason"], str(last["stop_reason"])),
                 # expected 0.5 chi^2 at the optimum: half the residual dimension minus the pose dof
                 "expected_error_at_optimum": 0.5 * (3 * (ne + len(g.prior_keys)) - 3 * n),
+                "tries_per_linearization": tries_lin,
             },
             "roofline": roofline,
             "linearize_kernel": {

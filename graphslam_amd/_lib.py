@@ -37,6 +37,7 @@ PGO_SOLVER_PCG = 0
 PGO_SOLVER_CHOLESKY = 1
 PGO_MULTI_SPECULATIVE = 0
 PGO_MULTI_PARTITION = 1
+PGO_MULTI_HYBRID = 2
 STOP_REASONS = {0: "converged", 1: "lambda_upper_bound", 2: "max_iterations", 3: "max_outer", 4: "small_cost_change",
                 5: "error"}
 
@@ -159,6 +160,9 @@ def lib():
         "pgo_comm_init_host": (C.c_int, [vp, C.POINTER(PgoHostComm)]),
         "pgo_comm_free": (C.c_int, [vp]),
         "pgo_comm_rank": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        "pgo_comm_init_rccl_part": (C.c_int, [vp, vp, C.c_size_t, C.c_int, C.c_int]),
+        "pgo_comm_init_host_part": (C.c_int, [vp, C.POINTER(PgoHostComm)]),
+        "pgo_comm_part_rank": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "pgo_comm_selftest": (C.c_int, [vp]),
         "pgo_get_trace": (C.c_int, [vp, dp, C.c_int]),
         "pgo_get_kernel_profile": (C.c_int, [vp, dp, C.c_int]),

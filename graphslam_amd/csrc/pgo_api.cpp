@@ -137,6 +137,13 @@ struct pgo_graph {
   Staging stage;                            // pinned upload staging (append_structure)
   // ---- multi-GPU speculative lambda search (pgo_comm_*) ----
   pgo::Comm comm;
+  // the partition group's communicator of the hybrid mode (pgo_comm_init_*_part:
+  // the ranks that split one factorisation; comm then links one rank of every
+  // group for the speculative search), and the communicator the partitioned
+  // factorisation exchanges over (set per optimize: pcomm in the hybrid mode,
+  // else comm)
+  pgo::Comm pcomm;
+  pgo::Comm* part_comm = &comm;
   std::vector<Lane> lanes;                  // lanes 1..L-1 (speculative tries on this GPU)
   double* xb = nullptr;                     // [L x 3n] solutions of a batched factor + solve
   size_t xb_n = 0;                          // ... allocated for this many vertices (capacity)
@@ -1063,7 +1070,7 @@ double ms_between(hipEvent_t a, hipEvent_t b);
 int exchange_allgather(void* ctx, const void* send, void* recv, size_t bytes, hipStream_t s) {
   pgo_graph* g = static_cast<pgo_graph*>(ctx);
   std::string why;
-  const int rc = pgo::comm_allgather_device(&g->comm, send, recv, bytes, s, &why);
+  const int rc = pgo::comm_allgather_device(g->part_comm, send, recv, bytes, s, &why);
   if (rc != PGO_OK) g->last_error = "partition exchange: " + why;
   return rc == PGO_OK ? 0 : -1;
 }
@@ -1071,7 +1078,7 @@ int exchange_allgather(void* ctx, const void* send, void* recv, size_t bytes, hi
 int exchange_broadcast(void* ctx, void* buf, size_t bytes, int root, hipStream_t s) {
   pgo_graph* g = static_cast<pgo_graph*>(ctx);
   std::string why;
-  const int rc = pgo::comm_broadcast_device_async(&g->comm, buf, bytes, root, s, &why);
+  const int rc = pgo::comm_broadcast_device_async(g->part_comm, buf, bytes, root, s, &why);
   if (rc != PGO_OK) g->last_error = "panel exchange: " + why;
   return rc == PGO_OK ? 0 : -1;
 }
@@ -1079,7 +1086,7 @@ int exchange_broadcast(void* ctx, void* buf, size_t bytes, int root, hipStream_t
 int exchange_group(void* ctx, int begin) {
   pgo_graph* g = static_cast<pgo_graph*>(ctx);
   std::string why;
-  const int rc = pgo::comm_group(&g->comm, begin, &why);
+  const int rc = pgo::comm_group(g->part_comm, begin, &why);
   if (rc != PGO_OK) g->last_error = "panel exchange group: " + why;
   return rc == PGO_OK ? 0 : -1;
 }
@@ -1103,7 +1110,7 @@ int unmix_slot_codes(pgo_graph* g) {
 }
 
 int ensure_chol(pgo_graph* g) {
-  const int psz = g->part_size > 1 ? g->comm.size : 1, prk = psz > 1 ? g->comm.rank : 0;
+  const int psz = g->part_size > 1 ? g->part_comm->size : 1, prk = psz > 1 ? g->part_comm->rank : 0;
   if (g->chol_ready && (g->chol.part_size != psz || g->chol.part_rank != prk)) {   // other partition: re-plan
     (void)hipStreamSynchronize(g->d.stream);
     free_lanes(g);
@@ -1687,8 +1694,9 @@ pgo_graph* pgo_create(const pgo_opts* opts) {
 
 void pgo_destroy(pgo_graph* g) {
   if (!g) return;
-  if (g->comm.nccl || g->comm.d_gather) (void)hipSetDevice(g->device);
+  if (g->comm.nccl || g->comm.d_gather || g->pcomm.nccl || g->pcomm.d_gather) (void)hipSetDevice(g->device);
   pgo::comm_free(&g->comm);
+  pgo::comm_free(&g->pcomm);
   if (g->hip_ready) {
     (void)hipSetDevice(g->device);
     (void)hipStreamSynchronize(g->d.stream);
@@ -1954,10 +1962,16 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   }
   hipEvent_t* ev = g->ev;
   // PGO_MULTI_PARTITION with ranks: every try's factorisation is split over
-  // the ranks (each rank then walks the same, replicated LM control)
-  const bool partition = p.multi_gpu == PGO_MULTI_PARTITION && g->comm.size > 1 &&
-                         p.linear_solver != PGO_SOLVER_PCG && p.algorithm != PGO_ALG_GN;
-  g->part_size = partition ? g->comm.size : 1;
+  // the ranks (each rank then walks the same, replicated LM control).
+  // PGO_MULTI_HYBRID: split over the partition group (pcomm), and the groups
+  // run the speculative search over comm (one rank of every group each)
+  const bool chol_lm = p.linear_solver != PGO_SOLVER_PCG && p.algorithm != PGO_ALG_GN;
+  const bool hybrid = p.multi_gpu == PGO_MULTI_HYBRID && g->pcomm.size > 1 && chol_lm;
+  if (p.multi_gpu == PGO_MULTI_HYBRID && g->pcomm.size <= 1 && g->comm.size > 1 && chol_lm)
+    return fail(g, PGO_E_ARG, "PGO_MULTI_HYBRID needs a partition-group communicator (pgo_comm_init_*_part)");
+  g->part_comm = hybrid ? &g->pcomm : &g->comm;
+  const bool partition = (hybrid || (p.multi_gpu == PGO_MULTI_PARTITION && g->comm.size > 1)) && chol_lm;
+  g->part_size = partition ? g->part_comm->size : 1;
   // Cholesky: the plan (and the owner bits it assigns) first, then the
   // linearisation writes only the blocks the assembly reads
   if (p.linear_solver != PGO_SOLVER_PCG && d.n > 0) {
@@ -2021,24 +2035,30 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
     return retried([&] { return run_try_once(lam_try, out); });
   };
   pgo::Comm& cm = g->comm;
-  // the speculative search's ranks (a partitioned run is one search: P = 1 here)
-  const int P = partition ? 1 : cm.size, me = partition ? 0 : cm.rank;
-  const bool exchange = !partition && (P > 1 || pgo::force_collectives(&cm));   // forced: 1-rank RCCL too
-  st.ranks = cm.size;
+  // the speculative search's ranks (a partitioned run is one search: P = 1
+  // here; the hybrid's search runs over the groups, one rank of each in cm)
+  const bool spec = !partition || hybrid;
+  const int P = spec ? cm.size : 1, me = spec ? cm.rank : 0;
+  const bool exchange = spec && (P > 1 || pgo::force_collectives(&cm));   // forced: 1-rank RCCL too
+  st.ranks = hybrid ? cm.size * g->pcomm.size : cm.size;
   // lanes: concurrent tries on this GPU (Cholesky LM only)
   int L = 1;
   if (p.algorithm != PGO_ALG_GN && p.linear_solver != PGO_SOLVER_PCG && p.lambda_lanes > 1 && d.n > 0)
     L = ensure_lanes(g, p.lambda_lanes);
   // every rank must agree on the lanes per rank (a lane allocation may fail on
-  // one); a partitioned run's ranks factor the same lanes together
-  if (exchange || (partition && cm.size > 1)) {
-    std::vector<double> all(cm.size);
+  // one); a partitioned run's ranks factor the same lanes together (the
+  // hybrid: the minimum over the group, then over the groups)
+  auto agree_lanes = [&](pgo::Comm& c) -> int {
+    std::vector<double> all(c.size);
     const double mineL = L;
     std::string why;
-    const int rc = pgo::comm_allgather(&cm, &mineL, 1, all.data(), d.stream, &why);
+    const int rc = pgo::comm_allgather(&c, &mineL, 1, all.data(), d.stream, &why);
     if (rc != PGO_OK) return fail(g, rc, "lane count all-gather: " + why);
     for (double v : all) L = std::min(L, (int)v);
-  }
+    return PGO_OK;
+  };
+  if (partition && g->part_comm->size > 1) RC_TRY(agree_lanes(*g->part_comm));
+  if (exchange && (!partition || hybrid)) RC_TRY(agree_lanes(cm));
   const int T = P * L;                       // tries per round
   std::vector<double> lam_k(T), fac_k(T), outs(4 * T);
   int last_outcome = PGO_STOP_CONVERGED;     // how the last linearisation's tries ended
@@ -2333,8 +2353,34 @@ int pgo_comm_init_host(pgo_graph* g, const pgo_host_comm* comm) {
 
 int pgo_comm_free(pgo_graph* g) {
   if (!g) return PGO_E_ARG;
-  if (g->comm.nccl) (void)hipSetDevice(g->device);
+  if (g->comm.nccl || g->pcomm.nccl) (void)hipSetDevice(g->device);
   pgo::comm_free(&g->comm);
+  pgo::comm_free(&g->pcomm);
+  g->part_comm = &g->comm;
+  return PGO_OK;
+}
+
+int pgo_comm_init_rccl_part(pgo_graph* g, const void* unique_id, size_t id_bytes, int rank, int size) {
+  if (!g) return PGO_E_ARG;
+  RC_TRY(ensure_hip(g));
+  HIP_TRY(g, hipSetDevice(g->device));
+  std::string why;
+  const int rc = pgo::comm_init_rccl(&g->pcomm, unique_id, id_bytes, rank, size, &why);
+  return rc == PGO_OK ? rc : fail(g, rc, why);
+}
+
+int pgo_comm_init_host_part(pgo_graph* g, const pgo_host_comm* comm) {
+  if (!g) return PGO_E_ARG;
+  if (g->pcomm.nccl) (void)hipSetDevice(g->device);
+  std::string why;
+  const int rc = pgo::comm_init_host(&g->pcomm, comm, &why);
+  return rc == PGO_OK ? rc : fail(g, rc, why);
+}
+
+int pgo_comm_part_rank(const pgo_graph* g, int* rank, int* size) {
+  if (!g || !rank || !size) return PGO_E_ARG;
+  *rank = g->pcomm.rank;
+  *size = g->pcomm.size;
   return PGO_OK;
 }
 

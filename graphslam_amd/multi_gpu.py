@@ -39,11 +39,14 @@ def attach_rccl(pg, dist, rank: int, world: int):
 
 
 class HostComm:
-    """pgo_host_comm over a torch.distributed (gloo) group, host buffers."""
+    """pgo_host_comm over a torch.distributed (gloo) group, host buffers.
+    `ranks`: the group's global ranks in group order (a sub-group: broadcast
+    roots are given in group numbering)."""
 
-    def __init__(self, dist, rank: int, world: int, group=None):
+    def __init__(self, dist, rank: int, world: int, group=None, ranks=None):
         import torch
         self._torch, self._dist, self._group = torch, dist, group
+        self._ranks = list(ranks) if ranks is not None else list(range(world))
         self.rank, self.world = rank, world
         self._ag = L.ALLGATHER_FN(self._allgather)
         self._bc = L.BROADCAST_FN(self._broadcast)
@@ -65,7 +68,7 @@ class HostComm:
 
     def _broadcast(self, ctx, buf, n, root):
         try:
-            self._dist.broadcast(self._view(buf, n), src=root, group=self._group)
+            self._dist.broadcast(self._view(buf, n), src=self._ranks[root], group=self._group)
             return 0
         except Exception:  # noqa: BLE001
             return 1
@@ -75,3 +78,45 @@ def attach_host(pg, dist, rank: int, world: int, group=None) -> HostComm:
     hc = HostComm(dist, rank, world, group)
     pg.comm_init_host(hc.struct)
     return hc
+
+
+def hybrid_layout(world: int, groups: int):
+    """PGO_MULTI_HYBRID rank layout: `groups` partition groups of world/groups
+    consecutive ranks; the speculative search links the ranks at the same
+    position of every group.  Returns (part_ranks, spec_ranks): for each group
+    its global ranks, for each position its global ranks."""
+    if groups < 1 or world % groups:
+        raise ValueError(f"{world} ranks do not split into {groups} equal groups")
+    pp = world // groups
+    part = [list(range(g * pp, (g + 1) * pp)) for g in range(groups)]
+    spec = [[g * pp + i for g in range(groups)] for i in range(pp)]
+    return part, spec
+
+
+def attach_hybrid(pg, dist, rank: int, world: int, groups: int, transport: str = "rccl"):
+    """Both communicators of the hybrid mode: the partition group's (ranks of
+    one group split every factorisation) and the speculative search's (one rank
+    per group).  Every rank must call this (torch.distributed sub-groups are
+    created collectively).  transport "rccl": ids made by each sub-group's
+    first rank and sent over gloo; "host": gloo sub-groups as host transports
+    (ranks sharing one GPU in tests).  Returns the objects to keep alive."""
+    part, spec = hybrid_layout(world, groups)
+    pp = world // groups
+    pgroups = [dist.new_group(r) for r in part]
+    sgroups = [dist.new_group(r) for r in spec]
+    g, i = rank // pp, rank % pp
+    keep = []
+    if transport == "host":
+        hp = HostComm(dist, i, pp, pgroups[g], part[g])
+        pg.comm_init_host_part(hp.struct)
+        hs = HostComm(dist, g, groups, sgroups[i], spec[i])
+        pg.comm_init_host(hs.struct)
+        keep += [hp, hs]
+    else:
+        for ranks, grp, me, size, init in ((part[g], pgroups[g], i, pp, pg.comm_init_rccl_part),
+                                           (spec[i], sgroups[i], g, groups, pg.comm_init_rccl)):
+            obj = [unique_id() if me == 0 else None]
+            if size > 1:
+                dist.broadcast_object_list(obj, src=ranks[0], group=grp)
+            init(obj[0], me, size)
+    return keep

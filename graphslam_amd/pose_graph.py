@@ -295,6 +295,21 @@ class PoseGraph:
         self._comm_keepalive = comm
         self._check(self._L.pgo_comm_init_host(self._h, C.byref(comm)))
 
+    def comm_init_rccl_part(self, unique_id: bytes, rank: int, size: int):
+        """The hybrid mode's partition-group communicator over RCCL (collective over the group)."""
+        buf = C.create_string_buffer(bytes(unique_id), len(unique_id))
+        self._check(self._L.pgo_comm_init_rccl_part(self._h, buf, len(unique_id), rank, size))
+
+    def comm_init_host_part(self, comm: L.PgoHostComm):
+        """The hybrid mode's partition-group communicator over the caller's host transport."""
+        self._pcomm_keepalive = comm
+        self._check(self._L.pgo_comm_init_host_part(self._h, C.byref(comm)))
+
+    def comm_part_rank(self):
+        r, n = C.c_int(), C.c_int()
+        self._check(self._L.pgo_comm_part_rank(self._h, C.byref(r), C.byref(n)))
+        return r.value, n.value
+
     def comm_free(self):
         self._check(self._L.pgo_comm_free(self._h))
 

@@ -117,12 +117,19 @@ typedef struct {
                                    all-gathered (the boundary reduction) and
                                    the top separators' columns are dealt to
                                    the ranks (each factored panel broadcast by
-                                   its rank); composes with lambda_lanes
-                                   [PGO_MULTI_SPECULATIVE] */
+                                   its rank); composes with lambda_lanes;
+                                   PGO_MULTI_HYBRID -- both: the ranks form
+                                   groups, each group splits every
+                                   factorisation over its partition-group
+                                   communicator (pgo_comm_init_*_part) and the
+                                   groups run the speculative search over the
+                                   main communicator (one rank of every group
+                                   each) [PGO_MULTI_SPECULATIVE] */
 } pgo_params;
 
 #define PGO_MULTI_SPECULATIVE 0
 #define PGO_MULTI_PARTITION 1
+#define PGO_MULTI_HYBRID 2
 
 typedef struct {
   int status;                   /* PGO_OK / PGO_W_MAXITER / error                 */
@@ -347,6 +354,13 @@ int pgo_comm_init_host(pgo_graph *g, const pgo_host_comm *comm);
 int pgo_comm_free(pgo_graph *g);
 /* rank / size of the handle's communicator (0 / 1 without one) */
 int pgo_comm_rank(const pgo_graph *g, int *rank, int *size);
+/* PGO_MULTI_HYBRID: the partition group's communicator (the ranks that split
+   one factorisation; collective over the group), RCCL or host transport; the
+   main communicator then holds one rank of every group (the same position in
+   each).  pgo_comm_free frees both. */
+int pgo_comm_init_rccl_part(pgo_graph *g, const void *unique_id, size_t id_bytes, int rank, int size);
+int pgo_comm_init_host_part(pgo_graph *g, const pgo_host_comm *comm);
+int pgo_comm_part_rank(const pgo_graph *g, int *rank, int *size);
 /* exchange check (no solve): all-gather of (rank, size, rank^2, 1) and a
    broadcast from rank size-1; PGO_OK when every rank saw the right data.  The
    host transport needs no GPU. */

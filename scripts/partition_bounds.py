@@ -9,7 +9,7 @@ Also graphslam_amd/multi_model.py's level-by-level time estimates of both tops
 and of the speculative search (bench.py's --multi auto uses the same model).
 Writes profiles/<out>.json.
 
-    python scripts/partition_bounds.py [--configs C3 C5] [--out r04_partition_bounds]
+    python scripts/partition_bounds.py [--configs C3 C5] [--out r05_partition_bounds]
 """
 from __future__ import annotations
 
@@ -21,14 +21,14 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from graphslam_amd.multi_model import estimate  # noqa: E402
+from graphslam_amd.multi_model import PlanData, choose, estimate  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", nargs="+", default=["C3", "C5"])
     ap.add_argument("--ranks", nargs="+", type=int, default=[2, 4, 8])
-    ap.add_argument("--out", default="r04_partition_bounds")
+    ap.add_argument("--out", default="r05_partition_bounds")
     args = ap.parse_args()
     from graphslam_amd import datasets
     from graphslam_amd.pose_graph import PoseGraph
@@ -36,13 +36,16 @@ def main():
     for c in args.configs:
         g = datasets.make(c)
         pg = PoseGraph.from_dataset(g)
+        pd = PlanData(pg, c)
         res[c] = {}
         for P in args.ranks:
-            b = pg.debug_partition_bound(P)
+            b = dict(pd.bound(P))
             b["rank_flops"] = [float(v) for v in b["rank_flops"]]
-            b.update(estimate(pg, P, c, bound=b))
+            b.update(estimate(pg, P, c, pd=pd))
+            mode, groups, dist = choose(b)
+            b["auto"] = {"mode": mode, "groups": groups, "distributed_top": dist}
             res[c][str(P)] = b
-            print(c, P, json.dumps({k: v for k, v in b.items() if k != "rank_flops"}))
+            print(c, P, json.dumps({k: v for k, v in b.items() if k not in ("rank_flops", "sensitivity")}), flush=True)
         pg.close()
     path = os.path.join(ROOT, "profiles", args.out + ".json")
     json.dump(res, open(path, "w"), indent=1)

@@ -65,6 +65,35 @@ def _run(world, target, args, timeout=300):
     return sorted(out, key=lambda o: o[0])
 
 
+def _hybrid_selftest_worker(rank, world, port, q, groups):
+    try:
+        dist = _init(rank, world, port)
+        from graphslam_amd import multi_gpu
+        from graphslam_amd.pose_graph import PoseGraph
+        pg = PoseGraph(device=0)
+        keep = multi_gpu.attach_hybrid(pg, dist, rank, world, groups, transport="host")
+        pg.comm_selftest()
+        q.put((rank, (pg.comm_rank(), pg.comm_part_rank()), None))
+        del keep
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("world,groups", [(4, 2), (6, 3), (4, 1), (4, 4)])
+def test_hybrid_layout_gloo(world, groups):
+    """PGO_MULTI_HYBRID's two communicators over gloo sub-groups (CPU, host
+    transport): rank r sits at position r % (world / groups) of group
+    r // (world / groups); the speculative communicator links one rank of every
+    group and passes the exchange self test (all-gather + broadcast from its
+    last rank, whose global rank differs from its group rank)."""
+    out = _run(world, _hybrid_selftest_worker, (groups,))
+    pp = world // groups
+    for rank, rs, err in out:
+        assert err is None, err
+        assert rs == ((rank // pp, groups), (rank % pp, pp))
+
+
 def test_host_comm_selftest_gloo_world2():
     out = _run(2, _selftest_worker, ())
     for rank, rs, err in out:
@@ -350,6 +379,82 @@ def test_c5_two_ranks_match_one_rank(mode):
     for rank, st, x, err in out:
         assert err is None, err
         assert st["ranks"] == 2
+        _same(st, x, st1, x1)
+
+
+def _hybrid_worker(rank, world, port, q, case, kw, groups, env=None):
+    try:
+        os.environ.update(env or {})
+        dist = _init(rank, world, port)
+        from graphslam_amd import multi_gpu
+        from graphslam_amd.pose_graph import PoseGraph
+        g, init = _graph(case)
+        pg = PoseGraph.from_dataset(g, device=0)
+        pg.set_poses(init)
+        keep = multi_gpu.attach_hybrid(pg, dist, rank, world, groups, transport="host")
+        st = pg.optimize(**kw)
+        st["trace"] = pg.trace()
+        q.put((rank, st, pg.poses(), None))
+        del keep
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, None, repr(e)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,world,groups,lanes,kw", [
+    ("C2p", 4, 2, 1, {}),                    # 2 groups x 2-rank partitions
+    ("C2p", 6, 3, 1, {}),                    # 3 groups x 2
+    ("C2p", 4, 2, 2, {}),                    # ... with 2 lambda lanes per group
+    ("C3", 4, 2, 1, {"max_outer": 3}),
+    ("C5", 4, 2, 1, {"max_outer": 1}),       # BASELINE config C5: 2 groups x 2-rank partitions
+])
+def test_hybrid_matches_one_rank(case, world, groups, lanes, kw):
+    """PGO_MULTI_HYBRID, ranks sharing cuda:0 over gloo sub-groups: each group
+    splits every factorisation over its ranks (subtrees + distributed top) and
+    the groups run the speculative lambda search (one rank of each group per
+    exchange) -- the trajectory and values are bitwise the one-rank run's, and
+    a round covers groups x lanes tries."""
+    st1, x1 = _single(case, kw)
+    out = _run(world, _hybrid_worker, (case, dict(kw, multi_gpu=2, lambda_lanes=lanes), groups), timeout=1200)
+    for rank, st, x, err in out:
+        assert err is None, err
+        assert st["ranks"] == world
+        _same(st, x, st1, x1)
+        if st1["inner_iterations"] > st1["linearizations"] and "max_outer" not in kw:
+            assert st["lambda_rounds"] < st1["lambda_rounds"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,world,groups", [("C2p", 2, 1), ("C3", 2, 1), ("C2p", 4, 2), ("C3", 4, 2)])
+def test_replicated_top_matches_one_rank(case, world, groups):
+    """The replicated top (PGO_DIST_TOP=0: every rank factors the top fronts
+    after one all-gather of the subtree roots' update matrices) -- what the
+    model prices faster than the distributed top at two ranks, so what --multi
+    auto runs there and inside 2-rank hybrid groups -- bitwise the one-rank
+    trajectory, alone (groups 1) and in the hybrid."""
+    kw = {"max_outer": 3} if case == "C3" else {}
+    st1, x1 = _single(case, kw)
+    env = {"PGO_DIST_TOP": "0"}
+    if groups == 1:
+        out = _run(world, _opt_worker, (case, dict(kw, multi_gpu=1, lambda_lanes=1), env), timeout=900)
+    else:
+        out = _run(world, _hybrid_worker, (case, dict(kw, multi_gpu=2, lambda_lanes=1), groups, env), timeout=900)
+    for rank, st, x, err in out:
+        assert err is None, err
+        _same(st, x, st1, x1)
+
+
+@pytest.mark.gpu
+def test_c5_four_ranks_partition_matches_one_rank():
+    """BASELINE config C5 partitioned over four ranks sharing cuda:0 (first
+    linearisation): bitwise the one-rank trajectory and values."""
+    kw = {"max_outer": 1}
+    st1, x1 = _single("C5", kw)
+    out = _run(4, _opt_worker, ("C5", dict(kw, multi_gpu=1, lambda_lanes=1)), timeout=1200)
+    for rank, st, x, err in out:
+        assert err is None, err
+        assert st["ranks"] == 4
         _same(st, x, st1, x1)
 
 

@@ -29,15 +29,37 @@ def test_plan_levels_partition_the_flops():
 
 
 def test_estimate_and_choice():
-    """Estimates are positive and finite; the choice follows the larger one."""
+    """Estimates are positive and finite over the whole sensitivity range; the
+    auto choice is the built mode with the best worst case."""
     from graphslam_amd import multi_model
     pg = _pg()
-    for P in (2, 8):
-        e = multi_model.estimate(pg, P, "C2")
+    pd = multi_model.PlanData(pg, "C2")
+    for P in (2, 4, 8):
+        e = multi_model.estimate(pg, P, "C2", pd=pd)
         for k in ("est_one_gpu_s", "est_replicated_top_s", "est_distributed_top_s"):
             assert np.isfinite(e[k]) and e[k] > 0
         assert e["level_times"].startswith("modelled")   # no measured C2 spans
-        mode = multi_model.choose_mode(e)
-        assert mode == ("partition" if e["est_speedup"] > e["est_speedup_spec"] else "spec")
-        assert multi_model.dist_top(e) == (e["est_speedup_distributed_top"] >= e["est_speedup_replicated_top"])
-    assert multi_model.spec_gain(8) == 2.3 and 1.4 < multi_model.spec_gain(3) < 2.0
+        assert len(e["sensitivity"]) == len(multi_model.B_RANGE) * len(multi_model.T_BCAST_RANGE)
+        for row in e["sensitivity"].values():
+            assert all(np.isfinite(v) and v > 0 for v in row.values())
+        assert set(e["est_speedup_hybrid"]) == {str(G) for G in range(2, P) if P % G == 0}
+        mode, groups, dist = multi_model.choose(e)
+        lo = e["range_min"]
+        best = max(v for k, v in lo.items() if k in ("spec", "partition") or k.startswith("hybrid"))
+        got = lo["partition"] if mode == "partition" else lo["spec"] if mode == "spec" else lo[f"hybrid{groups}"]
+        assert got == best
+        assert e["measured_on_hardware"] is False
+
+
+def test_rounds_follow_the_library_sizing():
+    """One GPU's rounds as pgo_optimize sizes them: one lane expected at the
+    first linearisation and after a first-try acceptance, two after a
+    multi-try one, the rest at all lanes (C3: 13 rounds, 26 factorisations, as
+    the bench's lambda_rounds / solves)."""
+    from graphslam_amd import multi_model
+    r = multi_model.one_gpu_rounds([1, 1, 1, 1, 10, 2, 3, 5], lanes=3)
+    assert len(r) == 13 and sum(r) == 26       # BENCH_r04: 13 lambda rounds, 26 solves
+    assert r[:5] == [1, 1, 1, 1, 1]
+    # spec: ceil(k / P) one-lane rounds
+    _, n = multi_model.trajectory_ms([1, 1, 1, 1, 10, 2, 3, 5], {1: 1.0}, 8)
+    assert n == 9
