@@ -49,7 +49,6 @@ struct CholDev {
   int vst, xst, pst;               // fv, xv, backward partials per lane
   unsigned long long poll_ticks;   // in-launch hand-off: give up after this many 10 ns ticks
   int diag_full;                   // PGO_DIAG_FULL=1 (A/B): diagonal tiles factored over all four 16-column blocks
-  int diag16;                      // PGO_DIAG16=1 (A/B): round 4's 16-column-block factor (diag_factor_invert)
 };
 
 // this workgroup's lane (blockIdx.y): every lane factors H + lambda_y I with
@@ -77,8 +76,6 @@ static CholDev dev_view(const CholPlan& P) {
   c.ns = P.ns;
   static const int diag_full = getenv("PGO_DIAG_FULL") && atoi(getenv("PGO_DIAG_FULL")) == 1;
   c.diag_full = diag_full;
-  static const int diag16 = getenv("PGO_DIAG16") && atoi(getenv("PGO_DIAG16")) == 1;
-  c.diag16 = diag16;
   c.fst = P.ftotal;
   c.tst = 2 * P.ttotal;
   c.tfo = P.ttotal;
@@ -1176,220 +1173,6 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
   return bad;
 }
 
-// (i, j) of the q-th element of an 8x8 lower triangle in P8 order (q < 36)
-__device__ __forceinline__ void unp8(int q, int& i, int& j) {
-  i = 0;
-  while (q > i) {
-    q -= i + 1;
-    i++;
-  }
-  j = q;
-}
-
-// Round 5: the same contract as diag_factor_invert (T: the 64x64 SPD tile in
-// LDS, ld 65, lower valid, identity beyond the live size nbl -> L; W: -> X =
-// L^-1, lower; bc: 64 doubles of scratch; wave 0 returns whether a pivot was
-// not positive and finite), over 8-column blocks J with the four waves
-// overlapped instead of wave 0 alone on 16-column blocks:
-//   B0(J)  wave 0 (the chain): chol8 of the updated A_JJ in registers (every
-//          lane the same values), then the rows below by forward substitution
-//          against that L_JJ, one row per lane (no inverse on the chain), L
-//          stored;  waves 1-2 meanwhile: block J-1's update of the columns
-//          past block J+1 (one task per row and 8-column block);  wave 3: X_JJ
-//          of block J-1 (inv8, lane-local).
-//   B1(J)  wave 0: the next diagonal block's update (one element per lane)
-//          and its reload;  waves 1-2: the next column block's rows below it.
-// then X's off-diagonal 16x16 blocks by 16x16x16 MFMA products (one wave
-// each): X_IJ = -X_II sum_K L_IK X_KJ, by distance from the diagonal.
-// Every element sees a fixed sequence of operations: bitwise reproducible.
-__device__ __forceinline__ bool diag_factor_invert8(double* T, double* W, double* bc, int nbl = 64) {
-  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
-  const int Jn = (nbl + 7) >> 3, R = 8 * Jn;   // 8-blocks with live columns; rows / columns processed
-  bool bad = false;
-  double a[36], iv[8];
-  auto ldT = [&](int i, int j) -> double& { return T[i + j * 65]; };
-  auto ldW = [&](int i, int j) -> double& { return W[i + j * 65]; };
-  DIAG_CLK(0);
-  if (wv == 0) {
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-      for (int j = 0; j <= i; j++) a[P8(i, j)] = ldT(i, j);
-  }
-  for (int J = 0; J < Jn; J++) {
-    const int o = 8 * J;
-    // ---------------- B0(J)
-    if (wv == 0) {
-      const int i = o + 8 + l;
-      const bool rv = i < R;
-      double x[8];
-#pragma unroll
-      for (int c = 0; c < 8; c++) x[c] = rv ? ldT(i, o + c) : 0.0;   // final: updated by every block < J
-      bad = chol8_lane(a, iv) || bad;
-#pragma unroll
-      for (int c = 0; c < 8; c++) {   // forward substitution: x_c = (a_ic - sum_{k<c} x_k L_ck) / L_cc
-        x[c] *= iv[c];
-#pragma unroll
-        for (int d = c + 1; d < 8; d++) x[d] = fma(-x[c], a[P8(d, c)], x[d]);
-      }
-      if (rv) {
-#pragma unroll
-        for (int c = 0; c < 8; c++) ldT(i, o + c) = x[c];
-      }
-      if (l == 0) {
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-          bc[o + r] = iv[r];
-#pragma unroll
-          for (int c = 0; c <= r; c++) ldT(o + r, o + c) = a[P8(r, c)];
-        }
-      }
-    } else if (J >= 1 && wv < 3) {
-      // block J-1's update of columns [8(J+1), R): task (row i, 8-block K),
-      // K > J, i >= 8K: A(i, 8K + r) -= sum_k L(i, o' + k) L(8K + r, o' + k)
-      const int op = o - 8;
-      int t = tid - 64;
-      for (int K = J + 1; K < Jn; K++) {
-        const int rows = R - 8 * K;
-        for (; t < rows; t += 128) {
-          const int i = 8 * K + t;
-          double li[8];
-#pragma unroll
-          for (int k = 0; k < 8; k++) li[k] = ldT(i, op + k);
-#pragma unroll
-          for (int r = 0; r < 8; r++) {
-            if (8 * K + r > i) break;
-            double s = ldT(i, 8 * K + r);
-#pragma unroll
-            for (int k = 0; k < 8; k++) s = fma(-li[k], ldT(8 * K + r, op + k), s);
-            ldT(i, 8 * K + r) = s;
-          }
-        }
-        t -= rows;
-      }
-    } else if (J >= 1 && wv == 3) {
-      // X_JJ of block J-1: inv8 of L_{J-1,J-1} (lane-local), stored to W
-      const int op = o - 8;
-      double b[36], jv[8];
-#pragma unroll
-      for (int r = 0; r < 8; r++) {
-        jv[r] = bc[op + r];
-#pragma unroll
-        for (int c = 0; c <= r; c++) b[P8(r, c)] = ldT(op + r, op + c);
-      }
-      inv8_lane(b, jv);
-      if (l == 0) {
-#pragma unroll
-        for (int r = 0; r < 8; r++)
-#pragma unroll
-          for (int c = 0; c <= r; c++) ldW(op + r, op + c) = b[P8(r, c)];
-      }
-    }
-    __syncthreads();
-    DIAG_CLK(1 + (J & 3));
-    if (J == Jn - 1) break;
-    // ---------------- B1(J)
-    const int on = o + 8;   // the next block
-    if (wv == 0) {
-      if (l < 36) {   // A_{J+1,J+1} -= L_{J+1,J} L_{J+1,J}'
-        int r, c;
-        unp8(l, r, c);
-        double s = ldT(on + r, on + c);
-#pragma unroll
-        for (int k = 0; k < 8; k++) s = fma(-ldT(on + r, o + k), ldT(on + c, o + k), s);
-        ldT(on + r, on + c) = s;
-      }
-      __builtin_amdgcn_wave_barrier();   // (one wave: its LDS accesses complete in order)
-#pragma unroll
-      for (int i = 0; i < 8; i++)
-#pragma unroll
-        for (int j = 0; j <= i; j++) a[P8(i, j)] = ldT(on + i, on + j);
-    } else if (wv < 3) {
-      // the next column block below its diagonal block: rows [on + 8, R)
-      const int rows = R - on - 8;
-      for (int e = tid - 64; e < rows * 8; e += 128) {
-        const int i = on + 8 + (e >> 3), c = e & 7;
-        double s = ldT(i, on + c);
-#pragma unroll
-        for (int k = 0; k < 8; k++) s = fma(-ldT(i, o + k), ldT(on + c, o + k), s);
-        ldT(i, on + c) = s;
-      }
-    }
-    __syncthreads();
-  }
-  // the last block's X_JJ, and identity for a padded 8-block of the last
-  // 16-block (X's 16x16 algebra below runs on whole 16-blocks)
-  const int J16 = (R + 15) >> 4;
-  if (wv == 3) {
-    const int op = R - 8;
-    double b[36], jv[8];
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-      jv[r] = bc[op + r];
-#pragma unroll
-      for (int c = 0; c <= r; c++) b[P8(r, c)] = ldT(op + r, op + c);
-    }
-    inv8_lane(b, jv);
-    if (l == 0) {
-#pragma unroll
-      for (int r = 0; r < 8; r++)
-#pragma unroll
-        for (int c = 0; c <= r; c++) ldW(op + r, op + c) = b[P8(r, c)];
-    }
-  } else if (wv == 2 && (R & 15) && l < 64) {   // rows / columns [R, R + 8): L = I (T is identity there), X = I
-    const int r = l >> 3, c = l & 7;
-    ldW(R + r, R + c) = r == c ? 1.0 : 0.0;
-    ldW(R + r, R - 8 + c) = 0.0;
-  }
-  __syncthreads();
-  DIAG_CLK(5);
-  // X's 16x16 diagonal blocks: X_ba = -X_bb (L_ba X_aa), one wave per block
-  if (wv < J16) {
-    const int b0 = 16 * wv, r = l >> 3, c = l & 7;
-    double y = 0.0;   // (L_ba X_aa)(r, c), X_aa(k, c) = 0 for k < c
-#pragma unroll
-    for (int k = 0; k < 8; k++) y = fma(ldT(b0 + 8 + r, b0 + k), k >= c ? ldW(b0 + k, b0 + c) : 0.0, y);
-    ldW(b0 + 8 + r, b0 + c) = y;
-    __builtin_amdgcn_wave_barrier();
-    double z = 0.0;   // X_bb(r, k) = 0 for k > r
-#pragma unroll
-    for (int k = 0; k < 8; k++) z = fma(k <= r ? ldW(b0 + 8 + r, b0 + 8 + k) : 0.0, ldW(b0 + 8 + k, b0 + c), z);
-    __builtin_amdgcn_wave_barrier();
-    ldW(b0 + 8 + r, b0 + c) = -z;
-  }
-  __syncthreads();
-  // off-diagonal 16x16 blocks by distance d from the diagonal: S = sum_K
-  // L_IK X_KJ into W_IJ, then W_IJ = -X_II S (one wave per block)
-  for (int d = 1; d < J16; d++) {
-    const int I = wv + d, Jb = wv;
-    if (I < J16) {
-      const int oi = 16 * I, oj = 16 * Jb;
-      d4 s = {0, 0, 0, 0};
-      for (int K = Jb; K < I; K++) {
-        const int ok = 16 * K;
-        const d4 p = mm16(T + oi + ok * 65, 1, 65, W + ok + oj * 65, 1, 65);
-#pragma unroll
-        for (int q = 0; q < 4; q++) s[q] += p[q];
-      }
-      st16(W + oi + oj * 65, s, false);
-      __builtin_amdgcn_wave_barrier();
-      const d4 v = mm16(W + oi + oi * 65, 1, 65, W + oi + oj * 65, 1, 65);
-      __builtin_amdgcn_wave_barrier();
-      st16(W + oi + oj * 65, -v, false);
-    }
-    __syncthreads();
-  }
-  DIAG_CLK(12);
-  return bad;
-}
-
-// the diagonal tile's factor + inverse: the 8-column-block form, or round 4's
-// (PGO_DIAG16=1, A/B)
-__device__ __forceinline__ bool factor_invert(const CholDev& c, double* T, double* W, double* bc, int nb) {
-  const int nbl = c.diag_full ? 64 : nb;
-  return c.diag16 ? diag_factor_invert(T, W, bc, nbl) : diag_factor_invert8(T, W, bc, nbl);
-}
-
 // ---- in-launch hand-off of a diagonal tile's inverse (MI355X_MICROARCH.md,
 // inter-workgroup visibility, the "sc1 stores / sc1 flag / sc1 loads" row): the
 // diagonal workgroup stores the inverse (trsm operand order) and the panel's y
@@ -1939,7 +1722,7 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
     Ws[i + j * 65] = 0.0;
   }
   __syncthreads();
-  if (factor_invert(c, Ts, Ws, bc, nb)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (diag_factor_invert(Ts, Ws, bc, c.diag_full ? 64 : nb)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   STAMP(slot, 2);
   double* Fs = fcol(c.F + c.foff[s], m, true, kn) + kn;   // the diagonal tile, ld m - kn
   double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;   // row-major L^-1 of the tile
@@ -1981,7 +1764,7 @@ __device__ __forceinline__ void first_diag_body(const CholDev& c, int s, double*
     Ws[i + j * 65] = 0.0;
   }
   __syncthreads();
-  if (factor_invert(c, Ts, Ws, bc, nb)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (diag_factor_invert(Ts, Ws, bc, c.diag_full ? 64 : nb)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   double* M = c.Tinv + c.toff[s];
   double* v = c.fv + c.voff[s];
   publish_inverse(M + c.tfo, Ws, nb);
