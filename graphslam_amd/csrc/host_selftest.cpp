@@ -84,11 +84,11 @@ void step_keys(const pgo::CholPlan& P, const pgo::PanelStep& ps, std::map<Key, i
       for (int col = c0; col < cend; col++)
         if (col <= r0 + 63) out[Key(0, s, r0, col, t.w)]++;
   }
-  for (int q = ps.sdiag_off; q < ps.sdiag_off + ps.sdiag_cnt + ps.fused_cnt; q++) {
+  for (int q = ps.sdiag_off; q < ps.sdiag_off + ps.sdiag_cnt; q++) {
     const int4 t = P.sdiag_tasks[q];
     out[Key(1, t.x, t.y, t.z, t.w)]++;
   }
-  for (int q = ps.col_off; q < ps.col_off + ps.fcol_cnt + 2 * ps.fused_cnt + ps.col_cnt + ps.prep_cnt; q++) {
+  for (int q = ps.col_off; q < ps.col_off + ps.fcol_cnt + ps.col_cnt + ps.prep_cnt; q++) {
     const int4 t = P.col_tasks[q];
     out[Key(2, t.x, t.y, t.z, t.w)]++;
   }
@@ -334,51 +334,6 @@ int check_append(const Pattern& G, int n0, int ordering) {
   return 0;
 }
 
-// The fused look-ahead tasks (PanelStep::fused_cnt) against the unfused plan
-// (PGO_FUSE_DIAG=0) of the same pattern: per level the same tasks, a fused
-// diagonal in the step before the one that would factor it, the column and
-// prep parts in their own step.
-int check_fused(const Pattern& G, int ordering, int* nfused) {
-  pgo::CholPlan F, U;
-  F.ordering = U.ordering = ordering;
-  pgo::chol_analyze(F, G.n, G.row_ptr, G.col);
-  setenv("PGO_FUSE_DIAG", "0", 1);
-  pgo::chol_analyze(U, G.n, G.row_ptr, G.col);
-  unsetenv("PGO_FUSE_DIAG");
-  if (F.schedule_error || U.schedule_error || F.levels.size() != U.levels.size()) return fail("fused: plans");
-  *nfused = 0;
-  using SK = std::tuple<int, int, int, int, int, int>;   // (step, kind, task)
-  for (size_t L = 0; L < F.levels.size(); L++) {
-    std::map<SK, int> a, b;
-    auto add = [](std::map<SK, int>& m, int j, int kind, int4 t) { m[SK(j, kind, t.x, t.y, t.z, t.w)]++; };
-    const auto& pf = F.levels[L].panels;
-    const auto& pu = U.levels[L].panels;
-    if (pf.size() != pu.size()) return fail("fused: steps");
-    for (size_t j = 0; j < pu.size(); j++) {
-      const pgo::PanelStep& u = pu[j];
-      if (u.fused_cnt) return fail("fused: PGO_FUSE_DIAG=0 plan has fused tasks");
-      for (int q = u.sdiag_off; q < u.sdiag_off + u.sdiag_cnt; q++) add(b, (int)j, 1, U.sdiag_tasks[q]);
-      for (int q = u.col_off; q < u.col_off + u.fcol_cnt + u.col_cnt + u.prep_cnt; q++) add(b, (int)j, 2, U.col_tasks[q]);
-      const pgo::PanelStep& f = pf[j];
-      *nfused += f.fused_cnt;
-      for (int q = f.sdiag_off; q < f.sdiag_off + f.sdiag_cnt; q++) add(a, (int)j, 1, F.sdiag_tasks[q]);
-      for (int q = f.sdiag_off + f.sdiag_cnt; q < f.sdiag_off + f.sdiag_cnt + f.fused_cnt; q++)
-        add(a, (int)j + 1, 1, F.sdiag_tasks[q]);
-      for (int q = f.col_off; q < f.col_off + f.fcol_cnt + 2 * f.fused_cnt + f.col_cnt + f.prep_cnt; q++)
-        add(a, (int)j, 2, F.col_tasks[q]);
-      for (int f2 = 0; f2 < f.fused_cnt; f2++) {   // parts of one front, the next panel's column tile
-        const int4 d = F.sdiag_tasks[f.sdiag_off + f.sdiag_cnt + f2];
-        const int4 c = F.col_tasks[f.col_off + f.fcol_cnt + f2];
-        const int4 p = F.col_tasks[f.col_off + f.fcol_cnt + f.fused_cnt + f.col_cnt + f.prep_cnt + f2];
-        if (c.x != d.x || p.x != d.x || c.y != d.y || p.y != d.y || p.z != d.y || c.z + pgo::kNB != d.y)
-          return fail("fused: parts of a task disagree");
-      }
-    }
-    if (a != b) return fail("fused: tasks differ from the unfused plan");
-  }
-  return 0;
-}
-
 }  // namespace
 
 int main() {
@@ -401,9 +356,6 @@ int main() {
     if (P.schedule_error) return fail("panel schedule bookkeeping");
     if (!pgo::chol_covers(P, G.n, G.row_ptr, G.col)) return fail("plan does not cover its own pattern");
     if (check_assembly(P) || check_tiles(P) || check_sources(P, G.row_ptr, G.col)) return 1;
-    int nfu = 0;
-    if (check_fused(G, ordering, &nfu)) return 1;
-    std::printf("fused look-ahead tasks (look-ahead threshold %s, ordering %d): %d\n", *la ? la : "default", ordering, nfu);
     for (int size : {2, 4}) {
       std::vector<double> rf;
       double top = 0;
@@ -460,9 +412,6 @@ int main() {
     pgo::CholPlan P;
     pgo::chol_analyze(P, G.n, G.row_ptr, G.col);
     if (check_tiles(P)) return 1;
-    int nfu = 0;
-    if (check_fused(G, pgo::kOrderNd, &nfu)) return 1;
-    std::printf("grid plan: %d fused look-ahead tasks\n", nfu);
     for (int size : {2, 3, 4, 8})
       if (check_distributed(G, pgo::kOrderNd, size)) return 1;
     int maxw = 0;

@@ -2550,7 +2550,7 @@ int pgo_debug_plan(pgo_graph* g, double* out, int cap) {
   for (const auto& lv : P.levels) {
     lf += (long long)lv.ea_off.size() + 1 + lv.small.size();
     for (const auto& ps : lv.panels)
-      lf += (ps.potrf_cnt > 0) + (ps.sdiag_cnt + ps.fused_cnt + ps.col_cnt + ps.prep_cnt + (ps.syrk_inline ? ps.syrk_cnt : 0) > 0) +
+      lf += (ps.potrf_cnt > 0) + (ps.sdiag_cnt + ps.col_cnt + ps.prep_cnt + (ps.syrk_inline ? ps.syrk_cnt : 0) > 0) +
             (ps.syrk_cnt > 0 && !ps.syrk_inline) + (ps.far_cnt > 0);
     ls += (lv.bwd_part.cnt > 0) + (long long)lv.bwd.size();
     for (const auto& ps : lv.panels) {

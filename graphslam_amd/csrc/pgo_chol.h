@@ -66,11 +66,6 @@ struct PanelStep {                 // one 64-column panel kb of every big front 
   int prep_cnt = 0;                // prep tiles (front, r0, kn + 64, k0): the block after next brought up
                                    // to panel kb (k_step workgroups, look-ahead fronts)
   int sdiag_off, sdiag_cnt;        // next panel's diagonal tiles (front, kn, kn, kb) updated + factored (k_step)
-  int fused_cnt = 0;               // fused look-ahead tasks (k_step, after the diagonal workgroups): the first
-                                   // column tile below the next panel's diagonal solved, the diagonal tile after
-                                   // it brought up (prep) and the panel after next's diagonal factored -- parts
-                                   // at sdiag_tasks[sdiag_off + sdiag_cnt + f], col_tasks[col_off + fcol_cnt + f]
-                                   // and col_tasks[col_off + fcol_cnt + fused_cnt + col_cnt + prep_cnt + f]
   int syrk_off, syrk_cnt;          // the other Schur-update tiles (front, row0, col0, kb)
   int syrk_tile;                   // kTile or kBigTile
   int syrk_inline;                 // 1: the (64-)tiles are k_step workgroups, 0: a concurrent launch

@@ -42,7 +42,6 @@ struct CholDev {
   const int *dg_front, *dg_loc, *perm;
   int* flag;
   int* stepflag;                   // [lane][ns] in-launch hand-off of the diagonal inverses
-  int* prepflag;                   // [lane][ns] ... of a fused task's diagonal tile after its prep (col0 / 64 + 1)
   int ns;
   // lambda lanes: lane y = blockIdx.y works on its own numeric workspace
   long long fst, tst;              // F, Tinv doubles per lane
@@ -62,7 +61,6 @@ __device__ __forceinline__ void lane_offset(CholDev& c) {
   c.xv += y * c.xst;
   c.flag += y;
   c.stepflag += (long long)y * c.ns;
-  c.prepflag += (long long)y * c.ns;
 }
 
 static CholDev dev_view(const CholPlan& P) {
@@ -75,7 +73,6 @@ static CholDev dev_view(const CholPlan& P) {
   c.asm_src = P.d_asm_src; c.dg_front = P.d_dg_front; c.dg_loc = P.d_dg_loc; c.perm = P.d_perm;
   c.flag = P.d_flag;
   c.stepflag = P.d_stepflag;
-  c.prepflag = P.d_stepflag + (long long)std::max(P.batch, 1) * std::max(P.ns, 1);   // (numeric_need: 2 regions)
   c.ns = P.ns;
   static const int diag_full = getenv("PGO_DIAG_FULL") && atoi(getenv("PGO_DIAG_FULL")) == 1;
   c.diag_full = diag_full;
@@ -1497,9 +1494,7 @@ __global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int4* __res
 // per chunk, issued one chunk ahead of the MFMAs).  Low register count, so
 // several workgroups per CU hide the load latency.
 // smem: 4 * 16 * 68 doubles (Sr[2], Sc[2])
-// kPub (a fused task's diagonal tile, k_step): the tile's stores go out sc1 and
-// the workgroup then publishes prepflag[front] = col0 / 64 + 1 (in-launch hand-off)
-template <bool kPrefC = false, bool kPub = false>   // kPrefC: the C tile's loads issued before the k loop
+template <bool kPrefC = false>   // true: the C tile's loads issued before the k loop (latency under the MFMAs)
 __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, int kb, double* smem) {
   constexpr int LD = 64 + 4;
   double(*Sr)[16 * LD] = reinterpret_cast<double(*)[16 * LD]>(smem);
@@ -1589,19 +1584,15 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
     if (ch + 1 < nch) stash(b ^ 1);
     __syncthreads();
   }
-  if (!active && !kPub) return;
+  if (!active) return;
   if (!kPrefC) load_c();
 #pragma unroll
   for (int p = 0; p < 8; p++)
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int row = row0 + qi + 16 * h + (l & 15), col = col0 + qj + 4 * p + lk;
-      if (active && row < m && col < colend && row >= col) {
-        if (kPub) st_sc1(Cb + row + (size_t)(col - col0) * ldc, cold[p][h] - acc[p][h]);
-        else Cb[row + (size_t)(col - col0) * ldc] = cold[p][h] - acc[p][h];
-      }
+      if (row < m && col < colend && row >= col) Cb[row + (size_t)(col - col0) * ldc] = cold[p][h] - acc[p][h];
     }
-  if (kPub) publish_step(c.prepflag + s, col0 / 64 + 1);
 }
 
 __global__ __launch_bounds__(256) void k_panel_syrk_lds(CholDev c, const int4* __restrict__ tasks, int kb) {
@@ -1623,8 +1614,6 @@ __global__ __launch_bounds__(256) void k_panel_syrk_lds_pc(CholDev c, const int4
 // flight during the MFMAs; the 10 lower 16x16 blocks are dealt 3/3/2/2 to the
 // waves.  Elements outside the live nb x nb block (nb < 64 at a front's last
 // panel) are written back to F here; the caller factors the live block.
-// kSc1C: the C tile is another workgroup's sc1 hand-off (a fused task's prep)
-template <bool kSc1C = false>
 __device__ __forceinline__ void diag_tile_update(const CholDev& c, const int4 t, int kb, double* Ts, double* Sp) {
   constexpr int LD = 68;
   const int s = t.x, r0 = t.y;
@@ -1654,8 +1643,7 @@ __device__ __forceinline__ void diag_tile_update(const CholDev& c, const int4 t,
 #pragma unroll
   for (int q = 0; q < 16; q++) {
     const int idx = tid + 256 * q, i = idx & 63, j = idx >> 6;
-    const bool in = i >= j && r0 + i < m && r0 + j < colend;
-    cv[q] = in ? (kSc1C ? ld_sc1(Db + i + (size_t)j * ldd) : Db[i + (size_t)j * ldd]) : 0.0;
+    cv[q] = (i >= j && r0 + i < m && r0 + j < colend) ? Db[i + (size_t)j * ldd] : 0.0;
   }
   load(0);
 #pragma unroll
@@ -1712,7 +1700,6 @@ __device__ __forceinline__ void diag_tile_update(const CholDev& c, const int4 t,
 // smem: kDiagSmem = 64*65 + 64*68 + 2*64 doubles.
 constexpr int kDiagSmem = 64 * 65 + 64 * 68 + 2 * 64;
 
-template <bool kSc1C = false>
 __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, int kb, double* smem, int slot = -1) {
   double* Ts = smem;
   double* Ws = smem + 64 * 65;
@@ -1723,7 +1710,7 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
   const int nb = min(kNB, w - kn);
   const int tid = threadIdx.x;
   STAMP(slot, 0);
-  diag_tile_update<kSc1C>(c, t, kb, Ts, Ws);
+  diag_tile_update(c, t, kb, Ts, Ws);
   __syncthreads();
   STAMP(slot, 1);
   double keep[16];
@@ -1909,45 +1896,16 @@ __global__ __launch_bounds__(256) void k_first_trsm(CholDev c, const int4* __res
 //   the rest            the other Schur-update tiles (syrk_lds_body)
 // The diagonal workgroups come first in dispatch order, so every waiting
 // workgroup waits on a workgroup dispatched before it.
-//   [nsd, nsd + 2 nfu)  fused look-ahead tasks (PanelStep::fused_cnt): first
-//                       the diagonal tiles after next brought up with their
-//                       prep tiles and handed off (prepflag), then per task the
-//                       column tile right below the next panel's diagonal
-//                       updated and solved (as a column workgroup), then in the
-//                       same workgroup that diagonal tile (once handed off)
-//                       updated with the panel just solved, factored and
-//                       published for the next launch -- the same bodies,
-//                       bitwise the unfused factor; the chain runs on from the
-//                       solve into the next factor without a launch boundary
-__global__ __launch_bounds__(256, 2) void k_step(CholDev c, const int4* __restrict__ sdiag, int nsd, int nfu,
+__global__ __launch_bounds__(256, 2) void k_step(CholDev c, const int4* __restrict__ sdiag, int nsd,
                                               const int4* __restrict__ col, int ncol, int nprep,
                                               const int4* __restrict__ tiles, int kb, int slot) {
   lane_offset(c);
   __shared__ __attribute__((aligned(16))) double smem[kDiagSmem];
-  int b = blockIdx.x;
+  const int b = blockIdx.x;
   if (b < nsd) {
     syrk_diag_body(c, sdiag[b], kb, smem, b == 0 && blockIdx.y == 0 ? slot : -1);
     return;
   }
-  if (b < nsd + nfu) {   // a fused task's diagonal tile brought up (prep), handed off
-    syrk_lds_body<false, true>(c, col[nfu + ncol + nprep + b - nsd], kb, smem);
-    return;
-  }
-  if (b < nsd + 2 * nfu) {
-    const int f = b - nsd - nfu;
-    const int4 ct = col[f];   // (front, kn + 64, kn, kw)
-    syrk_tile64<true>(c, ct, kb, smem);
-    __syncthreads();
-    const int s = ct.x, kn = ct.z, nb = min(kNB, c.w[s] - kn);
-    wait_step(c, c.stepflag + s, kn / 64 + 1);
-    trsm_rows(c, s, ct.y, kn, nb, smem, 1, 65, smem + 64 * 65);
-    __syncthreads();   // (the solved rows and frontal vector are this workgroup's stores)
-    wait_step(c, c.prepflag + s, ct.y / 64 + 1);
-    syrk_diag_body<true>(c, sdiag[nsd + f], kb + kNB, smem);
-    return;
-  }
-  b -= 2 * nfu;
-  col += nfu;
   if (b < nsd + ncol) {
     const int sl = b == nsd && blockIdx.y == 0 ? slot : -1;
     STAMP(sl, 5);
@@ -2628,7 +2586,7 @@ static NumericCap numeric_need(const CholPlan& P, int nb) {
   c.T = nb * std::max<long long>(2 * P.ttotal, 1);
   c.v = (long long)nb * std::max(P.vtotal, 1);
   c.x = (long long)nb * std::max(3 * P.n, 1);
-  c.sf = 2LL * nb * std::max(P.ns, 1);   // stepflag, prepflag
+  c.sf = (long long)nb * std::max(P.ns, 1);
   c.part = (long long)nb * std::max(P.npart, 1) * 64;
   return c;
 }
@@ -2988,8 +2946,6 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
          B256, 0, s, c, b, scale_b, P.n);
   CH_TRY(hipMemsetAsync(P.d_flag, 0, sizeof(int) * nb, s));
   CH_TRY(hipMemsetAsync(P.d_stepflag, 0, sizeof(int) * std::max(P.ns, 1) * nb, s));
-  CH_TRY(hipMemsetAsync(P.d_stepflag + (long long)std::max(P.batch, 1) * std::max(P.ns, 1), 0,
-                        sizeof(int) * std::max(P.ns, 1) * nb, s));   // prepflag
   const bool part = P.part_size > 1;
   if (part && (!hook || !hook->allgather || (!P.xchg.empty() && !hook->broadcast))) return hipErrorInvalidValue;
   auto exchange = [&]() -> hipError_t {   // subtree roots -> every rank
@@ -3165,7 +3121,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       const int4* tiles = (const int4*)(P.d_syrk + ps.syrk_off);
       const int nin = ps.syrk_inline && !off("plain") ? ps.syrk_cnt : 0;
       const bool apart = ps.syrk_cnt > 0 && !ps.syrk_inline && !off("plain");   // plain tiles in their own launch
-      const bool step = ps.sdiag_cnt + ps.fused_cnt + ps.col_cnt + ps.prep_cnt + nin > 0 && !off("step");
+      const bool step = ps.sdiag_cnt + ps.col_cnt + ps.prep_cnt + nin > 0 && !off("step");
       auto plain = [&](hipStream_t st, int first, int cnt, double flops) {
         const bool big = ps.syrk_tile == kBigTile;
         launch(prof, big ? kFamPanelSyrk128 : kFamPanelSyrk, [&] { return make_double2(flops * nb, 0); },
@@ -3183,9 +3139,7 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       // registers while they wait; same arithmetic (the tile kernels compute a
       // tile's elements alike), bitwise k_step's factor
       const int step_split = step_split_threshold();
-      // (a step with fused look-ahead tasks runs as one k_step)
-      const bool split = step && step_split > 0 && ps.sdiag_cnt * nb >= step_split && ps.col_cnt > 0 &&
-                         ps.fused_cnt == 0;
+      const bool split = step && step_split > 0 && ps.sdiag_cnt * nb >= step_split && ps.col_cnt > 0;
       if (split) {
         const int4* cupd = cols + ps.fcol_cnt;   // col then prep tasks: 64x64 tile updates
         CH_TRY(hipEventRecord(P.evs[0], s));
@@ -3203,9 +3157,8 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
                dim3(ps.col_cnt, nb), B256, 0, s, c, cupd);
       } else if (step)
         launch(prof, kFamStep, [&] { return make_double2(ps.step_flops * nb, 0); }, k_step,
-               dim3(ps.sdiag_cnt + 2 * ps.fused_cnt + ps.col_cnt + ps.prep_cnt + nin, nb), B256, 0, s, c,
-               (const int4*)(P.d_sdiag + ps.sdiag_off), ps.sdiag_cnt, ps.fused_cnt, cols + ps.fcol_cnt, ps.col_cnt,
-               ps.prep_cnt,
+               dim3(ps.sdiag_cnt + ps.col_cnt + ps.prep_cnt + nin, nb), B256, 0, s, c,
+               (const int4*)(P.d_sdiag + ps.sdiag_off), ps.sdiag_cnt, cols + ps.fcol_cnt, ps.col_cnt, ps.prep_cnt,
                tiles, ps.kb,
                stamps && li + 1 == P.levels.size() && ps.kb / kNB < kMaxStampSlots ? ps.kb / kNB : -1);
       if (apart) {   // (never on the main stream: an earlier plain may still run on P.side)

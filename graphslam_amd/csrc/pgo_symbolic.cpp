@@ -739,16 +739,6 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
     // marks the plan invalid (schedule_error).
     std::vector<std::vector<int>> applied(big.size());
     for (size_t i = 0; i < big.size(); i++) applied[i].assign(P.m[big[i]], 0);
-    // Fused look-ahead chain (round 5, one-rank plans, look-ahead fronts): the
-    // next step's diagonal tile is factored in this step's launch by the
-    // workgroup that solves the column tile right below this step's diagonal
-    // (the one the next diagonal update reads) after bringing that tile up with
-    // its prep tile -- the three existing task bodies in sequence, the same
-    // arithmetic: bitwise the unfused factor.  fused_pred[i]: the next step's
-    // diagonal task as fused here (.x = -1: none), checked against the task
-    // that step computes.  (PGO_FUSE_DIAG=0: off, an A/B knob.)
-    const bool fuse_on = !(getenv("PGO_FUSE_DIAG") && atoi(getenv("PGO_FUSE_DIAG")) == 0) && P.part_size <= 1;
-    std::vector<int4> fused_pred(big.size(), make_int4(-1, 0, 0, 0));
     auto uniform = [&](size_t i, int c0, int c1, int k0) {
       for (int j = c0; j < c1; j++)
         if (applied[i][j] != k0) return false;
@@ -772,7 +762,6 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       ps.syrk_off = (int)S.syrk_tasks.size();
       ps.potrf_off = (int)S.potrf_list.size();
       ps.sdiag_off = (int)S.sdiag_tasks.size();
-      std::vector<int4> fu_col, fu_prep, fu_diag;   // this step's fused tasks' parts
       // first panel of a front: k_panel_first (diagonal + trsm waiters)
       std::vector<int4> xfirst, xstep;   // distributed top: panels factored by the first / the step launch
       for (int s : big) {
@@ -876,29 +865,13 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
           const int depth = kn - k0, kw = inner ? (k0 | (int)0x80000000) : k0;
           if (dist) xstep.push_back(make_int4(s, kn, nb2, cowner(s, kn)));
           const bool own = mine(s, kn);
-          const int4 sd = make_int4(s, kn, kn, kw);
-          const bool done = fused_pred[i].x == s;   // factored in the previous step's launch
-          if (done && (fused_pred[i].y != sd.y || fused_pred[i].w != sd.w)) {
-            if (getenv("PGO_SCHED_DEBUG") && !S.schedule_error)
-              fprintf(stderr, "sched: fused diag front %d kb %d predicted (%d, %d) got (%d, %d)\n", s, kb,
-                      fused_pred[i].y, fused_pred[i].w, sd.y, sd.w);
-            S.schedule_error = true;
-          }
-          fused_pred[i].x = -1;
-          if (own && !done) S.sdiag_tasks.push_back(sd);
+          if (own) S.sdiag_tasks.push_back(make_int4(s, kn, kn, kw));
           const double fd = (double)depth * kNB * (kNB + 1) + 2.0 * nb2 * nb2 * (double)nb2 / 3.0 +
                             (double)std::min(kNB - nb2, m - kn - nb2) * nb2 * nb2;
-          if (!done) {   // (a fused diagonal's flops went to the previous step)
-            ps.step_flops += fd;
-            ps.diag_flops += fd;
-          }
-          // fuse the next step's diagonal into this step: its tile is brought up by
-          // this step's prep (whole blocks only) and the column tile below this
-          // step's diagonal is this front's first column task
-          const bool fuse = fuse_on && own && has_prep(s, kn) && kn + kNB < m;
+          ps.step_flops += fd;
+          ps.diag_flops += fd;
           for (int r0 = kn + kNB; r0 < m; r0 += kNB) {
-            if (own && fuse && r0 == kn + kNB) fu_col.push_back(make_int4(s, r0, kn, kw));
-            else if (own) S.col_tasks.push_back(make_int4(s, r0, kn, kw));
+            if (own) S.col_tasks.push_back(make_int4(s, r0, kn, kw));
             const int rows = std::min(kNB, m - r0);
             ps.step_flops += 2.0 * depth * rows * (c1 - kn) + (double)rows * nb2 * nb2;
             ps.colupd_flops += 2.0 * depth * rows * (c1 - kn);
@@ -915,21 +888,8 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
           }
           for (int j = b0; j < b1; j++) applied[i][j] = kn;
           touch.back()[i] = std::max(touch.back()[i], b1);
-          const bool fuse = fuse_on && mine(s, kn) && mine(s, b0) && kn + kNB < m;   // (as the column tasks' test)
           if (mine(s, b0))
-            for (int r0 = b0; r0 < m; r0 += kNB) {
-              if (fuse && r0 == b0) fu_prep.push_back(make_int4(s, r0, b0, k0));
-              else prep.push_back(make_int4(s, r0, b0, k0));
-            }
-          if (fuse) {   // the next step's diagonal task as that step will compute it (depth one panel)
-            const int kb2 = kn, kn2 = b0, bs2 = kb2 & ~(kKB - 1), be2 = std::min(bs2 + kKB, w);
-            const int kw2 = kn2 < be2 ? (kn | (int)0x80000000) : kn;
-            fu_diag.push_back(make_int4(s, kn2, kn2, kw2));
-            fused_pred[i] = fu_diag.back();
-            const double fd2 = (double)kNB * kNB * (kNB + 1) + 2.0 * kNB * kNB * (double)kNB / 3.0;
-            ps.step_flops += fd2;
-            ps.diag_flops += fd2;
-          }
+            for (int r0 = b0; r0 < m; r0 += kNB) prep.push_back(make_int4(s, r0, b0, k0));
           const double f = (double)(kn - k0) * kNB * (2.0 * m - b0 - b1 + 1.0);
           ps.step_flops += f;
           ps.colupd_flops += f;
@@ -985,13 +945,6 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
       ps.col_cnt = (int)S.col_tasks.size() - ps.col_off - ps.fcol_cnt;
       S.col_tasks.insert(S.col_tasks.end(), prep.begin(), prep.end());
       ps.prep_cnt = (int)prep.size();
-      // fused tasks: diagonal parts after the step's diagonal tasks, column parts
-      // ahead of its column tasks, prep parts after its prep tiles
-      if (fu_col.size() != fu_diag.size() || fu_prep.size() != fu_diag.size()) S.schedule_error = true;
-      ps.fused_cnt = (int)fu_diag.size();
-      S.sdiag_tasks.insert(S.sdiag_tasks.end(), fu_diag.begin(), fu_diag.end());
-      S.col_tasks.insert(S.col_tasks.begin() + ps.col_off + ps.fcol_cnt, fu_col.begin(), fu_col.end());
-      S.col_tasks.insert(S.col_tasks.end(), fu_prep.begin(), fu_prep.end());
       long long cnt128 = 0;
       for (const int4& u : plain)
         for (int c0 = u.y; c0 < u.z; c0 += kBigTile) cnt128 += (P.m[u.x] - c0 + kBigTile - 1) / kBigTile;
