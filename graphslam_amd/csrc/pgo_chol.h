@@ -45,16 +45,22 @@ constexpr int kRowMask = (1 << kClipShift) - 1;
 // Front storage.  A front on the blocked path (front_packed: more than
 // kSmallFront rows or more than kWaveW pivot columns) keeps only its lower
 // trapezoid, in 64-column blocks: block b (columns [64 b, 64 b + 64)) holds
-// rows [64 b, m) column-major with leading dimension m - 64 b, the blocks back
-// to back from fblock_off(m, b) -- about half the m x m square.  The small
+// rows [64 b, m) column-major with leading dimension fpad(m) - 64 b, the blocks
+// back to back from fblock_off(fpad(m), b) -- about half the m x m square.  The small
 // fronts (one wavefront / workgroup each, m <= kSmallFront) stay m x m
 // column-major.  front_elems: the doubles a front occupies.
+// Round 5: a packed front is stored for the height fpad(m) = m rounded up to 16
+// rows (the rows past m are never touched), so every leading dimension and
+// block start is a multiple of 16 doubles and, with 128-byte aligned fronts, a
+// 64-row tile column is exactly four 128-byte lines instead of straddling five.
 __host__ __device__ inline bool front_packed(int m, int w) { return m > kSmallFront || w > kWaveW; }
-__host__ __device__ inline long long fblock_off(int m, long long b) { return 64 * b * m - 2048 * b * (b - 1); }
+__host__ __device__ inline int fpad(int m) { return (m + 15) & ~15; }
+__host__ __device__ inline long long fblock_off(int mp, long long b) { return 64 * b * mp - 2048 * b * (b - 1); }
 __host__ __device__ inline long long front_elems(int m, int w) {
   if (!front_packed(m, w)) return (long long)m * m;
+  const int mp = fpad(m);
   const long long nb = (m + 63) / 64, r = m - 64 * (nb - 1);
-  return fblock_off(m, nb - 1) + r * r;
+  return fblock_off(mp, nb - 1) + (mp - 64 * (nb - 1)) * r;
 }
 
 struct PanelStep {                 // one 64-column panel kb of every big front of a level

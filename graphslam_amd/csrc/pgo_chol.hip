@@ -94,17 +94,18 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // Front storage (pgo_chol.h front_packed / front_elems): element (i, j) of the
 // front at Fs is fcol(Fs, m, pk, j)[i] -- for a packed front (the blocked
 // path) column block b = j / 64 holds rows [64 b, m) with leading dimension
-// fld(m, pk, j) = m - 64 b, so i >= 64 b; an unpacked one is m x m.
+// fld(m, pk, j) = fpad(m) - 64 b, so i >= 64 b; an unpacked one is m x m.
 __device__ __forceinline__ long long fcol_off(int m, bool pk, int j) {
   if (!pk) return (long long)j * m;
+  const int mp = fpad(m);
   const long long b = j >> 6, c0 = b << 6;
-  return fblock_off(m, b) + (j - c0) * (long long)(m - c0) - c0;
+  return fblock_off(mp, b) + (j - c0) * (long long)(mp - c0) - c0;
 }
 template <class T>
 __device__ __forceinline__ T* fcol(T* Fs, int m, bool pk, int j) {
   return Fs + fcol_off(m, pk, j);
 }
-__device__ __forceinline__ int fld(int m, bool pk, int j) { return pk ? m - (j & ~63) : m; }
+__device__ __forceinline__ int fld(int m, bool pk, int j) { return pk ? fpad(m) - (j & ~63) : m; }
 
 
 // Step timing stamps (diagnostics, PGO_STEP_STAMPS): k_step launches given a
@@ -775,6 +776,7 @@ __device__ __forceinline__ void front_wave2_body(const CholDev& c, int s, double
   constexpr int LDP = W + 1;
   const int m = c.m[s], w = c.w[s];
   const bool pk = front_packed(m, w);
+  const int ld0 = fld(m, pk, 0);  // the panel's columns (the first column block when packed)
   double* PR = S;                 // m x W row-major copy of L (after the factorisation)
   double* cb = S + m * LDP;       // the diagonal block's rows and v (8 x 9)
   double* invs = cb + 130;        // [W] 1 / L(k,k)
@@ -785,7 +787,7 @@ __device__ __forceinline__ void front_wave2_body(const CholDev& c, int s, double
   DIAG_CLK(23);
   double pa[W];
 #pragma unroll
-  for (int k = 0; k < W; k++) pa[k] = (ra && k < w && k <= row) ? Fs[row + (size_t)k * m] : 0.0;
+  for (int k = 0; k < W; k++) pa[k] = (ra && k < w && k <= row) ? Fs[row + (size_t)k * ld0] : 0.0;
   double va = ra ? fv[row] : 0.0;
   bool bad = false;
   DIAG_CLK(24);
@@ -863,7 +865,7 @@ __device__ __forceinline__ void front_wave2_body(const CholDev& c, int s, double
   // L back to the front (and the row-major LDS copy), y to the frontal vector
 #pragma unroll
   for (int k = 0; k < W; k++) {
-    if (ra && k < w && k <= row) Fs[row + (size_t)k * m] = pa[k];
+    if (ra && k < w && k <= row) Fs[row + (size_t)k * ld0] = pa[k];
     if (ra) PR[row * LDP + k] = k <= row ? pa[k] : 0.0;
   }
   if (ra) fv[row] = va;
@@ -1365,7 +1367,7 @@ __device__ __forceinline__ void trsm_rows(const CholDev& c, int s, int r0, int k
   __syncthreads();
   if (rw >= m) return;                                // (no barriers below)
   double* Fc = fcol(c.F + c.foff[s], m, true, kn);   // the panel's column block (blocked fronts are packed)
-  const int ldc = m - kn;
+  const int ldc = fld(m, true, kn);
   const int il = wv * 16 + (l & 15), arow = r0 + il;
   double a[16], tb[16][4];   // A fragments, inverse fragments
 #pragma unroll
@@ -1429,7 +1431,7 @@ __device__ __forceinline__ void syrk_tile64(const CholDev& c, const int4 t, int 
   const int li = l & 15, lk = l >> 4;
   double* Fs = c.F + c.foff[s];
   double* Cb = fcol(Fs, m, true, col0);   // the tile's columns: one column block (col0 = kn)
-  const int ldc = m - (col0 & ~63);
+  const int ldc = fld(m, true, col0);
   const int rA = row0 + qi + li, rB = rA + 16;          // C rows (B operand rows)
   const int cA = col0 + qj + li, cB = cA + 16;          // C columns (A operand rows)
   // C prefetch (output layout: lane l, reg r -> column col0+qj+16mj+lk+4r, row row0+qi+16mi+li)
@@ -1451,7 +1453,7 @@ __device__ __forceinline__ void syrk_tile64(const CholDev& c, const int4 t, int 
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const bool kin = kk + 4 * u + lk < K;   // (16 panel columns from k0 + kk: one column block)
-      const double* pk = fcol(Fs, m, true, k0 + kk) + (size_t)(4 * u + lk) * (m - ((k0 + kk) & ~63));
+      const double* pk = fcol(Fs, m, true, k0 + kk) + (size_t)(4 * u + lk) * fld(m, true, k0 + kk);
       ra[u] = (kin && vrA) ? pk[rA] : 0.0;
       rb[u] = (kin && vrB) ? pk[rB] : 0.0;
       ca[u] = (kin && vcA) ? pk[cA] : 0.0;
@@ -1519,7 +1521,7 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
     for (int q = 0; q < 4; q++) {
       // the chunk's 16 panel columns sit in one column block (k0: a panel start)
       const int idx = tid + 256 * q, k = 16 * ch + (idx >> 6), r = idx & 63;
-      const double* pk = fcol(Fs, m, true, k0 + 16 * ch) + (size_t)(idx >> 6) * (m - ((k0 + 16 * ch) & ~63));
+      const double* pk = fcol(Fs, m, true, k0 + 16 * ch) + (size_t)(idx >> 6) * fld(m, true, k0 + 16 * ch);
       st[q] = (k < K && row0 + r < m) ? pk[row0 + r] : 0.0;
       st[4 + q] = (k < K && col0 + r < m) ? pk[col0 + r] : 0.0;
     }
@@ -1547,7 +1549,7 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
   // C read-modify-write: lane l holds (row row0 + qi + 16h + (l & 15), column col0 + qj + 4p + (l >> 4));
   // the tile's columns lie in col0's column block (the planner never lets a tile straddle two)
   double* Cb = fcol(Fs, m, true, col0);
-  const int ldc = m - (col0 & ~63);
+  const int ldc = fld(m, true, col0);
   double cold[8][2];
   auto load_c = [&] {
 #pragma unroll
@@ -1630,15 +1632,15 @@ __device__ __forceinline__ void diag_tile_update(const CholDev& c, const int4 t,
   double st[16];
   auto load = [&](int ch) {   // chunk ch: panel columns k0 + 64 ch ..: one column block
     const double* Pb = fcol(Fs, m, true, k0 + 64 * ch);
-    const int ldp = m - k0 - 64 * ch;
+    const int ldp = fld(m, true, k0 + 64 * ch);
 #pragma unroll
     for (int q = 0; q < 16; q++) {
       const int idx = tid + 256 * q, i = idx & 63, k = 64 * ch + (idx >> 6);
       st[q] = (k < K && r0 + i < m) ? Pb[(r0 + i) + (size_t)(idx >> 6) * ldp] : 0.0;
     }
   };
-  double* Db = fcol(Fs, m, true, r0) + r0;   // the diagonal tile, ld m - r0
-  const int ldd = m - r0;
+  double* Db = fcol(Fs, m, true, r0) + r0;   // the diagonal tile
+  const int ldd = fld(m, true, r0);
   double cv[16];   // C, lower part of the updated region: its loads and the first chunk's in flight together
 #pragma unroll
   for (int q = 0; q < 16; q++) {
@@ -1724,7 +1726,7 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
   __syncthreads();
   if (diag_factor_invert(Ts, Ws, bc, c.diag_full ? 64 : nb)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   STAMP(slot, 2);
-  double* Fs = fcol(c.F + c.foff[s], m, true, kn) + kn;   // the diagonal tile, ld m - kn
+  double* Fs = fcol(c.F + c.foff[s], m, true, kn) + kn;   // the diagonal tile, ld fld(m, true, kn)
   double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;   // row-major L^-1 of the tile
   double* v = c.fv + c.voff[s] + kn;
   publish_inverse(M + c.tfo, Ws, nb);
@@ -1732,10 +1734,10 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
   STAMP(slot, 3);
   publish_step(c.stepflag + s, kn / 64 + 1);
   STAMP(slot, 4);
-  store_factor(Fs, m - kn, M, Ts, Ws, nb);
+  store_factor(Fs, fld(m, true, kn), M, Ts, Ws, nb);
   if (nb < kNB) {
     __syncthreads();
-    diag_own_rows(Fs, m - kn, m - kn, v, keep, Ts, Ws, ys, nb);
+    diag_own_rows(Fs, fld(m, true, kn), m - kn, v, keep, Ts, Ws, ys, nb);
   }
 }
 
@@ -1749,13 +1751,14 @@ __device__ __forceinline__ void first_diag_body(const CholDev& c, int s, double*
   const int m = c.m[s], w = c.w[s];
   const int nb = min(kNB, w);
   double* Fs = c.F + c.foff[s];
+  const int ld0 = fld(m, true, 0);   // (blocked fronts are packed)
   const int tid = threadIdx.x;
   double tv[16], keep[16];
 #pragma unroll
   for (int u = 0; u < 16; u++) {   // all loads in flight
     const int idx = tid + 256 * u, i = idx & 63, j = idx >> 6;
-    tv[u] = (i < nb && j < nb) ? (i >= j ? Fs[i + (size_t)j * m] : 0.0) : (i == j ? 1.0 : 0.0);
-    keep[u] = (i >= nb && i < m && j < nb) ? Fs[i + (size_t)j * m] : 0.0;
+    tv[u] = (i < nb && j < nb) ? (i >= j ? Fs[i + (size_t)j * ld0] : 0.0) : (i == j ? 1.0 : 0.0);
+    keep[u] = (i >= nb && i < m && j < nb) ? Fs[i + (size_t)j * ld0] : 0.0;
   }
 #pragma unroll
   for (int u = 0; u < 16; u++) {
@@ -1770,10 +1773,10 @@ __device__ __forceinline__ void first_diag_body(const CholDev& c, int s, double*
   publish_inverse(M + c.tfo, Ws, nb);
   panel_rhs(v, Ws, nb, bc, ys);
   publish_step(c.stepflag + s, 1);
-  store_factor(Fs, m, M, Ts, Ws, nb);
+  store_factor(Fs, ld0, M, Ts, Ws, nb);
   if (nb < kNB) {
     __syncthreads();
-    diag_own_rows(Fs, m, m, v, keep, Ts, Ws, ys, nb);
+    diag_own_rows(Fs, ld0, m, v, keep, Ts, Ws, ys, nb);
   }
 }
 
@@ -1792,7 +1795,7 @@ __global__ __launch_bounds__(256, 2) void k_panel_first(CholDev c, const int* __
   const int4 t = col[b - np];
   const int s = t.x, m = c.m[s], nb = min(kNB, c.w[s]);
   wait_step(c, c.stepflag + s, 1);
-  trsm_rows(c, s, t.y, 0, nb, c.F + c.foff[s] + t.y, 1, m, smem);
+  trsm_rows(c, s, t.y, 0, nb, c.F + c.foff[s] + t.y, 1, fld(m, true, 0), smem);
 }
 
 // The same first panel in two launches, for levels with many big fronts (the
@@ -1817,7 +1820,7 @@ __global__ __launch_bounds__(256) void k_first_trsm(CholDev c, const int4* __res
   __shared__ __attribute__((aligned(16))) double xs[4096];
   const int4 t = col[blockIdx.x];
   const int s = t.x, m = c.m[s], r0 = t.y, kn = max(t.z, 0), nb = min(kNB, c.w[s] - kn);
-  const int ld = m - kn;                                      // (blocked fronts are packed)
+  const int ld = fld(m, true, kn);                            // (blocked fronts are packed)
   const double* Mf = c.Tinv + c.tfo + c.toff[s] + (kn / 64) * 4096;
   double* fv = c.fv + c.voff[s];
   const double* A = fcol(c.F + c.foff[s], m, true, kn) + r0;  // A(i, k) = A[i + k ld]
@@ -1966,7 +1969,7 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
     for (int q = 0; q < 8; q++) {
       const int idx = tid + 256 * q, k = 16 * ch + (idx >> 7), r = idx & 127;
       const bool kin = k < K;
-      const double* pk = fcol(Fs, m, true, k0 + 16 * ch) + (size_t)(idx >> 7) * (m - ((k0 + 16 * ch) & ~63));
+      const double* pk = fcol(Fs, m, true, k0 + 16 * ch) + (size_t)(idx >> 7) * fld(m, true, k0 + 16 * ch);
       st[q] = (kin && row0 + r < m) ? pk[row0 + r] : 0.0;
       st[8 + q] = (kin && col0 + r < m) ? pk[col0 + r] : 0.0;
     }
@@ -2015,7 +2018,7 @@ __global__ __launch_bounds__(256) void k_panel_syrk128(CholDev c, const int4* __
   }
   if (!active) return;
   double* Cb = fcol(Fs, m, true, col0 + 64 * wj);   // the wave's columns: one column block
-  const int ldc = m - ((col0 + 64 * wj) & ~63);
+  const int ldc = fld(m, true, col0 + 64 * wj);
 #pragma unroll
   for (int p = 0; p < 16; p++) {
     double cold[4];

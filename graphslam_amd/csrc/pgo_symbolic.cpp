@@ -240,7 +240,7 @@ static void size_fronts(CholPlan& P) {
   P.flops = 0;
   P.nnzl = 0;
   for (int s = 0; s < ns; s++) {
-    P.foff[s + 1] = P.foff[s] + ((front_elems(P.m[s], P.w[s]) + 7) / 8) * 8;   // 64-byte aligned fronts
+    P.foff[s + 1] = P.foff[s] + ((front_elems(P.m[s], P.w[s]) + 15) / 16) * 16;   // 128-byte aligned fronts
     P.voff[s + 1] = P.voff[s] + ((P.m[s] + 7) / 8) * 8;
     P.toff[s + 1] = P.toff[s] + (long long)((P.w[s] + 63) / 64) * 4096;
     for (int k = 0; k < P.w[s]; k++) {
@@ -416,7 +416,7 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
   }
   if (psz > 1) {   // offsets over the needed fronts only
     for (int s = 0; s < ns; s++) {
-      P.foff[s + 1] = P.foff[s] + (need[s] ? ((front_elems(P.m[s], P.w[s]) + 7) / 8) * 8 : 0);
+      P.foff[s + 1] = P.foff[s] + (need[s] ? ((front_elems(P.m[s], P.w[s]) + 15) / 16) * 16 : 0);
       P.voff[s + 1] = P.voff[s] + (need[s] ? ((P.m[s] + 7) / 8) * 8 : 0);
       P.toff[s + 1] = P.toff[s] + (need[s] ? (long long)((P.w[s] + 63) / 64) * 4096 : 0);
     }
