@@ -1000,8 +1000,9 @@ __device__ __forceinline__ void inv8_lane(double (&a)[36], const double (&iv)[8]
 // by one wave, as 2x2 blocks of 8: A11 = L11 L11^T and X11 = L11^-1 lane-local
 // (chol8_lane, inv8_lane, every lane the same values), L21 = A21 X11^T and
 // A22 - L21 L21^T one element per lane, A22' lane-local again, then
-// X21 = -X22 (L21 X11).  Writes L to TJ (lower) and X to WJ (ld 65, lower,
-// zeros above); sc: LDS scratch of 64.  Same wave only: LDS accesses of one
+// X21 = -X22 (L21 X11).  Writes L21 to TJ (the 8x8 diagonal blocks of L are
+// not stored: round 5, nothing reads a diagonal tile's L) and X to WJ (ld 65,
+// lower, zeros above); sc: LDS scratch of 64.  Same wave only: LDS accesses of one
 // wave complete in order, so no barrier between a lane's store and another's
 // load.  (Solving rows of L21 against a lane-held L11 instead, with A22' formed
 // in registers, measured slower: 34.4 k against 33.0 k cycles per 64x64.)
@@ -1021,13 +1022,7 @@ __device__ __forceinline__ bool diag16_lane(double* TJ, double* WJ, double* sc) 
   DIAG_CLK(13);
   bool bad = chol8_lane(a, iv);
   DIAG_CLK(14);
-  if (l == 0) {
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-      for (int j = 0; j <= i; j++) TJ[i + j * 65] = a[P8(i, j)];
-  }
-  inv8_lane(a, iv);
+  inv8_lane(a, iv);   // (L11 itself is not stored: nothing reads a diagonal block's L, see store_factor)
   DIAG_CLK(15);
   if (l == 0) {
 #pragma unroll
@@ -1062,13 +1057,7 @@ __device__ __forceinline__ bool diag16_lane(double* TJ, double* WJ, double* sc) 
   DIAG_CLK(16);
   bad = chol8_lane(a, iv) || bad;
   DIAG_CLK(17);
-  if (l == 0) {
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-      for (int j = 0; j <= i; j++) TJ[(8 + i) + (8 + j) * 65] = a[P8(i, j)];
-  }
-  inv8_lane(a, iv);
+  inv8_lane(a, iv);   // (nor L22)
   if (l == 0) {
 #pragma unroll
     for (int i = 0; i < 8; i++)
@@ -1268,14 +1257,15 @@ __device__ __forceinline__ void publish_inverse(double* __restrict__ Mf, const d
   }
 }
 
-// After the hand-off: L (LDS Ts, ld 65) back into the front (Fs: the tile, ld
-// its column block's), X row-major to M (the backward solve's copy)
-__device__ __forceinline__ void store_factor(double* Fs, int ld, double* __restrict__ M, const double* Ts,
-                                             const double* Ws, int nb) {
+// After the hand-off: X row-major to M (the backward solve's copy).  The
+// tile's own L_bb is not written back to the front (round 5): every later
+// reader of a diagonal tile uses its inverse (the column solves' operand copy,
+// the backward solve and the marginals M, the panel exchange) and reads L
+// only below the tile, so those stores and the diagonal blocks' lane-0 stores
+// in diag16_lane were dead (the front keeps the assembled values there).
+__device__ __forceinline__ void store_factor(double* __restrict__ M, const double* Ws, int nb) {
   const int tid = threadIdx.x;
   for (int idx = tid; idx < 4096; idx += 256) {
-    const int i = idx & 63, j = idx >> 6;
-    if (i < nb && j < nb && i >= j) Fs[i + (size_t)j * ld] = Ts[i + j * 65];
     const int a = idx >> 6, b = idx & 63;
     M[idx] = (a < nb && b < nb && a >= b) ? Ws[a + b * 65] : 0.0;
   }
@@ -1513,7 +1503,7 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   const int qi = 32 * (wv >> 1), qj = 32 * (wv & 1);
   const bool active = !(row0 == col0 && qi < qj);
-  const int li = l & 15, lk = l >> 4;
+  const int lk = l >> 4;
   // staging map: thread -> (k = idx >> 6, r = idx & 63), idx = tid + 256 q, q < 4
   double st[8];
   auto load = [&](int ch) {
@@ -1734,7 +1724,7 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
   STAMP(slot, 3);
   publish_step(c.stepflag + s, kn / 64 + 1);
   STAMP(slot, 4);
-  store_factor(Fs, fld(m, true, kn), M, Ts, Ws, nb);
+  store_factor(M, Ws, nb);
   if (nb < kNB) {
     __syncthreads();
     diag_own_rows(Fs, fld(m, true, kn), m - kn, v, keep, Ts, Ws, ys, nb);
@@ -1773,7 +1763,7 @@ __device__ __forceinline__ void first_diag_body(const CholDev& c, int s, double*
   publish_inverse(M + c.tfo, Ws, nb);
   panel_rhs(v, Ws, nb, bc, ys);
   publish_step(c.stepflag + s, 1);
-  store_factor(Fs, ld0, M, Ts, Ws, nb);
+  store_factor(M, Ws, nb);
   if (nb < kNB) {
     __syncthreads();
     diag_own_rows(Fs, ld0, m, v, keep, Ts, Ws, ys, nb);
