@@ -1486,11 +1486,14 @@ __global__ __launch_bounds__(256) void k_panel_syrk(CholDev c, const int4* __res
 // per chunk, issued one chunk ahead of the MFMAs).  Low register count, so
 // several workgroups per CU hide the load latency.
 // smem: 4 * 16 * 68 doubles (Sr[2], Sc[2])
-template <bool kPrefC = false>   // true: the C tile's loads issued before the k loop (latency under the MFMAs)
+// KC: panel columns staged per chunk (16; 32 halves the round trips with the
+// same 4-deep MFMA steps in the same k order -- bitwise the same tile -- but
+// measured no faster, profiles/r05n_syrk_ubench.txt)
+template <bool kPrefC = false, int KC = 16>   // kPrefC: the C tile's loads issued before the k loop
 __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, int kb, double* smem) {
-  constexpr int LD = 64 + 4;
-  double(*Sr)[16 * LD] = reinterpret_cast<double(*)[16 * LD]>(smem);
-  double(*Sc)[16 * LD] = reinterpret_cast<double(*)[16 * LD]>(smem + 2 * 16 * LD);
+  constexpr int LD = 64 + 4, NQ = KC / 4;
+  double(*Sr)[KC * LD] = reinterpret_cast<double(*)[KC * LD]>(smem);
+  double(*Sc)[KC * LD] = reinterpret_cast<double(*)[KC * LD]>(smem + 2 * KC * LD);
   const int s = t.x, row0 = t.y & kRowMask, col0 = t.z, clip = t.y >> kClipShift;
   const bool inner = t.w < 0;
   const int k0 = t.w & 0x7fffffff;
@@ -1498,30 +1501,30 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
   const int kend = min(kb + kNB, w);
   int colend = inner ? min((kb & ~(kKB - 1)) + kKB, w) : m;
   if (clip) colend = min(colend, col0 + clip);   // a split tile: its columns only
-  const int K = kend - k0, nch = (K + 15) >> 4;
+  const int K = kend - k0, nch = (K + KC - 1) / KC;
   double* Fs = c.F + c.foff[s];
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   const int qi = 32 * (wv >> 1), qj = 32 * (wv & 1);
   const bool active = !(row0 == col0 && qi < qj);
   const int lk = l >> 4;
-  // staging map: thread -> (k = idx >> 6, r = idx & 63), idx = tid + 256 q, q < 4
-  double st[8];
+  // staging map: thread -> (k = idx >> 6, r = idx & 63), idx = tid + 256 q, q < NQ
+  double st[2 * NQ];
   auto load = [&](int ch) {
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      // the chunk's 16 panel columns sit in one column block (k0: a panel start)
-      const int idx = tid + 256 * q, k = 16 * ch + (idx >> 6), r = idx & 63;
-      const double* pk = fcol(Fs, m, true, k0 + 16 * ch) + (size_t)(idx >> 6) * fld(m, true, k0 + 16 * ch);
+    for (int q = 0; q < NQ; q++) {
+      // the chunk's KC panel columns sit in one column block (k0: a panel start)
+      const int idx = tid + 256 * q, k = KC * ch + (idx >> 6), r = idx & 63;
+      const double* pk = fcol(Fs, m, true, k0 + KC * ch) + (size_t)(idx >> 6) * fld(m, true, k0 + KC * ch);
       st[q] = (k < K && row0 + r < m) ? pk[row0 + r] : 0.0;
-      st[4 + q] = (k < K && col0 + r < m) ? pk[col0 + r] : 0.0;
+      st[NQ + q] = (k < K && col0 + r < m) ? pk[col0 + r] : 0.0;
     }
   };
   auto stash = [&](int b) {
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < NQ; q++) {
       const int idx = tid + 256 * q;
       Sr[b][(idx >> 6) * LD + (idx & 63)] = st[q];
-      Sc[b][(idx >> 6) * LD + (idx & 63)] = st[4 + q];
+      Sc[b][(idx >> 6) * LD + (idx & 63)] = st[NQ + q];
     }
   };
   // v_mfma_f64_4x4x4f64 (4 blocks of 4x4x4): the wave's 32x32 quadrant as 8
@@ -1559,7 +1562,7 @@ __device__ __forceinline__ void syrk_lds_body(const CholDev& c, const int4 t, in
     if (ch + 1 < nch) load(ch + 1);
     if (active) {
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < KC / 4; u++) {
         const double* sr = Sr[b] + (4 * u + lk) * LD + qi + (l & 15);
         const double* sc = Sc[b] + (4 * u + lk) * LD + qj + (l & 3);
         const double r0v = sr[0], r1v = sr[16];

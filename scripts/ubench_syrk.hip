@@ -4,14 +4,20 @@
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include scripts/ubench_syrk.hip -o graphslam_amd/build/ubench_syrk
 //   ./graphslam_amd/build/ubench_syrk [m] [w]
 #include "../graphslam_amd/csrc/pgo_chol.hip"
-#include "../graphslam_amd/csrc/pgo_symbolic.cpp"
-#include "../graphslam_amd/csrc/pgo_order.cpp"
 
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
 
 using namespace pgo;
+
+// 32 panel columns per chunk (69.6 KB of LDS: 2 workgroups per CU instead of
+// 4; bitwise the 16-column form) -- round 5's A/B, not kept
+__global__ __launch_bounds__(256) void k_panel_syrk_lds32(CholDev c, const int4* __restrict__ tasks, int kb) {
+  lane_offset(c);
+  __shared__ __attribute__((aligned(16))) double smem[4 * 32 * 68];
+  syrk_lds_body<false, 32>(c, tasks[blockIdx.x], kb, smem);
+}
 
 __device__ long long g_mclk[4];
 template <int NC>
@@ -127,15 +133,16 @@ int main(int argc, char** argv) {
   c.m = dm;
   c.w = dw;
   c.foff = dfo;
-  // outer update after panel kb = 192 (block 0 = columns 0..255): trailing [256, M), k0 = 0
-  const int kb = 192, be = 256;
-  const double flops = 256.0 * (M - be) * (M - be + 1.0);
-  for (int T : {64, 65, 66, 128}) {   // 65: the LDS-staged 64x64 kernel; 66: the same with the C tile prefetched
-    const int TT = (T == 65 || T == 66) ? 64 : T;
+  // outer update after panel kb = 192 (block 0 = columns 0..255): trailing [256, M), k0 = 0, depth 256;
+  // then the same tiles at depth 64 (kb = 0: one panel, the inner steps' depth)
+  for (const int kb : {192, 0}) {
+  const int be = 256, depth = kb + 64;
+  const double flops = (double)depth * (M - be) * (M - be + 1.0);
+  for (int T : {64, 65, 66, 67, 128}) {   // 65: the LDS-staged 64x64 kernel; 66: the same with the C tile prefetched; 67: 32-column chunks
+    const int TT = (T >= 65 && T <= 67) ? 64 : T;
     std::vector<int4> tasks;
     for (int c0 = be; c0 < M; c0 += TT)
       for (int r0 = c0; r0 < M; r0 += TT) tasks.push_back(make_int4(0, r0, c0, 0));
-    if (getenv("XCD")) xcd_order(tasks, TT);
     int4* dt;
     hipMalloc(&dt, tasks.size() * sizeof(int4));
     hipMemcpy(dt, tasks.data(), tasks.size() * sizeof(int4), hipMemcpyHostToDevice);
@@ -150,6 +157,7 @@ int main(int argc, char** argv) {
       if (T == 64) k_panel_syrk<<<(int)tasks.size(), 256, 0, st>>>(c, dt, kb);
       else if (T == 65) k_panel_syrk_lds<<<(int)tasks.size(), 256, 0, st>>>(c, dt, kb);
       else if (T == 66) k_panel_syrk_lds_pc<<<(int)tasks.size(), 256, 0, st>>>(c, dt, kb);
+      else if (T == 67) k_panel_syrk_lds32<<<(int)tasks.size(), 256, 0, st>>>(c, dt, kb);
       else k_panel_syrk128<<<(int)tasks.size(), 256, 0, st>>>(c, dt, kb);
       hipEventRecord(b, st);
       hipEventSynchronize(b);
@@ -163,9 +171,10 @@ int main(int argc, char** argv) {
     double cs = 0;
     for (int j = be; j < M; j += 7)
       for (int i = j; i < M; i += 5) cs += out[i + (size_t)j * M];
-    printf("m %d tile %3d: %6zu tasks  %8.1f us  %6.2f TFLOP/s  checksum %.10e\n", M, T, tasks.size(), best * 1e3,
-           flops / (best * 1e-3) / 1e12, cs);
+    printf("m %d depth %3d tile %3d: %6zu tasks  %8.1f us  %6.2f TFLOP/s  checksum %.10e\n", M, depth, T, tasks.size(),
+           best * 1e3, flops / (best * 1e-3) / 1e12, cs);
     hipFree(dt);
+  }
   }
   return 0;
 }
