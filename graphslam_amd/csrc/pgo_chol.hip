@@ -687,36 +687,17 @@ __device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double*
   __builtin_amdgcn_wave_barrier();
   if (bad && l == 0) *c.flag = 1;
   DIAG_CLK(25);
-  // L back to the front (and a row-major LDS copy), y to the frontal vector
-#pragma unroll
-  for (int k = 0; k < W; k++) {   // (columns k >= w of the LDS copy are zero)
-    if (k < w) {
-      if (ra && k <= l) Fs[l + (size_t)k * m] = pa[k];
-      if (rb) Fs[lb + (size_t)k * m] = pb[k];
-    }
-    if (ra) PR[l * LDP + k] = k <= l ? pa[k] : 0.0;
-    if (rb) PR[lb * LDP + k] = pb[k];
-  }
-  if (ra) fv[l] = va;
-  if (rb) fv[lb] = vb;
-  __builtin_amdgcn_wave_barrier();
-  DIAG_CLK(26);
-  // trailing update C[i][j] -= L[i,:] L[j,:]', w <= j <= i < m, on
-  // v_mfma_f64_16x16x4f64: per 16 x 16 lower tile D(jj, ii) = sum_k L[j0 + jj][k]
-  // L[i0 + ii][k] with both operands from the row-major LDS copy (zero beyond
-  // w); lane l holds rows i0 + (l & 15) of columns j0 + (l >> 4) + 4 r, so each
-  // column's 16 rows are one coalesced segment of the front.  A 16-column block
-  // at a time: all its tiles' loads in flight together (m <= 128: <= 8 tiles).
-  {
-    constexpr int NT = kTwoRows ? 8 : 4;   // tiles per column block (m <= 128 | 64)
+  if constexpr (kTwoRows) {
+    // m > 64 (up to 8 column blocks of the trailing update below): the first
+    // block's C loads issued before the panel's stores and the inverse, each
+    // next block's before this one's products (the blocks touch disjoint
+    // columns, none of the panel's): latency per front 12-16 % lower on 1 - 256
+    // fronts of m = 100, w = 8 / 16, bitwise the same fronts
+    // (profiles/r05u_front_wave_ahead.txt)
+    constexpr int NT = 8;   // tiles per column block (m <= 128)
     const int u = m - w, nt = (u + 15) >> 4, li = l & 15, lk = l >> 4;
-    for (int tj = 0; tj < nt; tj++) {
+    auto load_c = [&](int tj, double (&cv)[NT][4]) {
       const int j0 = w + 16 * tj;
-      const double* Aj = PR + min(j0 + li, m - 1) * LDP + lk;
-      double a[W / 4];
-#pragma unroll
-      for (int kc = 0; kc < W / 4; kc++) a[kc] = Aj[4 * kc];
-      double cv[NT][4];
 #pragma unroll
       for (int q = 0; q < NT; q++) {
         const int i = w + 16 * (tj + q) + li;
@@ -726,6 +707,13 @@ __device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double*
           cv[q][r] = (tj + q < nt && i < m && j <= i) ? Fs[i + (size_t)j * m] : 0.0;
         }
       }
+    };
+    auto update = [&](int tj, const double (&cv)[NT][4]) {   // as the m <= 64 branch's
+      const int j0 = w + 16 * tj;
+      const double* Aj = PR + min(j0 + li, m - 1) * LDP + lk;
+      double a[W / 4];
+#pragma unroll
+      for (int kc = 0; kc < W / 4; kc++) a[kc] = Aj[4 * kc];
 #pragma unroll
       for (int q = 0; q < NT; q++) {
         if (tj + q >= nt) break;   // uniform
@@ -740,23 +728,120 @@ __device__ __forceinline__ void front_wave_body(const CholDev& c, int s, double*
           if (i < m && j <= i) Fs[i + (size_t)j * m] = cv[q][r] - acc[r];
         }
       }
+    };
+    double c0[NT][4], c1[NT][4];
+    if (nt > 0) load_c(0, c0);
+    // L back to the front (and a row-major LDS copy), y to the frontal vector
+#pragma unroll
+    for (int k = 0; k < W; k++) {
+      if (k < w) {
+        if (ra && k <= l) Fs[l + (size_t)k * m] = pa[k];
+        if (rb) Fs[lb + (size_t)k * m] = pb[k];
+      }
+      if (ra) PR[l * LDP + k] = k <= l ? pa[k] : 0.0;
+      if (rb) PR[lb * LDP + k] = pb[k];
     }
-  }
-  DIAG_CLK(27);
-  // X = L11^-1 (w x w), lane = column: forward substitution of e_l
-  if (l < w) {
-    double x[W];
+    if (ra) fv[l] = va;
+    if (rb) fv[lb] = vb;
+    __builtin_amdgcn_wave_barrier();
+    DIAG_CLK(26);
+    // X = L11^-1 (w x w), lane = column: forward substitution of e_l
+    if (l < w) {
+      double x[W];
 #pragma unroll
-    for (int r = 0; r < W; r++) {
-      double acc = r == l ? 1.0 : 0.0;
+      for (int r = 0; r < W; r++) {
+        double acc = r == l ? 1.0 : 0.0;
 #pragma unroll
-      for (int t = 0; t < r; t++) acc = fma(-PR[min(r, m - 1) * LDP + t], x[t], acc);
-      x[r] = r < w ? acc * invs[r] : 0.0;
+        for (int t = 0; t < r; t++) acc = fma(-PR[min(r, m - 1) * LDP + t], x[t], acc);
+        x[r] = r < w ? acc * invs[r] : 0.0;
+      }
+      double* M = c.Tinv + c.toff[s];   // row-major, live w x w
+#pragma unroll
+      for (int r = 0; r < W; r++)
+        if (r < w) M[r * 64 + l] = r >= l ? x[r] : 0.0;
     }
-    double* M = c.Tinv + c.toff[s];   // row-major, live w x w
+    DIAG_CLK(27);
+    for (int tj = 0; tj < nt; tj += 2) {   // (the trailing update: see the m <= 64 branch)
+      if (tj + 1 < nt) load_c(tj + 1, c1);
+      update(tj, c0);
+      if (tj + 1 >= nt) break;
+      if (tj + 2 < nt) load_c(tj + 2, c0);
+      update(tj + 1, c1);
+    }
+  } else {
+    // m <= 64 (<= 4 blocks; the one-block-ahead form cost the leaves'
+    // 12288-front launch 4-5 % and saved < 0.5 us of latency)
+    // L back to the front (and a row-major LDS copy), y to the frontal vector
 #pragma unroll
-    for (int r = 0; r < W; r++)
-      if (r < w) M[r * 64 + l] = r >= l ? x[r] : 0.0;
+    for (int k = 0; k < W; k++) {   // (columns k >= w of the LDS copy are zero)
+      if (k < w) {
+        if (ra && k <= l) Fs[l + (size_t)k * m] = pa[k];
+        if (rb) Fs[lb + (size_t)k * m] = pb[k];
+      }
+      if (ra) PR[l * LDP + k] = k <= l ? pa[k] : 0.0;
+      if (rb) PR[lb * LDP + k] = pb[k];
+    }
+    if (ra) fv[l] = va;
+    if (rb) fv[lb] = vb;
+    __builtin_amdgcn_wave_barrier();
+    DIAG_CLK(26);
+    // trailing update C[i][j] -= L[i,:] L[j,:]', w <= j <= i < m, on
+    // v_mfma_f64_16x16x4f64: per 16 x 16 lower tile D(jj, ii) = sum_k L[j0 + jj][k]
+    // L[i0 + ii][k] with both operands from the row-major LDS copy (zero beyond
+    // w); lane l holds rows i0 + (l & 15) of columns j0 + (l >> 4) + 4 r, so each
+    // column's 16 rows are one coalesced segment of the front.  A 16-column block
+    // at a time: all its tiles' loads in flight together (m <= 128: <= 8 tiles).
+    {
+      constexpr int NT = kTwoRows ? 8 : 4;   // tiles per column block (m <= 128 | 64)
+      const int u = m - w, nt = (u + 15) >> 4, li = l & 15, lk = l >> 4;
+      for (int tj = 0; tj < nt; tj++) {
+        const int j0 = w + 16 * tj;
+        const double* Aj = PR + min(j0 + li, m - 1) * LDP + lk;
+        double a[W / 4];
+#pragma unroll
+        for (int kc = 0; kc < W / 4; kc++) a[kc] = Aj[4 * kc];
+        double cv[NT][4];
+#pragma unroll
+        for (int q = 0; q < NT; q++) {
+          const int i = w + 16 * (tj + q) + li;
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int j = j0 + lk + 4 * r;
+            cv[q][r] = (tj + q < nt && i < m && j <= i) ? Fs[i + (size_t)j * m] : 0.0;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < NT; q++) {
+          if (tj + q >= nt) break;   // uniform
+          const int i = w + 16 * (tj + q) + li;
+          const double* Bi = PR + min(i, m - 1) * LDP + lk;
+          d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int kc = 0; kc < W / 4; kc++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kc], Bi[4 * kc], acc, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int j = j0 + lk + 4 * r;
+            if (i < m && j <= i) Fs[i + (size_t)j * m] = cv[q][r] - acc[r];
+          }
+        }
+      }
+    }
+    DIAG_CLK(27);
+    // X = L11^-1 (w x w), lane = column: forward substitution of e_l
+    if (l < w) {
+      double x[W];
+#pragma unroll
+      for (int r = 0; r < W; r++) {
+        double acc = r == l ? 1.0 : 0.0;
+#pragma unroll
+        for (int t = 0; t < r; t++) acc = fma(-PR[min(r, m - 1) * LDP + t], x[t], acc);
+        x[r] = r < w ? acc * invs[r] : 0.0;
+      }
+      double* M = c.Tinv + c.toff[s];   // row-major, live w x w
+#pragma unroll
+      for (int r = 0; r < W; r++)
+        if (r < w) M[r * 64 + l] = r >= l ? x[r] : 0.0;
+    }
   }
   DIAG_CLK(28);
 }
@@ -871,6 +956,24 @@ __device__ __forceinline__ void front_wave2_body(const CholDev& c, int s, double
   if (ra) fv[row] = va;
   __syncthreads();
   DIAG_CLK(26);
+  // X = L11^-1 (w x w), lane = column, by the last wave ahead of its share of
+  // the trailing update (blocks tj = wq, wq + NW, ..: the last wave's share is
+  // the smallest); wave 0 did it after its larger share before
+  if (wq == NW - 1 && l < w) {
+    double x[W];
+#pragma unroll
+    for (int r = 0; r < W; r++) {
+      double acc = r == l ? 1.0 : 0.0;
+#pragma unroll
+      for (int t = 0; t < r; t++) acc = fma(-PR[min(r, m - 1) * LDP + t], x[t], acc);
+      x[r] = r < w ? acc * invs[r] : 0.0;
+    }
+    double* M = c.Tinv + c.toff[s];   // row-major, live w x w
+#pragma unroll
+    for (int r = 0; r < W; r++)
+      if (r < w) M[r * 64 + l] = r >= l ? x[r] : 0.0;
+  }
+  DIAG_CLK(27);
   {   // trailing update C[i][j] -= L[i,:] L[j,:]' as front_wave_body's, 16-column blocks dealt to the
       // waves, their row tiles 8 at a time
     const int u = m - w, nt = (u + 15) >> 4, li = l & 15, lk = l >> 4;
@@ -910,22 +1013,6 @@ __device__ __forceinline__ void front_wave2_body(const CholDev& c, int s, double
         }
       }
     }
-  }
-  DIAG_CLK(27);
-  // X = L11^-1 (w x w), thread = column (wave 0)
-  if (row < w) {
-    double x[W];
-#pragma unroll
-    for (int r = 0; r < W; r++) {
-      double acc = r == row ? 1.0 : 0.0;
-#pragma unroll
-      for (int t = 0; t < r; t++) acc = fma(-PR[min(r, m - 1) * LDP + t], x[t], acc);
-      x[r] = r < w ? acc * invs[r] : 0.0;
-    }
-    double* M = c.Tinv + c.toff[s];   // row-major, live w x w
-#pragma unroll
-    for (int r = 0; r < W; r++)
-      if (r < w) M[r * 64 + row] = r >= row ? x[r] : 0.0;
   }
   DIAG_CLK(28);
 }

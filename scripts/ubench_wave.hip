@@ -2,7 +2,9 @@
 // synthetic SPD fronts of one shape; per-phase clocks of front 0.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include scripts/ubench_wave.hip -o graphslam_amd/build/ubench_wave
 //   ./graphslam_amd/build/ubench_wave [fronts] [m] [w]
+#ifndef UB_NO_CLOCKS   // (-DUB_NO_CLOCKS: no fenced phase stamps -- the launch times without their fences)
 #define PGO_DIAG_CLOCKS 1
+#endif
 #include "../graphslam_amd/csrc/pgo_chol.hip"
 
 #include <cstdio>
@@ -133,13 +135,18 @@ int main(int argc, char** argv) {
     mix(tt);
     printf("  output fingerprint %016llx\n", hsh);
   }
+#ifndef UB_NO_CLOCKS
   long long clk[32];
   hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_diag_clk), sizeof(clk));
+#endif
   int fl = 0;
   hipMemcpy(&fl, flag, 4, hipMemcpyDeviceToHost);
   printf("fronts %d m %d w %d: %.1f us per launch (%.3f us per front), flag %d\n", N, M, W, best * 1e3,
          best * 1e3 / N, fl);
-  printf("  front 0 clocks: start->loads %lld factor %lld store %lld trailing %lld inverse %lld\n", clk[24] - clk[23],
+#ifndef UB_NO_CLOCKS
+  // (k_front_wave: stamps 27 / 28 close the inverse / the trailing update; k_front_wave2: the reverse)
+  printf("  front 0 clocks: start->loads %lld factor %lld store %lld then %lld, %lld\n", clk[24] - clk[23],
          clk[25] - clk[24], clk[26] - clk[25], clk[27] - clk[26], clk[28] - clk[27]);
+#endif
   return 0;
 }

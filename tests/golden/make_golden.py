@@ -6,12 +6,13 @@ output of the CPU restatements:
 
 * C1, C1-nn, C2, KAT square/chain -- oracle/pgo_numpy.py (numpy + scipy SuperLU/COLAMD),
   independent of the C oracle, which tests/test_oracle.py checks against them;
-* C3 (100k poses) -- oracle/pgo_oracle.c for the whole trajectory (the numpy
-  twin is too slow for all 24 tries at this size): final error, iteration
-  counts, the error trace and every 100th final pose;
-* C3-numpy2 -- the numpy twin's first 2 linearisations of C3 (max_outer = 2),
-  so the headline size is also pinned by a source independent of the C code
-  that provides the CPU baseline: trace, error and every 100th pose;
+* C3 (100k poses) -- oracle/pgo_oracle.c for the whole trajectory: final
+  error, iteration counts, the error trace and every 100th final pose;
+* C3-numpy -- the numpy twin's whole C3 trajectory (24 tries, 8
+  linearisations; ~40 min single-threaded SuperLU), so the headline size is
+  also pinned end to end by a source independent of the C code that provides
+  the CPU baseline: trace, error and every 100th pose; C3-numpy2 -- its first 2
+  linearisations (max_outer = 2);
 * C3-gn -- the C oracle's Gauss-Newton run of C3 (error per step, final error,
   every 100th final pose);
 * C5 -- the C oracle's first linearisation, first Cholesky step and first LM
@@ -66,6 +67,11 @@ def numpy_fixture(name):
 
 
 def numpy_truncated_fixture(name, max_outer=2, stride=100):
+    """The numpy twin's trajectory of a large graph, sampled: max_outer = 2 ->
+    golden_<name>-numpy2.npz; max_outer = 0 -> the whole GTSAM-default run,
+    golden_<name>-numpy.npz (round 5: C3's 8 linearisations / 24 tries, so the
+    headline trajectory is pinned end to end by a source independent of the C
+    oracle, which is also the CPU baseline)."""
     from oracle import pgo_numpy as tw
     import time
     g = graph_for(name)
@@ -73,7 +79,8 @@ def numpy_truncated_fixture(name, max_outer=2, stride=100):
     r = tw.optimize_graph(g, tw.LMParams(max_outer=max_outer))
     tr = np.array([[t["iteration"], t["lam"], t["new_error"], float(t["accepted"])] for t in r.trace])
     idx = np.arange(0, g.num_poses, stride)
-    np.savez_compressed(os.path.join(HERE, f"golden_{name}-numpy{max_outer}.npz"), source="pgo_numpy",
+    fname = f"golden_{name}-numpy{max_outer}.npz" if max_outer else f"golden_{name}-numpy.npz"
+    np.savez_compressed(os.path.join(HERE, fname), source="pgo_numpy",
                         digest=input_digest(g), max_outer=max_outer, sample_index=idx, final_sample=r.xyt()[idx],
                         trace=tr, final_error=r.error, initial_error=r.initial_error, iterations=r.iterations,
                         inner_iterations=r.inner_iterations)
@@ -192,6 +199,8 @@ if __name__ == "__main__":
             gn_fixture(n[: -len("-gn")])
         elif n.endswith("-numpy2"):
             numpy_truncated_fixture(n[: -len("-numpy2")], 2)
+        elif n.endswith("-numpy"):
+            numpy_truncated_fixture(n[: -len("-numpy")], 0)
         elif n == "C3":
             oracle_fixture(n)
         else:

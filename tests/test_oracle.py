@@ -232,6 +232,28 @@ def test_c3_numpy_truncated_fixture_matches_c_oracle(oracle_lib):
     assert pose_close(o.poses[gold["sample_index"]], gold["final_sample"], 1e-5, 1e-6)
 
 
+def test_c3_two_restatements_agree_on_whole_trajectory():
+    """The headline size's two independent full-trajectory fixtures -- the C
+    oracle's (golden_C3.npz: AMD supernodal Cholesky) and the numpy twin's
+    (golden_C3-numpy.npz: SuperLU/COLAMD) -- on the same inputs: the same 24
+    lambda tries and accept decisions, errors per try to 2e-6 relative (observed
+    8.8e-7), final error to 1e-6 (observed 4.2e-7), sampled poses to 1e-4 m /
+    5e-6 rad (observed 2.9e-5 m, 6.5e-7 rad)."""
+    c, n = load_golden("C3"), load_golden("C3-numpy")
+    assert str(n["source"]) == "pgo_numpy" and int(n["max_outer"]) == 0
+    assert str(c["digest"]) == str(n["digest"])
+    tc, tn = c["trace"], n["trace"]
+    assert tc.shape == tn.shape == (24, 4)
+    assert np.array_equal(tc[:, [0, 1, 3]], tn[:, [0, 1, 3]])
+    ok = np.isfinite(tn[:, 2])
+    assert np.allclose(tc[ok, 2], tn[ok, 2], rtol=2e-6, atol=0)
+    assert int(c["iterations"]) == int(n["iterations"]) and int(c["inner_iterations"]) == int(n["inner_iterations"])
+    fe = float(c["final_error"])
+    assert abs(float(n["final_error"]) - fe) <= 1e-6 * fe
+    assert np.array_equal(c["sample_index"], n["sample_index"])
+    assert pose_close(n["final_sample"], c["final_sample"], 1e-4, 5e-6)
+
+
 def test_oracle_given_ordering_same_solution(oracle_lib):
     """orc_create_ordered (the CPU baseline factorises on the GPU plan's
     nested-dissection order): any fill-reducing ordering gives the same LM
