@@ -602,9 +602,25 @@ def main():
     transport = "host" if args.same_device else "rccl"
     if spec:
         from graphslam_amd import multi_gpu
-        if hybrid:
-            hc = multi_gpu.attach_hybrid(pg, r.dist, rank, world, args.groups,
-                                         transport="host" if args.same_device else "rccl")
+        if hybrid and args.same_device:
+            hc = multi_gpu.attach_hybrid(pg, r.dist, rank, world, args.groups, transport="host")
+        elif hybrid:
+            # both RCCL communicators; should any rank fail to bring one up,
+            # every rank falls back to host-transport groups, as below
+            import torch
+            ok = 1
+            try:
+                hc = multi_gpu.attach_hybrid(pg, r.dist, rank, world, args.groups, transport="rccl")
+            except Exception as e:  # noqa: BLE001
+                ok = 0
+                print(f"rank {rank}: RCCL communicators failed ({e}); falling back to the host transport",
+                      file=sys.stderr)
+            flag = torch.tensor([ok], dtype=torch.int32)
+            r.dist.all_reduce(flag, op=r.dist.ReduceOp.MIN)
+            if int(flag.item()) == 0:
+                pg.comm_free()
+                hc = multi_gpu.attach_hybrid(pg, r.dist, rank, world, args.groups, transport="host")
+                transport = "host-fallback"
         elif args.same_device:
             hc = multi_gpu.attach_host(pg, r.dist, rank, world)
         else:
