@@ -141,12 +141,50 @@ __device__ long long g_diag_clk[32];
 // rectangles), and every element's loads are in flight together.
 constexpr int kAsmPairs = 16;
 constexpr int kAsmNone = (int)0x80000000;
+
+// Frontal vector of front s before its factorisation: own rows from the
+// permuted right-hand side, below rows zero, plus the children's update
+// vectors in child order (the factorisation then carries it as an extra
+// column: forward substitution fused into the panels).  Built in LDS (v:
+// kVecChunk doubles) a row range at a time -- each element sees the same adds
+// in the same order whatever the chunking.
+constexpr int kVecChunk = 1024;
+__device__ __forceinline__ void vec_assemble_body(const CholDev& c, int s, double* v) {
+  const int m = c.m[s], w = c.w[s];
+  const int* rows = c.rows + c.rptr[s];
+  double* fv = c.fv + c.voff[s];
+  const int tid = threadIdx.x;
+  for (int c0 = 0; c0 < m; c0 += kVecChunk) {
+    const int c1 = min(m, c0 + kVecChunk);
+    if (c0) __syncthreads();   // the previous range's reads of v are done
+    for (int r = c0 + tid; r < c1; r += 256) v[r - c0] = r < w ? c.xv[3 * rows[r / 3] + r % 3] : 0.0;
+    __syncthreads();
+    for (int q = c.cptr[s]; q < c.cptr[s + 1]; q++) {
+      const int ch = c.children[q];
+      const int uc = c.m[ch] - c.w[ch];
+      const double* uv = c.fv + c.voff[ch] + c.w[ch];
+      const int* rel = c.ea_rel + c.ea_ptr[ch];
+      for (int t = tid; t < uc; t += 256) {
+        const int r = 3 * rel[t / 3] + t % 3;
+        if (r >= c0 && r < c1) v[r - c0] += uv[t];
+      }
+      __syncthreads();
+    }
+    for (int r = c0 + tid; r < c1; r += 256) fv[r] = v[r - c0];
+  }
+}
+
+// The level's tile assembly and, in workgroups [ntile, ntile + nvec) of the
+// same launch, its frontal vectors (vec_assemble_body on the tile role's LDS
+// maps, fronts vfronts[b - ntile]): disjoint data (F / fv), one launch and no
+// side-stream fork and join per level
 template <int kUnroll>
 __global__ __launch_bounds__(256, 4) void k_assemble_tile(CholDev c, const int4* __restrict__ tasks,
                                                        const int2* __restrict__ iptr, const int* __restrict__ items,
                                                        const int4* __restrict__ pairs, const double* __restrict__ V,
                                                        long long S, const double* __restrict__ D,
-                                                       const double* __restrict__ lam_p) {
+                                                       const double* __restrict__ lam_p, int ntile = 1 << 30,
+                                                       const int* __restrict__ vfronts = nullptr) {
   lane_offset(c);
   __shared__ int bcode[22 * 22];   // H item of pose block (bi, bj): asm target >= 0, ~pose (diagonal), or none
   __shared__ int bsrc[22 * 22];    // ... its first slot's factor (off-diagonal) or its pose's old index (diagonal)
@@ -155,6 +193,11 @@ __global__ __launch_bounds__(256, 4) void k_assemble_tile(CholDev c, const int4*
   __shared__ int cmap[kAsmPairs][64];            // child column landing on tile column j (-1: none)
   __shared__ long long coff[kAsmPairs][64];      // ... its offset in the child front (row wc)
   __shared__ long long pbase[kAsmPairs];         // the child front's base
+  static_assert(sizeof(coff) >= kVecChunk * sizeof(double), "frontal-vector range in coff");
+  if ((int)blockIdx.x >= ntile) {   // (workgroup-uniform)
+    vec_assemble_body(c, vfronts[blockIdx.x - ntile], reinterpret_cast<double*>(&coff[0][0]));
+    return;
+  }
   const int4 t = tasks[blockIdx.x];
   const int p = t.x, mp = c.m[p];
   const int R0 = 64 * (t.y >> 16), C0 = 64 * (t.y & 0xffff);
@@ -3077,7 +3120,12 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
     // frontal vectors (fv) on the second side stream beside the tile assembly
     // (F): disjoint data, both need only the previous levels; joined before the
     // level's first factor launch
-    const bool vec = !off("vec");
+    static const bool asm_push = getenv("PGO_ASM_PUSH") && atoi(getenv("PGO_ASM_PUSH")) == 1;
+    // (PGO_VEC_FUSE=0, A/B: the frontal vectors in their own launch on the
+    // second side stream, as before round 5)
+    static const bool vec_fuse = !(getenv("PGO_VEC_FUSE") && atoi(getenv("PGO_VEC_FUSE")) == 0) && !asm_push;
+    const bool vec = !off("vec") && !vec_fuse;
+    const int nvec = !off("vec") && vec_fuse ? lv.front_cnt : 0;
     if (vec) {
       CH_TRY(hipEventRecord(P.evs[0], s));
       CH_TRY(hipStreamWaitEvent(P.side2, P.evs[0], 0));
@@ -3085,16 +3133,22 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
              (size_t)lv.maxm * sizeof(double), P.side2, c, (const int*)(P.d_level_fronts + lv.front_off));
       CH_TRY(hipEventRecord(P.evs[1], P.side2));
     }
-    static const bool asm_push = getenv("PGO_ASM_PUSH") && atoi(getenv("PGO_ASM_PUSH")) == 1;
     // (PGO_ASM_UNROLL: children whose loads are in flight together, 1 or 2)
     static const int asm_unroll = getenv("PGO_ASM_UNROLL") ? atoi(getenv("PGO_ASM_UNROLL")) : 1;
-    if (lv.ea_cnt[0] && !off("assemble"))
+    const int ntile = lv.ea_cnt[0] && !off("assemble") ? lv.ea_cnt[0] : 0;
+    if (asm_push && ntile)
       launch(prof, kFamAssemble, [&] { return make_double2(0, level_at_bytes(P, (int)li) * nb); },
-             asm_push ? k_assemble_tile_push : asm_unroll == 2 ? k_assemble_tile<2> : k_assemble_tile<1>,
-             dim3(lv.ea_cnt[0], nb), B256, 0, s, c,
+             k_assemble_tile_push, dim3(ntile, nb), B256, 0, s, c,
              (const int4*)(P.d_ea_tasks + lv.ea_off[0]), (const int2*)(P.d_at_iptr + lv.ea_off[0]),
              (const int*)P.d_at_items, (const int4*)P.d_ea_pairs, V, (long long)P.nslots, D,
              (const double*)P.d_lambda);
+    else if (ntile + nvec > 0)   // (the tile tasks' arrays are read only by workgroups < ntile)
+      launch(prof, kFamAssemble,
+             [&] { return make_double2(0, (level_at_bytes(P, (int)li) * (ntile > 0) + lv.vec_bytes * (nvec > 0)) * nb); },
+             asm_unroll == 2 ? k_assemble_tile<2> : k_assemble_tile<1>, dim3(ntile + nvec, nb), B256, 0, s, c,
+             (const int4*)(P.d_ea_tasks + lv.ea_off[0]), (const int2*)(P.d_at_iptr + lv.ea_off[0]),
+             (const int*)P.d_at_items, (const int4*)P.d_ea_pairs, V, (long long)P.nslots, D,
+             (const double*)P.d_lambda, ntile, (const int*)(P.d_level_fronts + lv.front_off));
     if (vec) CH_TRY(hipStreamWaitEvent(s, P.evs[1], 0));
     // small fronts on the second side stream, beside the blocked path of the
     // same level (disjoint fronts); joined before the next level
