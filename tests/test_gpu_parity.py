@@ -319,16 +319,19 @@ pg = PoseGraph.from_dataset(datasets.make({name!r}))
 st = pg.optimize(default_params(lambda_lanes=3, profile_every=1))
 prof = pg.kernel_profile()
 print(json.dumps({{"final": st["final_error"].hex(), "poses": hashlib.sha256(pg.poses().tobytes()).hexdigest(),
-                   "split_launches": prof.get("k_step_diag", {{}}).get("launches", 0)}}))
+                   "split_launches": prof.get("k_step_diag", {{}}).get("launches", 0),
+                   "vec_launches": prof.get("k_vec_assemble", {{}}).get("launches", 0)}}))
 """
 
 
 def test_step_split_bitwise_fresh_processes(pgo_lib):
     """The split step (k_step_diag beside k_panel_syrk_lds on a fifth stream,
-    then k_first_trsm; PGO_STEP_SPLIT) and the deferred far updates (PGO_FAR)
-    reorder launches across streams, never the arithmetic: forced on C2 (every
-    step split), each in a fresh process, the trajectory must be bitwise the
-    default's, and the forced run must actually have taken the split path."""
+    then k_first_trsm; PGO_STEP_SPLIT), the deferred far updates (PGO_FAR) and
+    the frontal vectors in their own side-stream launch instead of the tile
+    assembly's (PGO_VEC_FUSE=0) reorder launches across streams, never the
+    arithmetic: forced on C2 (every step split), each in a fresh process, the
+    trajectory must be bitwise the default's, and the forced runs must actually
+    have taken their path."""
     import json
     import subprocess
     import sys
@@ -336,14 +339,15 @@ def test_step_split_bitwise_fresh_processes(pgo_lib):
     code = _KNOB_RUN.format(root=root, name="C2")
     res = {}
     for tag, env in (("default", {}), ("split", {"PGO_STEP_SPLIT": "1"}), ("nosplit", {"PGO_STEP_SPLIT": "0"}),
-                     ("split_far", {"PGO_STEP_SPLIT": "1", "PGO_FAR": "1"})):
+                     ("split_far", {"PGO_STEP_SPLIT": "1", "PGO_FAR": "1"}), ("vec_sep", {"PGO_VEC_FUSE": "0"})):
         r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
                            timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         res[tag] = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["split"]["split_launches"] > 0 and res["split_far"]["split_launches"] > 0
     assert res["nosplit"]["split_launches"] == 0
-    for tag in ("split", "nosplit", "split_far"):
+    assert res["vec_sep"]["vec_launches"] > 0 and res["default"]["vec_launches"] == 0
+    for tag in ("split", "nosplit", "split_far", "vec_sep"):
         assert (res[tag]["final"], res[tag]["poses"]) == (res["default"]["final"], res["default"]["poses"]), tag
 
 
