@@ -38,6 +38,11 @@ PGO_SOLVER_CHOLESKY = 1
 PGO_MULTI_SPECULATIVE = 0
 PGO_MULTI_PARTITION = 1
 PGO_MULTI_HYBRID = 2
+PGO_TRANSPORT_NONE = 0
+PGO_TRANSPORT_RCCL = 1
+PGO_TRANSPORT_HOST = 2
+TRANSPORTS = {0: "none", 1: "rccl", 2: "host"}
+ABI_VERSION = 6
 STOP_REASONS = {0: "converged", 1: "lambda_upper_bound", 2: "max_iterations", 3: "max_outer", 4: "small_cost_change",
                 5: "error"}
 
@@ -71,7 +76,8 @@ class PgoStats(C.Structure):
                 ("solves", C.c_longlong), ("ms_comm", C.c_double),
                 ("ms_factor_profiled", C.c_double), ("ms_solve_profiled", C.c_double), ("stop_reason", C.c_int),
                 ("ms_factor_graph", C.c_double), ("factor_graph_flops", C.c_double),
-                ("plan_update", C.c_int), ("ms_plan", C.c_double), ("upload_kind", C.c_int)]
+                ("plan_update", C.c_int), ("ms_plan", C.c_double), ("upload_kind", C.c_int),
+                ("handoff_retries", C.c_int), ("transport", C.c_int), ("part_transport", C.c_int)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
@@ -183,7 +189,7 @@ def lib():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.pgo_abi_version() != 5:
+    if L.pgo_abi_version() != ABI_VERSION:
         raise RuntimeError("libpgo.so ABI version mismatch")
     _lib = L
     return L

@@ -144,6 +144,11 @@ struct pgo_graph {
   // else comm)
   pgo::Comm pcomm;
   pgo::Comm* part_comm = &comm;
+  // pcomm belongs to the main communicator set up right after it (the order
+  // multi_gpu.attach_hybrid uses): pcomm_fresh = set since the last main init;
+  // a main init binds a fresh pcomm and frees a stale one (round 6: a main
+  // communicator replaced without pgo_comm_free no longer keeps the old group's)
+  bool pcomm_fresh = false, pcomm_bound = false;
   std::vector<Lane> lanes;                  // lanes 1..L-1 (speculative tries on this GPU)
   double* xb = nullptr;                     // [L x 3n] solutions of a batched factor + solve
   size_t xb_n = 0;                          // ... allocated for this many vertices (capacity)
@@ -1966,9 +1971,11 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   // PGO_MULTI_HYBRID: split over the partition group (pcomm), and the groups
   // run the speculative search over comm (one rank of every group each)
   const bool chol_lm = p.linear_solver != PGO_SOLVER_PCG && p.algorithm != PGO_ALG_GN;
-  const bool hybrid = p.multi_gpu == PGO_MULTI_HYBRID && g->pcomm.size > 1 && chol_lm;
-  if (p.multi_gpu == PGO_MULTI_HYBRID && g->pcomm.size <= 1 && g->comm.size > 1 && chol_lm)
-    return fail(g, PGO_E_ARG, "PGO_MULTI_HYBRID needs a partition-group communicator (pgo_comm_init_*_part)");
+  // (a bound partition group of one rank is the speculative search alone)
+  const bool hybrid = p.multi_gpu == PGO_MULTI_HYBRID && g->pcomm_bound && g->pcomm.size > 1 && chol_lm;
+  if (p.multi_gpu == PGO_MULTI_HYBRID && !g->pcomm_bound && g->comm.size > 1 && chol_lm)
+    return fail(g, PGO_E_ARG, "PGO_MULTI_HYBRID needs a partition-group communicator (pgo_comm_init_*_part, "
+                              "set up before the main communicator)");
   g->part_comm = hybrid ? &g->pcomm : &g->comm;
   const bool partition = (hybrid || (p.multi_gpu == PGO_MULTI_PARTITION && g->comm.size > 1)) && chol_lm;
   g->part_size = partition ? g->part_comm->size : 1;
@@ -2027,6 +2034,7 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
     int rc = body();
     if (rc == PGO_E_HIP && g->handoff_timeout) {
       g->handoff_timeout = false;
+      st.handoff_retries++;   // visible in pgo_stats / the bench's per_step (round 6)
       rc = body();
     }
     return rc;
@@ -2041,6 +2049,11 @@ int pgo_optimize(pgo_graph* g, const pgo_params* params, pgo_stats* stats) {
   const int P = spec ? cm.size : 1, me = spec ? cm.rank : 0;
   const bool exchange = spec && (P > 1 || pgo::force_collectives(&cm));   // forced: 1-rank RCCL too
   st.ranks = hybrid ? cm.size * g->pcomm.size : cm.size;
+  auto transport_of = [](const pgo::Comm& c) {
+    return c.size <= 1 && !c.nccl ? PGO_TRANSPORT_NONE : (c.host ? PGO_TRANSPORT_HOST : PGO_TRANSPORT_RCCL);
+  };
+  st.transport = transport_of(cm);
+  st.part_transport = hybrid ? transport_of(g->pcomm) : PGO_TRANSPORT_NONE;
   // lanes: concurrent tries on this GPU (Cholesky LM only)
   int L = 1;
   if (p.algorithm != PGO_ALG_GN && p.linear_solver != PGO_SOLVER_PCG && p.lambda_lanes > 1 && d.n > 0)
@@ -2334,12 +2347,24 @@ int pgo_comm_unique_id(void* out, size_t cap) {
   return pgo::comm_unique_id(out, cap, &why);
 }
 
+// a main communicator (re)initialised: the partition group's communicator set
+// up since the previous main init is bound to it, an older one is freed
+static void bind_part_comm(pgo_graph* g) {
+  if (!g->pcomm_fresh) {
+    if (g->pcomm.nccl) (void)hipSetDevice(g->device);
+    pgo::comm_free(&g->pcomm);
+  }
+  g->pcomm_bound = g->pcomm_fresh;
+  g->pcomm_fresh = false;
+}
+
 int pgo_comm_init_rccl(pgo_graph* g, const void* unique_id, size_t id_bytes, int rank, int size) {
   if (!g) return PGO_E_ARG;
   RC_TRY(ensure_hip(g));
   HIP_TRY(g, hipSetDevice(g->device));
   std::string why;
   const int rc = pgo::comm_init_rccl(&g->comm, unique_id, id_bytes, rank, size, &why);
+  bind_part_comm(g);
   return rc == PGO_OK ? rc : fail(g, rc, why);
 }
 
@@ -2348,6 +2373,7 @@ int pgo_comm_init_host(pgo_graph* g, const pgo_host_comm* comm) {
   if (g->comm.nccl) (void)hipSetDevice(g->device);
   std::string why;
   const int rc = pgo::comm_init_host(&g->comm, comm, &why);
+  bind_part_comm(g);
   return rc == PGO_OK ? rc : fail(g, rc, why);
 }
 
@@ -2357,6 +2383,7 @@ int pgo_comm_free(pgo_graph* g) {
   pgo::comm_free(&g->comm);
   pgo::comm_free(&g->pcomm);
   g->part_comm = &g->comm;
+  g->pcomm_fresh = g->pcomm_bound = false;
   return PGO_OK;
 }
 
@@ -2366,6 +2393,8 @@ int pgo_comm_init_rccl_part(pgo_graph* g, const void* unique_id, size_t id_bytes
   HIP_TRY(g, hipSetDevice(g->device));
   std::string why;
   const int rc = pgo::comm_init_rccl(&g->pcomm, unique_id, id_bytes, rank, size, &why);
+  g->pcomm_fresh = rc == PGO_OK;
+  g->pcomm_bound = false;
   return rc == PGO_OK ? rc : fail(g, rc, why);
 }
 
@@ -2374,6 +2403,8 @@ int pgo_comm_init_host_part(pgo_graph* g, const pgo_host_comm* comm) {
   if (g->pcomm.nccl) (void)hipSetDevice(g->device);
   std::string why;
   const int rc = pgo::comm_init_host(&g->pcomm, comm, &why);
+  g->pcomm_fresh = rc == PGO_OK;
+  g->pcomm_bound = false;
   return rc == PGO_OK ? rc : fail(g, rc, why);
 }
 

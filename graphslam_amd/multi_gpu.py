@@ -30,12 +30,71 @@ def unique_id() -> bytes:
     return buf.raw[:n]
 
 
+class CommSetupError(RuntimeError):
+    """An RCCL communicator could not be brought up.  Raised on EVERY rank
+    together (the setup steps end in agreement points), so a caller can fall
+    back to the host transport on all ranks without a rank left waiting in a
+    collective."""
+
+
+def _agree(dist, ok: bool, group=None) -> bool:
+    """All-reduce(MIN) of a success flag over `group` (default: every rank,
+    gloo): True only when every rank succeeded.  Every rank must call it, the
+    failed ones included."""
+    import torch
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
+def _try(fn, errs):
+    try:
+        return fn(), True
+    except Exception as e:  # noqa: BLE001 -- turned into an agreed failure
+        errs.append(repr(e))
+        return None, False
+
+
+def _rccl_setup(pg, dist, setups):
+    """Bring up RCCL communicators with agreement points between the blocking
+    steps: (1) every sub-group's first rank makes its ids, (2) the
+    ids travel over gloo, (3) each communicator is initialised in turn -- a
+    collective inside its sub-group.  After each step every rank learns whether
+    all ranks succeeded; on any failure all ranks free what they made and raise
+    CommSetupError together, so no rank is left inside a collective its peers
+    have abandoned.  setups: [(global ranks of the sub-group, its gloo group or
+    None, my position, size, init fn)]."""
+    errs = []
+    ids = []
+    ok = True
+    for ranks, grp, me, size, init in setups:            # (1) ids, made by each group's first rank
+        uid, good = _try(unique_id, errs) if me == 0 else (None, True)
+        ids.append(uid)
+        ok = ok and good
+    if not _agree(dist, ok):
+        raise CommSetupError(f"RCCL unique id failed on some rank ({'; '.join(errs) or 'elsewhere'})")
+    for k, (ranks, grp, me, size, init) in enumerate(setups):   # (2) ids over gloo
+        if size > 1:
+            obj = [ids[k]]
+            _, good = _try(lambda: dist.broadcast_object_list(obj, src=ranks[0], group=grp), errs)
+            ids[k] = obj[0]
+            ok = ok and good and ids[k] is not None
+    if not _agree(dist, ok):
+        raise CommSetupError(f"RCCL id exchange failed on some rank ({'; '.join(errs) or 'elsewhere'})")
+    for k, (ranks, grp, me, size, init) in enumerate(setups):   # (3) one communicator at a time
+        _, good = _try(lambda: init(ids[k], me, size), errs)
+        if not _agree(dist, good):
+            try:
+                pg.comm_free()
+            except Exception:  # noqa: BLE001
+                pass
+            raise CommSetupError(f"RCCL communicator {k} failed on some rank ({'; '.join(errs) or 'elsewhere'})")
+
+
 def attach_rccl(pg, dist, rank: int, world: int):
-    """RCCL communicator over all `world` ranks of the default torch.distributed group."""
-    obj = [unique_id() if rank == 0 else None]
-    if world > 1:
-        dist.broadcast_object_list(obj, src=0)
-    pg.comm_init_rccl(obj[0], rank, world)
+    """RCCL communicator over all `world` ranks of the default torch.distributed
+    group; CommSetupError on every rank if any rank fails."""
+    _rccl_setup(pg, dist, [(list(range(world)), None, rank, world, pg.comm_init_rccl)])
 
 
 class HostComm:
@@ -112,11 +171,7 @@ def attach_hybrid(pg, dist, rank: int, world: int, groups: int, transport: str =
         hs = HostComm(dist, g, groups, sgroups[i], spec[i])
         pg.comm_init_host(hs.struct)
         keep += [hp, hs]
-    else:
-        for ranks, grp, me, size, init in ((part[g], pgroups[g], i, pp, pg.comm_init_rccl_part),
-                                           (spec[i], sgroups[i], g, groups, pg.comm_init_rccl)):
-            obj = [unique_id() if me == 0 else None]
-            if size > 1:
-                dist.broadcast_object_list(obj, src=ranks[0], group=grp)
-            init(obj[0], me, size)
+    else:   # partition group first, then the main communicator (pgo.h: the order binds them)
+        _rccl_setup(pg, dist, [(part[g], pgroups[g], i, pp, pg.comm_init_rccl_part),
+                               (spec[i], sgroups[i], g, groups, pg.comm_init_rccl)])
     return keep

@@ -259,16 +259,25 @@ def estimate(pg, P: int, config: str | None = None, pd: PlanData | None = None) 
             spec_ms, _ = trajectory_ms(tries, rm, P, extra)
             ps = partition_speedups(pd, P, B, tb)
             s_dist, s_rep = ps["one"] / ps["dist"], ps["one"] / ps["rep"]
-            row = {"spec": one_ms / spec_ms, "partition_dist": s_dist, "partition_rep": s_rep,
-                   "partition": max(s_dist, s_rep)}
-            for G in groups:
+            row = {"spec": one_ms / spec_ms, "partition_dist": s_dist, "partition_rep": s_rep}
+            for G in groups:   # each group's partition with one fixed top
                 qs = partition_speedups(pd, P // G, B, tb)
-                s_pp = max(qs["one"] / qs["dist"], qs["one"] / qs["rep"])
-                h_ms, _ = trajectory_ms(tries, rm, G, extra, rm[1] / s_pp)
-                row[f"hybrid{G}"] = one_ms / h_ms
-                if B == B_CENTRAL and tb == T_BCAST_CENTRAL:
-                    hybrid_dist[G] = qs["dist"] <= qs["rep"]
+                for top in ("dist", "rep"):
+                    h_ms, _ = trajectory_ms(tries, rm, G, extra, rm[1] * qs[top] / qs["one"])
+                    row[f"hybrid{G}_{top}"] = one_ms / h_ms
             grid[key] = row
+    # Only one top runs, so each candidate is priced with a fixed top over the
+    # whole sweep, and its top is the one with the better worst case (ADVICE
+    # r05: taking the better top per grid point overstated the worst case);
+    # "partition" / "hybrid<G>" are the chosen variants' figures
+    worst = lambda k: min(r[k] for r in grid.values())   # noqa: E731
+    part_dist = worst("partition_dist") >= worst("partition_rep")
+    for G in groups:
+        hybrid_dist[G] = worst(f"hybrid{G}_dist") >= worst(f"hybrid{G}_rep")
+    for row in grid.values():
+        row["partition"] = row["partition_dist" if part_dist else "partition_rep"]
+        for G in groups:
+            row[f"hybrid{G}"] = row[f"hybrid{G}_dist" if hybrid_dist[G] else f"hybrid{G}_rep"]
     central = grid[f"B{B_CENTRAL / 1e9:.0f}_t{T_BCAST_CENTRAL * 1e6:.0f}"]
     lo = {k: min(r[k] for r in grid.values()) for k in central}
     hi = {k: max(r[k] for r in grid.values()) for k in central}
@@ -278,7 +287,8 @@ def estimate(pg, P: int, config: str | None = None, pd: PlanData | None = None) 
            "est_speedup_replicated_top": central["partition_rep"],
            "est_speedup_distributed_top": central["partition_dist"],
            "est_speedup_spec": central["spec"], "est_speedup": central["partition"],
-           "est_speedup_hybrid": {k[6:]: v for k, v in central.items() if k.startswith("hybrid")},
+           "est_speedup_hybrid": {str(G): central[f"hybrid{G}"] for G in groups},
+           "partition_distributed_top": bool(part_dist),
            "hybrid_distributed_top": {str(G): bool(v) for G, v in hybrid_dist.items()},
            "range_min": lo, "range_max": hi, "sensitivity": grid,
            "allgather_bytes_per_rank": ps["ag_bytes"],
@@ -302,10 +312,10 @@ def choose(est: dict) -> tuple[str, int, bool]:
     lo = est["range_min"]
     cands = {"spec": lo["spec"], "partition": lo["partition"]}
     for k, v in lo.items():
-        if k.startswith("hybrid"):
+        if k.startswith("hybrid") and "_" not in k:   # (hybrid<G>: the fixed-top variant chosen in estimate)
             cands[k] = v
     best = max(cands, key=lambda k: cands[k])
-    dist = lo["partition_dist"] >= lo["partition_rep"]
+    dist = est.get("partition_distributed_top", lo["partition_dist"] >= lo["partition_rep"])
     if best.startswith("hybrid"):
         G = int(best[6:])
         return "hybrid", G, est.get("hybrid_distributed_top", {}).get(str(G), True)

@@ -33,7 +33,9 @@
 extern "C" {
 #endif
 
-#define PGO_ABI_VERSION 5
+#define PGO_ABI_VERSION 6   /* 6: pgo_stats.handoff_retries / transport / part_transport
+                                 (round 6); 5: the hybrid mode's partition-group
+                                 communicator, pgo_debug_poison_fronts */
 
 /* ---- status codes (GTSAM exception each one replaces) -------------------- */
 #define PGO_OK 0
@@ -185,7 +187,20 @@ typedef struct {
      full upload, 2 appended in place (new keyframes / factors after the
      previous ones: the live re-solve); its host+upload time is ms_upload */
   int upload_kind;
+  /* factorisations re-run because an in-launch hand-off timed out (a workgroup
+     starved on a time-sliced GPU: the poll gives up after
+     PGO_HANDOFF_TIMEOUT_MS and the try is run once more before the optimize
+     fails with PGO_E_HIP).  0 in a healthy run; the parity tests assert it. */
+  int handoff_retries;
+  /* the transport of the handle's communicators on this call: PGO_TRANSPORT_*
+     (main communicator; part_transport: the hybrid's partition group) */
+  int transport;
+  int part_transport;
 } pgo_stats;
+
+#define PGO_TRANSPORT_NONE 0     /* no communicator (one rank)                     */
+#define PGO_TRANSPORT_RCCL 1     /* RCCL over xGMI                                 */
+#define PGO_TRANSPORT_HOST 2     /* the caller's host callbacks (gloo in tests)    */
 
 /* pgo_stats.stop_reason.  GTSAM reports every one of these as convergence
    (an LM that gives up leaves the values unchanged, so checkConvergence sees a

@@ -17,12 +17,14 @@ output of the CPU restatements:
   every 100th final pose);
 * C5 -- the C oracle's first linearisation, first Cholesky step and first LM
   linearisation (sampled); C5-numpy -- the numpy twin's first linearisation
-  (0.5 chi^2, sampled gradient and H diagonal blocks), a second source.
+  (0.5 chi^2, sampled gradient and H diagonal blocks), a second source;
+  C5-lm5 -- the C oracle's first 5 LM linearisations of C5 (every lambda try,
+  the error after them, a 1000-pose sample of the values; round 6).
 
 Each fixture also records a SHA-256 of the generated inputs so a change of the
 generator is detected instead of silently comparing different graphs.
 
-    python tests/golden/make_golden.py [C1 C1-nn C2 C3 ...]
+    python tests/golden/make_golden.py [C1 C1-nn C2 C3 C3-gn C3-numpy C5 C5-numpy C5-lm5 ...]
 """
 from __future__ import annotations
 
@@ -119,6 +121,35 @@ def c5_fixture(stride=1000):
           "GFLOP", s["factor_flops"] / 1e9, "t", time.time() - t0)
 
 
+def c5_trajectory_fixture(max_outer=5, stride=1000):
+    """C5 past its first linearisation (round 6): the C oracle's first
+    `max_outer` LM linearisations -- every lambda try (iteration, lambda,
+    candidate error, accept decision), the error after each linearisation and
+    a 1000-pose sample of the values after the last -- on the GPU plan's
+    nested-dissection ordering, so a -m gpu test can walk the same tries
+    (golden_C5-lm<max_outer>.npz)."""
+    import time
+    from graphslam_amd.pose_graph import PoseGraph
+    from oracle.oracle import Oracle
+    g = graph_for("C5")
+    pg = PoseGraph.from_dataset(g)
+    order = pg.debug_ordering()
+    pg.close()
+    t0 = time.time()
+    o = Oracle(g, order=order)
+    r = o.optimize(max_outer=max_outer)
+    s = r.stats
+    idx = np.arange(0, g.num_poses, stride)
+    np.savez_compressed(os.path.join(HERE, f"golden_C5-lm{max_outer}.npz"), source="pgo_oracle.c",
+                        digest=input_digest(g), max_outer=max_outer, sample_index=idx,
+                        trace=r.trace[:, [0, 1, 4, 6]], initial_error=s["initial_error"],
+                        final_error=s["final_error"], iterations=s["iterations"],
+                        inner_iterations=s["inner_iterations"], linearizations=s["linearizations"],
+                        final_sample=r.poses[idx])
+    print("C5 max_outer", max_outer, "err", s["initial_error"], "->", s["final_error"], "tries",
+          s["inner_iterations"], "it", s["iterations"], "t", time.time() - t0)
+
+
 def c5_numpy_fixture(stride=1000):
     """C5's first linearisation pinned by the numpy twin (independent of the C
     oracle that made golden_C5.npz): 0.5 chi^2 at the dead-reckoned values, and
@@ -193,6 +224,8 @@ if __name__ == "__main__":
     for n in names:
         if n == "C5":
             c5_fixture()
+        elif n.startswith("C5-lm"):
+            c5_trajectory_fixture(int(n[len("C5-lm"):]))
         elif n == "C5-numpy":
             c5_numpy_fixture()
         elif n.endswith("-gn"):

@@ -55,7 +55,7 @@ int main(void) {
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", f"-I{ROOT}/include", str(src), "-o", str(exe),
                     _lib.LIB_PATH, f"-Wl,-rpath,{os.path.dirname(_lib.LIB_PATH)}"], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
-    assert r.returncode == 0 and r.stdout.startswith("ok 5"), (r.returncode, r.stdout, r.stderr)
+    assert r.returncode == 0 and r.stdout.startswith("ok 6"), (r.returncode, r.stdout, r.stderr)
 
 
 def test_default_params_are_gtsam_defaults(pgo_lib):

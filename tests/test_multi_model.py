@@ -45,9 +45,17 @@ def test_estimate_and_choice():
         assert set(e["est_speedup_hybrid"]) == {str(G) for G in range(2, P) if P % G == 0}
         mode, groups, dist = multi_model.choose(e)
         lo = e["range_min"]
-        best = max(v for k, v in lo.items() if k in ("spec", "partition") or k.startswith("hybrid"))
+        best = max(v for k, v in lo.items() if k in ("spec", "partition") or (k.startswith("hybrid") and "_" not in k))
         got = lo["partition"] if mode == "partition" else lo["spec"] if mode == "spec" else lo[f"hybrid{groups}"]
         assert got == best
+        # each candidate's worst case is that of ONE fixed top over the whole sweep
+        for G in (G for G in range(2, P) if P % G == 0):
+            top = "dist" if e["hybrid_distributed_top"][str(G)] else "rep"
+            assert lo[f"hybrid{G}"] == lo[f"hybrid{G}_{top}"] == max(lo[f"hybrid{G}_dist"], lo[f"hybrid{G}_rep"])
+        top = "dist" if e["partition_distributed_top"] else "rep"
+        assert lo["partition"] == lo[f"partition_{top}"]
+        if mode == "hybrid":
+            assert dist == e["hybrid_distributed_top"][str(groups)]
         assert e["measured_on_hardware"] is False
 
 
