@@ -49,6 +49,8 @@ struct CholDev {
   int vst, xst, pst;               // fv, xv, backward partials per lane
   unsigned long long poll_ticks;   // in-launch hand-off: give up after this many 10 ns ticks
   int diag_full;                   // PGO_DIAG_FULL=1 (A/B): diagonal tiles factored over all four 16-column blocks
+  int diag8;                       // diagonal tiles in 8-column steps on four concurrent waves (diag_factor_invert8;
+                                   // PGO_DIAG8=0: the 16-column blocks of diag_factor_invert)
 };
 
 // this workgroup's lane (blockIdx.y): every lane factors H + lambda_y I with
@@ -76,6 +78,8 @@ static CholDev dev_view(const CholPlan& P) {
   c.ns = P.ns;
   static const int diag_full = getenv("PGO_DIAG_FULL") && atoi(getenv("PGO_DIAG_FULL")) == 1;
   c.diag_full = diag_full;
+  static const int diag8 = getenv("PGO_DIAG8") ? atoi(getenv("PGO_DIAG8")) : 0;
+  c.diag8 = diag8;
   c.fst = P.ftotal;
   c.tst = 2 * P.ttotal;
   c.tfo = P.ttotal;
@@ -120,9 +124,12 @@ __device__ unsigned long long g_stamps[kMaxStampSlots][10];
 
 #ifdef PGO_DIAG_CLOCKS
 __device__ long long g_diag_clk[32];
+__device__ long long g_d8_clk[4][8][8];   // diag_factor_invert8: [wave][step][phase]
 #define DIAG_CLK(q) if (threadIdx.x == 0 && blockIdx.x == 0) g_diag_clk[q] = clock64()
+#define D8_CLK(k, q) if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) g_d8_clk[threadIdx.x >> 6][k][q] = clock64()
 #else
 #define DIAG_CLK(q)
+#define D8_CLK(k, q)
 #endif
 
 
@@ -1294,6 +1301,239 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
   return bad;
 }
 
+// ---- diagonal tile in 8-column steps on four concurrent waves (round 6) ----
+// The same output as diag_factor_invert -- X = L^-1 of the 64x64 SPD tile T
+// (LDS, ld 65, lower valid, identity past the live size nbl) into W (ld 65,
+// zeros on entry, lower X, zeros above) -- with the pivot chain cut to what
+// one wave must do in sequence: eight lane-redundant 8x8 factors (chol8_lane)
+// and, between them, two short element-parallel phases.  Everything else runs
+// beside the chain on the other waves, synchronised by LDS flags (workgroup
+// scope release / acquire, no s_barrier per step):
+//   wave 0 (the chain), step k (kb = 8k): A_kk (final) -> chol8_lane -> each
+//     lane i >= kb+8 solves its row of block column k against the lane-held
+//     L_kk (x_i = a_i L_kk^-T; stored transposed in T's strict upper part, at
+//     T[(kb + q) + 65 i], where row i's eight values are contiguous) -> the
+//     next diagonal block A_{k+1,k+1} -= L_{k+1,k} L_{k+1,k}^T one element per
+//     lane -> flag PANEL = k + 1;
+//   wave 1 (trailing updates, v_mfma_f64_16x16x4f64 tiles): after PANEL > k,
+//     panel k onto block column k+1 below its diagonal block (flag T1A), then
+//     onto the tile column from block k+2 (flag T1B: blocks k+2, k+3, what the
+//     chain's next two steps read), then the rest;
+//   waves 2 and 3 (the inverse, by 8-row blocks of parity p): X_ss =
+//     inv8(chol8(A_ss)) in registers for s = p mod 2, S_i += L_{i,s-1} X_{s-1}
+//     (MFMA, into W) for the wave's row blocks i >= s once row block s-1 of X
+//     is final (flag XDONE), then row block s of X = -X_ss [S_s | -I] (flag
+//     XDONE = s + 1).
+// Every element of T and W has one writer per update and sees its updates in
+// panel order (the flags order the writers), every sum has a fixed order: the
+// result does not depend on the waves' timing.  A flag wait gives up after a
+// bounded spin (never expected) and reports it as bit 2 of the return value,
+// which the callers OR into the pivot flag (the host's hand-off timeout path).
+namespace d8f {
+constexpr int PANEL = 0, T1A = 1, T1B = 2, XDONE = 3, ERR = 4;
+}
+__device__ __forceinline__ void lds_signal(int* fl, int which, int v) {
+  __hip_atomic_store(fl + which, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait(int* fl, int which, int v) {
+  int n = 0;
+  while (__hip_atomic_load(fl + which, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
+    if (++n > (1 << 21)) {   // ~0.1 s: a lost signal must never hang the GPU
+      __hip_atomic_store(fl + d8f::ERR, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// D(16x16) = sum_{q < 8} A(row, q) B(q, col) on one wave, operands read from
+// LDS by row: A(row, q) = Ar[row][q0 + q], B(q, col) = Bc[col][q0 + q] with
+// rows at pa(row), pb(col) (ld 65 "transposed" storage: element q of row r at
+// base[q + 65 r]); D in the f64 MFMA layout (lane l, reg r -> row (l >> 4) + 4r,
+// col l & 15); acc holds the initial values
+__device__ __forceinline__ d4 mm16x8(const double* A, const double* B, int q0, int ra, int rb, d4 acc) {
+  const int l = threadIdx.x & 63, kq = l >> 4;
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    const double a = A[(q0 + 4 * u + kq) + 65 * ra];
+    const double b = B[(q0 + 4 * u + kq) + 65 * rb];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// trailing tile on wave 1: T[R + row][C + col] -= sum_q L[R + row][kb + q] L[C + col][kb + q]
+// for row + R < nbl, col + C < cend, and (lower) R + row >= C + col
+__device__ __forceinline__ void d8_trail_tile(double* T, int kb, int R, int C, int nbl, int cend, bool lower) {
+  const int l = threadIdx.x & 63;
+  const d4 z = {0, 0, 0, 0};
+  const d4 v = mm16x8(T, T, kb, min(R + (l & 15), 63), min(C + (l & 15), 63), z);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int i = R + (l >> 4) + 4 * r, j = C + (l & 15);
+    if (i < nbl && j < cend && (!lower || i >= j)) {
+      double* p = T + i + 65 * j;
+      *p = *p - v[r];
+    }
+  }
+}
+
+__device__ __forceinline__ int diag_factor_invert8(double* T, double* W, double* bc, int nbl = 64) {
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  int* fl = reinterpret_cast<int*>(bc);
+  const int K = (nbl + 7) >> 3;   // live 8-column steps
+  if (tid < 8) fl[tid] = 0;
+  __syncthreads();
+  DIAG_CLK(0);
+  int ret = 0;
+  if (wv == 0) {   // ---------------- the pivot chain
+    for (int k = 0; k < K; k++) {
+      const int kb = 8 * k;
+      double a[36], iv[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++) a[P8(i, j)] = T[(kb + i) + 65 * (kb + j)];
+      D8_CLK(k, 0);
+      if (chol8_lane(a, iv)) ret |= 1;
+      D8_CLK(k, 1);
+      if (k == K - 1) break;
+      lds_wait(fl, d8f::T1A, k);   // block column k through panel k-1 (wave 1)
+      D8_CLK(k, 2);
+      const int i = l;
+      if (i >= kb + 8 && i < nbl) {   // row i of block column k: x = a L_kk^-T
+        double x[8];
+#pragma unroll
+        for (int c = 0; c < 8; c++) x[c] = T[i + 65 * (kb + c)];
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+          double s = x[c];
+#pragma unroll
+          for (int t = 0; t < c; t++) s = fma(-a[P8(c, t)], x[t], s);
+          x[c] = s * iv[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 8; c++) T[(kb + c) + 65 * i] = x[c];
+      }
+      __builtin_amdgcn_wave_barrier();
+      D8_CLK(k, 3);
+      lds_wait(fl, d8f::T1B, k);   // the next diagonal block through panel k-1 (wave 1)
+      D8_CLK(k, 4);
+      {   // A_{k+1,k+1} -= L_{k+1,k} L_{k+1,k}^T, lane (r, c), r >= c
+        const int r = l >> 3, c = l & 7, ii = kb + 8 + r, jj = kb + 8 + c;
+        if (c <= r && ii < nbl) {
+          double t = T[ii + 65 * jj];
+#pragma unroll
+          for (int q = 0; q < 8; q++) t = fma(-T[(kb + q) + 65 * ii], T[(kb + q) + 65 * jj], t);
+          T[ii + 65 * jj] = t;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      lds_signal(fl, d8f::PANEL, k + 1);
+      D8_CLK(k, 5);
+    }
+    DIAG_CLK(1);
+  } else if (wv == 1) {   // ---------------- trailing updates
+    for (int k = 0; k + 1 < K; k++) {
+      const int kb = 8 * k;
+      lds_wait(fl, d8f::PANEL, k + 1);
+      D8_CLK(k, 0);
+      for (int R = kb + 16; R < nbl; R += 16) d8_trail_tile(T, kb, R, kb + 8, nbl, min(kb + 16, nbl), false);
+      lds_signal(fl, d8f::T1A, k + 1);
+      D8_CLK(k, 1);
+      for (int R = kb + 16; R < nbl; R += 16) d8_trail_tile(T, kb, R, kb + 16, nbl, nbl, true);
+      lds_signal(fl, d8f::T1B, k + 1);
+      D8_CLK(k, 2);
+      for (int C = kb + 32; C < nbl; C += 16)
+        for (int R = C; R < nbl; R += 16) d8_trail_tile(T, kb, R, C, nbl, nbl, true);
+      D8_CLK(k, 3);
+    }
+  } else {   // ---------------- the inverse, row blocks of parity p
+    const int p = wv - 2;
+    for (int s = 0; s < K; s++) {
+      const int sb = 8 * s;
+      lds_wait(fl, d8f::PANEL, s);   // A_ss final, panels < s written
+      D8_CLK(s, 0);
+      double xs[36], iv[8];
+      const bool mine = (s & 1) == p;
+      if (mine) {   // X_ss = L_ss^-1, lane-redundant (the chain's own factor of the same A_ss)
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+          for (int j = 0; j <= i; j++) xs[P8(i, j)] = T[(sb + i) + 65 * (sb + j)];
+        chol8_lane(xs, iv);
+        inv8_lane(xs, iv);
+      }
+      D8_CLK(s, 1);
+      if (s >= 1) {   // S_i += L_{i,s-1} X_{s-1} for my row blocks i >= s
+        lds_wait(fl, d8f::XDONE, s);
+        D8_CLK(s, 2);
+        const int tb = sb - 8;                       // X_{s-1}: rows tb.., columns < sb
+        const int i0 = s + (((s & 1) == p) ? 0 : 1);  // my first row block >= s
+        const int nr = i0 < K ? 8 * ((K - i0 + 1) >> 1) : 0;   // stacked rows (8 per block)
+        for (int R = 0; R < nr; R += 16)
+          for (int C = 0; C < sb; C += 16) {
+            const int rr = R + (l & 15);                                   // A operand's stacked row
+            const int ra = min(8 * (i0 + 2 * (rr >> 3)) + (rr & 7), 63);
+            const int cb = min(C + (l & 15), 63);                          // B operand's column
+            // A(row, q) = L[ra][tb + q] = T[(tb + q) + 65 ra]; B(q, col) = X[tb + q][cb] = W[(tb + q) + 65 cb]
+            d4 acc;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+              const int ro = R + (l >> 4) + 4 * r, row = min(8 * (i0 + 2 * (ro >> 3)) + (ro & 7), 63);
+              acc[r] = W[row + 65 * min(C + (l & 15), 63)];
+            }
+            const int kq = l >> 4;
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+              const double av = T[(tb + 4 * u + kq) + 65 * ra];
+              const double bv = W[(tb + 4 * u + kq) + 65 * cb];
+              acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+              const int ro = R + (l >> 4) + 4 * r, blk = i0 + 2 * (ro >> 3), col = C + (l & 15);
+              if (ro < nr && blk < K && col < sb && 8 * blk + (ro & 7) < nbl) W[(8 * blk + (ro & 7)) + 65 * col] = acc[r];
+            }
+          }
+        __builtin_amdgcn_wave_barrier();
+      }
+      D8_CLK(s, 3);
+      if (mine) {   // row block s of X: -X_ss [S_s | -I], lane = column
+        const int col = l;
+        if (col < sb + 8) {
+          double sv[8];
+#pragma unroll
+          for (int q = 0; q < 8; q++) sv[q] = col < sb ? W[(sb + q) + 65 * col] : (q == col - sb ? -1.0 : 0.0);
+#pragma unroll
+          for (int r = 0; r < 8; r++) {
+            double o = 0.0;
+#pragma unroll
+            for (int q = 0; q <= r; q++) o = fma(xs[P8(r, q)], sv[q], o);
+            if (sb + r < nbl) W[(sb + r) + 65 * col] = -o;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        lds_signal(fl, d8f::XDONE, s + 1);
+        D8_CLK(s, 4);
+      }
+    }
+  }
+  __syncthreads();
+  DIAG_CLK(12);
+  if (fl[d8f::ERR]) ret |= 2;
+  return ret;
+}
+
+// the diagonal tile's factor + inverse by the configured form; a pivot that is
+// not positive and finite (bit 1) or a lost LDS flag (bit 2: the host's
+// hand-off timeout path) goes to the lane's pivot flag
+__device__ __forceinline__ void factor_invert_tile(const CholDev& c, double* Ts, double* Ws, double* bc, int nb) {
+  const int nbl = c.diag_full ? 64 : nb;
+  const int r = c.diag8 ? diag_factor_invert8(Ts, Ws, bc, nbl) : (diag_factor_invert(Ts, Ws, bc, nbl) ? 1 : 0);
+  if (r) __hip_atomic_fetch_or(c.flag, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---- in-launch hand-off of a diagonal tile's inverse (MI355X_MICROARCH.md,
 // inter-workgroup visibility, the "sc1 stores / sc1 flag / sc1 loads" row): the
 // diagonal workgroup stores the inverse (trsm operand order) and the panel's y
@@ -1847,7 +2087,7 @@ __device__ __forceinline__ void syrk_diag_body(const CholDev& c, const int4 t, i
     Ws[i + j * 65] = 0.0;
   }
   __syncthreads();
-  if (diag_factor_invert(Ts, Ws, bc, c.diag_full ? 64 : nb)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  factor_invert_tile(c, Ts, Ws, bc, nb);
   STAMP(slot, 2);
   double* Fs = fcol(c.F + c.foff[s], m, true, kn) + kn;   // the diagonal tile, ld fld(m, true, kn)
   double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;   // row-major L^-1 of the tile
@@ -1890,7 +2130,7 @@ __device__ __forceinline__ void first_diag_body(const CholDev& c, int s, double*
     Ws[i + j * 65] = 0.0;
   }
   __syncthreads();
-  if (diag_factor_invert(Ts, Ws, bc, c.diag_full ? 64 : nb)) __hip_atomic_fetch_or(c.flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  factor_invert_tile(c, Ts, Ws, bc, nb);
   double* M = c.Tinv + c.toff[s];
   double* v = c.fv + c.voff[s];
   publish_inverse(M + c.tfo, Ws, nb);
@@ -2230,9 +2470,12 @@ __global__ void k_set_flag(int* flag, int v) { flag[threadIdx.x] |= v; }
 // Distributed top: panels / tail columns between ranks.  Task (front, kn, nb |
 // kind << 16, owner); its payload sits in the owner's region of buf (owner *
 // rstride), lane y at y * lstride, + loff.  kind 0 (a factored panel): F rows
-// [kn, m) x columns [kn, kn + nb), the panel's row-major inverse (backward
-// solve), the frontal vector [kn, m) (y and the rows below, forward
-// substitution so far); kind 1 (tail): F rows [kn, m) x columns [kn, kn + nb).
+// [kn + nb, m) x columns [kn, kn + nb) -- the L below the diagonal tile; the
+// tile's own L is never stored (store_factor: every reader uses its inverse),
+// so its region is not sent (round 6) -- the panel's row-major
+// inverse (backward solve), the frontal vector [kn, m) (y and the rows below,
+// forward substitution so far); kind 1 (tail): F rows [kn, m) x columns
+// [kn, kn + nb).
 // Pack: this rank's items (owner == me); unpack: the others'.
 template <bool kPack>
 __global__ __launch_bounds__(256) void k_xpanel(CholDev c, const int4* __restrict__ tasks,
@@ -2244,9 +2487,9 @@ __global__ __launch_bounds__(256) void k_xpanel(CholDev c, const int4* __restric
   const int s = t.x, kn = t.y, nb = t.z & 0xffff, kind = t.z >> 16, m = c.m[s];
   double* b = buf + t.w * rstride + blockIdx.y * offs[2 * blockIdx.x + 1] + offs[2 * blockIdx.x];
   double* Fs = c.F + c.foff[s];
-  const int rows = m - kn, tid = threadIdx.x;
+  const int r0 = kind == 0 ? nb : 0, rows = m - kn - r0, tid = threadIdx.x;
   for (int cc = 0; cc < nb; cc++) {
-    double* col = fcol(Fs, m, true, kn + cc) + kn;   // (a top front on the blocked path)
+    double* col = fcol(Fs, m, true, kn + cc) + kn + r0;   // (a top front on the blocked path)
     double* bc = b + (size_t)cc * rows;
     for (int r = tid; r < rows; r += 256) {
       if (kPack) bc[r] = col[r];
@@ -2255,6 +2498,7 @@ __global__ __launch_bounds__(256) void k_xpanel(CholDev c, const int4* __restric
   }
   if (kind != 0) return;
   b += (size_t)rows * nb;
+  const int vrows = m - kn;
   double* M = c.Tinv + c.toff[s] + (kn / 64) * 4096;
   for (int i = tid; i < 4096; i += 256) {
     if (kPack) b[i] = M[i];
@@ -2262,7 +2506,7 @@ __global__ __launch_bounds__(256) void k_xpanel(CholDev c, const int4* __restric
   }
   b += 4096;
   double* v = c.fv + c.voff[s] + kn;
-  for (int r = tid; r < rows; r += 256) {
+  for (int r = tid; r < vrows; r += 256) {
     if (kPack) b[r] = v[r];
     else v[r] = b[r];
   }

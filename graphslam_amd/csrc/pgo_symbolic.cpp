@@ -500,7 +500,9 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
     x.size.assign(psz, 0);
     for (const int4& t : items) {
       const int s = t.x, kn = t.y, nb = t.z & 0xffff, kind = t.z >> 16, m = P.m[s];
-      const long long sz = kind == 0 ? (long long)(m - kn) * nb + 4096 + (m - kn) : (long long)(m - kn) * nb;
+      // kind 0: the L below the diagonal tile (the tile's own L is never stored),
+      // the inverse, the frontal vector; kind 1: the tail columns whole
+      const long long sz = kind == 0 ? (long long)(m - kn - nb) * nb + 4096 + (m - kn) : (long long)(m - kn) * nb;
       S.xp_tasks.push_back(t);
       S.xp_loff.push_back(x.size[t.w]);
       x.size[t.w] += sz;
