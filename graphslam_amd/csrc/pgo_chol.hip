@@ -49,8 +49,6 @@ struct CholDev {
   int vst, xst, pst;               // fv, xv, backward partials per lane
   unsigned long long poll_ticks;   // in-launch hand-off: give up after this many 10 ns ticks
   int diag_full;                   // PGO_DIAG_FULL=1 (A/B): diagonal tiles factored over all four 16-column blocks
-  int diag8;                       // diagonal tiles in 8-column steps on four concurrent waves (diag_factor_invert8;
-                                   // PGO_DIAG8=0: the 16-column blocks of diag_factor_invert)
 };
 
 // this workgroup's lane (blockIdx.y): every lane factors H + lambda_y I with
@@ -78,8 +76,6 @@ static CholDev dev_view(const CholPlan& P) {
   c.ns = P.ns;
   static const int diag_full = getenv("PGO_DIAG_FULL") && atoi(getenv("PGO_DIAG_FULL")) == 1;
   c.diag_full = diag_full;
-  static const int diag8 = getenv("PGO_DIAG8") ? atoi(getenv("PGO_DIAG8")) : 0;
-  c.diag8 = diag8;
   c.fst = P.ftotal;
   c.tst = 2 * P.ttotal;
   c.tfo = P.ttotal;
@@ -125,11 +121,20 @@ __device__ unsigned long long g_stamps[kMaxStampSlots][10];
 #ifdef PGO_DIAG_CLOCKS
 __device__ long long g_diag_clk[32];
 __device__ long long g_d8_clk[4][8][8];   // diag_factor_invert8: [wave][step][phase]
+__device__ int g_d8_dbg;   // diagnostics: 1 = waves 2-3 idle, 2 = no waits on wave 1, 4 = wave 1 idle
+#define D8_DBG(bit) (g_d8_dbg & (bit))
 #define DIAG_CLK(q) if (threadIdx.x == 0 && blockIdx.x == 0) g_diag_clk[q] = clock64()
-#define D8_CLK(k, q) if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) g_d8_clk[threadIdx.x >> 6][k][q] = clock64()
+#define D8_CLK(k, q)                                                                 \
+  do {                                                                               \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                              \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) g_d8_clk[threadIdx.x >> 6][k][q] = clock64(); \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+  } while (0)
 #else
 #define DIAG_CLK(q)
 #define D8_CLK(k, q)
+#define D8_DBG(bit) 0
 #endif
 
 
@@ -1212,6 +1217,72 @@ __device__ __forceinline__ bool diag16_lane(double* TJ, double* WJ, double* sc) 
   return bad;
 }
 
+// x = L^-1 x in place, L an 8x8 lower block held whole in every lane (packed,
+// iv[k] = 1 / L_kk): the forward substitution of one right-hand side per lane
+__device__ __forceinline__ void fwd8_lane(const double (&a)[36], const double (&iv)[8], double (&x)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    double s = x[k];
+#pragma unroll
+    for (int t = 0; t < k; t++) s = fma(-a[P8(k, t)], x[t], s);
+    x[k] = s * iv[k];
+  }
+}
+
+// diag16_lane's factor and inverse with the lane-redundant work cut to the two
+// 8x8 factors (round 6).  Every other piece is one forward substitution per
+// lane against the lane-held L11 / L22 -- lanes 0-7 one right-hand side e_c
+// each (a column of X11 / X22), lanes 8-15 a row of A21 (-> a row of L21) /
+// a column of -Y (-> a column of X21 = -X22 Y, Y = L21 X11) -- in the same
+// instructions, instead of inv8_lane's lane-redundant inverse and its lane-0
+// stores (36 each) and the L21 / X21 products through LDS.  Same outputs as
+// diag16_lane (L21 in TJ, X lower in WJ with zeros above); a different
+// operation order, so not bitwise its result (the oracle tolerances hold).
+__device__ __forceinline__ bool diag16_fs(double* TJ, double* WJ, double* sc) {
+  const int l = threadIdx.x & 63, r = l >> 3, c = l & 7;
+  double a[36], iv[8], x[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j <= i; j++) a[P8(i, j)] = TJ[i + j * 65];
+  const bool xl = l < 8, rl = l >= 8 && l < 16;
+#pragma unroll
+  for (int k = 0; k < 8; k++) x[k] = xl ? (k == l ? 1.0 : 0.0) : (rl ? TJ[l + k * 65] : 0.0);   // e_l / row l-8 of A21
+  WJ[r + (8 + c) * 65] = 0.0;   // block (0, 1) of X
+  bool bad = chol8_lane(a, iv);
+  fwd8_lane(a, iv, x);          // lanes 0-7: column l of X11; lanes 8-15: row l-8 of L21
+  if (xl || rl) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) (xl ? WJ[k + l * 65] : TJ[l + k * 65]) = x[k];
+  }
+  __builtin_amdgcn_wave_barrier();
+  // A22 -= L21 L21^T (lower), Y = L21 X11 (X11 (k, c) zero for k < c)
+  double t = TJ[(8 + r) + (8 + c) * 65], y = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const double lrk = TJ[(8 + r) + k * 65];
+    t = fma(-lrk, TJ[(8 + c) + k * 65], t);
+    y = fma(lrk, WJ[k + c * 65], y);
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (c <= r) TJ[(8 + r) + (8 + c) * 65] = t;
+  sc[r * 8 + c] = y;
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j <= i; j++) a[P8(i, j)] = TJ[(8 + i) + (8 + j) * 65];
+#pragma unroll
+  for (int k = 0; k < 8; k++) x[k] = xl ? (k == l ? 1.0 : 0.0) : (rl ? -sc[k * 8 + (l - 8)] : 0.0);   // e_l / -Y column
+  bad = chol8_lane(a, iv) || bad;
+  fwd8_lane(a, iv, x);          // lanes 0-7: column l of X22; lanes 8-15: column l-8 of X21
+  if (xl || rl) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) (xl ? WJ[(8 + k) + (8 + l) * 65] : WJ[(8 + k) + (l - 8) * 65]) = x[k];
+  }
+  return bad;
+}
+
 // Cholesky factor L and inverse X = L^-1 of the 64x64 SPD tile T (LDS,
 // column-major, ld 65, lower part valid, identity beyond the live size), by the
 // 4 waves of the workgroup: right-looking over 16-column blocks J; the 16x16
@@ -1229,6 +1300,7 @@ __device__ __forceinline__ bool diag16_lane(double* TJ, double* WJ, double* sc) 
 // element sees the same operations as with all four blocks, the callers read
 // only the live part of L and X.
 // Returns (wave 0) whether a pivot was not positive and finite.
+template <bool kFS = true>   // kFS: diag16_fs (round 6), else diag16_lane
 __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double* bc, int nbl = 64) {
   const int tid = threadIdx.x, wv = tid >> 6;
   const int Jn = (nbl + 15) >> 4;   // live 16-column blocks (1..4)
@@ -1243,7 +1315,7 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
         st16(TJ, v, true);
         __builtin_amdgcn_wave_barrier();
       }
-      bad = diag16_lane(TJ, W + o + o * 65, bc) || bad;
+      bad = (kFS ? diag16_fs(TJ, W + o + o * 65, bc) : diag16_lane(TJ, W + o + o * 65, bc)) || bad;
     }
     __syncthreads();
     DIAG_CLK(1 + 3 * J);
@@ -1332,18 +1404,24 @@ __device__ __forceinline__ bool diag_factor_invert(double* T, double* W, double*
 namespace d8f {
 constexpr int PANEL = 0, T1A = 1, T1B = 2, XDONE = 3, ERR = 4;
 }
+// signal: this wave's LDS writes have completed (lgkmcnt(0); the LDS is
+// coherent across the CU), then the flag store.  wait: poll the flag (the
+// loads after it are issued only once it is seen); no global-memory fence --
+// the flags order LDS traffic only.
 __device__ __forceinline__ void lds_signal(int* fl, int which, int v) {
-  __hip_atomic_store(fl + which, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  *reinterpret_cast<volatile int*>(fl + which) = v;
 }
 __device__ __forceinline__ void lds_wait(int* fl, int which, int v) {
   int n = 0;
-  while (__hip_atomic_load(fl + which, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
+  while (*reinterpret_cast<volatile int*>(fl + which) < v) {
     if (++n > (1 << 21)) {   // ~0.1 s: a lost signal must never hang the GPU
-      __hip_atomic_store(fl + d8f::ERR, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      *reinterpret_cast<volatile int*>(fl + d8f::ERR) = 1;
       break;
     }
     __builtin_amdgcn_s_sleep(1);
   }
+  asm volatile("" ::: "memory");
 }
 
 // D(16x16) = sum_{q < 8} A(row, q) B(q, col) on one wave, operands read from
@@ -1362,24 +1440,52 @@ __device__ __forceinline__ d4 mm16x8(const double* A, const double* B, int q0, i
   return acc;
 }
 
-// trailing tile on wave 1: T[R + row][C + col] -= sum_q L[R + row][kb + q] L[C + col][kb + q]
-// for row + R < nbl, col + C < cend, and (lower) R + row >= C + col
-__device__ __forceinline__ void d8_trail_tile(double* T, int kb, int R, int C, int nbl, int cend, bool lower) {
-  const int l = threadIdx.x & 63;
-  const d4 z = {0, 0, 0, 0};
-  const d4 v = mm16x8(T, T, kb, min(R + (l & 15), 63), min(C + (l & 15), 63), z);
+// trailing tiles on wave 1, up to 3 per call: T[R + row][C + col] -= sum_q
+// L[R + row][kb + q] L[C + col][kb + q] for row + R < nbl, col + C < cend and
+// (lower) R + row >= C + col.  Every tile's LDS loads (operands and C) are
+// issued first, then the MFMAs, then the stores: one LDS latency per call
+// instead of three per tile.
+__device__ __forceinline__ void d8_trail3(double* T, int kb, const int (&R)[3], const int (&C)[3], int nt, int nbl,
+                                          int cend, bool lower) {
+  // Branch-free: an element outside the region reads and writes the lane's own
+  // slot in T's padding row (T[64 + 65 l]: ld 65, rows 0..63 used), so no load
+  // or store needs an EXEC mask of its own (measured: the per-element masks cost
+  // more than the MFMAs, profiles/r06*_ubench_factor64.txt)
+  const int l = threadIdx.x & 63, kq = l >> 4, li = l & 15;
+  double a[3][2], b[3][2], cv[3][4];
+  int ad[3][4];
 #pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int i = R + (l >> 4) + 4 * r, j = C + (l & 15);
-    if (i < nbl && j < cend && (!lower || i >= j)) {
-      double* p = T + i + 65 * j;
-      *p = *p - v[r];
+  for (int t = 0; t < 3; t++) {
+    if (t >= nt) break;   // (wave-uniform)
+    const int ra = min(R[t] + li, 63), rb = min(C[t] + li, 63);
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      a[t][u] = T[(kb + 4 * u + kq) + 65 * ra];
+      b[t][u] = T[(kb + 4 * u + kq) + 65 * rb];
     }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int i = R[t] + kq + 4 * r, j = C[t] + li;
+      ad[t][r] = (i < nbl && j < cend && (!lower || i >= j)) ? i + 65 * j : 64 + 65 * l;
+      cv[t][r] = T[ad[t][r]];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    if (t >= nt) break;
+    d4 acc = {0, 0, 0, 0};
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][0], b[t][0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t][1], b[t][1], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; r++) T[ad[t][r]] = cv[t][r] - acc[r];
   }
 }
 
 __device__ __forceinline__ int diag_factor_invert8(double* T, double* W, double* bc, int nbl = 64) {
-  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int tid = threadIdx.x, l = tid & 63;
+  // roles by wave: 0 the chain, 1 the trailing updates, 2-3 the inverse
+  // (diagnostics bit 8: the trailing updates on wave 2, the inverse on waves 1, 3)
+  const int wv = D8_DBG(8) ? ((tid >> 6) == 1 ? 2 : (tid >> 6) == 2 ? 1 : (tid >> 6)) : tid >> 6;
   int* fl = reinterpret_cast<int*>(bc);
   const int K = (nbl + 7) >> 3;   // live 8-column steps
   if (tid < 8) fl[tid] = 0;
@@ -1398,7 +1504,7 @@ __device__ __forceinline__ int diag_factor_invert8(double* T, double* W, double*
       if (chol8_lane(a, iv)) ret |= 1;
       D8_CLK(k, 1);
       if (k == K - 1) break;
-      lds_wait(fl, d8f::T1A, k);   // block column k through panel k-1 (wave 1)
+      if (!D8_DBG(2)) lds_wait(fl, d8f::T1A, k);   // block column k through panel k-1 (wave 1)
       D8_CLK(k, 2);
       const int i = l;
       if (i >= kb + 8 && i < nbl) {   // row i of block column k: x = a L_kk^-T
@@ -1417,7 +1523,7 @@ __device__ __forceinline__ int diag_factor_invert8(double* T, double* W, double*
       }
       __builtin_amdgcn_wave_barrier();
       D8_CLK(k, 3);
-      lds_wait(fl, d8f::T1B, k);   // the next diagonal block through panel k-1 (wave 1)
+      if (!D8_DBG(2)) lds_wait(fl, d8f::T1B, k);   // the next diagonal block through panel k-1 (wave 1)
       D8_CLK(k, 4);
       {   // A_{k+1,k+1} -= L_{k+1,k} L_{k+1,k}^T, lane (r, c), r >= c
         const int r = l >> 3, c = l & 7, ii = kb + 8 + r, jj = kb + 8 + c;
@@ -1434,23 +1540,39 @@ __device__ __forceinline__ int diag_factor_invert8(double* T, double* W, double*
     }
     DIAG_CLK(1);
   } else if (wv == 1) {   // ---------------- trailing updates
-    for (int k = 0; k + 1 < K; k++) {
+    for (int k = 0; k + 1 < K && !D8_DBG(4); k++) {
       const int kb = 8 * k;
       lds_wait(fl, d8f::PANEL, k + 1);
       D8_CLK(k, 0);
-      for (int R = kb + 16; R < nbl; R += 16) d8_trail_tile(T, kb, R, kb + 8, nbl, min(kb + 16, nbl), false);
+      const int nt = (nbl - kb - 16 + 15) >> 4;   // 16-row tiles below the next diagonal block (<= 3)
+      {
+        const int R[3] = {kb + 16, kb + 32, kb + 48}, C[3] = {kb + 8, kb + 8, kb + 8};
+        d8_trail3(T, kb, R, C, nt, nbl, min(kb + 16, nbl), false);
+      }
       lds_signal(fl, d8f::T1A, k + 1);
       D8_CLK(k, 1);
-      for (int R = kb + 16; R < nbl; R += 16) d8_trail_tile(T, kb, R, kb + 16, nbl, nbl, true);
+      {
+        const int R[3] = {kb + 16, kb + 32, kb + 48}, C[3] = {kb + 16, kb + 16, kb + 16};
+        d8_trail3(T, kb, R, C, nt, nbl, nbl, true);
+      }
       lds_signal(fl, d8f::T1B, k + 1);
       D8_CLK(k, 2);
-      for (int C = kb + 32; C < nbl; C += 16)
-        for (int R = C; R < nbl; R += 16) d8_trail_tile(T, kb, R, C, nbl, nbl, true);
+      {   // the rest: tile columns from kb + 32 (<= 3 tiles)
+        int R[3] = {0, 0, 0}, C[3] = {0, 0, 0}, n = 0;
+        for (int c0 = kb + 32; c0 < nbl; c0 += 16)
+          for (int r0 = c0; r0 < nbl; r0 += 16)
+            if (n < 3) {
+              R[n] = r0;
+              C[n] = c0;
+              n++;
+            }
+        d8_trail3(T, kb, R, C, n, nbl, nbl, true);
+      }
       D8_CLK(k, 3);
     }
   } else {   // ---------------- the inverse, row blocks of parity p
     const int p = wv - 2;
-    for (int s = 0; s < K; s++) {
+    for (int s = 0; s < K && !D8_DBG(1); s++) {
       const int sb = 8 * s;
       lds_wait(fl, d8f::PANEL, s);   // A_ss final, panels < s written
       D8_CLK(s, 0);
@@ -1471,31 +1593,43 @@ __device__ __forceinline__ int diag_factor_invert8(double* T, double* W, double*
         const int tb = sb - 8;                       // X_{s-1}: rows tb.., columns < sb
         const int i0 = s + (((s & 1) == p) ? 0 : 1);  // my first row block >= s
         const int nr = i0 < K ? 8 * ((K - i0 + 1) >> 1) : 0;   // stacked rows (8 per block)
-        for (int R = 0; R < nr; R += 16)
-          for (int C = 0; C < sb; C += 16) {
-            const int rr = R + (l & 15);                                   // A operand's stacked row
-            const int ra = min(8 * (i0 + 2 * (rr >> 3)) + (rr & 7), 63);
-            const int cb = min(C + (l & 15), 63);                          // B operand's column
-            // A(row, q) = L[ra][tb + q] = T[(tb + q) + 65 ra]; B(q, col) = X[tb + q][cb] = W[(tb + q) + 65 cb]
-            d4 acc;
+        // tiles (stacked 16-row tile, 16-column tile), up to 8, four per batch:
+        // every load of a batch first, then its MFMAs, then its stores
+        const int nrt = (nr + 15) >> 4, nct = (sb + 15) >> 4, ntile = nrt * nct;
+        const int kq = l >> 4, li = l & 15;
+        for (int t0 = 0; t0 < ntile; t0 += 4) {
+          double av[4][2], bv[4][2];
+          d4 acc[4];
+          int wad[4][4];
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-              const int ro = R + (l >> 4) + 4 * r, row = min(8 * (i0 + 2 * (ro >> 3)) + (ro & 7), 63);
-              acc[r] = W[row + 65 * min(C + (l & 15), 63)];
-            }
-            const int kq = l >> 4;
+          for (int t = 0; t < 4; t++) {
+            if (t0 + t >= ntile) break;   // (wave-uniform)
+            const int R = 16 * ((t0 + t) / nct), C = 16 * ((t0 + t) % nct);
+            const int rr = R + li;                                                   // A operand's stacked row
+            const int ra = min(8 * (i0 + 2 * (rr >> 3)) + (rr & 7), 63);
+            const int cb = min(C + li, 63);                                          // B operand's column
+            // A(row, q) = L[ra][tb + q] = T[(tb + q) + 65 ra]; B(q, col) = X[tb + q][cb] = W[(tb + q) + 65 cb]
 #pragma unroll
             for (int u = 0; u < 2; u++) {
-              const double av = T[(tb + 4 * u + kq) + 65 * ra];
-              const double bv = W[(tb + 4 * u + kq) + 65 * cb];
-              acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+              av[t][u] = T[(tb + 4 * u + kq) + 65 * ra];
+              bv[t][u] = W[(tb + 4 * u + kq) + 65 * cb];
             }
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-              const int ro = R + (l >> 4) + 4 * r, blk = i0 + 2 * (ro >> 3), col = C + (l & 15);
-              if (ro < nr && blk < K && col < sb && 8 * blk + (ro & 7) < nbl) W[(8 * blk + (ro & 7)) + 65 * col] = acc[r];
+            for (int r = 0; r < 4; r++) {   // S so far (zeros before the first update); outside: the padding slot
+              const int ro = R + kq + 4 * r, blk = i0 + 2 * (ro >> 3), row = 8 * blk + (ro & 7), col = C + li;
+              wad[t][r] = (ro < nr && blk < K && col < sb && row < nbl) ? row + 65 * col : 64 + 65 * l;
+              acc[t][r] = W[wad[t][r]];
             }
           }
+#pragma unroll
+          for (int t = 0; t < 4; t++) {
+            if (t0 + t >= ntile) break;
+#pragma unroll
+            for (int u = 0; u < 2; u++) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t][u], bv[t][u], acc[t], 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; r++) W[wad[t][r]] = acc[t][r];
+          }
+        }
         __builtin_amdgcn_wave_barrier();
       }
       D8_CLK(s, 3);
@@ -1510,7 +1644,7 @@ __device__ __forceinline__ int diag_factor_invert8(double* T, double* W, double*
             double o = 0.0;
 #pragma unroll
             for (int q = 0; q <= r; q++) o = fma(xs[P8(r, q)], sv[q], o);
-            if (sb + r < nbl) W[(sb + r) + 65 * col] = -o;
+            W[sb + r < nbl ? (sb + r) + 65 * col : 64 + 65 * l] = -o;   // (outside: the padding slot)
           }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1525,12 +1659,25 @@ __device__ __forceinline__ int diag_factor_invert8(double* T, double* W, double*
   return ret;
 }
 
+// The diagonal tiles' factor + inverse, chosen at build time (one form per
+// library keeps k_step's code and registers to that form; A/B builds:
+// `make -C graphslam_amd/csrc ab-forms` -> graphslam_amd/build/libpgo_form<N>.so,
+// loaded with PGO_LIB_PATH): 1 diag_factor_invert over diag16_fs (default,
+// round 6), 0 over diag16_lane (round 5), 2 diag_factor_invert8 (8-column steps
+// on four concurrent waves; measured slower, profiles/r06*_ubench_factor64.txt)
+#ifndef PGO_DIAG_FORM
+#define PGO_DIAG_FORM 1
+#endif
 // the diagonal tile's factor + inverse by the configured form; a pivot that is
 // not positive and finite (bit 1) or a lost LDS flag (bit 2: the host's
 // hand-off timeout path) goes to the lane's pivot flag
 __device__ __forceinline__ void factor_invert_tile(const CholDev& c, double* Ts, double* Ws, double* bc, int nb) {
   const int nbl = c.diag_full ? 64 : nb;
-  const int r = c.diag8 ? diag_factor_invert8(Ts, Ws, bc, nbl) : (diag_factor_invert(Ts, Ws, bc, nbl) ? 1 : 0);
+#if PGO_DIAG_FORM == 2
+  const int r = diag_factor_invert8(Ts, Ws, bc, nbl);
+#else
+  const int r = diag_factor_invert<PGO_DIAG_FORM != 0>(Ts, Ws, bc, nbl) ? 1 : 0;
+#endif
   if (r) __hip_atomic_fetch_or(c.flag, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

@@ -26,7 +26,8 @@ __global__ __launch_bounds__(256) void u_factor(const double* A, double* out, in
     }
     __syncthreads();
     int bad;
-    if (mode == 0) bad = diag_factor_invert(T, W, bc, nbl) ? 1 : 0;
+    if (mode == 0) bad = diag_factor_invert<false>(T, W, bc, nbl) ? 1 : 0;
+    else if (mode == 2) bad = diag_factor_invert<true>(T, W, bc, nbl) ? 1 : 0;
     else bad = diag_factor_invert8(T, W, bc, nbl);
     __syncthreads();
     if (threadIdx.x == 0) out[0] += W[63 + 63 * 65] + bad;
@@ -73,29 +74,47 @@ int main() {
   double *dA, *dO, *dLX;
   hipMalloc(&dA, sizeof(double) * 4096);
   hipMalloc(&dO, 2 * sizeof(double));
-  hipMalloc(&dLX, sizeof(double) * 4096 * 2);
+  hipMalloc(&dLX, sizeof(double) * 4096 * 3);
   hipMemcpy(dA, A.data(), sizeof(double) * 4096, hipMemcpyHostToDevice);
   int fail = 0;
   for (int nbl : {64, 37, 8, 1}) {
-    std::vector<double> X0(4096), X1(4096);
-    for (int mode = 0; mode < 2; mode++) {
+    std::vector<double> X0(4096), X1(4096), X2(4096);
+    for (int mode = 0; mode < 3; mode++) {
       hipMemset(dO, 0, 2 * sizeof(double));
       u_factor<<<1, 256>>>(dA, dO, 1, mode, nbl, dLX + 4096 * mode);
       if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 1; }
       double o[2];
       hipMemcpy(o, dO, 2 * sizeof(double), hipMemcpyDeviceToHost);
-      std::vector<double>& X = mode ? X1 : X0;
+      std::vector<double>& X = mode == 2 ? X2 : mode ? X1 : X0;
       hipMemcpy(X.data(), dLX + 4096 * mode, sizeof(double) * 4096, hipMemcpyDeviceToHost);
       printf("nbl %d mode %d bad/err %.0f\n", nbl, mode, o[1]);
       if (check(A, X.data(), nbl) > 1e-9 || o[1] != 0) fail = 1;
     }
-    double d = 0, mx = 0;   // (the live part: the callers read nothing past nbl)
+    double d = 0, d2 = 0, mx = 0;   // (the live part: the callers read nothing past nbl)
     for (int i = 0; i < 4096; i++)
-      if ((i & 63) < nbl && (i >> 6) < nbl) { d = std::max(d, std::fabs(X0[i] - X1[i])); mx = std::max(mx, std::fabs(X0[i])); }
-    printf("  nbl %d: max |X_mode1 - X_mode0| %.3g (max |X| %.3g)\n", nbl, d, mx);
-    if (d > 1e-10 * mx) fail = 1;
+      if ((i & 63) < nbl && (i >> 6) < nbl) {
+        d = std::max(d, std::fabs(X0[i] - X1[i]));
+        d2 = std::max(d2, std::fabs(X0[i] - X2[i]));
+        mx = std::max(mx, std::fabs(X0[i]));
+      }
+    printf("  nbl %d: max |X_mode1 - X_mode0| %.3g, max |X_mode2 - X_mode0| %.3g (max |X| %.3g)\n", nbl, d, d2, mx);
+    if (d > 1e-10 * mx || d2 > 1e-10 * mx) fail = 1;
   }
-  for (int mode = 0; mode < 2; mode++) {
+  for (int dbg : {0, 8, 1, 1 | 8, 2 | 4, 2 | 4 | 1}) {   // diagnostics: which waves' work the chain waits on
+    hipMemcpyToSymbol(HIP_SYMBOL(g_d8_dbg), &dbg, sizeof(int));
+    u_factor<<<1, 256>>>(dA, dO, 3, 1, 64);
+    hipDeviceSynchronize();
+    long long clk[32], d8[4][8][8];
+    hipMemcpyFromSymbol(clk, HIP_SYMBOL(g_diag_clk), sizeof(clk));
+    hipMemcpyFromSymbol(d8, HIP_SYMBOL(g_d8_clk), sizeof(d8));
+    printf("dbg %d (1 = X waves idle, 2 = no waits, 4 = trailing wave idle, 8 = trailing on wave 2): total %lld, wave 0 done %lld; wave 0 per step:", dbg,
+           clk[12] - clk[0], clk[1] - clk[0]);
+    for (int k = 0; k < 7; k++) printf(" [%lld %lld %lld %lld %lld]", d8[0][k][1] - d8[0][k][0], d8[0][k][2] - d8[0][k][1],
+                                       d8[0][k][3] - d8[0][k][2], d8[0][k][4] - d8[0][k][3], d8[0][k][5] - d8[0][k][4]);
+    printf("\n");
+  }
+  { int z = 0; hipMemcpyToSymbol(HIP_SYMBOL(g_d8_dbg), &z, sizeof(int)); }
+  for (int mode = 0; mode < 3; mode++) {
     u_factor<<<1, 256>>>(dA, dO, 3, mode, 64);
     hipDeviceSynchronize();
     long long clk[32];
