@@ -483,10 +483,10 @@ def log(msg):
 def _partition_bounds(live):
     """{config: {P: {flop bounds, exchange points / bytes per rank, the model's
     speed-up per mode at its central constants and its min-max range over the
-    swept ones, the auto choice}}}: profiles/r05_partition_bounds.json
+    swept ones, the auto choice}}}: profiles/r06_partition_bounds.json
     (host-computed for C3 and C5, scripts/partition_bounds.py), plus this
     run's own rank count when it was computed live.  All unmeasured on 8 GPUs."""
-    path = os.path.join(ROOT, "profiles", "r05_partition_bounds.json")
+    path = os.path.join(ROOT, "profiles", "r06_partition_bounds.json")   # (round 6: fixed-top candidates)
     keep = ("bound", "bound_replicated_top", "exchange_points", "exchange_bytes", "est_speedup_distributed_top",
             "est_speedup_replicated_top", "est_speedup_spec", "est_speedup_hybrid", "range_min", "range_max", "auto")
     out = {}

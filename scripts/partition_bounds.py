@@ -9,7 +9,7 @@ Also graphslam_amd/multi_model.py's level-by-level time estimates of both tops
 and of the speculative search (bench.py's --multi auto uses the same model).
 Writes profiles/<out>.json.
 
-    python scripts/partition_bounds.py [--configs C3 C5] [--out r05_partition_bounds]
+    python scripts/partition_bounds.py [--configs C3 C5] [--out r06_partition_bounds]
 """
 from __future__ import annotations
 
@@ -28,7 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", nargs="+", default=["C3", "C5"])
     ap.add_argument("--ranks", nargs="+", type=int, default=[2, 4, 8])
-    ap.add_argument("--out", default="r05_partition_bounds")
+    ap.add_argument("--out", default="r06_partition_bounds")
     args = ap.parse_args()
     from graphslam_amd import datasets
     from graphslam_amd.pose_graph import PoseGraph
