@@ -1759,7 +1759,11 @@ __device__ __forceinline__ void panel_rhs(double* v, const double* X, int nb, do
 
 // X = L^-1 (LDS Ws, ld 65), stored sc1 in the trsm's operand order to Mf:
 // Mf[(4 ks + ct) * 64 + l] = X[16 ct + (l & 15)][4 ks + (l >> 4)] (what the
-// trsm's lane l needs for k-step ks, column tile ct) -- the hand-off payload
+// trsm's lane l needs for k-step ks, column tile ct) -- the hand-off payload.
+// X is lower triangular, so fragment (ks, ct) is all zeros when 4 ks > 16 ct +
+// 15, i.e. ct < ks / 4: 24 of the 64 (round 6) -- neither stored nor loaded,
+// and their MFMAs (products with zero) skipped by the readers (inv_frag_zero)
+__device__ __forceinline__ constexpr bool inv_frag_zero(int ks, int ct) { return ct < (ks >> 2); }
 __device__ __forceinline__ void publish_inverse(double* __restrict__ Mf, const double* Ws, int nb) {
   const int tid = threadIdx.x;
   const __amdgpu_buffer_rsrc_t r = wave_rsrc(Mf, 4096 * 8);
@@ -1767,6 +1771,7 @@ __device__ __forceinline__ void publish_inverse(double* __restrict__ Mf, const d
   for (int u = 0; u < 8; u++) {   // element pairs (idx, idx + 1): rows fa, fa + 1 of one column fb
     const int idx = 2 * (tid + 256 * u);
     const int l = idx & 63, ct = (idx >> 6) & 3, ks = idx >> 8;
+    if (inv_frag_zero(ks, ct)) continue;   // (a zero fragment: never read)
     const int fa = 16 * ct + (l & 15), fb = 4 * ks + (l >> 4);
     const double x0 = (fa < nb && fb < nb && fa >= fb) ? Ws[fa + fb * 65] : 0.0;
     const double x1 = (fa + 1 < nb && fb < nb && fa + 1 >= fb) ? Ws[fa + 1 + fb * 65] : 0.0;
@@ -1850,11 +1855,16 @@ __device__ __forceinline__ void trsm_rows(const CholDev& c, int s, int r0, int k
     const __amdgpu_buffer_rsrc_t r = wave_rsrc(Mf, 4096 * 8);
     double2 t[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) t[u] = ld2_sc1(r, 2 * (tid + 256 * u));
+    for (int u = 0; u < 8; u++) {   // (fragment ks = idx >> 8, ct = (idx >> 6) & 3 of idx = 2 (tid + 256 u))
+      const int idx = 2 * (tid + 256 * u);
+      t[u] = inv_frag_zero(idx >> 8, (idx >> 6) & 3) ? make_double2(0.0, 0.0) : ld2_sc1(r, idx);
+    }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      xs[2 * (tid + 256 * u)] = t[u].x;
-      xs[2 * (tid + 256 * u) + 1] = t[u].y;
+      const int idx = 2 * (tid + 256 * u);
+      if (inv_frag_zero(idx >> 8, (idx >> 6) & 3)) continue;
+      xs[idx] = t[u].x;
+      xs[idx + 1] = t[u].y;
     }
   }
   // the panel's y (handed off, sc1) and this lane's right-hand-side rows, in
@@ -1885,13 +1895,13 @@ __device__ __forceinline__ void trsm_rows(const CholDev& c, int s, int r0, int k
 #pragma unroll
   for (int ks = 0; ks < 16; ks++)
 #pragma unroll
-    for (int ct = 0; ct < 4; ct++) tb[ks][ct] = xs[(4 * ks + ct) * 64 + l];
+    for (int ct = 0; ct < 4; ct++) tb[ks][ct] = inv_frag_zero(ks, ct) ? 0.0 : xs[(4 * ks + ct) * 64 + l];
   d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0}, acc3 = {0, 0, 0, 0};
 #pragma unroll
-  for (int ks = 0; ks < 16; ks++) {
-    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[ks][0], acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[ks][1], acc1, 0, 0, 0);
-    acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[ks][2], acc2, 0, 0, 0);
+  for (int ks = 0; ks < 16; ks++) {   // (zero fragments: no product -- column tile ct takes k-steps ks < 4 ct + 4)
+    if (!inv_frag_zero(ks, 0)) acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[ks][0], acc0, 0, 0, 0);
+    if (!inv_frag_zero(ks, 1)) acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[ks][1], acc1, 0, 0, 0);
+    if (!inv_frag_zero(ks, 2)) acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[ks][2], acc2, 0, 0, 0);
     acc3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], tb[ks][3], acc3, 0, 0, 0);
   }
   double part[4] = {0, 0, 0, 0};   // L[row, panel] y for the lane's 4 rows
@@ -2338,11 +2348,17 @@ __global__ __launch_bounds__(256) void k_first_trsm(CholDev c, const int4* __res
   {
     double2 tq[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) tq[u] = reinterpret_cast<const double2*>(Mf)[tid + 256 * u];
+    for (int u = 0; u < 8; u++) {
+      const int idx = 2 * (tid + 256 * u);
+      tq[u] = inv_frag_zero(idx >> 8, (idx >> 6) & 3) ? make_double2(0.0, 0.0)
+                                                      : reinterpret_cast<const double2*>(Mf)[tid + 256 * u];
+    }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      xs[2 * (tid + 256 * u)] = tq[u].x;
-      xs[2 * (tid + 256 * u) + 1] = tq[u].y;
+      const int idx = 2 * (tid + 256 * u);
+      if (inv_frag_zero(idx >> 8, (idx >> 6) & 3)) continue;
+      xs[idx] = tq[u].x;
+      xs[idx + 1] = tq[u].y;
     }
   }
   const int rw = r0 + wv * 16, kl = l >> 4;
@@ -2369,11 +2385,11 @@ __global__ __launch_bounds__(256) void k_first_trsm(CholDev c, const int4* __res
   double* Fc = fcol(c.F + c.foff[s], m, true, kn);
   d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0}, acc3 = {0, 0, 0, 0};
 #pragma unroll
-  for (int ks = 0; ks < 16; ks++) {
+  for (int ks = 0; ks < 16; ks++) {   // (zero fragments of the inverse: no product, as trsm_rows)
     const double* x = xs + 4 * ks * 64 + l;
-    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], x[0], acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], x[64], acc1, 0, 0, 0);
-    acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], x[128], acc2, 0, 0, 0);
+    if (!inv_frag_zero(ks, 0)) acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], x[0], acc0, 0, 0, 0);
+    if (!inv_frag_zero(ks, 1)) acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], x[64], acc1, 0, 0, 0);
+    if (!inv_frag_zero(ks, 2)) acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], x[128], acc2, 0, 0, 0);
     acc3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], x[192], acc3, 0, 0, 0);
   }
   double part[4] = {0, 0, 0, 0};
