@@ -372,7 +372,12 @@ int pgo_comm_rank(const pgo_graph *g, int *rank, int *size);
 /* PGO_MULTI_HYBRID: the partition group's communicator (the ranks that split
    one factorisation; collective over the group), RCCL or host transport; the
    main communicator then holds one rank of every group (the same position in
-   each).  pgo_comm_free frees both. */
+   each).  Set it up BEFORE the main communicator: a main init binds the
+   group set up since the previous main init and frees an older one, so a
+   main communicator replaced without pgo_comm_free never runs with a stale
+   group.  A bound group of one rank makes PGO_MULTI_HYBRID the speculative
+   search alone; none bound with a main communicator of > 1 rank ->
+   PGO_E_ARG.  pgo_comm_free frees both. */
 int pgo_comm_init_rccl_part(pgo_graph *g, const void *unique_id, size_t id_bytes, int rank, int size);
 int pgo_comm_init_host_part(pgo_graph *g, const pgo_host_comm *comm);
 int pgo_comm_part_rank(const pgo_graph *g, int *rank, int *size);

@@ -431,6 +431,7 @@ def _hybrid_worker(rank, world, port, q, case, kw, groups, env=None):
     ("C2p", 4, 2, 2, {}, {}),                    # ... with 2 lambda lanes per group
     ("C3", 4, 2, 1, {"max_outer": 3}, {}),
     ("C5", 4, 2, 1, {"max_outer": 1}, {}),       # BASELINE config C5: 2 groups x 2-rank partitions
+    ("C5", 4, 2, 1, {"max_outer": 1}, {"PGO_DIST_TOP": "0"}),   # ... with the replicated top: auto's 4-rank pick
     # round 6: the 8-rank layouts -- --multi auto's picks, C3 and C5: 4
     # groups x 2-rank partitions with the replicated top (profiles/r06_partition_bounds.json);
     # C5 also 4 x 2 and 2 x 4 with the distributed top (the 2 x 4's best central estimate)
