@@ -123,6 +123,13 @@ __device__ long long g_diag_clk[32];
 __device__ long long g_d8_clk[4][8][8];   // diag_factor_invert8: [wave][step][phase]
 __device__ int g_d8_dbg;   // diagnostics: 1 = waves 2-3 idle, 2 = no waits on wave 1, 4 = wave 1 idle
 #define D8_DBG(bit) (g_d8_dbg & (bit))
+#define DIAG_CLKF(q)                                                                   \
+  do {                                                                                 \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_diag_clk[q] = clock64();                \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  } while (0)
 #define DIAG_CLK(q) if (threadIdx.x == 0 && blockIdx.x == 0) g_diag_clk[q] = clock64()
 #define D8_CLK(k, q)                                                                 \
   do {                                                                               \
@@ -133,6 +140,7 @@ __device__ int g_d8_dbg;   // diagnostics: 1 = waves 2-3 idle, 2 = no waits on w
   } while (0)
 #else
 #define DIAG_CLK(q)
+#define DIAG_CLKF(q)
 #define D8_CLK(k, q)
 #define D8_DBG(bit) 0
 #endif
@@ -1249,13 +1257,16 @@ __device__ __forceinline__ bool diag16_fs(double* TJ, double* WJ, double* sc) {
 #pragma unroll
   for (int k = 0; k < 8; k++) x[k] = xl ? (k == l ? 1.0 : 0.0) : (rl ? TJ[l + k * 65] : 0.0);   // e_l / row l-8 of A21
   WJ[r + (8 + c) * 65] = 0.0;   // block (0, 1) of X
+  DIAG_CLKF(20);
   bool bad = chol8_lane(a, iv);
+  DIAG_CLKF(21);
   fwd8_lane(a, iv, x);          // lanes 0-7: column l of X11; lanes 8-15: row l-8 of L21
   if (xl || rl) {
 #pragma unroll
     for (int k = 0; k < 8; k++) (xl ? WJ[k + l * 65] : TJ[l + k * 65]) = x[k];
   }
   __builtin_amdgcn_wave_barrier();
+  DIAG_CLKF(22);
   // A22 -= L21 L21^T (lower), Y = L21 X11 (X11 (k, c) zero for k < c)
   double t = TJ[(8 + r) + (8 + c) * 65], y = 0.0;
 #pragma unroll
@@ -1274,12 +1285,15 @@ __device__ __forceinline__ bool diag16_fs(double* TJ, double* WJ, double* sc) {
     for (int j = 0; j <= i; j++) a[P8(i, j)] = TJ[(8 + i) + (8 + j) * 65];
 #pragma unroll
   for (int k = 0; k < 8; k++) x[k] = xl ? (k == l ? 1.0 : 0.0) : (rl ? -sc[k * 8 + (l - 8)] : 0.0);   // e_l / -Y column
+  DIAG_CLKF(23);
   bad = chol8_lane(a, iv) || bad;
+  DIAG_CLKF(24);
   fwd8_lane(a, iv, x);          // lanes 0-7: column l of X22; lanes 8-15: column l-8 of X21
   if (xl || rl) {
 #pragma unroll
     for (int k = 0; k < 8; k++) (xl ? WJ[(8 + k) + (8 + l) * 65] : WJ[(8 + k) + (l - 8) * 65]) = x[k];
   }
+  DIAG_CLKF(25);
   return bad;
 }
 

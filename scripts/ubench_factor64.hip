@@ -17,7 +17,7 @@ using namespace pgo;
 
 __global__ __launch_bounds__(256) void u_factor(const double* A, double* out, int reps, int mode, int nbl,
                                                 double* LX = nullptr) {
-  __shared__ double T[64 * 65], W[64 * 65], bc[64];
+  __shared__ __attribute__((aligned(16))) double T[64 * 65], W[64 * 65], bc[64];
   for (int rep = 0; rep < reps; rep++) {
     for (int i = threadIdx.x; i < 64 * 65; i += 256) {
       const int r = i % 65, cc = i / 65;
@@ -140,6 +140,15 @@ int main() {
       }
     } else {
       printf("\n");
+      long long prev = clk[0];
+      for (int J = 0; J < 4; J++) {   // A: wave 0's diagonal block (+ the update before it), B: the panel / inverse-row products
+        const long long b = J < 3 ? clk[2 + 3 * J] : clk[12];
+        printf("  J%d A %lld  B %lld\n", J, clk[1 + 3 * J] - prev, b - clk[1 + 3 * J]);
+        prev = b;
+      }
+      if (mode == 2)
+        printf("  diag16_fs (J3, fenced): chol8 %lld, fwd+store %lld, A22/Y+load %lld, chol8 %lld, fwd+store %lld\n",
+               clk[21] - clk[20], clk[22] - clk[21], clk[23] - clk[22], clk[24] - clk[23], clk[25] - clk[24]);
     }
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
