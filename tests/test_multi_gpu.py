@@ -552,3 +552,85 @@ def test_rccl_one_rank_communicator(monkeypatch, force):
     assert st["inner_iterations"] == st1["inner_iterations"]
     np.testing.assert_array_equal(pg.poses(), x1)
     pg.comm_free()
+
+
+# ---------------------------------------------------------------- RCCL set-up agreement (CPU, gloo)
+class _FakeHandle:
+    """Stands in for a PoseGraph in multi_gpu's set-up: records the
+    communicator calls; `fail` names the init that raises on this rank."""
+
+    def __init__(self, fail=None):
+        self.calls, self.fail = [], fail
+
+    def _rec(self, name, *a):
+        self.calls.append(name)
+        if name == self.fail:
+            raise RuntimeError(f"forced {name} failure")
+
+    def comm_init_rccl_part(self, uid, rank, size):
+        self._rec("rccl_part", uid, rank, size)
+
+    def comm_init_rccl(self, uid, rank, size):
+        self._rec("rccl", uid, rank, size)
+
+    def comm_init_host_part(self, s):
+        self._rec("host_part")
+
+    def comm_init_host(self, s):
+        self._rec("host")
+
+    def comm_free(self):
+        self.calls.append("free")
+
+
+def _setup_worker(rank, world, port, q, groups, fail_rank, fail_what):
+    """attach_hybrid over RCCL with one rank failing at `fail_what` ('uid': its
+    unique id, or an init name), then the bench's fallback to host transport."""
+    try:
+        dist = _init(rank, world, port)
+        from graphslam_amd import multi_gpu
+        pg = _FakeHandle(fail_what if rank == fail_rank and fail_what != "uid" else None)
+        orig = multi_gpu.unique_id
+
+        def uid():
+            if rank == fail_rank and fail_what == "uid":
+                raise RuntimeError("forced unique id failure")
+            return b"x" * 128
+
+        multi_gpu.unique_id = uid
+        outcome = "rccl"
+        try:
+            multi_gpu.attach_hybrid(pg, dist, rank, world, groups, transport="rccl")
+        except multi_gpu.CommSetupError:
+            outcome = "fallback"
+            multi_gpu.attach_hybrid(pg, dist, rank, world, groups, transport="host")
+        multi_gpu.unique_id = orig
+        q.put((rank, (outcome, pg.calls), None))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("fail_rank,fail_what", [(2, "uid"), (1, "rccl_part"), (3, "rccl"), (None, None)])
+def test_rccl_setup_failure_falls_back_together(fail_rank, fail_what):
+    """one rank failing at any blocking step of the hybrid's RCCL
+    set-up (its group's unique id, its partition-group init, the main init)
+    makes EVERY rank raise CommSetupError at the same agreement point -- no rank
+    is left inside a collective -- so all fall back to the host transport
+    together; without a failure all stay on RCCL.  4 gloo ranks as 2 x 2, the
+    RCCL calls stubbed (CPU)."""
+    out = _run(4, _setup_worker, (2, fail_rank, fail_what))
+    outcomes = set()
+    for rank, res, err in out:
+        assert err is None, err
+        outcome, calls = res
+        outcomes.add(outcome)
+        if outcome == "fallback":
+            assert calls[-2:] == ["host_part", "host"], calls
+            if fail_what == "uid":   # agreed before any init
+                assert "rccl_part" not in calls and "rccl" not in calls, calls
+            else:                    # agreed after the failing init: every rank freed what it made
+                assert "free" in calls, calls
+        else:
+            assert calls == ["rccl_part", "rccl"], calls
+    assert outcomes == ({"rccl"} if fail_rank is None else {"fallback"})
