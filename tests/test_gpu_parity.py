@@ -388,9 +388,10 @@ def test_c3_gauss_newton_against_golden(pg_cls):
     against the C oracle's run (golden_C3-gn.npz): the step count, the error
     after every step, the final error and a 1000-pose sample of the final
     values.  Undamped steps from a start 3e5 x the optimum's error amplify the
-    two factorisations' different rounding (the first step's error differs by
-    1.4e-8 relative on the box): errors rel 1e-6, poses 1e-4 m / 1e-5 rad; the
-    observed differences are printed."""
+    two factorisations' different rounding: errors rel 3e-7, poses 3e-5 m /
+    5e-6 rad, about 5x the differences observed on the round-6 build (6.8e-8,
+    6.0e-6 m, 9.0e-7 rad, profiles/r06t_diffs.log; round 5: 1e-6, 1e-4 m,
+    1e-5 rad); the observed differences are printed."""
     gold = np.load(os.path.join(GOLDEN, "golden_C3-gn.npz"), allow_pickle=False)
     g = datasets.make("C3")
     pg = pg_cls.from_dataset(g)
@@ -403,10 +404,10 @@ def test_c3_gauss_newton_against_golden(pg_cls):
     dth = np.abs(np.angle(np.exp(1j * (x[:, 2] - gold["final_sample"][:, 2])))).max()
     print(f"C3 GN: per-step error rel diff {np.max(np.abs(errs / gold['errors'] - 1)):.2e}, "
           f"max |dxy| {dxy:.2e} m, max |dtheta| {dth:.2e} rad")
-    assert np.allclose(errs, gold["errors"], rtol=1e-6, atol=0)
+    assert np.allclose(errs, gold["errors"], rtol=3e-7, atol=0)
     fe = float(gold["final_error"])
-    assert abs(st["final_error"] - fe) <= 1e-6 * fe
-    assert_poses(x, gold["final_sample"], 1e-4, 1e-5)
+    assert abs(st["final_error"] - fe) <= 3e-7 * fe
+    assert_poses(x, gold["final_sample"], 3e-5, 5e-6)
 
 
 def test_c3_first_two_linearisations_vs_numpy_twin(pg_cls):
