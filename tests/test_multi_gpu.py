@@ -634,3 +634,62 @@ def test_rccl_setup_failure_falls_back_together(fail_rank, fail_what):
         else:
             assert calls == ["rccl_part", "rccl"], calls
     assert outcomes == ({"rccl"} if fail_rank is None else {"fallback"})
+
+
+def _hybrid_binding_worker(rank, world, port, q, case):
+    """case 'one-rank-groups': hybrid with partition groups of one rank (the
+    speculative search alone); 'stale': a hybrid set-up, then the main
+    communicator replaced without pgo_comm_free -- the old partition group must
+    not be used (PGO_MULTI_HYBRID then reports PGO_E_ARG)."""
+    try:
+        dist = _init(rank, world, port)
+        from graphslam_amd import multi_gpu
+        from graphslam_amd.pose_graph import PoseGraph
+        g, init = _graph("C2p")
+        pg = PoseGraph.from_dataset(g, device=0)
+        pg.set_poses(init)
+        if case == "one-rank-groups":
+            keep = multi_gpu.attach_hybrid(pg, dist, rank, world, world, transport="host")   # groups of 1
+            st = pg.optimize(multi_gpu=2, lambda_lanes=1)
+            q.put((rank, (st, pg.poses(), pg.comm_part_rank()), None))
+        else:
+            keep = multi_gpu.attach_hybrid(pg, dist, rank, world, 1, transport="host")       # one group of `world`
+            keep.append(multi_gpu.attach_host(pg, dist, rank, world))                       # main replaced, no free
+            try:
+                pg.optimize(multi_gpu=2, lambda_lanes=1)
+                res = "ran"
+            except Exception as e:  # noqa: BLE001
+                res = repr(e)
+            q.put((rank, (res, pg.comm_part_rank()), None))
+        del keep
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.gpu
+def test_hybrid_partition_groups_of_one_rank_are_the_speculative_search():
+    """PGO_MULTI_HYBRID with partition groups of one rank (groups ==
+    ranks) is a valid layout -- the speculative search alone -- and reproduces
+    the one-rank run bit for bit (it used to return PGO_E_ARG)."""
+    st1, x1 = _single("C2p", {})
+    out = _run(2, _hybrid_binding_worker, ("one-rank-groups",), timeout=600)
+    for rank, res, err in out:
+        assert err is None, err
+        st, x, part = res
+        assert part == (0, 1)
+        assert st["transport"] == _lib.PGO_TRANSPORT_HOST and st["part_transport"] == _lib.PGO_TRANSPORT_NONE
+        _same(st, x, st1, x1)
+
+
+@pytest.mark.gpu
+def test_replaced_main_communicator_drops_the_stale_partition_group():
+    """a main communicator initialised again without pgo_comm_free
+    frees the partition group set up before the previous one, so a hybrid
+    optimize cannot run on a stale group: PGO_E_ARG, the group gone (size 1)."""
+    out = _run(2, _hybrid_binding_worker, ("stale",), timeout=600)
+    for rank, res, err in out:
+        assert err is None, err
+        msg, part = res
+        assert "PGO_MULTI_HYBRID needs a partition-group communicator" in msg or "-1" in msg, msg
+        assert part == (0, 1)
