@@ -160,6 +160,10 @@ __device__ int g_d8_dbg;   // diagnostics: 1 = waves 2-3 idle, 2 = no waits on w
 // its column offset) of each tile column.  Two barriers per tile (per 16 child
 // rectangles), and every element's loads are in flight together.
 constexpr int kAsmPairs = 16;
+#ifndef PGO_ASM_GE
+#define PGO_ASM_GE 8
+#endif
+constexpr int kAsmGE = PGO_ASM_GE;   // a thread's 16 elements in 16 / kAsmGE groups: kAsmGE loads in flight per child
 constexpr int kAsmNone = (int)0x80000000;
 
 // Frontal vector of front s before its factorisation: own rows from the
@@ -286,12 +290,12 @@ __global__ __launch_bounds__(256, 4) void k_assemble_tile(CholDev c, const int4*
     }
     __syncthreads();
 #pragma unroll 1
-    for (int g = 0; g < 2; g++) {
-      double val[8];
+    for (int g = 0; g < 16 / kAsmGE; g++) {
+      double val[kAsmGE];
       if (pass == 0) {   // the H entries
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const int col = C0 + cg + 4 * (8 * g + u);
+        for (int u = 0; u < kAsmGE; u++) {
+          const int col = C0 + cg + 4 * (kAsmGE * g + u);
           const int bq = bi * 22 + (col / 3 - Q0), b3 = col - 3 * (col / 3);
           const int code = bcode[bq];
           double v = 0.0;
@@ -308,37 +312,37 @@ __global__ __launch_bounds__(256, 4) void k_assemble_tile(CholDev c, const int4*
         }
       } else {           // a later pass (more than 16 child rectangles): this thread's partial sums so far
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const int j = cg + 4 * (8 * g + u), col = C0 + j;
+        for (int u = 0; u < kAsmGE; u++) {
+          const int j = cg + 4 * (kAsmGE * g + u), col = C0 + j;
           val[u] = (row < mp && col < mp && row >= col) ? Fp[row + (size_t)j * ldp] : 0.0;
         }
       }
       // the children's elements, in child order; kUnroll children's loads in
       // flight together (the adds stay in child order: the same sums)
       for (int k1 = 0; k1 < np; k1 += kUnroll) {
-        double add[kUnroll][8];
-        bool in[kUnroll][8];
+        double add[kUnroll][kAsmGE];
+        bool in[kUnroll][kAsmGE];
 #pragma unroll
         for (int x = 0; x < kUnroll; x++) {
           const int kk = k1 + x;
           const int a = kk < np ? rmap[kk][i] : -1;
           const double* __restrict__ Fch = c.F + (kk < np ? pbase[kk] : 0) + a;
 #pragma unroll
-          for (int u = 0; u < 8; u++) {
-            const int b = a >= 0 ? cmap[kk][cg + 4 * (8 * g + u)] : -1;
+          for (int u = 0; u < kAsmGE; u++) {
+            const int b = a >= 0 ? cmap[kk][cg + 4 * (kAsmGE * g + u)] : -1;
             in[x][u] = b >= 0 && b <= a;
-            add[x][u] = in[x][u] ? Fch[coff[kk][cg + 4 * (8 * g + u)]] : 0.0;
+            add[x][u] = in[x][u] ? Fch[coff[kk][cg + 4 * (kAsmGE * g + u)]] : 0.0;
           }
         }
 #pragma unroll
         for (int x = 0; x < kUnroll; x++)
 #pragma unroll
-          for (int u = 0; u < 8; u++)
+          for (int u = 0; u < kAsmGE; u++)
             if (in[x][u]) val[u] += add[x][u];
       }
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int j = cg + 4 * (8 * g + u), col = C0 + j;
+      for (int u = 0; u < kAsmGE; u++) {
+        const int j = cg + 4 * (kAsmGE * g + u), col = C0 + j;
         if (row < mp && col < mp && row >= col) Fp[row + (size_t)j * ldp] = val[u];
       }
     }

@@ -156,6 +156,51 @@ void xcd_order(std::vector<int4>& tasks, int tile) {
   tasks.swap(out);
 }
 
+// XCD-aware order of a level's tile-assembly tasks [off, end): a child's
+// update-matrix column lands on a parent column as one run of child rows that
+// crosses the parent's row tiles, so vertically adjacent tiles read the same
+// 128-byte lines at their run boundaries.  Blocks of kCols x kRows tiles of a
+// front, column-major inside, are dealt round-robin to the 8 XCDs (blockIdx
+// b -> XCD b % 8 as observed: speed only, each tile is computed alike
+// wherever and whenever it runs).  PGO_ASM_XCD=0 keeps the natural order.
+static void ea_xcd_order(std::vector<int4>& tasks, size_t off) {
+  constexpr int kXcd = 8, kCols = 4, kRows = 16;
+  static const bool on = !getenv("PGO_ASM_XCD") || atoi(getenv("PGO_ASM_XCD")) != 0;
+  const size_t n = tasks.size() - off;
+  if (!on || n < (size_t)4 * kXcd * kCols * kRows) return;
+  // key: (block of the front in order of first appearance, column, row), task index
+  using u128 = unsigned __int128;
+  std::vector<u128> key(n);
+  int blk = -1, fprev = -1;
+  std::vector<int> bid;   // the front's blocks: (tj / kCols, ti / kRows) -> block number
+  int nbr = 0;
+  for (size_t i = 0; i < n; i++) {
+    const int4& t = tasks[off + i];
+    const int ti = t.y >> 16, tj = t.y & 0xffff;
+    if (t.x != fprev) {   // a front's tasks are contiguous (row-major lower triangle)
+      fprev = t.x;
+      int nt = 0;
+      for (size_t k = i; k < n && tasks[off + k].x == t.x; k++) nt = std::max(nt, (tasks[off + k].y >> 16) + 1);
+      nbr = (nt + kRows - 1) / kRows;
+      bid.assign((size_t)((nt + kCols - 1) / kCols) * nbr, -1);
+    }
+    int& b = bid[(size_t)(tj / kCols) * nbr + ti / kRows];
+    if (b < 0) b = ++blk;
+    key[i] = (u128)((unsigned long long)b << 32 | (unsigned)tj << 16 | (unsigned)ti) << 32 | i;
+  }
+  std::sort(key.begin(), key.end());
+  std::vector<std::vector<int4>> q(kXcd);
+  for (const u128 k : key) q[(int)(k >> 64) % kXcd].push_back(tasks[off + (size_t)(k & 0xffffffffu)]);
+  std::vector<size_t> pos(kXcd, 0);
+  size_t o = off;
+  for (size_t left = n; left;)
+    for (int x = 0; x < kXcd; x++)
+      if (pos[x] < q[x].size()) {
+        tasks[o++] = q[x][pos[x]++];
+        left--;
+      }
+}
+
 // dense Cholesky flops of the w pivot columns of an m-row front, plus the
 // inverses of its diagonal blocks (what the small-front kernels form)
 static double front_flops(int m, int w) {
@@ -659,6 +704,7 @@ static void chol_schedule(CholPlan& P, const std::vector<int>& row_ptr, const st
               S.ea_pairs[base + tpos[k]++] = make_int4(runs[i].x, runs[i].z, runs[j].z, runs[i].w | (runs[j].w << 8));
             }
       }
+      ea_xcd_order(S.ea_tasks, (size_t)lv.ea_off.back());
       lv.ea_cnt.push_back((int)S.ea_tasks.size() - lv.ea_off.back());
       return;
     }
