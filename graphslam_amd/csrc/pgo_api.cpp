@@ -1236,7 +1236,7 @@ int bind_plan(pgo_graph* g, bool full) {
     if (eside.capacity() < (size_t)ne) eside.reserve(std::max<size_t>(g->cap_ne, ne));
     eside.resize(ne, 0);
     // Cholesky-mode linearisation writes each factor's owner block at its
-    // device factor index (coalesced), so the assembly reads V[q*S + e]
+    // device factor index (one 72-byte record per factor), so the assembly reads V[9 e + q]
     auto own_bit = [&](int r, int k) {
       const bool own = g->chol.iperm[r] > g->chol.iperm[g->h_slot_col[k]];
       slot_edge[k] = (slot_edge[k] & ~2) | (own ? 2 : 0);
@@ -2682,7 +2682,7 @@ int pgo_debug_linearize_cholesky(pgo_graph* g, double* hdiag, double* hoff, doub
       const bool side0_owner = (se & 2) != 0;
       for (int r = 0; r < 3; r++)
         for (int c = 0; c < 3; c++)
-          hoff[9 * (size_t)e + 3 * r + c] = V[(side0_owner ? 3 * r + c : 3 * c + r) * (size_t)d.nslots + de];
+          hoff[9 * (size_t)e + 3 * r + c] = V[9 * de + (side0_owner ? 3 * r + c : 3 * c + r)];
     }
   if (grad && !G.empty()) std::memcpy(grad, G.data(), G.size() * 8);
   return PGO_OK;

@@ -326,8 +326,9 @@ struct ExchangeHook {
   bool failed = false;
 };
 
-// device: factor H + lambda I (D: 6 doubles/pose upper, V: slot blocks as structure of
-// arrays V[q * nslots + slot], old indexing; only the slots in asm_src are read)
+// device: factor H + lambda I (D: 6 doubles/pose upper, V: the Cholesky-mode
+// linearisation's owner blocks, V[9 f + q] = element q of device factor f; only
+// the factors in asm_src are read)
 // prof (optional): every launch of the factorisation / solve timed with
 // dispatch events (hipExtLaunchKernelGGL start/stop on the launch's stream),
 // with its kernel family and algorithmic flops / HBM bytes: pairs of events,

@@ -206,7 +206,7 @@ template <int kUnroll>
 __global__ __launch_bounds__(256, 4) void k_assemble_tile(CholDev c, const int4* __restrict__ tasks,
                                                        const int2* __restrict__ iptr, const int* __restrict__ items,
                                                        const int4* __restrict__ pairs, const double* __restrict__ V,
-                                                       long long S, const double* __restrict__ D,
+                                                       const double* __restrict__ D,
                                                        const double* __restrict__ lam_p, int ntile = 1 << 30,
                                                        const int* __restrict__ vfronts = nullptr) {
   lane_offset(c);
@@ -301,8 +301,8 @@ __global__ __launch_bounds__(256, 4) void k_assemble_tile(CholDev c, const int4*
           double v = 0.0;
           if (code >= 0) {
             const int e = 3 * a3 + b3;
-            v += V[bsrc[bq] + e * S];   // (0 + first slot: the sum's order and zero signs as before)
-            for (int k = 1; k < bcnt[bq]; k++) v += V[c.asm_src[c.asm_ptr[code] + k] + e * S];   // (repeated factors)
+            v += V[9 * (size_t)bsrc[bq] + e];   // (0 + first slot: the sum's order and zero signs as before)
+            for (int k = 1; k < bcnt[bq]; k++) v += V[9 * (size_t)c.asm_src[c.asm_ptr[code] + k] + e];   // (repeated factors)
           } else if (code != kAsmNone && a3 >= b3) {
             const double* d = D + 6 * (size_t)bsrc[bq];
             const int e = a3 == 0 ? 0 : (a3 == 1 ? (b3 == 0 ? 1 : 3) : (b3 == 0 ? 2 : (b3 == 1 ? 4 : 5)));
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256, 4) void k_assemble_tile(CholDev c, const int4*
 __global__ __launch_bounds__(256) void k_assemble_tile_push(CholDev c, const int4* __restrict__ tasks,
                                                        const int2* __restrict__ iptr, const int* __restrict__ items,
                                                        const int4* __restrict__ pairs, const double* __restrict__ V,
-                                                       long long S, const double* __restrict__ D,
+                                                       const double* __restrict__ D,
                                                        const double* __restrict__ lam_p) {
   lane_offset(c);
   __shared__ double T[64 * 65];
@@ -374,9 +374,9 @@ __global__ __launch_bounds__(256) void k_assemble_tile_push(CholDev c, const int
     if (code >= 0) {
       double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
       for (int k = c.asm_ptr[code]; k < c.asm_ptr[code + 1]; k++) {
-        const double* v = V + c.asm_src[k];   // element e at v[e * S]
+        const double* v = V + 9 * (size_t)c.asm_src[k];   // element e at v[e]
 #pragma unroll
-        for (int e = 0; e < 9; e++) acc[e] += v[e * S];
+        for (int e = 0; e < 9; e++) acc[e] += v[e];
       }
       const int i0 = 3 * c.asm_li[code] - R0, j0 = 3 * c.asm_lj[code] - C0;
 #pragma unroll
@@ -3565,14 +3565,14 @@ hipError_t chol_factor(const CholPlan& P, const double* D, const double* V, cons
       launch(prof, kFamAssemble, [&] { return make_double2(0, level_at_bytes(P, (int)li) * nb); },
              k_assemble_tile_push, dim3(ntile, nb), B256, 0, s, c,
              (const int4*)(P.d_ea_tasks + lv.ea_off[0]), (const int2*)(P.d_at_iptr + lv.ea_off[0]),
-             (const int*)P.d_at_items, (const int4*)P.d_ea_pairs, V, (long long)P.nslots, D,
+             (const int*)P.d_at_items, (const int4*)P.d_ea_pairs, V, D,
              (const double*)P.d_lambda);
     else if (ntile + nvec > 0)   // (the tile tasks' arrays are read only by workgroups < ntile)
       launch(prof, kFamAssemble,
              [&] { return make_double2(0, (level_at_bytes(P, (int)li) * (ntile > 0) + lv.vec_bytes * (nvec > 0)) * nb); },
              asm_unroll == 2 ? k_assemble_tile<2> : k_assemble_tile<1>, dim3(ntile + nvec, nb), B256, 0, s, c,
              (const int4*)(P.d_ea_tasks + lv.ea_off[0]), (const int2*)(P.d_at_iptr + lv.ea_off[0]),
-             (const int*)P.d_at_items, (const int4*)P.d_ea_pairs, V, (long long)P.nslots, D,
+             (const int*)P.d_at_items, (const int4*)P.d_ea_pairs, V, D,
              (const double*)P.d_lambda, ntile, (const int*)(P.d_level_fronts + lv.front_off));
     if (vec) CH_TRY(hipStreamWaitEvent(s, P.evs[1], 0));
     // small fronts on the second side stream, beside the blocked path of the

@@ -43,7 +43,7 @@ struct DevGraph {
                                     // 0: owner blocks only (the Cholesky assembly reads no others)
   int* slot_col = nullptr;
   // Cholesky-mode linearisation (write_all = 0 with a plan: owner blocks in
-  // device factor order, V[q * S + e]; see k_linearize_own)
+  // device factor order, V[9 e + q]: a factor's 9 elements together; see k_linearize_own)
   int G1 = 8;                       // lanes per row for the side-0 / side-1 sweeps
   int* erow = nullptr;              // [n+1] side-0 factors of row i: [erow[i], erow[i+1])
   int nlb = 0;                      // k_linearize_own blocks

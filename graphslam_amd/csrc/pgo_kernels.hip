@@ -156,24 +156,26 @@ __global__ __launch_bounds__(kThreads) void k_linearize(DevGraph d) {
 // [brow[b], brow[b+1]) (at most kThreads rows, their side-0 factors in chunks
 // of kThreads), so a wave streams eij / z / Omega once each, coalesced, with
 // every lane busy and no erow -> factor load chain.  Each factor's owner block
-// goes to V[q * S + e] in factor order (the assembly's source index), its
-// Omega e to W[s1pos[e]] (row ej's side-1 list) for k_linearize_side1; the factor's
-// side-0 terms (J1' Omega J1, J1' Omega e) go through LDS to one thread per
-// row, which sums them in factor order and adds Dc[i] (sum of Omega over the
-// row's side-1 factors) and the row's priors.  No error partials: the error
-// is k_error's.
+// goes to V[9 e + q] in factor order (the assembly's source index: a factor's
+// block is one 72-byte record, so the assembly's gathers read one or two lines
+// per block instead of nine), staged through LDS so a chunk's records leave as
+// contiguous 16-byte stores; its Omega e to W[s1pos[e]] (row ej's side-1 list)
+// for k_linearize_side1; the factor's side-0 terms (J1' Omega J1, J1' Omega e)
+// go through LDS to one thread per row, which sums them in factor order and
+// adds Dc[i] (sum of Omega over the row's side-1 factors) and the row's
+// priors.  No error partials: the error is k_error's.
 __global__ __launch_bounds__(kThreads) void k_linearize_own(DevGraph d) {
   __shared__ double sm[9][kThreads];
   const int t = threadIdx.x;
   const int r0 = d.brow[blockIdx.x], r1 = d.brow[blockIdx.x + 1];
   const int e0 = d.erow[r0], e1 = d.erow[r1];
-  const size_t S = d.nslots;
   const int row = r0 + t;
   const bool rowt = row < r1;
   const int rb = rowt ? d.erow[row] : 0, re = rowt ? d.erow[row + 1] : 0;
   double a00 = 0, a01 = 0, a02 = 0, a11 = 0, a12 = 0, a22 = 0, g0 = 0, g1 = 0, g2 = 0;
   for (int c0 = e0; c0 < e1; c0 += kThreads) {
     const int e = c0 + t;
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0, s7 = 0, s8 = 0;
     if (e < e1) {
       const int2 ij = d.eij[e];
       const double4 p1 = d.pose[ij.x], p2 = d.pose[ij.y], z = d.ez[e];
@@ -194,26 +196,41 @@ __global__ __launch_bounds__(kThreads) void k_linearize_own(DevGraph d) {
       const double w0 = o00 * r0e + o01 * r1e + o02 * r2e;
       const double w1 = o01 * r0e + o11 * r1e + o12 * r2e;
       const double w2 = o02 * r0e + o12 * r1e + o22 * r2e;
-      double* v = d.V + e;
+      double* v = &sm[0][0] + 9 * t;   // this factor's record, staged
       if (d.eside[e] == 0) {   // owner block H_ij = M'
-        v[0] = m00; v[S] = m10; v[2 * S] = m20;
-        v[3 * S] = m01; v[4 * S] = m11; v[5 * S] = m21;
-        v[6 * S] = m02; v[7 * S] = m12; v[8 * S] = m22;
+        v[0] = m00; v[1] = m10; v[2] = m20;
+        v[3] = m01; v[4] = m11; v[5] = m21;
+        v[6] = m02; v[7] = m12; v[8] = m22;
       } else {                 // owner block H_ji = M
-        v[0] = m00; v[S] = m01; v[2 * S] = m02;
-        v[3 * S] = m10; v[4 * S] = m11; v[5 * S] = m12;
-        v[6 * S] = m20; v[7 * S] = m21; v[8 * S] = m22;
+        v[0] = m00; v[1] = m01; v[2] = m02;
+        v[3] = m10; v[4] = m11; v[5] = m12;
+        v[6] = m20; v[7] = m21; v[8] = m22;
       }
       d.W[d.s1pos[e]] = make_double4(w0, w1, w2, 0.0);   // row ej's side-1 list order
-      sm[0][t] = -hc * m00 + hs * m10;
-      sm[1][t] = -hc * m01 + hs * m11;
-      sm[2][t] = -hc * m02 + hs * m12;
-      sm[3][t] = -hs * m01 - hc * m11;
-      sm[4][t] = -hs * m02 - hc * m12;
-      sm[5][t] = dt1 * m02 + dt2 * m12 - m22;
-      sm[6][t] = -hc * w0 + hs * w1;
-      sm[7][t] = -hs * w0 - hc * w1;
-      sm[8][t] = dt1 * w0 + dt2 * w1 - w2;
+      s0 = -hc * m00 + hs * m10;
+      s1 = -hc * m01 + hs * m11;
+      s2 = -hc * m02 + hs * m12;
+      s3 = -hs * m01 - hc * m11;
+      s4 = -hs * m02 - hc * m12;
+      s5 = dt1 * m02 + dt2 * m12 - m22;
+      s6 = -hc * w0 + hs * w1;
+      s7 = -hs * w0 - hc * w1;
+      s8 = dt1 * w0 + dt2 * w1 - w2;
+    }
+    __syncthreads();
+    {   // the chunk's records [9 c0, 9 c0 + nv): 16-byte stores from an even element on
+      const double* sv = &sm[0][0];
+      const int nv = 9 * min(kThreads, e1 - c0), head = c0 & 1;   // (9 c0 odd <=> c0 odd)
+      double* dst = d.V + 9 * (size_t)c0;
+      if (head && t == 0) dst[0] = sv[0];
+      for (int k = t; 2 * k + 1 < nv - head; k += kThreads)
+        *reinterpret_cast<double2*>(dst + head + 2 * k) = make_double2(sv[head + 2 * k], sv[head + 2 * k + 1]);
+      if (((nv - head) & 1) && t == 0) dst[nv - 1] = sv[nv - 1];
+    }
+    __syncthreads();
+    if (e < e1) {
+      sm[0][t] = s0; sm[1][t] = s1; sm[2][t] = s2; sm[3][t] = s3; sm[4][t] = s4;
+      sm[5][t] = s5; sm[6][t] = s6; sm[7][t] = s7; sm[8][t] = s8;
     }
     __syncthreads();
     if (rowt) {
@@ -480,11 +497,12 @@ __global__ __launch_bounds__(kThreads) void k_model_decrease(DevGraph d, const d
       const int se = d.slot_edge[k];
       if (!(se & 2)) continue;
       const int c = d.slot_col[k];
-      const double* v = d.V + (own_at_edge ? (se >> 2) : k);
+      const double* v = d.V + (own_at_edge ? 9 * (size_t)(se >> 2) : k);
+      const size_t st = own_at_edge ? 1 : S;   // (k_linearize_own: a factor's 9 elements together)
       const double x0 = X[3 * c], x1 = X[3 * c + 1], x2 = X[3 * c + 2];
-      const double y0 = v[0] * x0 + v[S] * x1 + v[2 * S] * x2;
-      const double y1 = v[3 * S] * x0 + v[4 * S] * x1 + v[5 * S] * x2;
-      const double y2 = v[6 * S] * x0 + v[7 * S] * x1 + v[8 * S] * x2;
+      const double y0 = v[0] * x0 + v[st] * x1 + v[2 * st] * x2;
+      const double y1 = v[3 * st] * x0 + v[4 * st] * x1 + v[5 * st] * x2;
+      const double y2 = v[6 * st] * x0 + v[7 * st] * x1 + v[8 * st] * x2;
       t += r0 * y0 + r1 * y1 + r2 * y2;
     }
     t = sg_sum<G>(t);
