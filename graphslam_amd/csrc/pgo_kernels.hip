@@ -164,7 +164,7 @@ __global__ __launch_bounds__(kThreads) void k_linearize(DevGraph d) {
 // go through LDS to one thread per row, which sums them in factor order and
 // adds Dc[i] (sum of Omega over the row's side-1 factors) and the row's
 // priors.  No error partials: the error is k_error's.
-__global__ __launch_bounds__(kThreads) void k_linearize_own(DevGraph d) {
+__global__ __launch_bounds__(kThreads, 4) void k_linearize_own(DevGraph d) {
   __shared__ double sm[9][kThreads];
   const int t = threadIdx.x;
   const int r0 = d.brow[blockIdx.x], r1 = d.brow[blockIdx.x + 1];
