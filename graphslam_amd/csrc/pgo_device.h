@@ -8,11 +8,13 @@
 //                (O00,O01)(O02,O11)(O12,O22) -- Omega upper triangle.  Factors
 //                are stored in device order, sorted by (ei, ej), so the side-0
 //                slots of a row read consecutive factors.
-//   per slot   : V 9 doubles, structure of arrays: V[q * S + k] = element q
-//                (row-major) of the 3x3 block H_{row,col} of slot k (coalesced
-//                in slot order); slot_edge int (factor << 2 | owner << 1 | side),
-//                slot_col int.  Slots of a row are contiguous (block-CSR over
-//                vertices, full symmetric storage), each between factor owns two
+//   per slot   : V 9 doubles, structure of arrays (write_all = 1: PCG and
+//                diagnostics): V[q * S + k] = element q (row-major) of the 3x3
+//                block H_{row,col} of slot k (coalesced in slot order); the
+//                Cholesky mode keeps one record per factor instead, V[9 e + q];
+//                slot_edge int (factor << 2 | owner << 1 | side), slot_col int.
+//                Slots of a row are contiguous (block-CSR over vertices, full
+//                symmetric storage), each between factor owns two
 //                slots: side 0 in row ei holds H_{ei,ej} = J1^T Omega, side 1 in
 //                row ej holds H_{ej,ei} = Omega J1.  One of the two is the
 //                factor's owner slot (side 0, or with the Cholesky plan the
