@@ -173,6 +173,20 @@ int check_assembly(const pgo::CholPlan& P) {
     if (it.y != (int)want.size() || !std::equal(want.begin(), want.end(), P.at_items.begin() + it.x))
       return fail("assembly: a tile's H entries");
   }
+  // every front's lower tiles exactly once, whatever the order (the tasks of
+  // a level are dealt to the XCDs in blocks, ea_xcd_order)
+  std::vector<std::vector<char>> seen(P.ns);
+  for (const int4& t : P.ea_tasks) {
+    const int s = t.x, ti = t.y >> 16, tj = t.y & 0xffff, nt = (P.m[s] + 63) / 64;
+    if (ti >= nt || tj > ti) return fail("assembly: a tile outside its front's lower triangle");
+    if (seen[s].empty()) seen[s].assign((size_t)nt * (nt + 1) / 2, 0);
+    char& k = seen[s][(size_t)ti * (ti + 1) / 2 + tj];
+    if (k) return fail("assembly: a tile listed twice");
+    k = 1;
+  }
+  for (int s = 0; s < P.ns; s++)
+    for (char k : seen[s])
+      if (!k) return fail("assembly: a front's tile missing");
   return 0;
 }
 

@@ -162,12 +162,13 @@ void xcd_order(std::vector<int4>& tasks, int tile) {
 // 128-byte lines at their run boundaries.  Blocks of kCols x kRows tiles of a
 // front, column-major inside, are dealt round-robin to the 8 XCDs (blockIdx
 // b -> XCD b % 8 as observed: speed only, each tile is computed alike
-// wherever and whenever it runs).  PGO_ASM_XCD=0 keeps the natural order.
+// wherever and whenever it runs).  PGO_ASM_XCD=0 keeps the natural order;
+// 2 orders every level, however few its tiles (host self-test).
 static void ea_xcd_order(std::vector<int4>& tasks, size_t off) {
   constexpr int kXcd = 8, kCols = 4, kRows = 16;
-  static const bool on = !getenv("PGO_ASM_XCD") || atoi(getenv("PGO_ASM_XCD")) != 0;
+  static const int mode = getenv("PGO_ASM_XCD") ? atoi(getenv("PGO_ASM_XCD")) : 1;
   const size_t n = tasks.size() - off;
-  if (!on || n < (size_t)4 * kXcd * kCols * kRows) return;
+  if (mode == 0 || (mode == 1 && n < (size_t)4 * kXcd * kCols * kRows)) return;
   // key: (block of the front in order of first appearance, column, row), task index
   using u128 = unsigned __int128;
   std::vector<u128> key(n);

@@ -28,10 +28,14 @@ def test_oracle_under_asan_ubsan():
     assert r.returncode == 0 and "selftest ok" in r.stdout, (r.stdout + r.stderr)[-3000:]
 
 
-def test_planner_under_asan_ubsan():
+@pytest.mark.parametrize("xcd_order", ["1", "2"])
+def test_planner_under_asan_ubsan(xcd_order):
+    """xcd_order 2: the tile-assembly tasks of every level dealt to the XCDs
+    (the default does it only on levels of >= 2048 tiles, none in the self-test's
+    graphs) -- the assembly checks then see the reordered lists."""
     b = _run(["make", "-s", "-C", "graphslam_amd/csrc", "asan-host"], timeout=600)
     assert b.returncode == 0, b.stderr[-2000:]
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="halt_on_error=1")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="halt_on_error=1", PGO_ASM_XCD=xcd_order)
     r = _run([os.path.join(ROOT, "graphslam_amd", "csrc", "build", "host_selftest_asan")], env=env)
     assert r.returncode == 0 and "host selftest ok" in r.stdout, (r.stdout + r.stderr)[-3000:]
 
