@@ -671,6 +671,33 @@ def test_c5_full_size_against_fixture(pg_cls):
     assert_poses(pg.poses()[idx], gold["poses_after_sample"], 1e-6, 1e-7)
 
 
+def _c5_trajectory_against_fixture(pg_cls, n_lin):
+    gold = np.load(os.path.join(GOLDEN, f"golden_C5-lm{n_lin}.npz"), allow_pickle=False)
+    g = datasets.make("C5")
+    import sys
+    sys.path.insert(0, GOLDEN)
+    from make_golden import input_digest
+    assert input_digest(g) == str(gold["digest"])
+    pg = pg_cls.from_dataset(g)
+    st = pg.optimize(max_outer=n_lin, lambda_lanes=3)
+    tr, gt = pg.trace(), gold["trace"]
+    assert st["linearizations"] == int(gold["linearizations"]) == n_lin
+    assert st["iterations"] == int(gold["iterations"])
+    assert tr.shape[0] == gt.shape[0] == int(gold["inner_iterations"])
+    assert np.array_equal(tr[:, 1], gt[:, 1]) and np.array_equal(tr[:, 6], gt[:, 3])
+    ok = np.isfinite(gt[:, 2])
+    assert np.array_equal(np.isfinite(tr[:, 4]), ok)
+    fe = float(gold["final_error"])
+    x = pg.poses()[gold["sample_index"]]
+    print(f"C5 lm{n_lin}: per-try error rel diff {np.max(np.abs(tr[ok, 4] / gt[ok, 2] - 1)):.2e}, "
+          f"final {abs(st['final_error'] - fe) / fe:.2e}, "
+          f"max |dxy| {np.abs(x[:, :2] - gold['final_sample'][:, :2]).max():.2e} m, "
+          f"max |dtheta| {angdiff(x[:, 2], gold['final_sample'][:, 2]).max():.2e} rad")
+    assert np.allclose(tr[ok, 4], gt[ok, 2], rtol=3e-8, atol=0)
+    assert abs(st["final_error"] - fe) <= 3e-8 * fe
+    assert_poses(x, gold["final_sample"], 1e-6, 1e-7)
+
+
 def test_c5_five_linearisations_against_fixture(pg_cls):
     """C5 past its first linearisation (round 6): the C oracle's first 5 LM
     linearisations of the 1M-pose graph (golden_C5-lm5.npz, 18 lambda tries:
@@ -680,30 +707,14 @@ def test_c5_five_linearisations_against_fixture(pg_cls):
     3e-8, poses 1e-6 m / 1e-7 rad).  Run with the bench's 3 lambda lanes
     (bitwise the sequential search, test_lanes_match_sequential).  The observed
     differences are printed."""
-    gold = np.load(os.path.join(GOLDEN, "golden_C5-lm5.npz"), allow_pickle=False)
-    g = datasets.make("C5")
-    import sys
-    sys.path.insert(0, GOLDEN)
-    from make_golden import input_digest
-    assert input_digest(g) == str(gold["digest"])
-    pg = pg_cls.from_dataset(g)
-    st = pg.optimize(max_outer=5, lambda_lanes=3)
-    tr, gt = pg.trace(), gold["trace"]
-    assert st["linearizations"] == int(gold["linearizations"]) == 5
-    assert st["iterations"] == int(gold["iterations"])
-    assert tr.shape[0] == gt.shape[0] == int(gold["inner_iterations"])
-    assert np.array_equal(tr[:, 1], gt[:, 1]) and np.array_equal(tr[:, 6], gt[:, 3])
-    ok = np.isfinite(gt[:, 2])
-    assert np.array_equal(np.isfinite(tr[:, 4]), ok)
-    fe = float(gold["final_error"])
-    x = pg.poses()[gold["sample_index"]]
-    print(f"C5 lm5: per-try error rel diff {np.max(np.abs(tr[ok, 4] / gt[ok, 2] - 1)):.2e}, "
-          f"final {abs(st['final_error'] - fe) / fe:.2e}, "
-          f"max |dxy| {np.abs(x[:, :2] - gold['final_sample'][:, :2]).max():.2e} m, "
-          f"max |dtheta| {angdiff(x[:, 2], gold['final_sample'][:, 2]).max():.2e} rad")
-    assert np.allclose(tr[ok, 4], gt[ok, 2], rtol=3e-8, atol=0)
-    assert abs(st["final_error"] - fe) <= 3e-8 * fe
-    assert_poses(x, gold["final_sample"], 1e-6, 1e-7)
+    _c5_trajectory_against_fixture(pg_cls, 5)
+
+
+def test_c5_twenty_five_linearisations_against_fixture(pg_cls):
+    """The same over the C oracle's first 25 linearisations of C5
+    (golden_C5-lm25.npz: a quarter of the bench's timed c5 line, whose 100
+    linearisations and 208 tries no CPU fixture covers whole), same tolerances."""
+    _c5_trajectory_against_fixture(pg_cls, 25)
 
 
 # ------------------------------------------------------------ incremental re-solve (SURVEY 8f row 2)
