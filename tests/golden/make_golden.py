@@ -18,14 +18,14 @@ output of the CPU restatements:
 * C5 -- the C oracle's first linearisation, first Cholesky step and first LM
   linearisation (sampled); C5-numpy -- the numpy twin's first linearisation
   (0.5 chi^2, sampled gradient and H diagonal blocks), a second source;
-  C5-lm5, C5-lm25 -- the C oracle's first 5 / 25 LM linearisations of C5
+  C5-lm5, C5-lm25, C5-lm100 -- the C oracle's first 5 / 25 / 100 LM linearisations of C5
   (every lambda try, the error after them, a 1000-pose sample of the values;
   round 6).
 
 Each fixture also records a SHA-256 of the generated inputs so a change of the
 generator is detected instead of silently comparing different graphs.
 
-    python tests/golden/make_golden.py [C1 C1-nn C2 C3 C3-gn C3-numpy C5 C5-numpy C5-lm5 C5-lm25 ...]
+    python tests/golden/make_golden.py [C1 C1-nn C2 C3 C3-gn C3-numpy C5 C5-numpy C5-lm5 C5-lm25 C5-lm100 ...]
 """
 from __future__ import annotations
 

@@ -671,7 +671,7 @@ def test_c5_full_size_against_fixture(pg_cls):
     assert_poses(pg.poses()[idx], gold["poses_after_sample"], 1e-6, 1e-7)
 
 
-def _c5_trajectory_against_fixture(pg_cls, n_lin):
+def _c5_trajectory_against_fixture(pg_cls, n_lin, rtol=3e-8, tol_xy=1e-6, tol_th=1e-7):
     gold = np.load(os.path.join(GOLDEN, f"golden_C5-lm{n_lin}.npz"), allow_pickle=False)
     g = datasets.make("C5")
     import sys
@@ -693,9 +693,9 @@ def _c5_trajectory_against_fixture(pg_cls, n_lin):
           f"final {abs(st['final_error'] - fe) / fe:.2e}, "
           f"max |dxy| {np.abs(x[:, :2] - gold['final_sample'][:, :2]).max():.2e} m, "
           f"max |dtheta| {angdiff(x[:, 2], gold['final_sample'][:, 2]).max():.2e} rad")
-    assert np.allclose(tr[ok, 4], gt[ok, 2], rtol=3e-8, atol=0)
-    assert abs(st["final_error"] - fe) <= 3e-8 * fe
-    assert_poses(x, gold["final_sample"], 1e-6, 1e-7)
+    assert np.allclose(tr[ok, 4], gt[ok, 2], rtol=rtol, atol=0)
+    assert abs(st["final_error"] - fe) <= rtol * fe
+    assert_poses(x, gold["final_sample"], tol_xy, tol_th)
 
 
 def test_c5_five_linearisations_against_fixture(pg_cls):
@@ -715,6 +715,16 @@ def test_c5_twenty_five_linearisations_against_fixture(pg_cls):
     (golden_C5-lm25.npz: a quarter of the bench's timed c5 line, whose 100
     linearisations and 208 tries no CPU fixture covers whole), same tolerances."""
     _c5_trajectory_against_fixture(pg_cls, 25)
+
+
+def test_c5_whole_timed_trajectory_against_fixture(pg_cls):
+    """The same over the bench's whole c5 line: the C oracle's 100
+    linearisations of C5 (golden_C5-lm100.npz, 208 tries, stopped at GTSAM's
+    maxIterations): every try's lambda and accept decision identical; the
+    errors and values drift apart over the 100 damped steps (the bench's own
+    run ends 3.0e-8 relative from the oracle's chi^2 of 3.6e12, far from the
+    optimum), so this one is held to rel 1e-6 and 1e-3 m / 1e-4 rad."""
+    _c5_trajectory_against_fixture(pg_cls, 100, rtol=1e-6, tol_xy=1e-3, tol_th=1e-4)
 
 
 # ------------------------------------------------------------ incremental re-solve (SURVEY 8f row 2)
